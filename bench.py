@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident quACK encode throughput (identifiers/s).
+
+Metric (BASELINE.json): "quACK encode identifiers/s (device-resident), u32
+ids, threshold t=32".  Workload at N=1 is configs[1]: encode 1e9 u32 ids at
+t=32 on one MI355X, ids already resident in HBM.  One step = one pass of the
+encode path over the GPU's batch: the encode kernel + finalize kernel, and,
+for N > 1, the single RCCL sum-reduce of the partial power-sum vectors to
+rank 0 (weak scaling: every GPU owns a fixed 1e9-id shard of one global
+stream).
+
+    python bench.py [--gpus N --steps K --warmup W --n IDS_PER_GPU --t 32 --bits 32]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Alongside the metric it reports
+  roofline      the encode kernel's achieved algorithmic HBM bytes/s (4 B per
+                u32 id) over its average launch duration, measured with HIP
+                events on the launch stream, against the 8 TB/s HBM3E peak;
+                plus the integer-VALU view (modmuls/s);
+  cpu_baseline  the oracle's scalar C restatement of the reference insert
+                loop on ONE host core over a bounded prefix of the same
+                stream (rank 0, N = 1 only), with a GPU/CPU parity check on
+                that prefix.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_traffic(bits: int, t: int, n: int):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (FETCH_SIZE
+    corrected x2 per MI355X_MICROARCH.md §HBM), scaled to n ids."""
+    path = os.path.join(ROOT, "profiles", "pmc_encode.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d["encode"][f"u{bits}_t{t}"]
+        return e["hbm_read_bytes_corrected"] / e["n_ids"] * n, os.path.relpath(path, ROOT)
+    except Exception:
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=float, default=1e9, help="ids per GPU")
+    ap.add_argument("--t", type=int, default=32)
+    ap.add_argument("--bits", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
+    ap.add_argument("--cpu-sample", type=float, default=1e8, help="ids for the CPU baseline (0 disables)")
+    ap.add_argument("--grid", type=int, default=0, help="override workgroups per launch")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import sidekick_amd as sk
+    from sidekick_amd import dist as skd
+    from sidekick_amd.quack import encode_device_async, fill_splitmix, merge_partial, partial_words
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n = int(args.n)
+    t, bits = args.t, args.bits
+    n_total = n * world
+    start, cnt = skd.shard(n_total, rank, world)
+    ctx = sk.get_context(local)
+    if args.grid:
+        ctx.set_grid(args.grid)
+    stream = torch.cuda.current_stream(local)
+
+    idt = torch.int32 if bits == 32 else torch.int64
+    ids = torch.empty(cnt, dtype=idt, device=f"cuda:{local}")
+    fill_splitmix(ctx, ids, args.seed, start, bits=bits)
+    partial = torch.zeros(partial_words(t, bits), dtype=torch.int64, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    def step():
+        encode_device_async(ctx, ids, t, partial, bits=bits)
+        if world > 1:
+            skd.reduce_partial_(partial, t, bits, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ctx.kernel_stats()  # drop warmup events
+    ctx.set_profiling(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    kern_ms, launches = ctx.kernel_stats()
+    if world > 1:
+        el = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    kern_avg_ms = kern_ms / max(launches, 1)
+
+    # result of the last step (rank 0 holds the reduced sum)
+    part_host = partial.cpu().numpy().view(np.uint64)
+    if rank == 0:
+        S, count = skd.fold_partial_sum(part_host, t, bits)
+        log(f"encode result: count={count} S[0..3]={S[:3]}")
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    bytes_per_id = 4 if bits == 32 else 8
+    value = n_total * args.steps / elapsed
+    achieved_gbs = bytes_per_id * cnt / (kern_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(bits, t, cnt)
+    modmul_rate = cnt * (t - 1) / (kern_avg_ms * 1e-3)
+
+    out = {
+        "metric": f"quACK encode identifiers/s (device-resident), u{bits} ids, threshold t={t}",
+        "value": value,
+        "unit": "identifiers/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32" if bits == 32 else "u64",
+        "data": "synthetic: splitmix64 uniform ids generated in HBM (seeded), no host copies in the timed region",
+        "config": {
+            "workload": f"encode {n:.0e} u{bits} ids per GPU at t={t}, device-resident"
+                        + ("" if world == 1 else f", {world} contiguous shards + one RCCL reduce"),
+            "ids_per_gpu": cnt, "global_ids": n_total, "threshold": t, "bits": bits,
+            "seed": hex(args.seed), "parallelism": f"shard{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": f"k_encode_u{bits} (avg of {launches} launches, HIP events on the launch stream)",
+            "kernel_avg_ms": kern_avg_ms,
+            "algorithmic_bytes_per_launch": bytes_per_id * cnt,
+            "int_valu_view": {"modmuls_per_s": modmul_rate, "ids_per_s_per_gpu": cnt / (kern_avg_ms * 1e-3)},
+        },
+        "cpu_baseline": None,
+    }
+
+    if world == 1 and args.cpu_sample > 0:
+        from oracle import coracle
+        m = int(min(args.cpu_sample, cnt))
+        tc = time.perf_counter()
+        if bits == 32:
+            cpu_S = coracle.encode_u32_seed(args.seed, m, t, start=start)
+        else:
+            cpu_S = coracle.encode_u64_seed(args.seed, m, t, start=start)
+        cpu_s = time.perf_counter() - tc
+        # GPU on the same prefix: bit-exact parity check
+        q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
+        q.insert_batch(ids[:m])
+        parity = q.power_sums() == cpu_S
+        out["cpu_baseline"] = {
+            "value": m / cpu_s, "unit": "identifiers/s", "cores": 1, "kind": "port",
+            "sample": f"first {m} ids of the same stream (seed {hex(args.seed)}), scalar C restatement of the "
+                      f"reference insert loop (oracle/quack_oracle.c), 1 host core, {cpu_s:.1f} s",
+            "parity_with_gpu": parity,
+        }
+        if not parity:
+            log("PARITY FAILURE: GPU power sums differ from the CPU oracle on the sample prefix")
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,211 @@
+/*
+ * quack_hip.h — C ABI of the MI355X-native quACK power-sum engine
+ * (libquack_hip.so).
+ *
+ * This is the drop-in boundary for the `quack` crate's encode/decode path.
+ * The reference exposes it as a Rust crate API, not an FFI;
+ * each entry point below names the reference call it replaces, and
+ * INTEGRATION.md shows the Rust `extern "C"` binding a maintainer adds so
+ * sidekick/ and media/ keep compiling against `quack::PowerSumQuackU32`.
+ *
+ * Conventions
+ *   - Plain C types only; every buffer is caller-owned.  No ownership crosses
+ *     the ABI except the opaque qk_ctx (create/destroy).
+ *   - Every function returns an int status (QK_OK == 0, negative on error)
+ *     unless documented otherwise.  No C++ exception crosses the ABI.
+ *   - Sketch state is a POD with a flexible array; size it with
+ *     qk_u32_size()/qk_u64_size().  Copying the bytes is Clone
+ *     (sidekick.rs:203-205).  The state is not internally synchronised
+ *     (the reference guards it with a Mutex: sidekick.rs:107).
+ *   - "device" functions run hand-written gfx950 kernels.  They never fall
+ *     back to the CPU: with no GPU they return QK_E_NO_DEVICE.
+ *   - `stream` is a hipStream_t passed as void*; NULL selects the context's
+ *     own stream.  "_async" functions only enqueue work on that stream.
+ *
+ * Field and semantics:  p32 = 2^32-5, p64 = 2^64-59; an id is
+ * mapped to x = id mod p; S[k-1] = sum_i x_i^k mod p for k = 1..threshold;
+ * count is a wrapping u32; last_value is the last inserted (unreduced) id.
+ */
+#ifndef QUACK_HIP_H
+#define QUACK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QK_P32 4294967291u
+#define QK_P64 18446744073709551557ull
+#define QK_MAX_THRESHOLD 1024u /* largest threshold the device kernels accept */
+
+enum {
+    QK_OK = 0,
+    QK_E_INVAL = -1,        /* bad argument (null pointer, host pointer where device expected, ...) */
+    QK_E_THRESHOLD = -2,    /* threshold 0 on insert/remove, or > QK_MAX_THRESHOLD on device */
+    QK_E_MISMATCH = -3,     /* thresholds of two sketches differ (reference panics) */
+    QK_E_UNDECODABLE = -4,  /* count > threshold: caller must reset (media_client.rs:258-261) */
+    QK_E_CAPACITY = -5,     /* output buffer too small; *n_out holds the required size */
+    QK_E_HIP = -6,          /* a HIP runtime call failed */
+    QK_E_NO_DEVICE = -7,    /* no usable gfx950 device */
+    QK_E_NOMEM = -8,
+    QK_E_FORMAT = -9        /* malformed serialized bytes */
+};
+
+const char *qk_strerror(int status);
+const char *qk_version(void);
+
+/* ------------------------------------------------------------------------
+ * Sketch state (PowerSumQuackU32 / PowerSumQuackU64)
+ * ---------------------------------------------------------------------- */
+typedef struct qk_u32 {
+    uint32_t threshold;
+    uint32_t count;       /* wrapping */
+    uint32_t has_last;    /* Option tag of last_value */
+    uint32_t last_value;
+    uint32_t power_sums[]; /* threshold entries, canonical (< QK_P32) */
+} qk_u32;
+
+typedef struct qk_u64 {
+    uint32_t threshold;
+    uint32_t count;
+    uint32_t has_last;
+    uint32_t reserved;
+    uint64_t last_value;
+    uint64_t power_sums[]; /* threshold entries, canonical (< QK_P64) */
+} qk_u64;
+
+size_t qk_u32_size(uint32_t threshold);                 /* bytes of a qk_u32 */
+size_t qk_u64_size(uint32_t threshold);
+
+/* PowerSumQuackU32::new(threshold)   — sidekick/src/sidekick.rs:32 */
+int qk_u32_init(qk_u32 *q, uint32_t threshold);
+int qk_u64_init(qk_u64 *q, uint32_t threshold);
+
+/* ---- host scalar path (per packet; a kernel launch costs more than an
+ *      insert, so these never touch the GPU) ---------------------------- */
+/* quack.insert(id)                   — sidekick.rs:42, sidekick_multi.rs:82 */
+int qk_u32_insert(qk_u32 *q, uint32_t id);
+int qk_u64_insert(qk_u64 *q, uint64_t id);
+/* my_quack.remove(id)                — media_client.rs:319 */
+int qk_u32_remove(qk_u32 *q, uint32_t id);
+int qk_u64_remove(qk_u64 *q, uint64_t id);
+/* diff_quack.sub_assign(quack)       — media_client.rs:296 (keeps q->last_value) */
+int qk_u32_sub_assign(qk_u32 *q, const qk_u32 *rhs);
+int qk_u64_sub_assign(qk_u64 *q, const qk_u64 *rhs);
+/* union of two disjoint streams, `later` following q in stream order
+ * (additivity): sums add, counts add, last from `later`. */
+int qk_u32_merge(qk_u32 *q, const qk_u32 *later);
+int qk_u64_merge(qk_u64 *q, const qk_u64 *later);
+/* diff_quack.to_coeffs()             — media_client.rs:304.
+ * Writes d = q->count coefficients c_1..c_d of prod(z - x_missing).
+ * d > threshold -> QK_E_UNDECODABLE; cap < d -> QK_E_CAPACITY (*d set). */
+int qk_u32_to_coeffs(const qk_u32 *q, uint32_t *coeffs, uint32_t cap, uint32_t *d);
+int qk_u64_to_coeffs(const qk_u64 *q, uint64_t *coeffs, uint32_t cap, uint32_t *d);
+/* quack::arithmetic::eval(&coeffs, x).value()   — media_client.rs:310.
+ * Returns the canonical value of the monic polynomial at x (d == 0 -> 1). */
+uint32_t qk_u32_eval(const uint32_t *coeffs, uint32_t d, uint32_t x);
+uint64_t qk_u64_eval(const uint64_t *coeffs, uint32_t d, uint64_t x);
+
+/* bincode 1.3 image of the serde-derived struct
+ * {power_sums: Vec<ModularInteger>, last_value: Option<T>, count: u32}
+ * (sidekick.rs:187, media_client.rs:227; layout [RECALL]). */
+size_t qk_u32_serialized_size(const qk_u32 *q);
+int qk_u32_serialize(const qk_u32 *q, uint8_t *buf, size_t cap, size_t *len);
+/* Reads the threshold from the bytes; *threshold_out lets the caller size q
+ * first (call with q == NULL). */
+int qk_u32_deserialize(const uint8_t *buf, size_t len, qk_u32 *q, uint32_t *threshold_out);
+size_t qk_u64_serialized_size(const qk_u64 *q);
+int qk_u64_serialize(const qk_u64 *q, uint8_t *buf, size_t cap, size_t *len);
+int qk_u64_deserialize(const uint8_t *buf, size_t len, qk_u64 *q, uint32_t *threshold_out);
+
+/* ------------------------------------------------------------------------
+ * Device context
+ * ---------------------------------------------------------------------- */
+typedef struct qk_ctx qk_ctx;
+
+int qk_device_count(int *n);
+int qk_ctx_create(int device, qk_ctx **out);
+void qk_ctx_destroy(qk_ctx *ctx);
+int qk_ctx_synchronize(qk_ctx *ctx, void *stream);
+/* When on, every launch of the dominant kernel (encode / root test) is
+ * bracketed by hipEvents on its stream; qk_ctx_kernel_stats() waits for them
+ * and returns the summed duration and launch count, then resets. */
+int qk_ctx_set_profiling(qk_ctx *ctx, int on);
+int qk_ctx_kernel_stats(qk_ctx *ctx, double *total_ms, uint64_t *launches);
+/* Tuning knobs (0 = automatic): workgroups per launch. */
+int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
+/* Pinned host memory for the host-input path: ids written here by the
+ * sniffer are DMA'd without a staging copy. */
+int qk_host_alloc(size_t bytes, void **out);
+int qk_host_free(void *p);
+
+/* ------------------------------------------------------------------------
+ * Batch encode — the hot path.  Replaces the per-id loop
+ *   for id in ids { quack.insert(id) }   (sidekick.rs:42 under :76-124;
+ *   media_client.rs:247-252; quack benchmark_construct) for an id array.
+ * ---------------------------------------------------------------------- */
+/* Partial vector written by the _async encoders, u64 words:
+ *   u32: [S_1..S_t (canonical), n, last_id]            (t + 2 words)
+ *   u64: [lo32(S_k), hi32(S_k) for k = 1..t, n, last_id] (2t + 2 words)
+ * The first t+1 (u32) / 2t+1 (u64) words of several partials may be summed
+ * elementwise as unsigned 64-bit integers (e.g. an RCCL sum-reduce) without
+ * overflow for up to 2^27 partials; qk_*_from_partial folds such a sum. */
+size_t qk_u32_partial_words(uint32_t threshold);
+size_t qk_u64_partial_words(uint32_t threshold);
+
+int qk_u32_encode_device_async(qk_ctx *ctx, const uint32_t *d_ids, size_t n, uint32_t threshold,
+                               uint64_t *d_partial, void *stream);
+int qk_u64_encode_device_async(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t threshold,
+                               uint64_t *d_partial, void *stream);
+/* Fold a (possibly summed) host copy of the partial into q as the stream that
+ * follows q: sums and count add; last_value taken from `last` if has_last. */
+int qk_u32_merge_partial(qk_u32 *q, const uint64_t *partial, int has_last, uint32_t last);
+int qk_u64_merge_partial(qk_u64 *q, const uint64_t *partial, int has_last, uint64_t last);
+
+/* Synchronous: encode device-resident ids and merge them into q (as if
+ * inserted in array order after q's existing content). */
+int qk_u32_encode_device(qk_ctx *ctx, const uint32_t *d_ids, size_t n, qk_u32 *q, void *stream);
+int qk_u64_encode_device(qk_ctx *ctx, const uint64_t *d_ids, size_t n, qk_u64 *q, void *stream);
+/* Synchronous: encode HOST-resident ids (the sniffed-packet case): chunked
+ * H2D through pinned staging on two streams, overlapped with the kernel. */
+int qk_u32_encode_host(qk_ctx *ctx, const uint32_t *h_ids, size_t n, qk_u32 *q);
+int qk_u64_encode_host(qk_ctx *ctx, const uint64_t *h_ids, size_t n, qk_u64 *q);
+
+/* ------------------------------------------------------------------------
+ * Decode-missing root test.  Replaces media_client.rs:306-313:
+ *   for id in log { if arithmetic::eval(&coeffs, id).value() == 0 { hit } }
+ * Hit positions (indices into the log) are returned ascending (log order);
+ * every log entry congruent to a root is a hit, duplicates included.
+ * With stop_at_value != 0 only positions before the first entry equal to
+ * stop_value are returned (the `break` at media_client.rs:307-309).
+ * *n_hits is set to the number of hits; cap < *n_hits -> QK_E_CAPACITY.
+ * ---------------------------------------------------------------------- */
+int qk_u32_root_test_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t d, const uint32_t *d_log,
+                            size_t n, int stop_at_value, uint32_t stop_value, uint64_t *hits,
+                            size_t cap, size_t *n_hits, void *stream);
+int qk_u64_root_test_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log,
+                            size_t n, int stop_at_value, uint64_t stop_value, uint64_t *hits,
+                            size_t cap, size_t *n_hits, void *stream);
+/* decode_with_log on the device: to_coeffs(diff) on the host (O(t^2)), then
+ * the root test over the device-resident log.  diff->count == 0 -> no hits;
+ * diff->count > threshold -> QK_E_UNDECODABLE. */
+int qk_u32_decode_device(qk_ctx *ctx, const qk_u32 *diff, const uint32_t *d_log, size_t n,
+                         int stop_at_last, uint64_t *hits, size_t cap, size_t *n_hits, void *stream);
+int qk_u64_decode_device(qk_ctx *ctx, const qk_u64 *diff, const uint64_t *d_log, size_t n,
+                         int stop_at_last, uint64_t *hits, size_t cap, size_t *n_hits, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Synthetic identifier streams (benchmarks/tests): counter-based splitmix64,
+ * id_i = mix(seed + (start+i+1)*0x9E3779B97F4A7C15); u32 ids = high 32 bits.
+ * ---------------------------------------------------------------------- */
+int qk_fill_splitmix_u32(qk_ctx *ctx, uint32_t *d_out, size_t n, uint64_t seed, uint64_t start,
+                         void *stream);
+int qk_fill_splitmix_u64(qk_ctx *ctx, uint64_t *d_out, size_t n, uint64_t seed, uint64_t start,
+                         void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QUACK_HIP_H */

@@ -1,0 +1,123 @@
+"""ctypes loader for oracle/_build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this.  See quack_oracle.c for what it restates (parity unpinned).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(HERE, "quack_oracle.c")
+        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+            build()
+        L = C.CDLL(LIB_PATH)
+        u32p, u64p, i64p = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_int64)
+        sig = {
+            "qo_splitmix_u32": (None, [C.c_uint64, C.c_uint64, C.c_uint64, u32p]),
+            "qo_splitmix_u64": (None, [C.c_uint64, C.c_uint64, C.c_uint64, u64p]),
+            "qo_encode_u32": (None, [u32p, C.c_uint64, C.c_uint32, u32p]),
+            "qo_encode_u32_seed": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p]),
+            "qo_encode_u64": (None, [u64p, C.c_uint64, C.c_uint32, u64p]),
+            "qo_encode_u64_seed": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
+            "qo_to_coeffs_u32": (None, [u32p, C.c_uint32, u32p]),
+            "qo_to_coeffs_u64": (None, [u64p, C.c_uint32, u64p]),
+            "qo_eval_u32": (C.c_uint32, [u32p, C.c_uint32, C.c_uint32]),
+            "qo_eval_u64": (C.c_uint64, [u64p, C.c_uint32, C.c_uint64]),
+            "qo_root_test_u32": (C.c_uint64, [u32p, C.c_uint32, u32p, C.c_uint64, i64p, C.c_uint64]),
+            "qo_root_test_u64": (C.c_uint64, [u64p, C.c_uint32, u64p, C.c_uint64, i64p, C.c_uint64]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def splitmix_u32(seed, n, start=0):
+    out = np.empty(n, dtype=np.uint32)
+    lib().qo_splitmix_u32(seed, start, n, _p(out, C.c_uint32))
+    return out
+
+
+def splitmix_u64(seed, n, start=0):
+    out = np.empty(n, dtype=np.uint64)
+    lib().qo_splitmix_u64(seed, start, n, _p(out, C.c_uint64))
+    return out
+
+
+def encode_u32(ids, t):
+    ids = np.ascontiguousarray(ids, dtype=np.uint32)
+    S = np.zeros(t, dtype=np.uint32)
+    lib().qo_encode_u32(_p(ids, C.c_uint32), len(ids), t, _p(S, C.c_uint32))
+    return [int(v) for v in S]
+
+
+def encode_u32_seed(seed, n, t, start=0):
+    S = np.zeros(t, dtype=np.uint32)
+    lib().qo_encode_u32_seed(seed, start, n, t, _p(S, C.c_uint32))
+    return [int(v) for v in S]
+
+
+def encode_u64(ids, t):
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    S = np.zeros(t, dtype=np.uint64)
+    lib().qo_encode_u64(_p(ids, C.c_uint64), len(ids), t, _p(S, C.c_uint64))
+    return [int(v) for v in S]
+
+
+def encode_u64_seed(seed, n, t, start=0):
+    S = np.zeros(t, dtype=np.uint64)
+    lib().qo_encode_u64_seed(seed, start, n, t, _p(S, C.c_uint64))
+    return [int(v) for v in S]
+
+
+def to_coeffs_u32(S):
+    S = np.ascontiguousarray(S, dtype=np.uint32)
+    c = np.zeros(len(S), dtype=np.uint32)
+    lib().qo_to_coeffs_u32(_p(S, C.c_uint32), len(S), _p(c, C.c_uint32))
+    return [int(v) for v in c]
+
+
+def to_coeffs_u64(S):
+    S = np.ascontiguousarray(np.array([int(v) for v in S], dtype=np.uint64))
+    c = np.zeros(len(S), dtype=np.uint64)
+    lib().qo_to_coeffs_u64(_p(S, C.c_uint64), len(S), _p(c, C.c_uint64))
+    return [int(v) for v in c]
+
+
+def root_test_u32(coeffs, log, cap=1 << 20):
+    c = np.ascontiguousarray(coeffs, dtype=np.uint32)
+    log = np.ascontiguousarray(log, dtype=np.uint32)
+    hits = np.zeros(cap, dtype=np.int64)
+    nh = lib().qo_root_test_u32(_p(c, C.c_uint32), len(c), _p(log, C.c_uint32), len(log), _p(hits, C.c_int64), cap)
+    return hits[:min(nh, cap)].copy(), int(nh)
+
+
+def root_test_u64(coeffs, log, cap=1 << 20):
+    c = np.ascontiguousarray(np.array([int(v) for v in coeffs], dtype=np.uint64))
+    log = np.ascontiguousarray(log, dtype=np.uint64)
+    hits = np.zeros(cap, dtype=np.int64)
+    nh = lib().qo_root_test_u64(_p(c, C.c_uint64), len(c), _p(log, C.c_uint64), len(log), _p(hits, C.c_int64), cap)
+    return hits[:min(nh, cap)].copy(), int(nh)

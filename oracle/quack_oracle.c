@@ -1,0 +1,162 @@
+/*
+ * quack_oracle.c — scalar C restatement of the quACK power-sum path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg load this (as liboracle.so via ctypes); the
+ * product library libquack_hip.so never links or calls it.
+ *
+ * PARITY STATUS: parity unpinned against the reference (the `quack` crate is
+ * an empty, un-vendored submodule: /root/reference/.gitmodules:9-11; no Rust
+ * toolchain here).  Pinned instead by algebraic known-answer tests and by
+ * agreement with the independent Python big-int restatement
+ * (oracle/quack_oracle.py) — see tests/test_oracle.py and DESIGN.md §1.
+ *
+ * The per-id loop mirrors the reference insert as called from
+ * sidekick/src/sidekick.rs:42 and sidekick_multi.rs:82: x = id mod p, then
+ * t-1 dependent modular multiplies and t modular adds, reducing with a plain
+ * `%` by the constant prime after every multiply and a compare-subtract after
+ * every add (the crate's ModularInteger arithmetic).  No SIMD, no threads:
+ * it is also the single-core CPU baseline that bench.py times.
+ *
+ * Decode (media_client.rs:295-313): Newton's identities (to_coeffs) and the
+ * Horner root test (arithmetic::eval(&coeffs, id).value() == 0).
+ */
+#include <stdint.h>
+#include <stddef.h>
+
+#define QO_P32 4294967291u                 /* 2^32 - 5  */
+#define QO_P64 18446744073709551557ull     /* 2^64 - 59 */
+#define QO_GAMMA 0x9E3779B97F4A7C15ull
+
+typedef unsigned __int128 u128;
+
+static inline uint64_t qo_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+uint64_t qo_splitmix64_at(uint64_t seed, uint64_t i) { return qo_mix(seed + (i + 1) * QO_GAMMA); }
+
+void qo_splitmix_u32(uint64_t seed, uint64_t start, uint64_t n, uint32_t *out) {
+    for (uint64_t i = 0; i < n; ++i) out[i] = (uint32_t)(qo_mix(seed + (start + i + 1) * QO_GAMMA) >> 32);
+}
+
+void qo_splitmix_u64(uint64_t seed, uint64_t start, uint64_t n, uint64_t *out) {
+    for (uint64_t i = 0; i < n; ++i) out[i] = qo_mix(seed + (start + i + 1) * QO_GAMMA);
+}
+
+/* ---- GF(p32) ---------------------------------------------------------- */
+static inline uint32_t add32(uint32_t a, uint32_t b) {
+    uint64_t s = (uint64_t)a + b;
+    return (uint32_t)(s >= QO_P32 ? s - QO_P32 : s);
+}
+static inline uint32_t sub32(uint32_t a, uint32_t b) { return a >= b ? a - b : (uint32_t)((uint64_t)a + QO_P32 - b); }
+static inline uint32_t mul32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) % QO_P32); }
+static uint32_t pow32(uint32_t a, uint32_t e) {
+    uint32_t r = 1;
+    while (e) { if (e & 1) r = mul32(r, a); a = mul32(a, a); e >>= 1; }
+    return r;
+}
+
+static inline void insert32(uint32_t *S, uint32_t t, uint32_t id) {
+    uint32_t x = id % QO_P32, y = x;
+    for (uint32_t k = 0; k + 1 < t; ++k) { S[k] = add32(S[k], y); y = mul32(y, x); }
+    S[t - 1] = add32(S[t - 1], y);
+}
+
+/* S (length t, canonical, accumulated in place) += power sums of ids. */
+void qo_encode_u32(const uint32_t *ids, uint64_t n, uint32_t t, uint32_t *S) {
+    if (t == 0) return;
+    for (uint64_t i = 0; i < n; ++i) insert32(S, t, ids[i]);
+}
+
+/* Same, over the synthetic stream ids[start..start+n) of `seed` without
+ * materialising it (bench.py cpu_baseline). */
+void qo_encode_u32_seed(uint64_t seed, uint64_t start, uint64_t n, uint32_t t, uint32_t *S) {
+    if (t == 0) return;
+    for (uint64_t i = 0; i < n; ++i) insert32(S, t, (uint32_t)(qo_mix(seed + (start + i + 1) * QO_GAMMA) >> 32));
+}
+
+void qo_remove_u32(uint32_t *S, uint32_t t, uint32_t id) {
+    uint32_t x = id % QO_P32, y = x;
+    for (uint32_t k = 0; k < t; ++k) { S[k] = sub32(S[k], y); y = mul32(y, x); }
+}
+
+/* Newton's identities: c[i] = -(S[i] + sum_{j<i} S[j] c[i-j-1]) / (i+1). */
+void qo_to_coeffs_u32(const uint32_t *S, uint32_t d, uint32_t *c) {
+    for (uint32_t i = 0; i < d; ++i) {
+        uint32_t acc = S[i];
+        for (uint32_t j = 0; j < i; ++j) acc = add32(acc, mul32(S[j], c[i - j - 1]));
+        c[i] = mul32(sub32(0, acc), pow32(i + 1, QO_P32 - 2));
+    }
+}
+
+uint32_t qo_eval_u32(const uint32_t *c, uint32_t d, uint32_t id) {
+    if (d == 0) return 1;
+    uint32_t x = id % QO_P32, r = x;
+    for (uint32_t i = 0; i + 1 < d; ++i) r = mul32(add32(r, c[i]), x);
+    return add32(r, c[d - 1]);
+}
+
+/* Hit positions in log order; returns the number of hits (may exceed cap,
+ * only the first cap are written). */
+uint64_t qo_root_test_u32(const uint32_t *c, uint32_t d, const uint32_t *log, uint64_t n,
+                          int64_t *hits, uint64_t cap) {
+    uint64_t nh = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        if (qo_eval_u32(c, d, log[i]) == 0) { if (nh < cap) hits[nh] = (int64_t)i; ++nh; }
+    return nh;
+}
+
+/* ---- GF(p64) ---------------------------------------------------------- */
+static inline uint64_t add64(uint64_t a, uint64_t b) {
+    u128 s = (u128)a + b;
+    return (uint64_t)(s >= QO_P64 ? s - QO_P64 : s);
+}
+static inline uint64_t sub64(uint64_t a, uint64_t b) { return a >= b ? a - b : (uint64_t)((u128)a + QO_P64 - b); }
+static inline uint64_t mul64(uint64_t a, uint64_t b) { return (uint64_t)(((u128)a * b) % QO_P64); }
+static uint64_t pow64(uint64_t a, uint64_t e) {
+    uint64_t r = 1;
+    while (e) { if (e & 1) r = mul64(r, a); a = mul64(a, a); e >>= 1; }
+    return r;
+}
+
+static inline void insert64(uint64_t *S, uint32_t t, uint64_t id) {
+    uint64_t x = id % QO_P64, y = x;
+    for (uint32_t k = 0; k + 1 < t; ++k) { S[k] = add64(S[k], y); y = mul64(y, x); }
+    S[t - 1] = add64(S[t - 1], y);
+}
+
+void qo_encode_u64(const uint64_t *ids, uint64_t n, uint32_t t, uint64_t *S) {
+    if (t == 0) return;
+    for (uint64_t i = 0; i < n; ++i) insert64(S, t, ids[i]);
+}
+
+void qo_encode_u64_seed(uint64_t seed, uint64_t start, uint64_t n, uint32_t t, uint64_t *S) {
+    if (t == 0) return;
+    for (uint64_t i = 0; i < n; ++i) insert64(S, t, qo_mix(seed + (start + i + 1) * QO_GAMMA));
+}
+
+void qo_to_coeffs_u64(const uint64_t *S, uint32_t d, uint64_t *c) {
+    for (uint32_t i = 0; i < d; ++i) {
+        uint64_t acc = S[i];
+        for (uint32_t j = 0; j < i; ++j) acc = add64(acc, mul64(S[j], c[i - j - 1]));
+        c[i] = mul64(sub64(0, acc), pow64(i + 1, QO_P64 - 2));
+    }
+}
+
+uint64_t qo_eval_u64(const uint64_t *c, uint32_t d, uint64_t id) {
+    if (d == 0) return 1;
+    uint64_t x = id % QO_P64, r = x;
+    for (uint32_t i = 0; i + 1 < d; ++i) r = mul64(add64(r, c[i]), x);
+    return add64(r, c[d - 1]);
+}
+
+uint64_t qo_root_test_u64(const uint64_t *c, uint32_t d, const uint64_t *log, uint64_t n,
+                          int64_t *hits, uint64_t cap) {
+    uint64_t nh = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        if (qo_eval_u64(c, d, log[i]) == 0) { if (nh < cap) hits[nh] = (int64_t)i; ++nh; }
+    return nh;
+}

@@ -1,0 +1,481 @@
+// api.hip — device half of the quACK C ABI: context, scratch management,
+// profiling events, batch encode entry points (device- and host-resident
+// ids), the decode root test, and the synthetic id generators.
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "ctx.h"
+#include "field.h"
+
+using namespace qk;
+
+// teardown paths ignore the status of hipFree/hipEventDestroy/... by design
+#pragma clang diagnostic ignored "-Wunused-value"
+#pragma clang diagnostic ignored "-Wunused-result"
+
+namespace qk {
+
+hipStream_t pick_stream(qk_ctx *ctx, void *stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+int ensure_scratch(qk_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->scratch_bytes) return QK_OK;
+    // scratch may still be in use by queued work on any stream of this ctx
+    if (ctx->d_scratch) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+    }
+    size_t sz = std::max(bytes, (size_t)1 << 20);
+    if (hipMalloc(&ctx->d_scratch, sz) != hipSuccess) return QK_E_NOMEM;
+    ctx->scratch_bytes = sz;
+    return QK_OK;
+}
+
+int ensure_hits(qk_ctx *ctx, size_t cap) {
+    if (cap <= ctx->hits_cap) return QK_OK;
+    if (ctx->d_hits) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->d_hits);
+        ctx->d_hits = nullptr;
+        ctx->hits_cap = 0;
+    }
+    size_t c = std::max(cap, (size_t)1 << 16);
+    if (hipMalloc(&ctx->d_hits, c * sizeof(uint64_t)) != hipSuccess) return QK_E_NOMEM;
+    ctx->hits_cap = c;
+    return QK_OK;
+}
+
+int ensure_stage(qk_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->stage_bytes) return QK_OK;
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->h_stage[i]) hipHostFree(ctx->h_stage[i]);
+        if (ctx->d_stage[i]) hipFree(ctx->d_stage[i]);
+        ctx->h_stage[i] = ctx->d_stage[i] = nullptr;
+    }
+    ctx->stage_bytes = 0;
+    for (int i = 0; i < 2; ++i) {
+        if (hipHostMalloc(&ctx->h_stage[i], bytes, hipHostMallocDefault) != hipSuccess) return QK_E_NOMEM;
+        if (hipMalloc(&ctx->d_stage[i], bytes) != hipSuccess) return QK_E_NOMEM;
+    }
+    ctx->stage_bytes = bytes;
+    return QK_OK;
+}
+
+bool is_device_ptr(const void *p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+static bool is_pinned_host_ptr(const void *p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+hipEvent_t prof_begin(qk_ctx *ctx, hipStream_t s) {
+    if (!ctx->profiling) return nullptr;
+    hipEvent_t e;
+    if (!ctx->ev_pool.empty()) {
+        e = ctx->ev_pool.back();
+        ctx->ev_pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        return nullptr;
+    }
+    (void)hipEventRecord(e, s);
+    return e;
+}
+
+void prof_end(qk_ctx *ctx, hipStream_t s, hipEvent_t begin) {
+    if (!ctx->profiling || !begin) return;
+    hipEvent_t e;
+    if (!ctx->ev_pool.empty()) {
+        e = ctx->ev_pool.back();
+        ctx->ev_pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        ctx->ev_pool.push_back(begin);
+        return;
+    }
+    (void)hipEventRecord(e, s);
+    ctx->prof_pending.emplace_back(begin, e);
+}
+
+// ------------------------------------------------------------ fill kernels
+__global__ void k_fill_u32(uint32_t *out, uint64_t n, uint64_t seed, uint64_t start) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr)
+        out[i] = (uint32_t)(splitmix_mix(seed + (start + i + 1) * GAMMA) >> 32);
+}
+__global__ void k_fill_u64(uint64_t *out, uint64_t n, uint64_t seed, uint64_t start) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthr)
+        out[i] = splitmix_mix(seed + (start + i + 1) * GAMMA);
+}
+
+__global__ void k_init_counters(uint64_t *c) {
+    c[0] = 0;
+    c[1] = ~0ull;
+}
+
+// Host-resident ids: chunked H2D on copy_stream overlapped with the encode
+// kernel on ctx->stream; two device slots.  Pinned input is DMA'd directly,
+// pageable input is first copied into pinned staging.
+template <typename IdT, typename Launch>
+static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t, size_t words, Launch launch,
+                            uint64_t *partial_out) {
+    const size_t chunk_ids = (size_t)64 << 20 >> (sizeof(IdT) == 4 ? 2 : 3); // 64 MiB chunks
+    const size_t chunk_bytes = chunk_ids * sizeof(IdT);
+    int rc = ensure_stage(ctx, chunk_bytes);
+    if (rc) return rc;
+    const bool pinned = is_pinned_host_ptr(h_ids);
+    hipStream_t cs = ctx->copy_stream, ks = ctx->stream;
+    hipEvent_t copied[2], consumed[2];
+    for (int i = 0; i < 2; ++i) {
+        if (hipEventCreateWithFlags(&copied[i], hipEventDisableTiming) != hipSuccess) return QK_E_HIP;
+        if (hipEventCreateWithFlags(&consumed[i], hipEventDisableTiming) != hipSuccess) return QK_E_HIP;
+    }
+    // zero the accumulating partial
+    QK_HIP_TRY(hipMemsetAsync(ctx->d_small, 0, words * 8, ks));
+    bool used[2] = {false, false};
+    for (size_t off = 0, c = 0; off < n; off += chunk_ids, ++c) {
+        const int slot = (int)(c & 1);
+        const size_t m = std::min(chunk_ids, n - off);
+        if (used[slot]) {
+            // the kernel that read d_stage[slot] (and the copy that read
+            // h_stage[slot]) must be done before we overwrite them
+            QK_HIP_TRY(hipStreamWaitEvent(cs, consumed[slot], 0));
+            if (!pinned) QK_HIP_TRY(hipEventSynchronize(copied[slot]));
+        }
+        const void *src = h_ids + off;
+        if (!pinned) {
+            memcpy(ctx->h_stage[slot], h_ids + off, m * sizeof(IdT));
+            src = ctx->h_stage[slot];
+        }
+        QK_HIP_TRY(hipMemcpyAsync(ctx->d_stage[slot], src, m * sizeof(IdT), hipMemcpyHostToDevice, cs));
+        QK_HIP_TRY(hipEventRecord(copied[slot], cs));
+        QK_HIP_TRY(hipStreamWaitEvent(ks, copied[slot], 0));
+        rc = launch(ctx, (const IdT *)ctx->d_stage[slot], m, t, ctx->d_small, ks);
+        if (rc) return rc;
+        QK_HIP_TRY(hipEventRecord(consumed[slot], ks));
+        used[slot] = true;
+    }
+    QK_HIP_TRY(hipMemcpyAsync(partial_out, ctx->d_small, words * 8, hipMemcpyDeviceToHost, ks));
+    QK_HIP_TRY(hipStreamSynchronize(ks));
+    QK_HIP_TRY(hipStreamSynchronize(cs));
+    for (int i = 0; i < 2; ++i) { hipEventDestroy(copied[i]); hipEventDestroy(consumed[i]); }
+    return QK_OK;
+}
+
+template <typename T, typename Launch>
+static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop,
+                          T stop_value, uint64_t *hits, size_t cap, size_t *n_hits, void *stream, Launch launch) {
+    if (!ctx || !n_hits || (d && !coeffs) || (n && !d_log)) return QK_E_INVAL;
+    *n_hits = 0;
+    if (d == 0 || n == 0) return QK_OK; // P == 1 has no roots
+    if (d > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if (!is_device_ptr(d_log)) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = pick_stream(ctx, stream);
+    // layout of d_small: [0, SMALL_NHITS) coefficients, [SMALL_NHITS] hit count, [SMALL_STOP] stop index
+    uint64_t *d_counters = ctx->d_small + SMALL_NHITS;
+    T *d_c = (T *)ctx->d_small;
+    memcpy(ctx->h_small, coeffs, (size_t)d * sizeof(T));
+    QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, (size_t)d * sizeof(T), hipMemcpyHostToDevice, s));
+    size_t dev_cap = std::max(cap, (size_t)4096);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        int rc = ensure_hits(ctx, dev_cap);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_init_counters, dim3(1), dim3(1), 0, s, d_counters);
+        rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap, d_counters, s);
+        if (rc) return rc;
+        uint64_t cnt[2];
+        QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_NHITS, d_counters, 16, hipMemcpyDeviceToHost, s));
+        QK_HIP_TRY(hipStreamSynchronize(s));
+        cnt[0] = ctx->h_small[SMALL_NHITS];
+        cnt[1] = ctx->h_small[SMALL_STOP];
+        if (cnt[0] > ctx->hits_cap) { dev_cap = (size_t)cnt[0]; continue; } // grow and rerun once
+        std::vector<uint64_t> h(cnt[0]);
+        if (cnt[0]) {
+            QK_HIP_TRY(hipMemcpyAsync(h.data(), ctx->d_hits, cnt[0] * 8, hipMemcpyDeviceToHost, s));
+            QK_HIP_TRY(hipStreamSynchronize(s));
+        }
+        std::sort(h.begin(), h.end());
+        size_t m = h.size();
+        if (use_stop) m = (size_t)(std::lower_bound(h.begin(), h.end(), cnt[1]) - h.begin());
+        *n_hits = m;
+        if (m > cap || (m && !hits)) return QK_E_CAPACITY;
+        std::copy(h.begin(), h.begin() + m, hits);
+        return QK_OK;
+    }
+    return QK_E_HIP;
+}
+
+} // namespace qk
+
+// =========================================================================
+extern "C" {
+
+int qk_device_count(int *n) {
+    if (!n) return QK_E_INVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) {
+        (void)hipGetLastError();
+        *n = 0;
+        return QK_E_NO_DEVICE;
+    }
+    *n = c;
+    return c > 0 ? QK_OK : QK_E_NO_DEVICE;
+}
+
+int qk_ctx_create(int device, qk_ctx **out) {
+    if (!out) return QK_E_INVAL;
+    *out = nullptr;
+    int n = 0;
+    if (qk_device_count(&n) != QK_OK || device < 0 || device >= n) return QK_E_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return QK_E_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return QK_E_NO_DEVICE; // code objects are gfx950-only
+    if (hipSetDevice(device) != hipSuccess) return QK_E_HIP;
+    qk_ctx *ctx = new (std::nothrow) qk_ctx();
+    if (!ctx) return QK_E_NOMEM;
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&ctx->d_small, SMALL_WORDS * sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_small, SMALL_WORDS * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->stage_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->stage_ev[1], hipEventDisableTiming) != hipSuccess) {
+        qk_ctx_destroy(ctx);
+        return QK_E_HIP;
+    }
+    *out = ctx;
+    return QK_OK;
+}
+
+void qk_ctx_destroy(qk_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    for (auto &pr : ctx->prof_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+    for (auto e : ctx->ev_pool) hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->h_stage[i]) hipHostFree(ctx->h_stage[i]);
+        if (ctx->d_stage[i]) hipFree(ctx->d_stage[i]);
+        if (ctx->stage_ev[i]) hipEventDestroy(ctx->stage_ev[i]);
+    }
+    if (ctx->d_scratch) hipFree(ctx->d_scratch);
+    if (ctx->d_hits) hipFree(ctx->d_hits);
+    if (ctx->d_small) hipFree(ctx->d_small);
+    if (ctx->h_small) hipHostFree(ctx->h_small);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->copy_stream) hipStreamDestroy(ctx->copy_stream);
+    delete ctx;
+}
+
+int qk_ctx_synchronize(qk_ctx *ctx, void *stream) {
+    if (!ctx) return QK_E_INVAL;
+    QK_HIP_TRY(hipStreamSynchronize(pick_stream(ctx, stream)));
+    return QK_OK;
+}
+
+int qk_ctx_set_profiling(qk_ctx *ctx, int on) {
+    if (!ctx) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->profiling = on != 0;
+    return QK_OK;
+}
+
+int qk_ctx_kernel_stats(qk_ctx *ctx, double *total_ms, uint64_t *launches) {
+    if (!ctx || !total_ms || !launches) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    double tot = 0;
+    uint64_t cnt = 0;
+    int rc = QK_OK;
+    for (auto &pr : ctx->prof_pending) {
+        if (hipEventSynchronize(pr.second) != hipSuccess) rc = QK_E_HIP;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) { tot += ms; ++cnt; }
+        ctx->ev_pool.push_back(pr.first);
+        ctx->ev_pool.push_back(pr.second);
+    }
+    ctx->prof_pending.clear();
+    *total_ms = tot;
+    *launches = cnt;
+    return rc;
+}
+
+int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks) {
+    if (!ctx) return QK_E_INVAL;
+    ctx->grid_override = blocks;
+    return QK_OK;
+}
+
+int qk_host_alloc(size_t bytes, void **out) {
+    if (!out) return QK_E_INVAL;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) { *out = nullptr; return QK_E_NOMEM; }
+    return QK_OK;
+}
+int qk_host_free(void *p) {
+    if (p && hipHostFree(p) != hipSuccess) return QK_E_HIP;
+    return QK_OK;
+}
+
+// ------------------------------------------------------------ encode
+int qk_u32_encode_device_async(qk_ctx *ctx, const uint32_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial,
+                               void *stream) {
+    if (!ctx || !d_partial || (n && !d_ids)) return QK_E_INVAL;
+    if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if ((n && !is_device_ptr(d_ids)) || !is_device_ptr(d_partial)) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    return launch_encode_u32(ctx, d_ids, n, t, d_partial, pick_stream(ctx, stream));
+}
+
+int qk_u64_encode_device_async(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial,
+                               void *stream) {
+    if (!ctx || !d_partial || (n && !d_ids)) return QK_E_INVAL;
+    if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if ((n && !is_device_ptr(d_ids)) || !is_device_ptr(d_partial)) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    return launch_encode_u64(ctx, d_ids, n, t, d_partial, pick_stream(ctx, stream));
+}
+
+int qk_u32_encode_device(qk_ctx *ctx, const uint32_t *d_ids, size_t n, qk_u32 *q, void *stream) {
+    if (!ctx || !q || (n && !d_ids)) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if (n == 0) return QK_OK;
+    if (!is_device_ptr(d_ids)) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = pick_stream(ctx, stream);
+    int rc = launch_encode_u32(ctx, d_ids, n, t, ctx->d_small, s);
+    if (rc) return rc;
+    const size_t w = qk_u32_partial_words(t);
+    QK_HIP_TRY(hipMemcpyAsync(ctx->h_small, ctx->d_small, w * 8, hipMemcpyDeviceToHost, s));
+    QK_HIP_TRY(hipStreamSynchronize(s));
+    return qk_u32_merge_partial(q, ctx->h_small, 1, (uint32_t)ctx->h_small[t + 1]);
+}
+
+int qk_u64_encode_device(qk_ctx *ctx, const uint64_t *d_ids, size_t n, qk_u64 *q, void *stream) {
+    if (!ctx || !q || (n && !d_ids)) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if (n == 0) return QK_OK;
+    if (!is_device_ptr(d_ids)) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = pick_stream(ctx, stream);
+    int rc = launch_encode_u64(ctx, d_ids, n, t, ctx->d_small, s);
+    if (rc) return rc;
+    const size_t w = qk_u64_partial_words(t);
+    QK_HIP_TRY(hipMemcpyAsync(ctx->h_small, ctx->d_small, w * 8, hipMemcpyDeviceToHost, s));
+    QK_HIP_TRY(hipStreamSynchronize(s));
+    return qk_u64_merge_partial(q, ctx->h_small, 1, ctx->h_small[2 * t + 1]);
+}
+
+int qk_u32_encode_host(qk_ctx *ctx, const uint32_t *h_ids, size_t n, qk_u32 *q) {
+    if (!ctx || !q || (n && !h_ids)) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if (n == 0) return QK_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    const size_t w = qk_u32_partial_words(t);
+    int rc = encode_host_impl<uint32_t>(ctx, h_ids, n, t, w, launch_encode_u32_acc, ctx->h_small);
+    if (rc) return rc;
+    return qk_u32_merge_partial(q, ctx->h_small, 1, h_ids[n - 1]);
+}
+
+int qk_u64_encode_host(qk_ctx *ctx, const uint64_t *h_ids, size_t n, qk_u64 *q) {
+    if (!ctx || !q || (n && !h_ids)) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if (n == 0) return QK_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    const size_t w = qk_u64_partial_words(t);
+    int rc = encode_host_impl<uint64_t>(ctx, h_ids, n, t, w, launch_encode_u64_acc, ctx->h_small);
+    if (rc) return rc;
+    return qk_u64_merge_partial(q, ctx->h_small, 1, h_ids[n - 1]);
+}
+
+// ------------------------------------------------------------ root test
+int qk_u32_root_test_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t d, const uint32_t *d_log, size_t n,
+                            int stop_at_value, uint32_t stop_value, uint64_t *hits, size_t cap, size_t *n_hits,
+                            void *stream) {
+    return root_test_impl<uint32_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
+                                    launch_root_test_u32);
+}
+
+int qk_u64_root_test_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log, size_t n,
+                            int stop_at_value, uint64_t stop_value, uint64_t *hits, size_t cap, size_t *n_hits,
+                            void *stream) {
+    return root_test_impl<uint64_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
+                                    launch_root_test_u64);
+}
+
+int qk_u32_decode_device(qk_ctx *ctx, const qk_u32 *diff, const uint32_t *d_log, size_t n, int stop_at_last,
+                         uint64_t *hits, size_t cap, size_t *n_hits, void *stream) {
+    if (!ctx || !diff || !n_hits) return QK_E_INVAL;
+    *n_hits = 0;
+    if (diff->count == 0) return QK_OK;
+    std::vector<uint32_t> c(diff->threshold ? diff->threshold : 1);
+    uint32_t d = 0;
+    int rc = qk_u32_to_coeffs(diff, c.data(), (uint32_t)c.size(), &d);
+    if (rc) return rc;
+    return qk_u32_root_test_device(ctx, c.data(), d, d_log, n, stop_at_last && diff->has_last, diff->last_value,
+                                   hits, cap, n_hits, stream);
+}
+
+int qk_u64_decode_device(qk_ctx *ctx, const qk_u64 *diff, const uint64_t *d_log, size_t n, int stop_at_last,
+                         uint64_t *hits, size_t cap, size_t *n_hits, void *stream) {
+    if (!ctx || !diff || !n_hits) return QK_E_INVAL;
+    *n_hits = 0;
+    if (diff->count == 0) return QK_OK;
+    std::vector<uint64_t> c(diff->threshold ? diff->threshold : 1);
+    uint32_t d = 0;
+    int rc = qk_u64_to_coeffs(diff, c.data(), (uint32_t)c.size(), &d);
+    if (rc) return rc;
+    return qk_u64_root_test_device(ctx, c.data(), d, d_log, n, stop_at_last && diff->has_last, diff->last_value,
+                                   hits, cap, n_hits, stream);
+}
+
+// ------------------------------------------------------------ fills
+int qk_fill_splitmix_u32(qk_ctx *ctx, uint32_t *d_out, size_t n, uint64_t seed, uint64_t start, void *stream) {
+    if (!ctx || (n && !d_out)) return QK_E_INVAL;
+    if (n == 0) return QK_OK;
+    if (!is_device_ptr(d_out)) return QK_E_INVAL;
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 16);
+    hipLaunchKernelGGL(k_fill_u32, dim3((uint32_t)blocks), dim3(256), 0, pick_stream(ctx, stream), d_out,
+                       (uint64_t)n, seed, start);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
+}
+
+int qk_fill_splitmix_u64(qk_ctx *ctx, uint64_t *d_out, size_t n, uint64_t seed, uint64_t start, void *stream) {
+    if (!ctx || (n && !d_out)) return QK_E_INVAL;
+    if (n == 0) return QK_OK;
+    if (!is_device_ptr(d_out)) return QK_E_INVAL;
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 16);
+    hipLaunchKernelGGL(k_fill_u64, dim3((uint32_t)blocks), dim3(256), 0, pick_stream(ctx, stream), d_out,
+                       (uint64_t)n, seed, start);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,80 @@
+// ctx.h — internal: the device context behind qk_ctx* and launch helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
+
+#include "quack_hip.h"
+
+struct qk_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;      // own stream (NULL stream arg selects it)
+    hipStream_t copy_stream = nullptr; // second stream for the host-input pipeline
+    uint32_t grid_override = 0;
+
+    // scratch: block partials of the encode kernels, hit buffers of the root test
+    void *d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    uint64_t *d_small = nullptr;       // partial output / hit counters (small, fixed)
+    uint64_t *h_small = nullptr;       // pinned mirror of d_small
+    uint64_t *d_hits = nullptr;
+    size_t hits_cap = 0;
+
+    // host-input pipeline: pinned staging + device chunk buffers (2 slots)
+    void *h_stage[2] = {nullptr, nullptr};
+    void *d_stage[2] = {nullptr, nullptr};
+    size_t stage_bytes = 0;
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+
+    // profiling of the dominant kernel
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_pending;
+    std::vector<hipEvent_t> ev_pool;
+
+    std::mutex mu;
+};
+
+#define QK_HIP_TRY(expr)                                                                           \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) return QK_E_HIP;                                                     \
+    } while (0)
+
+namespace qk {
+
+// Small-buffer layout (u64 words) inside ctx->d_small.
+constexpr size_t SMALL_WORDS = 4096;   // >= max partial words (2*1024+2) plus counters
+constexpr size_t SMALL_NHITS = 3072;   // hit counter
+constexpr size_t SMALL_STOP = 3073;    // first stop index
+
+hipStream_t pick_stream(qk_ctx *ctx, void *stream);
+int ensure_scratch(qk_ctx *ctx, size_t bytes);
+int ensure_hits(qk_ctx *ctx, size_t cap);
+int ensure_stage(qk_ctx *ctx, size_t bytes);
+bool is_device_ptr(const void *p);
+hipEvent_t prof_begin(qk_ctx *ctx, hipStream_t s);
+void prof_end(qk_ctx *ctx, hipStream_t s, hipEvent_t begin);
+
+// encode launchers (encode.hip): enqueue main kernel + finalize writing the
+// (t+2)-word / (2t+2)-word partial to d_partial.
+int launch_encode_u32(qk_ctx *ctx, const uint32_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial,
+                      hipStream_t s);
+int launch_encode_u64(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial,
+                      hipStream_t s);
+// accumulate-variant used by the host pipeline: adds into d_partial instead
+// of overwriting (words 0..t-1 / 0..2t-1 and the count word; last word set).
+int launch_encode_u32_acc(qk_ctx *ctx, const uint32_t *d_ids, size_t n, uint32_t t,
+                          uint64_t *d_partial, hipStream_t s);
+int launch_encode_u64_acc(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t t,
+                          uint64_t *d_partial, hipStream_t s);
+
+int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uint32_t *log, size_t n,
+                         int use_stop, uint32_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
+                         hipStream_t s);
+int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uint64_t *log, size_t n,
+                         int use_stop, uint64_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
+                         hipStream_t s);
+
+} // namespace qk

@@ -1,0 +1,206 @@
+// decode.hip — decode-missing root test on gfx950.
+//
+// Replaces the candidate scan of media_client.rs:306-313
+//     for (seqno, id) in log { if Some(id) == diff.last_value() { break }
+//                              if arithmetic::eval(&coeffs, id).value() == 0 { missing.push } }
+// for a candidate log resident in HBM.  Each lane tests 4 (u32) or 2 (u64)
+// candidates per 16-byte load; the d coefficients are wave-uniform and come
+// from the scalar cache.  The polynomial is evaluated in the fused form
+// r <- r*x + c_i (one lazy mad per coefficient), which is the same
+// polynomial z^d + c_1 z^(d-1) + ... + c_d as the reference's
+// r <- (r + c_i)*x form, so the canonical value (and the ==0 test) is
+// identical.  Hits are rare (d roots among n candidates): appended with an
+// atomic ticket; the host sorts them into log order.  The `break` at the
+// first log entry equal to diff.last_value() becomes an atomicMin of that
+// position; the host drops hits at or after it.
+#include "ctx.h"
+#include "field.h"
+
+namespace qk {
+
+constexpr int RT_BLOCK = 256;
+
+__device__ __forceinline__ void rt_record(uint64_t pos, bool hit, bool stop, uint64_t *hits, uint64_t cap,
+                                          uint64_t *counters) {
+    if (hit) {
+        const uint64_t slot = atomicAdd((unsigned long long *)&counters[0], 1ull);
+        if (slot < cap) hits[slot] = pos;
+    }
+    if (stop) atomicMin((unsigned long long *)&counters[1], (unsigned long long)pos);
+}
+
+// ------------------------------------------------------------------ u32
+__device__ __forceinline__ bool is_root32(uint32_t x, const uint32_t *__restrict__ c, uint32_t d) {
+    // P(x) = (((x + c1) x + c2) x + ... ) x + c_d, evaluated as r = r*x + c
+    uint32_t r = mad32_lazy(1u, x, c[0]);
+    for (uint32_t i = 1; i < d; ++i) r = mad32_lazy(r, x, c[i]);
+    return canon32(r) == 0;
+}
+
+template <int D> // D > 0: compile-time degree, coefficients fully in SGPRs
+__device__ __forceinline__ void horner32x4(uint4 w, const uint32_t *__restrict__ c, uint32_t d, bool (&hit)[4]) {
+    uint32_t r0, r1, r2, r3;
+    r0 = mad32_lazy(1u, w.x, c[0]);
+    r1 = mad32_lazy(1u, w.y, c[0]);
+    r2 = mad32_lazy(1u, w.z, c[0]);
+    r3 = mad32_lazy(1u, w.w, c[0]);
+    if constexpr (D > 0) {
+#pragma unroll
+        for (int i = 1; i < D; ++i) {
+            const uint32_t ci = c[i];
+            r0 = mad32_lazy(r0, w.x, ci);
+            r1 = mad32_lazy(r1, w.y, ci);
+            r2 = mad32_lazy(r2, w.z, ci);
+            r3 = mad32_lazy(r3, w.w, ci);
+        }
+    } else {
+#pragma unroll 4
+        for (uint32_t i = 1; i < d; ++i) {
+            const uint32_t ci = c[i];
+            r0 = mad32_lazy(r0, w.x, ci);
+            r1 = mad32_lazy(r1, w.y, ci);
+            r2 = mad32_lazy(r2, w.z, ci);
+            r3 = mad32_lazy(r3, w.w, ci);
+        }
+    }
+    hit[0] = canon32(r0) == 0;
+    hit[1] = canon32(r1) == 0;
+    hit[2] = canon32(r2) == 0;
+    hit[3] = canon32(r3) == 0;
+}
+
+template <int D>
+__global__ __launch_bounds__(RT_BLOCK) void k_root_test_u32(const uint32_t *__restrict__ log, uint64_t n,
+                                                            uint32_t head, const uint32_t *__restrict__ c,
+                                                            uint32_t d, int use_stop, uint32_t stop_value,
+                                                            uint64_t *__restrict__ hits, uint64_t cap,
+                                                            uint64_t *__restrict__ counters) {
+    const uint64_t gtid = (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * RT_BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t body = (n - h) >> 2;
+    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(log + h);
+    for (uint64_t i = gtid; i < body; i += nthr) {
+        const uint4 w = v[i];
+        bool hit[4];
+        horner32x4<D>(w, c, d, hit);
+        const uint64_t pos = h + 4 * i;
+        const bool s0 = use_stop && w.x == stop_value, s1 = use_stop && w.y == stop_value;
+        const bool s2 = use_stop && w.z == stop_value, s3 = use_stop && w.w == stop_value;
+        if (hit[0] | hit[1] | hit[2] | hit[3] | s0 | s1 | s2 | s3) {
+            rt_record(pos + 0, hit[0], s0, hits, cap, counters);
+            rt_record(pos + 1, hit[1], s1, hits, cap, counters);
+            rt_record(pos + 2, hit[2], s2, hits, cap, counters);
+            rt_record(pos + 3, hit[3], s3, hits, cap, counters);
+        }
+    }
+    const uint64_t tail0 = h + (body << 2);
+    if (gtid < h) {
+        const uint32_t x = log[gtid];
+        rt_record(gtid, is_root32(x, c, d), use_stop && x == stop_value, hits, cap, counters);
+    }
+    if (gtid < n - tail0) {
+        const uint64_t pos = tail0 + gtid;
+        const uint32_t x = log[pos];
+        rt_record(pos, is_root32(x, c, d), use_stop && x == stop_value, hits, cap, counters);
+    }
+}
+
+// ------------------------------------------------------------------ u64
+__device__ __forceinline__ bool is_root64(uint64_t x, const uint64_t *__restrict__ c, uint32_t d) {
+    uint64_t r = mad64_lazy(1ull, x, c[0]);
+    for (uint32_t i = 1; i < d; ++i) r = mad64_lazy(r, x, c[i]);
+    return canon64(r) == 0;
+}
+
+__global__ __launch_bounds__(RT_BLOCK) void k_root_test_u64(const uint64_t *__restrict__ log, uint64_t n,
+                                                            uint32_t head, const uint64_t *__restrict__ c,
+                                                            uint32_t d, int use_stop, uint64_t stop_value,
+                                                            uint64_t *__restrict__ hits, uint64_t cap,
+                                                            uint64_t *__restrict__ counters) {
+    const uint64_t gtid = (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * RT_BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t body = (n - h) >> 1;
+    const ulonglong2 *__restrict__ v = reinterpret_cast<const ulonglong2 *>(log + h);
+    for (uint64_t i = gtid; i < body; i += nthr) {
+        const ulonglong2 w = v[i];
+        uint64_t r0 = mad64_lazy(1ull, w.x, c[0]), r1 = mad64_lazy(1ull, w.y, c[0]);
+#pragma unroll 2
+        for (uint32_t k = 1; k < d; ++k) {
+            const uint64_t ck = c[k];
+            r0 = mad64_lazy(r0, w.x, ck);
+            r1 = mad64_lazy(r1, w.y, ck);
+        }
+        const bool h0 = canon64(r0) == 0, h1 = canon64(r1) == 0;
+        const bool s0 = use_stop && w.x == stop_value, s1 = use_stop && w.y == stop_value;
+        if (h0 | h1 | s0 | s1) {
+            rt_record(h + 2 * i, h0, s0, hits, cap, counters);
+            rt_record(h + 2 * i + 1, h1, s1, hits, cap, counters);
+        }
+    }
+    const uint64_t tail0 = h + (body << 1);
+    if (gtid < h) {
+        const uint64_t x = log[gtid];
+        rt_record(gtid, is_root64(x, c, d), use_stop && x == stop_value, hits, cap, counters);
+    }
+    if (gtid < n - tail0) {
+        const uint64_t pos = tail0 + gtid;
+        const uint64_t x = log[pos];
+        rt_record(pos, is_root64(x, c, d), use_stop && x == stop_value, hits, cap, counters);
+    }
+}
+
+// ---------------------------------------------------------- launchers
+template <typename KernelT>
+static uint32_t rt_grid(qk_ctx *ctx, KernelT kern, uint64_t units) {
+    if (ctx->grid_override) return ctx->grid_override;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, RT_BLOCK, 0) != hipSuccess || occ < 1) occ = 1;
+    const uint64_t full = (uint64_t)ctx->num_cus * occ;
+    uint64_t need = (units + RT_BLOCK - 1) / RT_BLOCK;
+    if (need < 1) need = 1;
+    return (uint32_t)(need < full ? need : full);
+}
+
+int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uint32_t *log, size_t n,
+                         int use_stop, uint32_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
+                         hipStream_t s) {
+    const uintptr_t a = (uintptr_t)log;
+    if (a & 3) return QK_E_INVAL;
+    const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 4);
+    const uint64_t units = (n + 3) / 4;
+    hipEvent_t e0 = prof_begin(ctx, s);
+#define QK_RT32(DD)                                                                                \
+    hipLaunchKernelGGL(k_root_test_u32<DD>, dim3(rt_grid(ctx, k_root_test_u32<DD>, units)),        \
+                       dim3(RT_BLOCK), 0, s, log, (uint64_t)n, head, d_c, d, use_stop, stop_value, \
+                       hits, cap, counters)
+    switch (d) {
+    case 8: QK_RT32(8); break;
+    case 16: QK_RT32(16); break;
+    case 20: QK_RT32(20); break;
+    case 32: QK_RT32(32); break;
+    default: QK_RT32(0); break;
+    }
+#undef QK_RT32
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
+}
+
+int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uint64_t *log, size_t n,
+                         int use_stop, uint64_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
+                         hipStream_t s) {
+    const uintptr_t a = (uintptr_t)log;
+    if (a & 7) return QK_E_INVAL;
+    const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
+    const uint64_t units = (n + 1) / 2;
+    hipEvent_t e0 = prof_begin(ctx, s);
+    hipLaunchKernelGGL(k_root_test_u64, dim3(rt_grid(ctx, k_root_test_u64, units)), dim3(RT_BLOCK), 0, s, log,
+                       (uint64_t)n, head, d_c, d, use_stop, stop_value, hits, cap, counters);
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
+}
+
+} // namespace qk

@@ -1,0 +1,495 @@
+// encode.hip — batch power-sum encode on gfx950 (the hot path).
+//
+// Replaces the reference's per-id loop `for id in ids { quack.insert(id) }`
+// (sidekick/src/sidekick.rs:42 inside the sniff loop :76-124; quack's
+// benchmark_construct, figures/fig2_microbenchmarks.py:220-228) for an id
+// array resident in HBM.
+//
+// Work decomposition:
+//   * A lane group of G lanes owns one id at a time; lane j of the group
+//     computes the powers j+1, j+1+G, ..., j+1+(K-1)G of x = id (mod p) with
+//     a step of x^G, keeping K lazy accumulators in VGPRs.  G*K >= t.
+//     t = 32 (the headline) is G = 1, K = 32: each lane streams its own ids
+//     with 16-byte loads and runs 31 dependent lazy modmuls per id.
+//   * The ids are never reduced mod p up front: x^k is congruent either way
+//     and the lazy accumulators are folded once per lane at the end.
+//   * Lane partials -> wavefront butterfly (shfl_xor over lanes with equal
+//     lane % G) -> LDS across the 4 waves -> one partial per block per power,
+//     stored [power][block] -> a finalize kernel (t workgroups) sums the
+//     block partials and writes the canonical partial vector.
+// Integer VALU bound (no MFMA: nothing here is a contraction); the HBM read
+// of 4 B/id is ~5% of the roofline at t = 32.
+#include "ctx.h"
+#include "field.h"
+
+namespace qk {
+
+constexpr int BLOCK = 256;
+constexpr int WAVES = BLOCK / 64;
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = __shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ------------------------------------------------------------------ u32
+template <int K>
+__device__ __forceinline__ void chain32(uint64_t (&acc)[K], uint32_t start, uint32_t step) {
+    uint32_t y = start;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        acc[k] += y;
+        if (k + 1 < K) y = mul32_lazy(y, step);
+    }
+}
+
+// four independent ids in lockstep (ILP for the dependent modmul chains)
+template <int K>
+__device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
+    uint32_t y0 = w.x, y1 = w.y, y2 = w.z, y3 = w.w;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        acc[k] += (uint64_t)y0 + y1 + ((uint64_t)y2 + y3);
+        if (k + 1 < K) {
+            y0 = mul32_lazy(y0, w.x);
+            y1 = mul32_lazy(y1, w.y);
+            y2 = mul32_lazy(y2, w.z);
+            y3 = mul32_lazy(y3, w.w);
+        }
+    }
+}
+
+// lane j of a G-group: start = x^(j+1), step = x^G (square-and-multiply).
+template <int G>
+__device__ __forceinline__ void group_powers32(uint32_t x, int j, uint32_t &start, uint32_t &step) {
+    uint32_t b = x, r = 1;
+    const uint32_t e = (uint32_t)j + 1;
+#pragma unroll
+    for (int bit = 0; (1 << bit) <= G; ++bit) {
+        const uint32_t rb = mul32_lazy(r, b);
+        r = ((e >> bit) & 1) ? rb : r;
+        if ((1 << bit) < G) b = mul32_lazy(b, b);
+    }
+    start = r;
+    step = b; // after log2(G) squarings b = x^G
+}
+
+// Reduce per-lane accumulators to one partial per (power, block).
+// acc[k] of lane with (lane % G) == j belongs to power m = j + k*G (0-based).
+template <int G, int K, typename Fold>
+__device__ __forceinline__ void block_store(const uint64_t (&acc)[K], uint32_t T, uint64_t *partials,
+                                            uint64_t *sm, Fold fold) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uint64_t v = fold(acc[k]);                   // < 2^32
+#pragma unroll
+        for (int off = 32; off >= G; off >>= 1) v += shfl_xor_u64(v, off); // < 2^38
+        if (lane < G) sm[wave * (G * K) + lane + k * G] = v;
+    }
+    __syncthreads();
+    for (uint32_t m = threadIdx.x; m < T; m += BLOCK) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) s += sm[w * (G * K) + m];   // < 2^40
+        partials[(size_t)m * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+struct Fold32 {
+    __device__ uint64_t operator()(uint64_t a) const { return fold64_32(a); }
+};
+
+// G == 1: each lane streams ids with 16-byte loads.
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_encode_u32_g1(const uint32_t *__restrict__ ids, uint64_t n,
+                                                         uint32_t head, uint32_t T,
+                                                         uint64_t *__restrict__ partials) {
+    __shared__ uint64_t sm[WAVES * K];
+    uint64_t acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0;
+
+    const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t body = (n - h) >> 2;
+    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
+
+    for (uint64_t i = gtid; i < body; i += nthr) chain32x4<K>(acc, v[i]);
+    // unaligned head (< 4 ids) and tail (< 4 ids)
+    const uint64_t tail0 = h + (body << 2);
+    if (gtid < h) chain32<K>(acc, ids[gtid], ids[gtid]);
+    if (gtid < n - tail0) chain32<K>(acc, ids[tail0 + gtid], ids[tail0 + gtid]);
+
+    block_store<1, K>(acc, T, partials, sm, Fold32{});
+}
+
+// G > 1: lane groups share one id (scalar loads; G lanes read one address).
+template <int G, int K>
+__global__ __launch_bounds__(BLOCK) void k_encode_u32_gn(const uint32_t *__restrict__ ids, uint64_t n,
+                                                         uint32_t head, uint32_t T,
+                                                         uint64_t *__restrict__ partials) {
+    (void)head;
+    __shared__ uint64_t sm[WAVES * G * K];
+    uint64_t acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0;
+    const int j = threadIdx.x % G;
+    const uint64_t grp = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / G;
+    const uint64_t ngrp = (uint64_t)gridDim.x * BLOCK / G;
+    for (uint64_t i = grp; i < n; i += ngrp) {
+        uint32_t start, step;
+        group_powers32<G>(ids[i], j, start, step);
+        chain32<K>(acc, start, step);
+    }
+    block_store<G, K>(acc, T, partials, sm, Fold32{});
+}
+
+// Sum block partials of power m = blockIdx.x; write canonical S_m (or add it
+// into out when accumulate), count and last id.
+__global__ __launch_bounds__(BLOCK) void k_finalize_u32(const uint64_t *__restrict__ partials,
+                                                        uint32_t nblocks, uint32_t T,
+                                                        const uint32_t *__restrict__ ids, uint64_t n,
+                                                        uint64_t *__restrict__ out, int accumulate) {
+    __shared__ uint64_t sm[WAVES];
+    const uint32_t m = blockIdx.x;
+    uint64_t s = 0;
+    for (uint32_t b = threadIdx.x; b < nblocks; b += BLOCK) s += partials[(size_t)m * nblocks + b]; // < 2^60
+    s = fold64_32(s);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += shfl_xor_u64(s, off);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tot = 0;
+        for (int w = 0; w < WAVES; ++w) tot += sm[w];
+        uint32_t c = canon32(fold64_32(tot));
+        out[m] = accumulate ? (uint64_t)add32((uint32_t)out[m], c) : (uint64_t)c;
+        if (m == 0) {
+            out[T] = accumulate ? out[T] + n : n;
+            if (n) out[T + 1] = ids[n - 1];
+            else if (!accumulate) out[T + 1] = 0;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ u64
+// 96-bit lazy accumulators: lo (u64) + hi (u32 carry count).
+template <int K>
+__device__ __forceinline__ void chain64(uint64_t (&lo)[K], uint32_t (&hi)[K], uint64_t start, uint64_t step) {
+    uint64_t y = start;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t s = lo[k] + y;
+        hi[k] += (s < y) ? 1u : 0u;
+        lo[k] = s;
+        if (k + 1 < K) y = mul64_lazy(y, step);
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void group_powers64(uint64_t x, int j, uint64_t &start, uint64_t &step) {
+    uint64_t b = x, r = 1;
+    const uint32_t e = (uint32_t)j + 1;
+#pragma unroll
+    for (int bit = 0; (1 << bit) <= G; ++bit) {
+        const uint64_t rb = mul64_lazy(r, b);
+        r = ((e >> bit) & 1) ? rb : r;
+        if ((1 << bit) < G) b = mul64_lazy(b, b);
+    }
+    start = r;
+    step = b;
+}
+
+// u64 partials: two 32-bit limbs per power, stored [2m + limb][block].
+template <int G, int K>
+__device__ __forceinline__ void block_store64(const uint64_t (&lo)[K], const uint32_t (&hi)[K], uint32_t T,
+                                              uint64_t *partials, uint64_t *sm) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t f = fold96_64(hi[k], lo[k]);
+        uint64_t a = (uint32_t)f, b = f >> 32;
+#pragma unroll
+        for (int off = 32; off >= G; off >>= 1) {
+            a += shfl_xor_u64(a, off);
+            b += shfl_xor_u64(b, off);
+        }
+        if (lane < G) {
+            sm[wave * (2 * G * K) + 2 * (lane + k * G)] = a;
+            sm[wave * (2 * G * K) + 2 * (lane + k * G) + 1] = b;
+        }
+    }
+    __syncthreads();
+    for (uint32_t m = threadIdx.x; m < 2 * T; m += BLOCK) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) s += sm[w * (2 * G * K) + m];
+        partials[(size_t)m * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_encode_u64_g1(const uint64_t *__restrict__ ids, uint64_t n,
+                                                         uint32_t head, uint32_t T,
+                                                         uint64_t *__restrict__ partials) {
+    __shared__ uint64_t sm[WAVES * 2 * K];
+    uint64_t lo[K];
+    uint32_t hi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) { lo[k] = 0; hi[k] = 0; }
+    const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t body = (n - h) >> 1;
+    const ulonglong2 *__restrict__ v = reinterpret_cast<const ulonglong2 *>(ids + h);
+    for (uint64_t i = gtid; i < body; i += nthr) {
+        const ulonglong2 w = v[i];
+        chain64<K>(lo, hi, w.x, w.x);
+        chain64<K>(lo, hi, w.y, w.y);
+    }
+    const uint64_t tail0 = h + (body << 1);
+    if (gtid < h) chain64<K>(lo, hi, ids[gtid], ids[gtid]);
+    if (gtid < n - tail0) chain64<K>(lo, hi, ids[tail0 + gtid], ids[tail0 + gtid]);
+    block_store64<1, K>(lo, hi, T, partials, sm);
+}
+
+template <int G, int K>
+__global__ __launch_bounds__(BLOCK) void k_encode_u64_gn(const uint64_t *__restrict__ ids, uint64_t n,
+                                                         uint32_t head, uint32_t T,
+                                                         uint64_t *__restrict__ partials) {
+    (void)head;
+    __shared__ uint64_t sm[WAVES * 2 * G * K];
+    uint64_t lo[K];
+    uint32_t hi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) { lo[k] = 0; hi[k] = 0; }
+    const int j = threadIdx.x % G;
+    const uint64_t grp = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / G;
+    const uint64_t ngrp = (uint64_t)gridDim.x * BLOCK / G;
+    for (uint64_t i = grp; i < n; i += ngrp) {
+        uint64_t start, step;
+        group_powers64<G>(ids[i], j, start, step);
+        chain64<K>(lo, hi, start, step);
+    }
+    block_store64<G, K>(lo, hi, T, partials, sm);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restrict__ partials,
+                                                        uint32_t nblocks, uint32_t T,
+                                                        const uint64_t *__restrict__ ids, uint64_t n,
+                                                        uint64_t *__restrict__ out, int accumulate) {
+    __shared__ uint64_t sm[2][WAVES];
+    const uint32_t m = blockIdx.x; // power index
+    uint64_t a = 0, b = 0;         // limb sums, each < nblocks * 2^40
+    for (uint32_t i = threadIdx.x; i < nblocks; i += BLOCK) {
+        a += partials[(size_t)(2 * m) * nblocks + i];
+        b += partials[(size_t)(2 * m + 1) * nblocks + i];
+    }
+    // fold each limb sum to < 2^64 congruent, then re-split to limbs so the
+    // cross-lane sums cannot overflow: value = a + b*2^32.
+    {
+        const uint64_t av = canon64(a), bv = mul64_lazy(canon64(b), 1ull << 32);
+        const uint64_t vv = canon64(add64(canon64(av), canon64(bv)));
+        a = (uint32_t)vv;
+        b = vv >> 32;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        a += shfl_xor_u64(a, off);
+        b += shfl_xor_u64(b, off);
+    }
+    if ((threadIdx.x & 63) == 0) { sm[0][threadIdx.x >> 6] = a; sm[1][threadIdx.x >> 6] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t sa = 0, sb = 0;
+        for (int w = 0; w < WAVES; ++w) { sa += sm[0][w]; sb += sm[1][w]; } // < 2^40
+        uint64_t v = add64(canon64(sa), mul64(canon64(sb), 1ull << 32));
+        if (accumulate) v = add64(canon64(out[2 * m] | (out[2 * m + 1] << 32)), v);
+        out[2 * m] = (uint32_t)v;
+        out[2 * m + 1] = v >> 32;
+        if (m == 0) {
+            out[2 * T] = accumulate ? out[2 * T] + n : n;
+            if (n) out[2 * T + 1] = ids[n - 1];
+            else if (!accumulate) out[2 * T + 1] = 0;
+        }
+    }
+}
+
+// ------------------------------------------------------------- dispatch
+template <typename KernelT>
+static uint32_t grid_for(qk_ctx *ctx, KernelT kern, uint64_t units, uint32_t per_block) {
+    if (ctx->grid_override) return ctx->grid_override;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BLOCK, 0) != hipSuccess || occ < 1) occ = 1;
+    const uint64_t full = (uint64_t)ctx->num_cus * (uint64_t)occ;
+    uint64_t need = (units + per_block - 1) / per_block;
+    if (need < 1) need = 1;
+    return (uint32_t)(need < full ? need : full);
+}
+
+// Launch main kernel (+profiling events) then finalize.
+template <typename IdT, typename KernelT, typename FinT>
+static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t words_per_power,
+                      const IdT *d_ids, size_t n, uint32_t head, uint32_t T, uint64_t units,
+                      uint32_t per_block, uint64_t *d_partial, int accumulate, hipStream_t s) {
+    const uint32_t nb = grid_for(ctx, kern, units, per_block);
+    const size_t need = (size_t)nb * words_per_power * GK * sizeof(uint64_t);
+    int rc = ensure_scratch(ctx, need);
+    if (rc) return rc;
+    uint64_t *partials = (uint64_t *)ctx->d_scratch;
+    hipEvent_t e0 = prof_begin(ctx, s);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, T, partials);
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(fin, dim3(T), dim3(BLOCK), 0, s, partials, nb, T, d_ids, (uint64_t)n, d_partial,
+                       accumulate);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
+}
+
+// Choose (G, K): the smallest G whose K = ceil(T/G) fits the register
+// budget, then the smallest instantiated K >= ceil(T/G).
+static const int K32_G1[] = {1, 2, 4, 8, 12, 16, 20, 24, 28, 32};
+static const int K32_GN[] = {20, 24, 28, 32};
+static const int K64_G1[] = {1, 2, 4, 8, 12, 16, 20};
+static const int K64_GN[] = {12, 16, 20};
+
+template <int G, int K>
+static int enc32_gk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                    int acc, hipStream_t s) {
+    if constexpr (G == 1)
+        return run_encode<uint32_t>(ctx, k_encode_u32_g1<K>, k_finalize_u32, K, 1, ids, n, head, T,
+                                    (n + 3) / 4, BLOCK, out, acc, s);
+    else
+        return run_encode<uint32_t>(ctx, k_encode_u32_gn<G, K>, k_finalize_u32, G * K, 1, ids, n, head, T,
+                                    n, BLOCK / G, out, acc, s);
+}
+
+template <int G>
+static int enc32_g(qk_ctx *ctx, int K, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                   int acc, hipStream_t s) {
+    if constexpr (G == 1) {
+        switch (K) {
+        case 1: return enc32_gk<1, 1>(ctx, ids, n, head, T, out, acc, s);
+        case 2: return enc32_gk<1, 2>(ctx, ids, n, head, T, out, acc, s);
+        case 4: return enc32_gk<1, 4>(ctx, ids, n, head, T, out, acc, s);
+        case 8: return enc32_gk<1, 8>(ctx, ids, n, head, T, out, acc, s);
+        case 12: return enc32_gk<1, 12>(ctx, ids, n, head, T, out, acc, s);
+        case 16: return enc32_gk<1, 16>(ctx, ids, n, head, T, out, acc, s);
+        case 20: return enc32_gk<1, 20>(ctx, ids, n, head, T, out, acc, s);
+        case 24: return enc32_gk<1, 24>(ctx, ids, n, head, T, out, acc, s);
+        case 28: return enc32_gk<1, 28>(ctx, ids, n, head, T, out, acc, s);
+        case 32: return enc32_gk<1, 32>(ctx, ids, n, head, T, out, acc, s);
+        }
+    } else {
+        switch (K) {
+        case 20: return enc32_gk<G, 20>(ctx, ids, n, head, T, out, acc, s);
+        case 24: return enc32_gk<G, 24>(ctx, ids, n, head, T, out, acc, s);
+        case 28: return enc32_gk<G, 28>(ctx, ids, n, head, T, out, acc, s);
+        case 32: return enc32_gk<G, 32>(ctx, ids, n, head, T, out, acc, s);
+        }
+    }
+    return QK_E_THRESHOLD;
+}
+
+template <int G, int K>
+static int enc64_gk(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                    int acc, hipStream_t s) {
+    if constexpr (G == 1)
+        return run_encode<uint64_t>(ctx, k_encode_u64_g1<K>, k_finalize_u64, K, 2, ids, n, head, T,
+                                    (n + 1) / 2, BLOCK, out, acc, s);
+    else
+        return run_encode<uint64_t>(ctx, k_encode_u64_gn<G, K>, k_finalize_u64, G * K, 2, ids, n, head, T,
+                                    n, BLOCK / G, out, acc, s);
+}
+
+template <int G>
+static int enc64_g(qk_ctx *ctx, int K, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                   int acc, hipStream_t s) {
+    if constexpr (G == 1) {
+        switch (K) {
+        case 1: return enc64_gk<1, 1>(ctx, ids, n, head, T, out, acc, s);
+        case 2: return enc64_gk<1, 2>(ctx, ids, n, head, T, out, acc, s);
+        case 4: return enc64_gk<1, 4>(ctx, ids, n, head, T, out, acc, s);
+        case 8: return enc64_gk<1, 8>(ctx, ids, n, head, T, out, acc, s);
+        case 12: return enc64_gk<1, 12>(ctx, ids, n, head, T, out, acc, s);
+        case 16: return enc64_gk<1, 16>(ctx, ids, n, head, T, out, acc, s);
+        case 20: return enc64_gk<1, 20>(ctx, ids, n, head, T, out, acc, s);
+        }
+    } else {
+        switch (K) {
+        case 12: return enc64_gk<G, 12>(ctx, ids, n, head, T, out, acc, s);
+        case 16: return enc64_gk<G, 16>(ctx, ids, n, head, T, out, acc, s);
+        case 20: return enc64_gk<G, 20>(ctx, ids, n, head, T, out, acc, s);
+        }
+    }
+    return QK_E_THRESHOLD;
+}
+
+static void choose_gk(uint32_t T, int kmax, const int *kg1, int nkg1, const int *kgn, int nkgn, int &G, int &K) {
+    G = 1;
+    while ((T + G - 1) / G > (uint32_t)kmax) G *= 2;
+    const uint32_t kneed = (T + G - 1) / G;
+    const int *ks = G == 1 ? kg1 : kgn;
+    const int nk = G == 1 ? nkg1 : nkgn;
+    K = ks[nk - 1];
+    for (int i = 0; i < nk; ++i)
+        if ((uint32_t)ks[i] >= kneed) { K = ks[i]; break; }
+}
+
+static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc, hipStream_t s) {
+    if (T == 0 || T > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    const uintptr_t a = (uintptr_t)ids;
+    if (a & 3) return QK_E_INVAL;
+    const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 4);
+    int G, K;
+    choose_gk(T, 32, K32_G1, 10, K32_GN, 4, G, K);
+    switch (G) {
+    case 1: return enc32_g<1>(ctx, K, ids, n, head, T, out, acc, s);
+    case 2: return enc32_g<2>(ctx, K, ids, n, head, T, out, acc, s);
+    case 4: return enc32_g<4>(ctx, K, ids, n, head, T, out, acc, s);
+    case 8: return enc32_g<8>(ctx, K, ids, n, head, T, out, acc, s);
+    case 16: return enc32_g<16>(ctx, K, ids, n, head, T, out, acc, s);
+    case 32: return enc32_g<32>(ctx, K, ids, n, head, T, out, acc, s);
+    }
+    return QK_E_THRESHOLD;
+}
+
+static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_t *out, int acc, hipStream_t s) {
+    if (T == 0 || T > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    const uintptr_t a = (uintptr_t)ids;
+    if (a & 7) return QK_E_INVAL;
+    const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
+    int G, K;
+    choose_gk(T, 20, K64_G1, 7, K64_GN, 3, G, K);
+    switch (G) {
+    case 1: return enc64_g<1>(ctx, K, ids, n, head, T, out, acc, s);
+    case 2: return enc64_g<2>(ctx, K, ids, n, head, T, out, acc, s);
+    case 4: return enc64_g<4>(ctx, K, ids, n, head, T, out, acc, s);
+    case 8: return enc64_g<8>(ctx, K, ids, n, head, T, out, acc, s);
+    case 16: return enc64_g<16>(ctx, K, ids, n, head, T, out, acc, s);
+    case 32: return enc64_g<32>(ctx, K, ids, n, head, T, out, acc, s);
+    case 64: return enc64_g<64>(ctx, K, ids, n, head, T, out, acc, s);
+    }
+    return QK_E_THRESHOLD;
+}
+
+int launch_encode_u32(qk_ctx *ctx, const uint32_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial, hipStream_t s) {
+    return enc32(ctx, d_ids, n, t, d_partial, 0, s);
+}
+int launch_encode_u64(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial, hipStream_t s) {
+    return enc64(ctx, d_ids, n, t, d_partial, 0, s);
+}
+int launch_encode_u32_acc(qk_ctx *ctx, const uint32_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial,
+                          hipStream_t s) {
+    return enc32(ctx, d_ids, n, t, d_partial, 1, s);
+}
+int launch_encode_u64_acc(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t t, uint64_t *d_partial,
+                          hipStream_t s) {
+    return enc64(ctx, d_ids, n, t, d_partial, 1, s);
+}
+
+} // namespace qk

@@ -1,0 +1,303 @@
+// host.cpp — host-side (scalar) half of the quACK C ABI: sketch state,
+// per-packet insert/remove, subtract/merge, Newton's identities, Horner
+// evaluation and the bincode wire image.  These are the per-packet calls of
+// the reference (sidekick.rs:42, media_client.rs:249,296,304,310,319); they
+// stay on the host because one insert (~75 ns on CPU at t=20) is far below a
+// kernel launch.  The batch paths live in encode.hip / decode.hip.
+#include "quack_hip.h"
+#include "field.h"
+
+#include <string.h>
+#include <vector>
+
+using namespace qk;
+
+namespace {
+static inline void put_le(uint8_t *p, uint64_t v, int nbytes) {
+    for (int i = 0; i < nbytes; ++i) p[i] = (uint8_t)(v >> (8 * i));
+}
+static inline uint64_t get_le(const uint8_t *p, int nbytes) {
+    uint64_t v = 0;
+    for (int i = 0; i < nbytes; ++i) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+
+template <typename Q, typename T>
+int deser(const uint8_t *buf, size_t len, Q *q, uint32_t *t_out, T modulus) {
+    if (!buf || len < 8) return QK_E_FORMAT;
+    const uint64_t t = get_le(buf, 8);
+    if (t > 0xFFFFFFFFull) return QK_E_FORMAT;
+    if (t_out) *t_out = (uint32_t)t;
+    const size_t body = 8 + sizeof(T) * (size_t)t;
+    if (len < body + 1 + 4) return QK_E_FORMAT;
+    const uint8_t tag = buf[body];
+    if (tag > 1) return QK_E_FORMAT;
+    const size_t need = body + 1 + (tag ? sizeof(T) : 0) + 4;
+    if (len != need) return QK_E_FORMAT;
+    if (!q) return QK_OK;
+    for (uint64_t k = 0; k < t; ++k) {
+        const T v = (T)get_le(buf + 8 + sizeof(T) * k, sizeof(T));
+        if (v >= modulus) return QK_E_FORMAT; // ModularInteger values are canonical
+    }
+    q->threshold = (uint32_t)t;
+    for (uint64_t k = 0; k < t; ++k) q->power_sums[k] = (T)get_le(buf + 8 + sizeof(T) * k, sizeof(T));
+    q->has_last = tag;
+    q->last_value = tag ? (T)get_le(buf + body + 1, sizeof(T)) : 0;
+    q->count = (uint32_t)get_le(buf + need - 4, 4);
+    return QK_OK;
+}
+} // namespace
+
+extern "C" {
+
+const char *qk_strerror(int s) {
+    switch (s) {
+    case QK_OK: return "ok";
+    case QK_E_INVAL: return "invalid argument";
+    case QK_E_THRESHOLD: return "invalid threshold";
+    case QK_E_MISMATCH: return "threshold mismatch";
+    case QK_E_UNDECODABLE: return "undecodable: count exceeds threshold";
+    case QK_E_CAPACITY: return "output buffer too small";
+    case QK_E_HIP: return "HIP runtime error";
+    case QK_E_NO_DEVICE: return "no usable gfx950 device";
+    case QK_E_NOMEM: return "out of memory";
+    case QK_E_FORMAT: return "malformed serialized quACK";
+    default: return "unknown error";
+    }
+}
+
+const char *qk_version(void) { return "quack-hip 0.1.0 (gfx950)"; }
+
+size_t qk_u32_size(uint32_t t) { return sizeof(qk_u32) + (size_t)t * sizeof(uint32_t); }
+size_t qk_u64_size(uint32_t t) { return sizeof(qk_u64) + (size_t)t * sizeof(uint64_t); }
+
+int qk_u32_init(qk_u32 *q, uint32_t t) {
+    if (!q) return QK_E_INVAL;
+    memset(q, 0, qk_u32_size(t));
+    q->threshold = t;
+    return QK_OK;
+}
+int qk_u64_init(qk_u64 *q, uint32_t t) {
+    if (!q) return QK_E_INVAL;
+    memset(q, 0, qk_u64_size(t));
+    q->threshold = t;
+    return QK_OK;
+}
+
+// ---------------------------------------------------------------- insert
+int qk_u32_insert(qk_u32 *q, uint32_t id) {
+    if (!q) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0) return QK_E_THRESHOLD; // reference: index underflow panic
+    const uint32_t x = canon32(id);
+    uint32_t y = x;
+    for (uint32_t k = 0; k < t; ++k) {
+        q->power_sums[k] = add32(q->power_sums[k], y);
+        y = mul32(y, x);
+    }
+    q->count += 1u;
+    q->has_last = 1;
+    q->last_value = id;
+    return QK_OK;
+}
+
+int qk_u64_insert(qk_u64 *q, uint64_t id) {
+    if (!q) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0) return QK_E_THRESHOLD;
+    const uint64_t x = canon64(id);
+    uint64_t y = x;
+    for (uint32_t k = 0; k < t; ++k) {
+        q->power_sums[k] = add64(q->power_sums[k], y);
+        y = mul64(y, x);
+    }
+    q->count += 1u;
+    q->has_last = 1;
+    q->last_value = id;
+    return QK_OK;
+}
+
+int qk_u32_remove(qk_u32 *q, uint32_t id) {
+    if (!q) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0) return QK_E_THRESHOLD;
+    const uint32_t x = canon32(id);
+    uint32_t y = x;
+    for (uint32_t k = 0; k < t; ++k) {
+        q->power_sums[k] = sub32(q->power_sums[k], y);
+        y = mul32(y, x);
+    }
+    q->count -= 1u;
+    return QK_OK;
+}
+
+int qk_u64_remove(qk_u64 *q, uint64_t id) {
+    if (!q) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    if (t == 0) return QK_E_THRESHOLD;
+    const uint64_t x = canon64(id);
+    uint64_t y = x;
+    for (uint32_t k = 0; k < t; ++k) {
+        q->power_sums[k] = sub64(q->power_sums[k], y);
+        y = mul64(y, x);
+    }
+    q->count -= 1u;
+    return QK_OK;
+}
+
+// ---------------------------------------------------------- sub / merge
+int qk_u32_sub_assign(qk_u32 *q, const qk_u32 *r) {
+    if (!q || !r) return QK_E_INVAL;
+    if (q->threshold != r->threshold) return QK_E_MISMATCH;
+    for (uint32_t k = 0; k < q->threshold; ++k) q->power_sums[k] = sub32(q->power_sums[k], r->power_sums[k]);
+    q->count -= r->count;
+    return QK_OK;
+}
+int qk_u64_sub_assign(qk_u64 *q, const qk_u64 *r) {
+    if (!q || !r) return QK_E_INVAL;
+    if (q->threshold != r->threshold) return QK_E_MISMATCH;
+    for (uint32_t k = 0; k < q->threshold; ++k) q->power_sums[k] = sub64(q->power_sums[k], r->power_sums[k]);
+    q->count -= r->count;
+    return QK_OK;
+}
+int qk_u32_merge(qk_u32 *q, const qk_u32 *r) {
+    if (!q || !r) return QK_E_INVAL;
+    if (q->threshold != r->threshold) return QK_E_MISMATCH;
+    for (uint32_t k = 0; k < q->threshold; ++k) q->power_sums[k] = add32(q->power_sums[k], r->power_sums[k]);
+    q->count += r->count;
+    if (r->has_last) { q->has_last = 1; q->last_value = r->last_value; }
+    return QK_OK;
+}
+int qk_u64_merge(qk_u64 *q, const qk_u64 *r) {
+    if (!q || !r) return QK_E_INVAL;
+    if (q->threshold != r->threshold) return QK_E_MISMATCH;
+    for (uint32_t k = 0; k < q->threshold; ++k) q->power_sums[k] = add64(q->power_sums[k], r->power_sums[k]);
+    q->count += r->count;
+    if (r->has_last) { q->has_last = 1; q->last_value = r->last_value; }
+    return QK_OK;
+}
+
+// ------------------------------------------------------------ partials
+size_t qk_u32_partial_words(uint32_t t) { return (size_t)t + 2; }
+size_t qk_u64_partial_words(uint32_t t) { return 2 * (size_t)t + 2; }
+
+int qk_u32_merge_partial(qk_u32 *q, const uint64_t *part, int has_last, uint32_t last) {
+    if (!q || !part) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    for (uint32_t k = 0; k < t; ++k) q->power_sums[k] = add32(q->power_sums[k], canon32(fold64_32(part[k])));
+    q->count += (uint32_t)part[t];
+    if (has_last) { q->has_last = 1; q->last_value = last; }
+    return QK_OK;
+}
+int qk_u64_merge_partial(qk_u64 *q, const uint64_t *part, int has_last, uint64_t last) {
+    if (!q || !part) return QK_E_INVAL;
+    const uint32_t t = q->threshold;
+    for (uint32_t k = 0; k < t; ++k) {
+        // value = lo_sum + hi_sum * 2^32, each limb sum < 2^59
+        const uint64_t lo = part[2 * k], hi = part[2 * k + 1];
+        unsigned __int128 v = (unsigned __int128)hi * (1ull << 32) + lo; // < 2^92
+        const uint64_t vhi = (uint64_t)(v >> 64), vlo = (uint64_t)v;    // vhi < 2^28
+        q->power_sums[k] = add64(q->power_sums[k], canon64(fold96_64((uint32_t)vhi, vlo)));
+    }
+    q->count += (uint32_t)part[2 * t];
+    if (has_last) { q->has_last = 1; q->last_value = last; }
+    return QK_OK;
+}
+
+// ----------------------------------------------------------- to_coeffs
+// Newton's identities, 0-indexed: c[i] = -(S[i] + sum_{j<i} S[j] c[i-j-1]) / (i+1).
+// Inverses of 1..d by the linear recurrence inv[i] = -(p/i) * inv[p mod i].
+int qk_u32_to_coeffs(const qk_u32 *q, uint32_t *c, uint32_t cap, uint32_t *d_out) {
+    if (!q || !d_out) return QK_E_INVAL;
+    const uint32_t d = q->count;
+    if (d > q->threshold) { *d_out = d; return QK_E_UNDECODABLE; }
+    *d_out = d;
+    if (cap < d || (d && !c)) return QK_E_CAPACITY;
+    std::vector<uint32_t> inv(d + 2, 1);
+    for (uint32_t i = 2; i <= d; ++i) inv[i] = mul32(P32 - P32 / i, inv[P32 % i]);
+    for (uint32_t i = 0; i < d; ++i) {
+        uint64_t acc = q->power_sums[i];            // lazy: < 2^32 + i * 2^32
+        for (uint32_t j = 0; j < i; ++j) acc += mul32(q->power_sums[j], c[i - j - 1]);
+        c[i] = mul32(neg32(canon32(fold64_32(acc))), inv[i + 1]);
+    }
+    return QK_OK;
+}
+
+int qk_u64_to_coeffs(const qk_u64 *q, uint64_t *c, uint32_t cap, uint32_t *d_out) {
+    if (!q || !d_out) return QK_E_INVAL;
+    const uint32_t d = q->count;
+    if (d > q->threshold) { *d_out = d; return QK_E_UNDECODABLE; }
+    *d_out = d;
+    if (cap < d || (d && !c)) return QK_E_CAPACITY;
+    std::vector<uint64_t> inv(d + 2, 1);
+    for (uint32_t i = 2; i <= d; ++i) inv[i] = mul64(P64 - P64 / i, inv[P64 % i]);
+    for (uint32_t i = 0; i < d; ++i) {
+        uint64_t acc = q->power_sums[i];
+        for (uint32_t j = 0; j < i; ++j) acc = add64(acc, mul64(q->power_sums[j], c[i - j - 1]));
+        c[i] = mul64(neg64(acc), inv[i + 1]);
+    }
+    return QK_OK;
+}
+
+// ---------------------------------------------------------------- eval
+uint32_t qk_u32_eval(const uint32_t *c, uint32_t d, uint32_t id) {
+    if (d == 0 || !c) return 1;
+    const uint32_t x = canon32(id);
+    uint32_t r = x;
+    for (uint32_t i = 0; i + 1 < d; ++i) r = mul32(add32(r, c[i]), x);
+    return add32(r, c[d - 1]);
+}
+uint64_t qk_u64_eval(const uint64_t *c, uint32_t d, uint64_t id) {
+    if (d == 0 || !c) return 1;
+    const uint64_t x = canon64(id);
+    uint64_t r = x;
+    for (uint32_t i = 0; i + 1 < d; ++i) r = mul64(add64(r, c[i]), x);
+    return add64(r, c[d - 1]);
+}
+
+// ------------------------------------------------------------- bincode
+// bincode 1.3 default options: little-endian fixed-width ints, u64 length
+// prefix for Vec, u8 tag for Option.  Field order as declared in the
+// crate's struct: power_sums, last_value, count  ([RECALL]).
+size_t qk_u32_serialized_size(const qk_u32 *q) {
+    return q ? 8 + 4 * (size_t)q->threshold + 1 + (q->has_last ? 4 : 0) + 4 : 0;
+}
+size_t qk_u64_serialized_size(const qk_u64 *q) {
+    return q ? 8 + 8 * (size_t)q->threshold + 1 + (q->has_last ? 8 : 0) + 4 : 0;
+}
+
+int qk_u32_serialize(const qk_u32 *q, uint8_t *buf, size_t cap, size_t *len) {
+    if (!q || !len) return QK_E_INVAL;
+    const size_t need = qk_u32_serialized_size(q);
+    *len = need;
+    if (cap < need || !buf) return QK_E_CAPACITY;
+    uint8_t *p = buf;
+    put_le(p, q->threshold, 8); p += 8;
+    for (uint32_t k = 0; k < q->threshold; ++k) { put_le(p, q->power_sums[k], 4); p += 4; }
+    *p++ = q->has_last ? 1 : 0;
+    if (q->has_last) { put_le(p, q->last_value, 4); p += 4; }
+    put_le(p, q->count, 4);
+    return QK_OK;
+}
+int qk_u64_serialize(const qk_u64 *q, uint8_t *buf, size_t cap, size_t *len) {
+    if (!q || !len) return QK_E_INVAL;
+    const size_t need = qk_u64_serialized_size(q);
+    *len = need;
+    if (cap < need || !buf) return QK_E_CAPACITY;
+    uint8_t *p = buf;
+    put_le(p, q->threshold, 8); p += 8;
+    for (uint32_t k = 0; k < q->threshold; ++k) { put_le(p, q->power_sums[k], 8); p += 8; }
+    *p++ = q->has_last ? 1 : 0;
+    if (q->has_last) { put_le(p, q->last_value, 8); p += 8; }
+    put_le(p, q->count, 4);
+    return QK_OK;
+}
+
+int qk_u32_deserialize(const uint8_t *buf, size_t len, qk_u32 *q, uint32_t *t_out) {
+    return deser<qk_u32, uint32_t>(buf, len, q, t_out, P32);
+}
+int qk_u64_deserialize(const uint8_t *buf, size_t len, qk_u64 *q, uint32_t *t_out) {
+    return deser<qk_u64, uint64_t>(buf, len, q, t_out, P64);
+}
+
+} // extern "C"

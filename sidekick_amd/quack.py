@@ -1,0 +1,386 @@
+"""Host-side mirror of the reference `quack` crate API over libquack_hip.so.
+
+Same names, argument meaning and error behaviour as the Rust calls the
+reference tree makes:
+
+    PowerSumQuackU32::new(threshold)        sidekick/src/sidekick.rs:32
+    quack.insert(id)                        sidekick.rs:42, sidekick_multi.rs:82
+    quack.remove(id)                        media_client.rs:319
+    quack.count() / quack.last_value()      media_client.rs:231-233,259-260
+    diff.sub_assign(quack)                  media_client.rs:296
+    diff.to_coeffs()                        media_client.rs:304
+    arithmetic::eval(&coeffs, id).value()   media_client.rs:310
+    clone(), bincode serialize/deserialize  sidekick.rs:187,204; media_client.rs:227
+
+plus the batch entry points of the MI355X engine:
+
+    insert_batch(ids)        encode an id array on the GPU (device tensor:
+                             HBM-resident path; numpy array: host path with
+                             pipelined H2D).
+    decode_with_log(log)     to_coeffs on the host, root test on the GPU.
+
+Per-packet insert/remove stay on the host (one insert is far cheaper than a
+kernel launch); every batch call runs the gfx950 kernels and raises if the
+device or the library is unavailable -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+
+import numpy as np
+
+from ._lib import (P32, P64, QK_E_CAPACITY, QuackError, check, lib)
+
+__all__ = [
+    "PowerSumQuackU32", "PowerSumQuackU64", "ModularInteger", "CoefficientVector",
+    "arithmetic", "Context", "get_context", "device_count",
+]
+
+
+# --------------------------------------------------------------------------
+# Device contexts (one per device, created lazily)
+# --------------------------------------------------------------------------
+class Context:
+    """Owns a qk_ctx* (device scratch, streams, profiling events)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib().qk_ctx_create(int(device), C.byref(h)), f"qk_ctx_create({device})")
+        self.handle = h
+        self.device = int(device)
+
+    def close(self):
+        if self.handle:
+            lib().qk_ctx_destroy(self.handle)
+            self.handle = None
+
+    def synchronize(self, stream=None):
+        check(lib().qk_ctx_synchronize(self.handle, stream), "synchronize")
+
+    def set_profiling(self, on: bool):
+        check(lib().qk_ctx_set_profiling(self.handle, int(bool(on))))
+
+    def kernel_stats(self):
+        """(total_ms, launches) of the dominant kernel since the last call."""
+        ms = C.c_double()
+        n = C.c_uint64()
+        check(lib().qk_ctx_kernel_stats(self.handle, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def set_grid(self, blocks: int):
+        check(lib().qk_ctx_set_grid(self.handle, int(blocks)))
+
+
+_ctx_lock = threading.Lock()
+_contexts: dict = {}
+
+
+def device_count() -> int:
+    n = C.c_int()
+    lib().qk_device_count(C.byref(n))
+    return n.value
+
+
+def get_context(device: int = 0) -> Context:
+    with _ctx_lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = _contexts[device] = Context(device)
+        return ctx
+
+
+# --------------------------------------------------------------------------
+# Field values and coefficient vectors
+# --------------------------------------------------------------------------
+class ModularInteger:
+    """quack::arithmetic::ModularInteger: canonical value in [0, p)."""
+    __slots__ = ("_v", "bits")
+
+    def __init__(self, v: int, bits: int = 32):
+        self.bits = bits
+        self._v = int(v) % (P32 if bits == 32 else P64)
+
+    def value(self) -> int:
+        return self._v
+
+    def __eq__(self, other):
+        if isinstance(other, ModularInteger):
+            return self._v == other._v and self.bits == other.bits
+        return self._v == other
+
+    def __hash__(self):
+        return hash((self._v, self.bits))
+
+    def __repr__(self):
+        return f"ModularInteger<u{self.bits}>({self._v})"
+
+
+class CoefficientVector(list):
+    """Result of to_coeffs(): c_1..c_d of prod(z - x_missing), canonical ints."""
+
+    def __init__(self, values, bits: int):
+        super().__init__(int(v) for v in values)
+        self.bits = bits
+
+
+class _Arithmetic:
+    """quack::arithmetic (media_client.rs:21,310)."""
+
+    @staticmethod
+    def eval(coeffs: CoefficientVector, x: int) -> ModularInteger:
+        bits = getattr(coeffs, "bits", 32)
+        d = len(coeffs)
+        if bits == 32:
+            arr = (C.c_uint32 * max(d, 1))(*coeffs)
+            return ModularInteger(lib().qk_u32_eval(arr, d, int(x) & 0xFFFFFFFF), 32)
+        arr = (C.c_uint64 * max(d, 1))(*coeffs)
+        return ModularInteger(lib().qk_u64_eval(arr, d, int(x) & 0xFFFFFFFFFFFFFFFF), 64)
+
+
+arithmetic = _Arithmetic()
+
+
+# --------------------------------------------------------------------------
+# Array plumbing (torch device tensors, numpy host arrays)
+# --------------------------------------------------------------------------
+def _device_array(a, bits: int):
+    """(ptr, n, device_index, stream_ptr) of a contiguous CUDA tensor, or None."""
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return None
+    if not isinstance(a, torch.Tensor):
+        return None
+    if not a.is_cuda:
+        raise TypeError("CPU torch tensors are not accepted; pass a numpy array for the host path")
+    ok = {32: (torch.int32, getattr(torch, "uint32", None)), 64: (torch.int64, getattr(torch, "uint64", None))}[bits]
+    if a.dtype not in ok:
+        raise TypeError(f"u{bits} ids must be a torch int{bits}/uint{bits} tensor, got {a.dtype}")
+    if not a.is_contiguous():
+        raise ValueError("ids tensor must be contiguous")
+    dev = a.device.index if a.device.index is not None else torch.cuda.current_device()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    return a.data_ptr(), a.numel(), dev, stream
+
+
+def _host_array(a, bits: int) -> np.ndarray:
+    dt = np.uint32 if bits == 32 else np.uint64
+    arr = np.asarray(a)
+    if arr.dtype != dt:
+        arr = arr.astype(dt)
+    return np.ascontiguousarray(arr)
+
+
+# --------------------------------------------------------------------------
+# The sketch
+# --------------------------------------------------------------------------
+class _PowerSumQuack:
+    BITS = 32
+    _ELEM = C.c_uint32
+    _P = P32
+    _pre = "qk_u32_"
+
+    def __init__(self, threshold: int):
+        if threshold < 0 or threshold > 0xFFFFFFFF:
+            raise ValueError("threshold must fit u32")
+        self._t = int(threshold)
+        self._buf = C.create_string_buffer(self._f("size")(self._t))
+        check(self._f("init")(self._buf, self._t), "init")
+
+    # -- plumbing -----------------------------------------------------------
+    @classmethod
+    def _f(cls, name):
+        return getattr(lib(), cls._pre + name)
+
+    @classmethod
+    def new(cls, threshold: int):
+        return cls(threshold)
+
+    def _hdr(self):
+        return np.frombuffer(self._buf, dtype=np.uint32, count=4)
+
+    # -- accessors ----------------------------------------------------------
+    def threshold(self) -> int:
+        return self._t
+
+    def count(self) -> int:
+        return int(self._hdr()[1])
+
+    def last_value(self):
+        h = self._hdr()
+        if not h[2]:
+            return None
+        if self.BITS == 32:
+            return int(h[3])
+        return int(np.frombuffer(self._buf, dtype=np.uint64, count=1, offset=16)[0])
+
+    def power_sums(self) -> list:
+        if self.BITS == 32:
+            return [int(v) for v in np.frombuffer(self._buf, dtype=np.uint32, count=self._t, offset=16)]
+        return [int(v) for v in np.frombuffer(self._buf, dtype=np.uint64, count=self._t, offset=24)]
+
+    def clone(self):
+        q = type(self).__new__(type(self))
+        q._t = self._t
+        q._buf = C.create_string_buffer(self._buf.raw, len(self._buf))
+        return q
+
+    __copy__ = clone
+
+    def __eq__(self, other):
+        return type(self) is type(other) and self._buf.raw == other._buf.raw
+
+    def __repr__(self):
+        return (f"{type(self).__name__}(threshold={self._t}, count={self.count()}, "
+                f"last_value={self.last_value()})")
+
+    # -- per-packet host path -------------------------------------------------
+    def insert(self, ident: int) -> None:
+        check(self._f("insert")(self._buf, int(ident)), "insert")
+
+    def remove(self, ident: int) -> None:
+        check(self._f("remove")(self._buf, int(ident)), "remove")
+
+    def sub_assign(self, rhs) -> None:
+        check(self._f("sub_assign")(self._buf, rhs._buf), "sub_assign")
+
+    def __isub__(self, rhs):
+        self.sub_assign(rhs)
+        return self
+
+    def merge(self, later) -> None:
+        """Union with the disjoint stream that follows this one (additivity)."""
+        check(self._f("merge")(self._buf, later._buf), "merge")
+
+    def to_coeffs(self) -> CoefficientVector:
+        d = C.c_uint32()
+        cap = max(self._t, 1)
+        out = (self._ELEM * cap)()
+        check(self._f("to_coeffs")(self._buf, out, cap, C.byref(d)), "to_coeffs")
+        return CoefficientVector(out[: d.value], self.BITS)
+
+    # -- bincode wire image ----------------------------------------------------
+    def serialize(self) -> bytes:
+        n = self._f("serialized_size")(self._buf)
+        out = (C.c_uint8 * n)()
+        ln = C.c_size_t()
+        check(self._f("serialize")(self._buf, out, n, C.byref(ln)), "serialize")
+        return bytes(out[: ln.value])
+
+    @classmethod
+    def deserialize(cls, data: bytes):
+        src = (C.c_uint8 * len(data)).from_buffer_copy(data)
+        t = C.c_uint32()
+        check(cls._f("deserialize")(src, len(data), None, C.byref(t)), "deserialize")
+        q = cls(t.value)
+        check(cls._f("deserialize")(src, len(data), q._buf, None), "deserialize")
+        return q
+
+    # -- batch (GPU) path -------------------------------------------------------
+    def insert_batch(self, ids, ctx: Context | None = None) -> None:
+        """Insert every id of `ids` in array order, on the GPU.
+
+        A CUDA tensor is encoded where it lies (HBM-resident path); a numpy
+        array / sequence goes through the pipelined host->device path."""
+        if self._t == 0:
+            raise QuackError(-2, "insert_batch into a threshold-0 quACK")
+        dev = _device_array(ids, self.BITS)
+        if dev is not None:
+            ptr, n, d, stream = dev
+            ctx = ctx or get_context(d)
+            check(self._f("encode_device")(ctx.handle, ptr, n, self._buf, stream), "encode_device")
+            return
+        arr = _host_array(ids, self.BITS)
+        ctx = ctx or get_context(0)
+        check(self._f("encode_host")(ctx.handle, arr.ctypes.data, arr.size, self._buf), "encode_host")
+
+    def root_test(self, coeffs, log, stop_value=None, ctx: Context | None = None, cap: int = 1 << 16):
+        """Positions (log order) of entries of `log` that are roots of
+        `coeffs`; with stop_value, only positions before its first
+        occurrence (media_client.rs:306-313)."""
+        coeffs = list(coeffs)
+        d = len(coeffs)
+        carr = (self._ELEM * max(d, 1))(*coeffs)
+        keep = None
+        dev = _device_array(log, self.BITS)
+        if dev is None:
+            import torch  # device memory for a host log: one H2D copy, then the GPU test
+            arr = _host_array(log, self.BITS)
+            keep = torch.from_numpy(arr.view(np.int32 if self.BITS == 32 else np.int64)).cuda()
+            dev = _device_array(keep, self.BITS)
+        ptr, n, dv, stream = dev
+        ctx = ctx or get_context(dv)
+        while True:
+            hits = (C.c_uint64 * max(cap, 1))()
+            nh = C.c_size_t()
+            rc = self._f("root_test_device")(ctx.handle, carr, d, ptr, n, int(stop_value is not None),
+                                             int(stop_value or 0), hits, cap, C.byref(nh), stream)
+            if rc == QK_E_CAPACITY:
+                cap = nh.value
+                continue
+            check(rc, "root_test_device")
+            return [int(h) for h in hits[: nh.value]]
+
+    def decode_with_log(self, log, ctx: Context | None = None) -> list:
+        """quack's decode_with_log: the ids of `log` that are missing (every
+        log entry congruent to a root, in log order)."""
+        if self.count() == 0:
+            return []
+        coeffs = self.to_coeffs()
+        pos = self.root_test(coeffs, log, ctx=ctx)
+        dev = _device_array(log, self.BITS)
+        if dev is not None:
+            import torch
+            idx = torch.tensor(pos, dtype=torch.int64, device=log.device)
+            vals = log[idx].cpu().numpy()
+        else:
+            vals = _host_array(log, self.BITS)[pos]
+        mask = 0xFFFFFFFF if self.BITS == 32 else 0xFFFFFFFFFFFFFFFF
+        return [int(v) & mask for v in vals]
+
+
+class PowerSumQuackU32(_PowerSumQuack):
+    """quack::PowerSumQuackU32 — u32 ids over GF(2^32 - 5)."""
+    BITS = 32
+    _ELEM = C.c_uint32
+    _P = P32
+    _pre = "qk_u32_"
+
+
+class PowerSumQuackU64(_PowerSumQuack):
+    """quack::PowerSumQuackU64 — u64 ids over GF(2^64 - 59)."""
+    BITS = 64
+    _ELEM = C.c_uint64
+    _P = P64
+    _pre = "qk_u64_"
+
+
+# --------------------------------------------------------------------------
+# Low-level async encode (bench / multi-GPU): partial vectors on the device
+# --------------------------------------------------------------------------
+def partial_words(threshold: int, bits: int = 32) -> int:
+    return int(getattr(lib(), f"qk_u{bits}_partial_words")(threshold))
+
+
+def encode_device_async(ctx: Context, ids, threshold: int, partial, bits: int = 32, stream=None) -> None:
+    """Enqueue encode of a CUDA id tensor into a CUDA int64 `partial` tensor
+    of partial_words(threshold, bits) words (layout: include/quack_hip.h)."""
+    ptr, n, _, s = _device_array(ids, bits)
+    if stream is None:
+        stream = s
+    check(getattr(lib(), f"qk_u{bits}_encode_device_async")(ctx.handle, ptr, n, threshold,
+                                                              partial.data_ptr(), stream), "encode_device_async")
+
+
+def merge_partial(q: _PowerSumQuack, partial_host, has_last: bool, last: int) -> None:
+    arr = np.ascontiguousarray(np.asarray(partial_host).astype(np.uint64))
+    check(q._f("merge_partial")(q._buf, arr.ctypes.data_as(C.POINTER(C.c_uint64)), int(has_last), int(last)),
+          "merge_partial")
+
+
+def fill_splitmix(ctx: Context, out, seed: int, start: int = 0, bits: int = 32, stream=None) -> None:
+    """Fill a CUDA tensor with the synthetic splitmix64 id stream (device-side)."""
+    ptr, n, _, s = _device_array(out, bits)
+    check(getattr(lib(), f"qk_fill_splitmix_u{bits}")(ctx.handle, ptr, n, seed & 0xFFFFFFFFFFFFFFFF, start,
+                                                        s if stream is None else stream), "fill_splitmix")

@@ -1,0 +1,147 @@
+"""GPU parity of the decode-missing path (host Newton's identities + gfx950
+root-test kernel through the C ABI) against the oracle and golden fixtures.
+Mirrors media_client.rs:295-313: diff = mine - received; coeffs =
+diff.to_coeffs(); every log entry with eval(coeffs, id) == 0 is missing."""
+import numpy as np
+import pytest
+import torch
+
+import sidekick_amd as sk
+from sidekick_amd.quack import fill_splitmix
+from oracle import coracle, quack_oracle as qo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def dev(a, bits=32):
+    if bits == 32:
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(DEV)
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(DEV)
+
+
+def QT(bits):
+    return sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+
+
+def test_golden_decodes(golden):
+    for g in golden["decodes"]:
+        bits, n, t = g["bits"], g["n"], g["t"]
+        log = qo.ids_u32(g["seed"], n) if bits == 32 else qo.ids_u64(g["seed"], n)
+        if g["dup_at"] is not None:
+            log[g["dup_at"]] = log[g["dup_of"]]
+        keep = np.ones(n, dtype=bool)
+        keep[g["drops"]] = False
+        sent, recv = QT(bits)(t), QT(bits)(t)
+        sent.insert_batch(dev(log, bits))
+        recv.insert_batch(dev(log[keep], bits))
+        diff = sent.clone()
+        diff.sub_assign(recv)
+        assert diff.count() == g["diff_count"]
+        assert diff.power_sums() == [int(v) for v in g["diff_power_sums"]], g["name"]
+        coeffs = diff.to_coeffs()
+        assert list(coeffs) == [int(c) for c in g["coeffs"]]
+        assert diff.root_test(coeffs, dev(log, bits)) == g["hits"], g["name"]
+        missing = diff.decode_with_log(dev(log, bits))
+        assert missing == [int(log[i]) for i in g["hits"]]
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+@pytest.mark.parametrize("d", [1, 2, 3, 7, 8, 15, 16, 20, 31, 32, 33, 64, 100])
+def test_root_test_vs_oracle(bits, d):
+    rng = np.random.default_rng(d * 7 + bits)
+    n = 50_001
+    log = coracle.splitmix_u32(1000 + d, n) if bits == 32 else coracle.splitmix_u64(1000 + d, n)
+    roots_at = rng.choice(n, size=d, replace=False)
+    q = QT(bits)(max(d, 1))
+    for i in roots_at:
+        q.insert(int(log[i]))
+    c = q.to_coeffs()
+    # plant extra copies of two roots
+    log[(roots_at[0] + 17) % n] = log[roots_at[0]]
+    log[n - 1] = log[roots_at[-1]]
+    want, _ = (coracle.root_test_u32 if bits == 32 else coracle.root_test_u64)(c, log)
+    got = q.root_test(c, dev(log, bits))
+    assert got == want.tolist()
+    assert set(roots_at.tolist()) <= set(got)
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+def test_root_test_misaligned_small(bits):
+    log = coracle.splitmix_u32(3, 300) if bits == 32 else coracle.splitmix_u64(3, 300)
+    q = QT(bits)(8)
+    for i in (0, 5, 6, 150, 299):
+        q.insert(int(log[i]))
+    c = q.to_coeffs()
+    d = dev(log, bits)
+    for off in range(5):
+        for n in (0, 1, 2, 3, 4, 5, 6, 7, 9, 151, 295):
+            sub = log[off:off + n]
+            want, _ = (coracle.root_test_u32 if bits == 32 else coracle.root_test_u64)(c, sub)
+            assert q.root_test(c, d[off:off + n]) == want.tolist(), (off, n)
+
+
+def test_stop_at_last_value():
+    log = coracle.splitmix_u32(44, 10_000)
+    q = sk.PowerSumQuackU32(8)
+    for i in (10, 20, 9000):
+        q.insert(int(log[i]))
+    c = q.to_coeffs()
+    d = dev(log)
+    assert q.root_test(c, d) == [10, 20, 9000]
+    assert q.root_test(c, d, stop_value=int(log[500])) == [10, 20]
+    assert q.root_test(c, d, stop_value=int(log[10])) == []
+    assert q.root_test(c, d, stop_value=0xFFFFFFFF if 0xFFFFFFFF not in log else 1) == [10, 20, 9000]
+    want = qo.root_test_indices(list(c), log.tolist(), qo.P32, stop_value=int(log[5000]))
+    assert q.root_test(c, d, stop_value=int(log[5000])) == want
+
+
+def test_many_hits_capacity_growth():
+    # a log made mostly of roots: > the 4096 default device hit capacity
+    roots = coracle.splitmix_u32(8, 4)
+    log = np.tile(roots, 5000)
+    log[::7] = 12345
+    q = sk.PowerSumQuackU32(4)
+    for r in roots.tolist():
+        q.insert(r)
+    c = q.to_coeffs()
+    got = q.root_test(c, dev(log), cap=16)
+    want, _ = coracle.root_test_u32(c, log, cap=1 << 20)
+    assert got == want.tolist() and len(got) > 16000
+
+
+def test_undecodable_and_empty():
+    q = sk.PowerSumQuackU32(4)
+    assert q.decode_with_log(dev(np.arange(10, dtype=np.uint32))) == []
+    for i in range(1, 6):
+        q.insert(i)
+    with pytest.raises(sk.UndecodableError):
+        q.decode_with_log(dev(np.arange(10, dtype=np.uint32)))
+
+
+def test_config5_full_size():
+    """configs[4]: two quACKs built from 1e8 u32 ids, 32 dropped; recover them
+    by the GPU root test against the full candidate log.  Expected hits are
+    every position whose id is congruent to a dropped id (duplicates
+    included), computed independently with numpy set membership."""
+    n, t, seed = 100_000_000, 32, 0x5EED0005
+    ctx = sk.get_context(0)
+    log = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, log, seed)
+    rng = np.random.default_rng(seed)
+    drops = np.sort(rng.choice(n, size=32, replace=False))
+    keep = torch.ones(n, dtype=torch.bool, device=DEV)
+    keep[torch.from_numpy(drops).to(DEV)] = False
+    sent, recv = sk.PowerSumQuackU32(t), sk.PowerSumQuackU32(t)
+    sent.insert_batch(log)
+    recv.insert_batch(log[keep].contiguous())
+    diff = sent.clone()
+    diff.sub_assign(recv)
+    assert diff.count() == 32
+    hits = diff.root_test(diff.to_coeffs(), log)
+    h = log.cpu().numpy().view(np.uint32).astype(np.uint64)
+    p = np.uint64(qo.P32)
+    dropped_vals = np.unique(h[drops] % p)
+    want = np.nonzero(np.isin(h % p, dropped_vals))[0].tolist()
+    assert hits == want
+    assert set(drops.tolist()) <= set(hits)

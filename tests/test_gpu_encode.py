@@ -1,0 +1,233 @@
+"""GPU parity of the batch encode path (gfx950 kernels through the C ABI)
+against the oracle and the golden fixtures; bit-exact (integer arithmetic).
+Full-size (1e9) behaviour is checked through size-independent properties:
+additivity under arbitrary splits and grid-shape independence."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import sidekick_amd as sk
+from sidekick_amd._lib import lib
+from sidekick_amd.quack import encode_device_async, fill_splitmix, merge_partial, partial_words
+from oracle import coracle, quack_oracle as qo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def dev_u32(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(DEV)
+
+
+def dev_u64(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(DEV)
+
+
+def gpu_state(ids, t, bits=32, ctx=None):
+    q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
+    q.insert_batch(ids if isinstance(ids, torch.Tensor) else (dev_u32(ids) if bits == 32 else dev_u64(ids)), ctx=ctx)
+    return q
+
+
+def test_kats_and_empty(golden):
+    for k in golden["kats"]:
+        q = gpu_state(np.array(k["ids"], dtype=np.uint32 if k["bits"] == 32 else np.uint64), k["t"], k["bits"])
+        assert q.power_sums() == k["expect"]["power_sums"], k["name"]
+        assert q.count() == k["expect"]["count"]
+        assert q.last_value() == k["expect"]["last_value"]
+
+
+def test_edges(golden):
+    for e in golden["edges"]:
+        ids = np.array([int(v) for v in e["ids"]], dtype=np.uint32 if e["bits"] == 32 else np.uint64)
+        q = gpu_state(ids, e["t"], e["bits"])
+        assert q.power_sums() == [int(v) for v in e["expect"]["power_sums"]], (e["bits"], e["t"])
+        assert q.last_value() == int(e["expect"]["last_value"])
+
+
+def test_golden_streams(golden):
+    for s in golden["streams"]:
+        if s["bits"] == 32:
+            q = gpu_state(qo.ids_u32(s["seed"], s["n"]), s["t"], 32)
+        else:
+            q = gpu_state(qo.ids_u64(s["seed"], s["n"]), s["t"], 64)
+        assert q.power_sums() == [int(v) for v in s["expect"]["power_sums"]], (s["bits"], s["n"], s["t"])
+        assert q.count() == s["n"]
+
+
+U32_TS = list(range(1, 34)) + [40, 47, 64, 65, 80, 100, 128, 129, 256, 300, 513, 1024]
+U64_TS = [1, 2, 3, 5, 8, 12, 16, 19, 20, 21, 32, 40, 64, 80, 81, 160, 300, 1024]
+
+
+@pytest.mark.parametrize("t", U32_TS)
+def test_u32_threshold_sweep(t):
+    ids = coracle.splitmix_u32(0xABC0 + t, 20011)
+    assert gpu_state(ids, t).power_sums() == coracle.encode_u32(ids, t)
+
+
+@pytest.mark.parametrize("t", U64_TS)
+def test_u64_threshold_sweep(t):
+    ids = coracle.splitmix_u64(0xDEF0 + t, 3001)
+    assert gpu_state(ids, t, 64).power_sums() == coracle.encode_u64(ids, t)
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+def test_misaligned_and_ragged(bits):
+    base_n = 4099
+    ids = coracle.splitmix_u32(5, base_n) if bits == 32 else coracle.splitmix_u64(5, base_n)
+    d = dev_u32(ids) if bits == 32 else dev_u64(ids)
+    enc = coracle.encode_u32 if bits == 32 else coracle.encode_u64
+    for off in range(0, 5):
+        for n in (0, 1, 2, 3, 4, 5, 7, 8, 9, 17, 64, 257, 1000):
+            q = gpu_state(d[off:off + n], 32, bits)
+            assert q.power_sums() == enc(ids[off:off + n], 32), (off, n)
+            assert q.count() == n
+            assert q.last_value() == (int(ids[off + n - 1]) if n else None)
+
+
+@pytest.mark.parametrize("bits,t", [(32, 32), (32, 16), (32, 80), (64, 80), (64, 16)])
+def test_grid_shape_independent(bits, t):
+    n = 300_007
+    ids = coracle.splitmix_u32(77, n) if bits == 32 else coracle.splitmix_u64(77, n)
+    want = (coracle.encode_u32 if bits == 32 else coracle.encode_u64)(ids, t)
+    ctx = sk.Context(0)
+    try:
+        for g in (0, 1, 3, 8, 255, 1024, 4096):
+            ctx.set_grid(g)
+            assert gpu_state(ids, t, bits, ctx=ctx).power_sums() == want, g
+    finally:
+        ctx.close()
+
+
+def test_device_fill_matches_oracle_generator():
+    ctx = sk.get_context(0)
+    out = torch.empty(100_003, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, out, 0x1234, start=999, bits=32)
+    assert (out.cpu().numpy().view(np.uint32) == coracle.splitmix_u32(0x1234, 100_003, start=999)).all()
+    out64 = torch.empty(50_001, dtype=torch.int64, device=DEV)
+    fill_splitmix(ctx, out64, 0x1234, start=5, bits=64)
+    assert (out64.cpu().numpy().view(np.uint64) == coracle.splitmix_u64(0x1234, 50_001, start=5)).all()
+
+
+def test_large_stream_vs_oracle():
+    """1e7 ids at t = 32 against the scalar C oracle (a few seconds of CPU)."""
+    n, t, seed = 10_000_000, 32, 0x5EED0002
+    ctx = sk.get_context(0)
+    d = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, d, seed)
+    q = gpu_state(d, t)
+    assert q.power_sums() == coracle.encode_u32_seed(seed, n, t)
+
+
+def test_async_partial_api():
+    ctx = sk.get_context(0)
+    n, t = 1_000_003, 32
+    ids = coracle.splitmix_u32(9, n)
+    d = dev_u32(ids)
+    part = torch.zeros(partial_words(t), dtype=torch.int64, device=DEV)
+    encode_device_async(ctx, d, t, part)
+    torch.cuda.synchronize()
+    h = part.cpu().numpy().view(np.uint64)
+    assert h[:t].tolist() == coracle.encode_u32(ids, t)
+    assert int(h[t]) == n and int(h[t + 1]) == int(ids[-1])
+    q = sk.PowerSumQuackU32(t)
+    merge_partial(q, h, True, int(ids[-1]))
+    assert q.power_sums() == h[:t].tolist() and q.count() == n
+
+
+def test_u64_async_partial_limbs():
+    ctx = sk.get_context(0)
+    n, t = 100_003, 80
+    ids = coracle.splitmix_u64(10, n)
+    part = torch.zeros(partial_words(t, 64), dtype=torch.int64, device=DEV)
+    encode_device_async(ctx, dev_u64(ids), t, part, bits=64)
+    torch.cuda.synchronize()
+    h = [int(v) for v in part.cpu().numpy().view(np.uint64)]
+    S = [h[2 * k] + (h[2 * k + 1] << 32) for k in range(t)]
+    assert S == coracle.encode_u64(ids, t)
+    assert all(h[2 * k] < 2**32 and h[2 * k + 1] < 2**32 for k in range(t))
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_input_path_multi_chunk(pinned):
+    """Host-resident ids (the sniffed-packet case): > one 64 MiB chunk."""
+    n, t = 40_000_003, 32
+    ids = coracle.splitmix_u32(0x77, n)
+    if pinned:
+        buf = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        buf.numpy().view(np.uint32)[:] = ids
+        ids = buf.numpy().view(np.uint32)
+    q = sk.PowerSumQuackU32(t)
+    q.insert_batch(ids)
+    ref = gpu_state(dev_u32(ids), t)
+    assert q == ref
+    assert q.count() == n and q.last_value() == int(ids[-1])
+
+
+def test_incremental_batches_equal_single_batch():
+    ids = coracle.splitmix_u32(0x99, 100_000)
+    whole = gpu_state(ids, 32)
+    inc = sk.PowerSumQuackU32(32)
+    for a, b in ((0, 1), (1, 33_333), (33_333, 33_334), (33_334, 100_000)):
+        inc.insert_batch(dev_u32(ids[a:b]))
+    assert inc == whole
+    # mixing the per-packet host insert and the batch path
+    mix = sk.PowerSumQuackU32(32)
+    for x in ids[:10].tolist():
+        mix.insert(x)
+    mix.insert_batch(dev_u32(ids[10:]))
+    assert mix == whole
+
+
+def test_rejects_host_pointer_on_device_entry():
+    ctx = sk.get_context(0)
+    arr = np.arange(16, dtype=np.uint32)
+    q = sk.PowerSumQuackU32(4)
+    rc = lib().qk_u32_encode_device(ctx.handle, arr.ctypes.data, arr.size, q._buf, None)
+    assert rc == -1  # QK_E_INVAL, not a fault
+
+
+def test_full_size_1e9_properties():
+    """configs[1] size: 1e9 u32 ids at t = 32.  Size-independent checks: the
+    whole-array encode equals the merge of uneven pieces and is independent
+    of the grid shape; count / last_value are exact."""
+    n, t, seed = 1_000_000_000, 32, 0x5EED0002
+    ctx = sk.get_context(0)
+    d = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, d, seed)
+    whole = gpu_state(d, t)
+    assert whole.count() == n
+    assert whole.last_value() == int(coracle.splitmix_u32(seed, 1, start=n - 1)[0])
+    pieces = sk.PowerSumQuackU32(t)
+    for a, b in ((0, 123_456_789), (123_456_789, 123_456_790), (123_456_790, 999_999_999), (999_999_999, n)):
+        pieces.insert_batch(d[a:b])
+    assert pieces == whole
+    c2 = sk.Context(0)
+    try:
+        c2.set_grid(1000)
+        assert gpu_state(d, t, ctx=c2) == whole
+    finally:
+        c2.close()
+    # the first 2e6 ids against the oracle (same stream, same kernels)
+    assert gpu_state(d[:2_000_000], t).power_sums() == coracle.encode_u32_seed(seed, 2_000_000, t)
+    del d
+    torch.cuda.empty_cache()
+
+
+def test_full_size_u64_properties():
+    """configs[2] size class: u64 ids at t = 80 (2.5e8 ids, 2 GB) — additivity
+    and oracle agreement on a prefix."""
+    n, t, seed = 250_000_000, 80, 0x5EED0003
+    ctx = sk.get_context(0)
+    d = torch.empty(n, dtype=torch.int64, device=DEV)
+    fill_splitmix(ctx, d, seed, bits=64)
+    whole = gpu_state(d, t, 64)
+    pieces = sk.PowerSumQuackU64(t)
+    for a, b in ((0, 77_777_777), (77_777_777, n)):
+        pieces.insert_batch(d[a:b])
+    assert pieces == whole
+    assert gpu_state(d[:200_000], t, 64).power_sums() == coracle.encode_u64_seed(seed, 200_000, t)
+    del d
+    torch.cuda.empty_cache()

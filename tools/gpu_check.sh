@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box session: microbench, smoke, GPU parity tests, bench, rocprof.
+# Every GPU step has its own time limit; a crash (not a test failure) stops
+# the script.  Output goes to gpurun_out/.
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+cd "$ROOT"
+step() {  # name timeout cmd...
+    local name=$1 to=$2; shift 2
+    echo "== $name: $*" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+    return $rc
+}
+ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+
+STEPS="${STEPS:-ubench smoke pytest bench prof}"
+for s in $STEPS; do
+  case $s in
+    ubench) step ubench 120 ./tools/ubench_int || exit 3 ;;
+    smoke) step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
+    pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA ${PYTEST_ARGS:-}; rc=$?; ok_or_testfail $rc || exit 3 ;;
+    bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
+    prof)
+      export TMPDIR=/tmp
+      step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --cpu-sample 0 || exit 3 ;;
+    pmc)
+      export TMPDIR=/tmp
+      step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
+  esac
+done
+echo ALLDONE | tee -a "$OUT/steps.log"
