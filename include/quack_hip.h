@@ -19,8 +19,9 @@
  *     (the reference guards it with a Mutex: sidekick.rs:107).
  *   - "device" functions run hand-written gfx950 kernels.  They never fall
  *     back to the CPU: with no GPU they return QK_E_NO_DEVICE.
- *   - `stream` is a hipStream_t passed as void*; NULL selects the context's
- *     own stream.  "_async" functions only enqueue work on that stream.
+ *   - `stream` is a hipStream_t passed as void*; NULL is the HIP null
+ *     (legacy default) stream, so work is ordered with the caller's
+ *     default-stream work.  "_async" functions only enqueue on that stream.
  *
  * Field and semantics:  p32 = 2^32-5, p64 = 2^64-59; an id is
  * mapped to x = id mod p; S[k-1] = sum_i x_i^k mod p for k = 1..threshold;

@@ -17,7 +17,24 @@ using namespace qk;
 
 namespace qk {
 
-hipStream_t pick_stream(qk_ctx *ctx, void *stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+// NULL is the HIP null (legacy default) stream, as in every HIP API: work
+// enqueued there is ordered with the caller's default-stream work (torch's
+// default stream has handle 0).
+hipStream_t pick_stream(qk_ctx *ctx, void *stream) {
+    (void)ctx;
+    return (hipStream_t)stream;
+}
+
+int scratch_acquire(qk_ctx *ctx, hipStream_t s) {
+    if (ctx->scratch_ev_valid) QK_HIP_TRY(hipStreamWaitEvent(s, ctx->scratch_ev, 0));
+    return QK_OK;
+}
+
+int scratch_release(qk_ctx *ctx, hipStream_t s) {
+    QK_HIP_TRY(hipEventRecord(ctx->scratch_ev, s));
+    ctx->scratch_ev_valid = true;
+    return QK_OK;
+}
 
 int ensure_scratch(qk_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->scratch_bytes) return QK_OK;
@@ -255,7 +272,8 @@ int qk_ctx_create(int device, qk_ctx **out) {
         hipMalloc(&ctx->d_small, SMALL_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&ctx->h_small, SMALL_WORDS * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->stage_ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->stage_ev[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&ctx->stage_ev[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess) {
         qk_ctx_destroy(ctx);
         return QK_E_HIP;
     }
@@ -274,6 +292,7 @@ void qk_ctx_destroy(qk_ctx *ctx) {
         if (ctx->d_stage[i]) hipFree(ctx->d_stage[i]);
         if (ctx->stage_ev[i]) hipEventDestroy(ctx->stage_ev[i]);
     }
+    if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
     if (ctx->d_scratch) hipFree(ctx->d_scratch);
     if (ctx->d_hits) hipFree(ctx->d_hits);
     if (ctx->d_small) hipFree(ctx->d_small);

@@ -33,6 +33,11 @@ struct qk_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_pending;
     std::vector<hipEvent_t> ev_pool;
 
+    // scratch hand-off between streams: every launch that uses d_scratch /
+    // d_small / d_hits waits for the previous user's event, then records its own
+    hipEvent_t scratch_ev = nullptr;
+    bool scratch_ev_valid = false;
+
     std::mutex mu;
 };
 
@@ -50,6 +55,10 @@ constexpr size_t SMALL_NHITS = 3072;   // hit counter
 constexpr size_t SMALL_STOP = 3073;    // first stop index
 
 hipStream_t pick_stream(qk_ctx *ctx, void *stream);
+// order stream s after the previous user of the context's scratch buffers
+int scratch_acquire(qk_ctx *ctx, hipStream_t s);
+// mark the end of s's use of the scratch buffers
+int scratch_release(qk_ctx *ctx, hipStream_t s);
 int ensure_scratch(qk_ctx *ctx, size_t bytes);
 int ensure_hits(qk_ctx *ctx, size_t cap);
 int ensure_stage(qk_ctx *ctx, size_t bytes);

@@ -340,6 +340,8 @@ static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t
     int rc = ensure_scratch(ctx, need);
     if (rc) return rc;
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
+    rc = scratch_acquire(ctx, s);
+    if (rc) return rc;
     hipEvent_t e0 = prof_begin(ctx, s);
     hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, T, partials);
     prof_end(ctx, s, e0);
@@ -347,7 +349,7 @@ static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t
     hipLaunchKernelGGL(fin, dim3(T), dim3(BLOCK), 0, s, partials, nb, T, d_ids, (uint64_t)n, d_partial,
                        accumulate);
     QK_HIP_TRY(hipGetLastError());
-    return QK_OK;
+    return scratch_release(ctx, s);
 }
 
 // Choose (G, K): the smallest G whose K = ceil(T/G) fits the register
