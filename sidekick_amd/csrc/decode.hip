@@ -30,43 +30,46 @@ __device__ __forceinline__ void rt_record(uint64_t pos, bool hit, bool stop, uin
 }
 
 // ------------------------------------------------------------------ u32
-__device__ __forceinline__ bool is_root32(uint32_t x, const uint32_t *__restrict__ c, uint32_t d) {
-    // P(x) = (((x + c1) x + c2) x + ... ) x + c_d, evaluated as r = r*x + c
-    uint32_t r = mad32_lazy(1u, x, c[0]);
-    for (uint32_t i = 1; i < d; ++i) r = mad32_lazy(r, x, c[i]);
-    return canon32(r) == 0;
+// Horner in t-form (field.h tstep32): r <- r*x + c_i is three mads + one sub.
+__device__ __forceinline__ bool t_is_zero32(uint32_t lo, uint32_t hi) {
+    return canon32(fold64_32(((uint64_t)hi << 32) | lo)) == 0;
 }
 
-template <int D> // D > 0: compile-time degree, coefficients fully in SGPRs
+__device__ __forceinline__ bool is_root32(uint32_t id, const uint32_t *__restrict__ c, uint32_t d) {
+    const uint32_t x = canon32(id), x5 = times5_32(x);
+    uint32_t lo = 1, hi = 0;
+    for (uint32_t i = 0; i < d; ++i) tstep32(lo, hi, x, x5, c[i]);
+    return t_is_zero32(lo, hi);
+}
+
+template <int D> // D > 0: compile-time degree (fully unrolled); D == 0: runtime d
 __device__ __forceinline__ void horner32x4(uint4 w, const uint32_t *__restrict__ c, uint32_t d, bool (&hit)[4]) {
-    uint32_t r0, r1, r2, r3;
-    r0 = mad32_lazy(1u, w.x, c[0]);
-    r1 = mad32_lazy(1u, w.y, c[0]);
-    r2 = mad32_lazy(1u, w.z, c[0]);
-    r3 = mad32_lazy(1u, w.w, c[0]);
+    const uint32_t x0 = canon32(w.x), x1 = canon32(w.y), x2 = canon32(w.z), x3 = canon32(w.w);
+    const uint32_t f0 = times5_32(x0), f1 = times5_32(x1), f2 = times5_32(x2), f3 = times5_32(x3);
+    uint32_t l0 = 1, l1 = 1, l2 = 1, l3 = 1, h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     if constexpr (D > 0) {
 #pragma unroll
-        for (int i = 1; i < D; ++i) {
+        for (int i = 0; i < D; ++i) {
             const uint32_t ci = c[i];
-            r0 = mad32_lazy(r0, w.x, ci);
-            r1 = mad32_lazy(r1, w.y, ci);
-            r2 = mad32_lazy(r2, w.z, ci);
-            r3 = mad32_lazy(r3, w.w, ci);
+            tstep32(l0, h0, x0, f0, ci);
+            tstep32(l1, h1, x1, f1, ci);
+            tstep32(l2, h2, x2, f2, ci);
+            tstep32(l3, h3, x3, f3, ci);
         }
     } else {
 #pragma unroll 4
-        for (uint32_t i = 1; i < d; ++i) {
+        for (uint32_t i = 0; i < d; ++i) {
             const uint32_t ci = c[i];
-            r0 = mad32_lazy(r0, w.x, ci);
-            r1 = mad32_lazy(r1, w.y, ci);
-            r2 = mad32_lazy(r2, w.z, ci);
-            r3 = mad32_lazy(r3, w.w, ci);
+            tstep32(l0, h0, x0, f0, ci);
+            tstep32(l1, h1, x1, f1, ci);
+            tstep32(l2, h2, x2, f2, ci);
+            tstep32(l3, h3, x3, f3, ci);
         }
     }
-    hit[0] = canon32(r0) == 0;
-    hit[1] = canon32(r1) == 0;
-    hit[2] = canon32(r2) == 0;
-    hit[3] = canon32(r3) == 0;
+    hit[0] = t_is_zero32(l0, h0);
+    hit[1] = t_is_zero32(l1, h1);
+    hit[2] = t_is_zero32(l2, h2);
+    hit[3] = t_is_zero32(l3, h3);
 }
 
 template <int D>

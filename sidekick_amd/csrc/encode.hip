@@ -34,28 +34,40 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
 }
 
 // ------------------------------------------------------------------ u32
+// Power chain in t-form (field.h: tstep32): per power three v_mad_u64_u32,
+// one v_sub_u32 and one 64-bit accumulate; x and x5 = 5x are canonical.
+
 template <int K>
 __device__ __forceinline__ void chain32(uint64_t (&acc)[K], uint32_t start, uint32_t step) {
-    uint32_t y = start;
+    // start: any value < 2^32 (t-form with hi = 0); step canonical
+    const uint32_t step5 = times5_32(step);
+    uint64_t t = start;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        acc[k] += y;
-        if (k + 1 < K) y = mul32_lazy(y, step);
+        acc[k] += t;
+        if (k + 1 < K) t = tstep32p(t, step, step5, 0u);
     }
 }
 
-// four independent ids in lockstep (ILP for the dependent modmul chains)
+// four independent ids in lockstep (ILP for the dependent modmul chains);
+// the four t-form values of a power are summed before the accumulate
+// (each < 6*2^32, so the sum and the lane accumulator stay far below 2^64).
 template <int K>
 __device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
-    uint32_t y0 = w.x, y1 = w.y, y2 = w.z, y3 = w.w;
+    const uint32_t x0 = canon32(w.x), x1 = canon32(w.y), x2 = canon32(w.z), x3 = canon32(w.w);
+    const uint32_t f0 = times5_32(x0), f1 = times5_32(x1), f2 = times5_32(x2), f3 = times5_32(x3);
+    uint64_t t0 = x0, t1 = x1, t2 = x2, t3 = x3;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        acc[k] += (uint64_t)y0 + y1 + ((uint64_t)y2 + y3);
+        acc[k] += t0;
+        acc[k] += t1;
+        acc[k] += t2;
+        acc[k] += t3;
         if (k + 1 < K) {
-            y0 = mul32_lazy(y0, w.x);
-            y1 = mul32_lazy(y1, w.y);
-            y2 = mul32_lazy(y2, w.z);
-            y3 = mul32_lazy(y3, w.w);
+            t0 = tstep32p(t0, x0, f0, 0u);
+            t1 = tstep32p(t1, x1, f1, 0u);
+            t2 = tstep32p(t2, x2, f2, 0u);
+            t3 = tstep32p(t3, x3, f3, 0u);
         }
     }
 }
@@ -72,7 +84,7 @@ __device__ __forceinline__ void group_powers32(uint32_t x, int j, uint32_t &star
         if ((1 << bit) < G) b = mul32_lazy(b, b);
     }
     start = r;
-    step = b; // after log2(G) squarings b = x^G
+    step = canon32(b); // after log2(G) squarings b = x^G; the chain needs it canonical
 }
 
 // Reduce per-lane accumulators to one partial per (power, block).
@@ -120,8 +132,8 @@ __global__ __launch_bounds__(BLOCK) void k_encode_u32_g1(const uint32_t *__restr
     for (uint64_t i = gtid; i < body; i += nthr) chain32x4<K>(acc, v[i]);
     // unaligned head (< 4 ids) and tail (< 4 ids)
     const uint64_t tail0 = h + (body << 2);
-    if (gtid < h) chain32<K>(acc, ids[gtid], ids[gtid]);
-    if (gtid < n - tail0) chain32<K>(acc, ids[tail0 + gtid], ids[tail0 + gtid]);
+    if (gtid < h) chain32<K>(acc, ids[gtid], canon32(ids[gtid]));
+    if (gtid < n - tail0) chain32<K>(acc, ids[tail0 + gtid], canon32(ids[tail0 + gtid]));
 
     block_store<1, K>(acc, T, partials, sm, Fold32{});
 }

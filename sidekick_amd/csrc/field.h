@@ -49,6 +49,40 @@ QK_HD uint32_t mad32_lazy(uint32_t y, uint32_t x, uint32_t c) {
     return (uint32_t)u + C32 * (uint32_t)(u >> 32);
 }
 
+// ---- "t-form": the chain representation used by the gfx950 kernels -------
+// A residue is held as t = lo + hi*2^32 with hi <= 5 (t < 6*2^32).  With x and
+// x5 = 5x mod p both canonical (<= p-1), one step t <- t*x + c (c <= p-1) is
+//     P  = lo*x + (hi*x5 + c)      <= (2^32-1)(p-1) + 6(p-1) = (p-1)(2^32+5)
+//                                   = 2^64 - 2^32 - 30 < 2^64   (no overflow)
+//     t' = P_lo + 5*P_hi           P_hi <= 2^32-2  =>  t' < 6*2^32 (hi' <= 5)
+// and t' == t*x + c (mod p) because hi*x5 == hi*5x == hi*2^32*x.  t' is
+// formed as Q = P + 5*P_hi (mod 2^64) then Q_hi -= P_hi, i.e. P + 5P_hi -
+// P_hi*2^32 = t' exactly (t' < 2^64): three v_mad_u64_u32 and one v_sub_u32,
+// with no carry handling and no canonicalisation inside the chain.
+QK_HD void tstep32(uint32_t &lo, uint32_t &hi, uint32_t x, uint32_t x5, uint32_t c) {
+    const uint64_t P = (uint64_t)lo * x + ((uint64_t)hi * x5 + c);
+    const uint32_t Ph = (uint32_t)(P >> 32);
+    const uint64_t Q = P + (uint64_t)Ph * C32;
+    lo = (uint32_t)Q;
+    hi = (uint32_t)(Q >> 32) - Ph;
+}
+// Same step on a t-form value kept as one 64-bit register pair, so the
+// accumulate that follows is a single 64-bit add of the pair.
+QK_HD uint64_t tstep32p(uint64_t t, uint32_t x, uint32_t x5, uint32_t c) {
+    const uint64_t P = (uint64_t)(uint32_t)t * x + ((uint64_t)(uint32_t)(t >> 32) * x5 + c);
+    const uint32_t Ph = (uint32_t)(P >> 32);
+    const uint64_t Q = P + (uint64_t)Ph * C32;
+    return Q - ((uint64_t)Ph << 32);
+}
+// 5x mod p for canonical x (x5 in the step above)
+QK_HD uint32_t times5_32(uint32_t x) {
+    const uint64_t v = (uint64_t)x * C32;                   // < 5*2^32
+    const uint64_t u = (v >> 32) * C32 + (uint32_t)v;        // < 2^32 + 20
+    const uint32_t r = (uint32_t)u + C32 * (uint32_t)(u >> 32);
+    const uint32_t a = r + C32;                              // canon
+    return a < r ? a : r;
+}
+
 // Fold a 64-bit lazy accumulator (any value) to [0, 2^32), congruent.
 QK_HD uint32_t fold64_32(uint64_t a) {
     uint64_t t = (a >> 32) * C32 + (uint32_t)a;         // < 6*2^32
