@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Secondary measurements for DESIGN.md (not the driver's bench line):
+
+  u64      configs[2]: encode 1e9 u64 ids at t=80, device-resident
+  decode   configs[4]: subtract two quACKs built from 1e8 u32 ids, 32 missing,
+           root test over the 1e8-entry candidate log (device-resident)
+  host     encode 1e9 u32 ids at t=32 starting from HOST memory (pinned and
+           pageable): the PCIe-inclusive rate the sniffer-fed path sees
+  sweep    encode rate vs threshold t (u32)
+
+Each prints one JSON line per measurement.  Kernel times come from HIP events
+on the launch stream (qk_ctx_set_profiling); wall times from perf_counter
+around synchronised loops.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import sidekick_amd as sk  # noqa: E402
+from sidekick_amd.quack import encode_device_async, fill_splitmix, partial_words  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def emit(d):
+    print(json.dumps(d), flush=True)
+
+
+def time_encode(ctx, ids, t, bits, steps, warmup=2):
+    part = torch.zeros(partial_words(t, bits), dtype=torch.int64, device=DEV)
+    for _ in range(warmup):
+        encode_device_async(ctx, ids, t, part, bits=bits)
+    torch.cuda.synchronize()
+    ctx.kernel_stats()
+    ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        encode_device_async(ctx, ids, t, part, bits=bits)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    ms, n = ctx.kernel_stats()
+    return wall / steps, ms / max(n, 1) / 1e3
+
+
+def run_u64(args, ctx):
+    n, t = int(args.n64), 80
+    ids = torch.empty(n, dtype=torch.int64, device=DEV)
+    fill_splitmix(ctx, ids, 0x5EED0003, bits=64)
+    wall, kern = time_encode(ctx, ids, t, 64, args.steps)
+    emit({"config": "encode u64 t=80 device-resident", "n": n, "ids_per_s": n / wall, "kernel_s": kern,
+          "hbm_GBps_algorithmic": 8 * n / kern / 1e9, "frac_hbm_8TBs": 8 * n / kern / 8e12})
+    if args.cpu:
+        from oracle import coracle
+        m = int(args.cpu_sample64)
+        tc = time.perf_counter()
+        S = coracle.encode_u64_seed(0x5EED0003, m, t)
+        cs = time.perf_counter() - tc
+        q = sk.PowerSumQuackU64(t)
+        q.insert_batch(ids[:m])
+        emit({"config": "cpu baseline u64 t=80 (oracle C, 1 core)", "n": m, "ids_per_s": m / cs,
+              "parity_with_gpu": q.power_sums() == S})
+
+
+def run_decode(args, ctx):
+    n, t, seed = int(args.ndec), 32, 0x5EED0005
+    log = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, log, seed)
+    rng = np.random.default_rng(seed)
+    drops = np.sort(rng.choice(n, size=32, replace=False))
+    keep = torch.ones(n, dtype=torch.bool, device=DEV)
+    keep[torch.from_numpy(drops).to(DEV)] = False
+    kept = log[keep].contiguous()
+    torch.cuda.synchronize()
+    # the timed decode step: encode both sides, subtract, to_coeffs, root test
+    reps = []
+    for r in range(args.steps + 1):
+        t0 = time.perf_counter()
+        sent, recv = sk.PowerSumQuackU32(t), sk.PowerSumQuackU32(t)
+        sent.insert_batch(log)
+        recv.insert_batch(kept)
+        diff = sent.clone()
+        diff.sub_assign(recv)
+        t1 = time.perf_counter()
+        c = diff.to_coeffs()
+        t2 = time.perf_counter()
+        ctx.set_profiling(True)
+        hits = diff.root_test(c, log)
+        ctx.set_profiling(False)
+        t3 = time.perf_counter()
+        ms, k = ctx.kernel_stats()
+        if r:
+            reps.append((t1 - t0, t2 - t1, t3 - t2, ms / 1e3))
+    a = np.median(np.array(reps), axis=0)
+    ok = set(drops.tolist()) <= set(hits)
+    emit({"config": "decode-missing u32 n=1e8 d=32 (configs[4])", "n": n, "hits": len(hits), "drops_recovered": ok,
+          "encode_both_s": a[0], "to_coeffs_s": a[1], "root_test_wall_s": a[2], "root_test_kernel_s": a[3],
+          "root_test_candidates_per_s": n / a[3], "total_s": a[0] + a[1] + a[2]})
+    if args.cpu:
+        from oracle import coracle
+        m = int(args.cpu_sample_dec)
+        h = log[:m].cpu().numpy().view(np.uint32)
+        tc = time.perf_counter()
+        w, nh = coracle.root_test_u32(list(c), h)
+        cs = time.perf_counter() - tc
+        emit({"config": "cpu baseline root test d=32 (oracle C, 1 core)", "n": m, "candidates_per_s": m / cs,
+              "extrapolated_1e8_s": cs * n / m, "hits_match_gpu_prefix": w.tolist() == [x for x in hits if x < m]})
+
+
+def run_host(args, ctx):
+    n, t = int(args.nhost), 32
+    d = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, d, 0x5EED0002)
+    pinned = torch.empty(n, dtype=torch.int32, pin_memory=True)
+    pinned.copy_(d)
+    pageable = d.cpu().numpy()
+    ref = sk.PowerSumQuackU32(t)
+    ref.insert_batch(d)
+    for name, arr in (("pinned", pinned.numpy()), ("pageable", pageable)):
+        times = []
+        for r in range(3):
+            q = sk.PowerSumQuackU32(t)
+            t0 = time.perf_counter()
+            q.insert_batch(arr.view(np.uint32))
+            times.append(time.perf_counter() - t0)
+        assert q == ref
+        tm = min(times)
+        emit({"config": f"encode u32 t=32 from {name} host memory (H2D + kernel, pipelined)", "n": n,
+              "ids_per_s": n / tm, "GBps_h2d_equiv": 4 * n / tm / 1e9, "seconds": tm})
+    # raw H2D copy rate for reference
+    tmp = torch.empty(n, dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tmp.copy_(pinned, non_blocking=True)
+    torch.cuda.synchronize()
+    emit({"config": "raw H2D copy, pinned (torch)", "GBps": 4 * n / (time.perf_counter() - t0) / 1e9})
+
+
+def run_sweep(args, ctx):
+    n = int(args.nsweep)
+    ids = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, ids, 0x5EED0002)
+    for t in (1, 4, 8, 16, 20, 24, 32, 40, 64, 80, 128, 256, 300):
+        wall, kern = time_encode(ctx, ids, t, 32, max(3, args.steps // 2))
+        emit({"config": f"encode u32 t={t}", "n": n, "ids_per_s": n / kern, "ns_per_id_per_power": kern / n / t * 1e9 * 1})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep"])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--n64", type=float, default=1e9)
+    ap.add_argument("--ndec", type=float, default=1e8)
+    ap.add_argument("--nhost", type=float, default=1e9)
+    ap.add_argument("--nsweep", type=float, default=2.5e8)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--cpu-sample64", type=float, default=5e6)
+    ap.add_argument("--cpu-sample-dec", type=float, default=2e7)
+    args = ap.parse_args()
+    ctx = sk.get_context(0)
+    for w in args.what:
+        {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep}[w](args, ctx)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -24,9 +24,10 @@ for s in $STEPS; do
     smoke) step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
     pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA ${PYTEST_ARGS:-}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
+    configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
     prof)
       export TMPDIR=/tmp
-      step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --cpu-sample 0 || exit 3 ;;
+      step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 1 --cpu-sample 0 || exit 3 ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
