@@ -72,6 +72,131 @@ __device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
     }
 }
 
+// ---- baby-step / giant-step encode for t <= 32 ---------
+// power m+1 = a*NB + b + 1 with B_b = x^(b+1) (b < NB) and A_a = x^(a*NB)
+// (a < NA; A_0 = 1), so S_{m+1} = sum_i A_a(x_i) * B_b(x_i): NB-1 + NA-2
+// lazy modmuls per id, then (NA-1)*NB 32x32->64 multiply-accumulates into
+// 64-bit accumulators whose wraps are counted (2^64 == 25 mod p), plus NB
+// plain adds for the a = 0 row.
+// One MAC = v_mad_u64_u32 with its carry-out in VCC + v_addc_co_u32 of that
+// carry into a 32-bit wrap counter.
+__device__ __forceinline__ void mac_carry(uint64_t &acc, uint32_t &cnt, uint32_t a, uint32_t b) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(cnt)
+        : "v"(a), "v"(b)
+        : "vcc");
+}
+
+template <int NB, int NA>
+struct BsgsAcc {
+    uint64_t a0[NB];          // a = 0 row: sum of B_b
+    uint64_t m[NA - 1][NB];   // a >= 1: sum of A_a * B_b mod 2^64
+    uint32_t c[NA - 1][NB];   // ... and its wrap count
+};
+
+// powers of one id; returns nonzero if a lazy fold wrapped (then B/A are
+// recomputed exactly by the caller)
+template <int NB, int NA>
+__device__ __forceinline__ uint32_t bsgs_powers(uint32_t id, uint32_t (&B)[NB], uint32_t (&A)[NA > 1 ? NA - 1 : 1]) {
+    uint32_t wrapped = 0;
+    B[0] = canon32(id);
+#pragma unroll
+    for (int b = 1; b < NB; ++b) B[b] = mulfold32_fast(B[b - 1], B[0], wrapped);
+    if constexpr (NA > 1) {
+        A[0] = B[NB - 1];
+#pragma unroll
+        for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_fast(A[a - 1], A[0], wrapped);
+    }
+    return wrapped;
+}
+template <int NB, int NA>
+__device__ __forceinline__ void bsgs_powers_exact(uint32_t (&B)[NB], uint32_t (&A)[NA > 1 ? NA - 1 : 1]) {
+#pragma unroll
+    for (int b = 1; b < NB; ++b) B[b] = mulfold32_exact(B[b - 1], B[0]);
+    if constexpr (NA > 1) {
+        A[0] = B[NB - 1];
+#pragma unroll
+        for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_exact(A[a - 1], A[0]);
+    }
+}
+
+template <int NB, int NA>
+__device__ __forceinline__ void bsgs_accumulate(BsgsAcc<NB, NA> &S, const uint32_t (&B)[NB],
+                                                const uint32_t (&A)[NA > 1 ? NA - 1 : 1]) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) S.a0[b] += B[b];
+#pragma unroll
+    for (int a = 0; a < NA - 1; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) mac_carry(S.m[a][b], S.c[a][b], A[a], B[b]);
+}
+
+template <int NB, int NA>
+__device__ __forceinline__ void bsgs_one(BsgsAcc<NB, NA> &S, uint32_t id) {
+    uint32_t B[NB], A[NA > 1 ? NA - 1 : 1];
+    if (bsgs_powers<NB, NA>(id, B, A)) bsgs_powers_exact<NB, NA>(B, A);
+    bsgs_accumulate<NB, NA>(S, B, A);
+}
+
+template <int NB, int NA>
+__global__ __launch_bounds__(BLOCK) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids, uint64_t n,
+                                                           uint32_t head, uint32_t T,
+                                                           uint64_t *__restrict__ partials) {
+    __shared__ uint64_t sm[WAVES * NB * NA];
+    BsgsAcc<NB, NA> S;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        S.a0[b] = 0;
+#pragma unroll
+        for (int a = 0; a < NA - 1; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; }
+    }
+    const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t body = (n - h) >> 2;
+    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
+    for (uint64_t i = gtid; i < body; i += nthr) {
+        const uint4 w = v[i];
+        const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t B[NB], A[NA > 1 ? NA - 1 : 1];
+            const uint32_t wrapped = bsgs_powers<NB, NA>(wv[c], B, A);
+            if (__builtin_expect(__any(wrapped), 0)) {
+                if (wrapped) bsgs_powers_exact<NB, NA>(B, A);
+            }
+            bsgs_accumulate<NB, NA>(S, B, A);
+        }
+    }
+    const uint64_t tail0 = h + (body << 2);
+    if (gtid < h) bsgs_one<NB, NA>(S, ids[gtid]);
+    if (gtid < n - tail0) bsgs_one<NB, NA>(S, ids[tail0 + gtid]);
+
+    // lane partials -> wave butterfly -> LDS -> one partial per (power, block)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            uint64_t x;
+            if (a == 0) x = fold64_32(S.a0[b]);
+            else // m + c*2^64, 2^64 == 25 (mod p); c*25 < 2^37
+                x = (uint64_t)fold64_32(S.m[a - 1][b]) + fold64_32((uint64_t)S.c[a - 1][b] * 25u);
+            x = fold64_32(x);                                  // < 2^32
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) x += shfl_xor_u64(x, off); // < 2^38
+            if (lane == 0) sm[wave * (NB * NA) + a * NB + b] = x;
+        }
+    }
+    __syncthreads();
+    for (uint32_t m = threadIdx.x; m < T; m += BLOCK) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) s += sm[w * (NB * NA) + m];
+        partials[(size_t)m * gridDim.x + blockIdx.x] = s;
+    }
+}
+
 // lane j of a G-group: start = x^(j+1), step = x^G (square-and-multiply).
 template <int G>
 __device__ __forceinline__ void group_powers32(uint32_t x, int j, uint32_t &start, uint32_t &step) {
@@ -459,6 +584,20 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const uintptr_t a = (uintptr_t)ids;
     if (a & 3) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 4);
+    // baby-step / giant-step for 9 <= T <= 32 (fewer modmuls per id); the
+    // power chain otherwise
+    if (T >= 9 && T <= 12)
+        return run_encode<uint32_t>(ctx, k_encode_u32_bsgs<4, 3>, k_finalize_u32, 12, 1, ids, n, head, T,
+                                    (n + 3) / 4, BLOCK, out, acc, s);
+    if (T >= 13 && T <= 16)
+        return run_encode<uint32_t>(ctx, k_encode_u32_bsgs<4, 4>, k_finalize_u32, 16, 1, ids, n, head, T,
+                                    (n + 3) / 4, BLOCK, out, acc, s);
+    if (T >= 17 && T <= 24)
+        return run_encode<uint32_t>(ctx, k_encode_u32_bsgs<6, 4>, k_finalize_u32, 24, 1, ids, n, head, T,
+                                    (n + 3) / 4, BLOCK, out, acc, s);
+    if (T >= 25 && T <= 32)
+        return run_encode<uint32_t>(ctx, k_encode_u32_bsgs<8, 4>, k_finalize_u32, 32, 1, ids, n, head, T,
+                                    (n + 3) / 4, BLOCK, out, acc, s);
     int G, K;
     choose_gk(T, 32, K32_G1, 10, K32_GN, 4, G, K);
     switch (G) {

@@ -74,6 +74,31 @@ QK_HD uint64_t tstep32p(uint64_t t, uint32_t x, uint32_t x5, uint32_t c) {
     const uint64_t Q = P + (uint64_t)Ph * C32;
     return Q - ((uint64_t)Ph << 32);
 }
+// 32-bit lazy product for the baby-step/giant-step encode: y, x < 2^32 ->
+// r < 2^32, r == y*x (mod p), except when t_lo + 5 t_hi wraps 2^32 (prob.
+// <= 25/2^32 per call), which is reported through `wrapped` instead of being
+// fixed inline; callers redo the (rare) id with mulfold32_exact.
+QK_HD uint32_t mulfold32_fast(uint32_t y, uint32_t x, uint32_t &wrapped) {
+    const uint64_t P = (uint64_t)y * x;
+    const uint32_t Ph = (uint32_t)(P >> 32);
+    const uint64_t Q = P + (uint64_t)Ph * C32;
+    const uint32_t tl = (uint32_t)Q, th = (uint32_t)(Q >> 32) - Ph;  // t = tl + th*2^32, th <= 5
+    const uint32_t m = th * C32;
+    const uint32_t r = tl + m;
+    wrapped |= (r < m);
+    return r;
+}
+QK_HD uint32_t mulfold32_exact(uint32_t y, uint32_t x) {
+    const uint64_t P = (uint64_t)y * x;
+    const uint32_t Ph = (uint32_t)(P >> 32);
+    const uint64_t Q = P + (uint64_t)Ph * C32;
+    const uint32_t tl = (uint32_t)Q, th = (uint32_t)(Q >> 32) - Ph;
+    const uint32_t m = th * C32;
+    uint32_t r = tl + m;
+    if (r < m) r += C32;  // wrapped past 2^32 == 5 (mod p); then r < 25, no second wrap
+    return r;
+}
+
 // 5x mod p for canonical x (x5 in the step above)
 QK_HD uint32_t times5_32(uint32_t x) {
     const uint64_t v = (uint64_t)x * C32;                   // < 5*2^32

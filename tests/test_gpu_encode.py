@@ -231,3 +231,23 @@ def test_full_size_u64_properties():
     assert gpu_state(d[:200_000], t, 64).power_sums() == coracle.encode_u64_seed(seed, 200_000, t)
     del d
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("t", [9, 12, 13, 16, 17, 20, 24, 25, 31, 32])
+def test_bsgs_rare_wrap_branch(golden, t):
+    """Ids whose lazy folds wrap (prob ~2.6e-8 per id) force the exact
+    recompute branch of the baby-step/giant-step kernel: alone in a wave,
+    several in one wave, and in the unaligned head/tail (scalar path)."""
+    cfg = "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4"
+    wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
+    ids = coracle.splitmix_u32(0xF00D + t, 20_003)
+    ids[100] = wraps[0]                      # one lane of one wave
+    ids[4096:4096 + 4] = wraps[:4]           # four chains of one lane
+    ids[5000:5000 + 64 * 4:64] = wraps[:4]   # several lanes of one wave
+    ids[-1] = wraps[-1]                      # tail (scalar path)
+    d = dev_u32(ids)
+    for off in (0, 1, 3):                    # head (scalar path) at off 1, 3
+        sub = ids[off:]
+        assert gpu_state(d[off:], t).power_sums() == coracle.encode_u32(sub, t), (t, off)
+    only = dev_u32(np.tile(wraps, 11))
+    assert gpu_state(only, t).power_sums() == coracle.encode_u32(np.tile(wraps, 11), t)

@@ -28,6 +28,11 @@ for s in $STEPS; do
     prof)
       export TMPDIR=/tmp
       step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 1 --cpu-sample 0 || exit 3 ;;
+    tune) step tune 600 ./tools/tune_encode ${TUNE_ARGS:-} || exit 3 ;;
+    listctr) step listctr 120 rocprofv3 -L || true ;;
+    pmcsq)
+      export TMPDIR=/tmp
+      step pmcsq 600 rocprofv3 --pmc ${PMC_SQ:-SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE} --output-format csv -d "$OUT/pmcsq" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
