@@ -58,12 +58,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=float, default=1e9, help="ids per GPU")
+    ap.add_argument("--ids-per-gpu", type=float, default=1e9, help="ids per GPU (weak scaling)")
     ap.add_argument("--t", type=int, default=32)
     ap.add_argument("--bits", type=int, default=32, choices=(32, 64))
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     ap.add_argument("--cpu-sample", type=float, default=1e8, help="ids for the CPU baseline (0 disables)")
     ap.add_argument("--grid", type=int, default=0, help="override workgroups per launch")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
 
     import numpy as np
@@ -79,29 +81,38 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    dev_index = local % ndev  # == local on a real node (one process per GPU)
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
 
-    n = int(args.n)
+    n = int(args.ids_per_gpu)
     t, bits = args.t, args.bits
     n_total = n * world
     start, cnt = skd.shard(n_total, rank, world)
-    ctx = sk.get_context(local)
+    ctx = sk.get_context(dev_index)
     if args.grid:
         ctx.set_grid(args.grid)
-    stream = torch.cuda.current_stream(local)
 
     idt = torch.int32 if bits == 32 else torch.int64
-    ids = torch.empty(cnt, dtype=idt, device=f"cuda:{local}")
+    ids = torch.empty(cnt, dtype=idt, device=f"cuda:{dev_index}")
     fill_splitmix(ctx, ids, args.seed, start, bits=bits)
-    partial = torch.zeros(partial_words(t, bits), dtype=torch.int64, device=f"cuda:{local}")
+    partial = torch.zeros(partial_words(t, bits), dtype=torch.int64, device=f"cuda:{dev_index}")
     torch.cuda.synchronize()
 
     def step():
         encode_device_async(ctx, ids, t, partial, bits=bits)
         if world > 1:
-            skd.reduce_partial_(partial, t, bits, dst=0)
+            if args.dist_backend == "nccl":
+                skd.reduce_partial_(partial, t, bits, dst=0)      # one RCCL reduce of t+1 words
+            else:
+                host = partial.cpu()                              # rehearsal only (gloo is CPU)
+                skd.reduce_partial_(host, t, bits, dst=0)
+                partial.copy_(host)
 
     for _ in range(args.warmup):
         step()
@@ -123,7 +134,8 @@ def main():
     ctx.set_profiling(False)
     kern_ms, launches = ctx.kernel_stats()
     if world > 1:
-        el = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        el = torch.tensor([elapsed], dtype=torch.float64,
+                          device=f"cuda:{dev_index}" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -134,6 +146,8 @@ def main():
     if rank == 0:
         S, count = skd.fold_partial_sum(part_host, t, bits)
         log(f"encode result: count={count} S[0..3]={S[:3]}")
+        import hashlib
+        digest = hashlib.sha256((",".join(str(v) for v in S) + f"|{count}").encode()).hexdigest()[:16]
 
     if rank != 0:
         if world > 1:
@@ -180,6 +194,8 @@ def main():
             "int_valu_view": {"modmuls_per_s": modmul_rate, "ids_per_s_per_gpu": cnt / (kern_avg_ms * 1e-3)},
         },
         "cpu_baseline": None,
+        "result": {"count": count, "power_sums_head": S[:4], "digest": digest,
+                   "note": "sha256 of the folded power sums of the whole global stream (identical for any N)"},
     }
 
     if world == 1 and args.cpu_sample > 0:

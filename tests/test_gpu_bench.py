@@ -1,0 +1,45 @@
+"""bench.py end to end on the GPU: the JSON contract, and the sharded N-rank
+path (contiguous shards + one sum-reduce) giving the same folded power sums
+as one rank over the same global stream, and as the CPU oracle."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(cmd, timeout=600):
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_contract_and_sharded_parity():
+    n_total, seed, t = 40_000_000, 0x5EED0002, 32
+    one = run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--ids-per-gpu", str(n_total),
+               "--cpu-sample", "2e6"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in one
+    assert one["n_gpus"] == 1 and one["steps"] == 3 and one["value"] > 0
+    rf = one["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    cb = one["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["parity_with_gpu"] is True
+    want = coracle.encode_u32_seed(seed, n_total, t)
+    assert one["result"]["power_sums_head"] == want[:4] and one["result"]["count"] == n_total
+
+    two = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", "29561", "bench.py", "--gpus", "2", "--steps", "3",
+               "--warmup", "1", "--ids-per-gpu", str(n_total // 2), "--dist-backend", "gloo"])
+    assert two["n_gpus"] == 2 and two["cpu_baseline"] is None
+    assert two["result"]["digest"] == one["result"]["digest"]
+    assert two["result"]["count"] == n_total
