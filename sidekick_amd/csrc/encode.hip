@@ -78,13 +78,46 @@ __device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
 // lazy modmuls per id, then (NA-1)*NB 32x32->64 multiply-accumulates into
 // 64-bit accumulators whose wraps are counted (2^64 == 25 mod p), plus NB
 // plain adds for the a = 0 row.
-// One MAC = v_mad_u64_u32 with its carry-out in VCC + v_addc_co_u32 of that
-// carry into a 32-bit wrap counter.
-__device__ __forceinline__ void mac_carry(uint64_t &acc, uint32_t &cnt, uint32_t a, uint32_t b) {
-    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
-        : "+v"(acc), "+v"(cnt)
-        : "v"(a), "v"(b)
-        : "vcc");
+// MACs: v_mad_u64_u32 acc += A*B with the carry-out in an SGPR pair, then
+// v_addc_co_u32 adds that carry into a 32-bit wrap counter.  gfx950 needs two
+// wait states between a VALU SGPR/VCC write and a VALU carry-in read of it
+// (hipcc pads the same pattern with s_nop), so MACs are issued in groups of
+// four with four distinct carry pairs: each v_addc is >= 3 VALU instructions
+// after the v_mad_u64_u32 whose carry it reads.
+__device__ __forceinline__ void mac4(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t &c0,
+                                     uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t A, uint32_t b0,
+                                     uint32_t b1, uint32_t b2, uint32_t b3) {
+    uint64_t k0, k1, k2, k3;
+    asm("v_mad_u64_u32 %0, %8, %12, %13, %0\n\t"
+        "v_mad_u64_u32 %1, %9, %12, %14, %1\n\t"
+        "v_mad_u64_u32 %2, %10, %12, %15, %2\n\t"
+        "v_mad_u64_u32 %3, %11, %12, %16, %3\n\t"
+        "v_addc_co_u32_e64 %4, %8, %4, 0, %8\n\t"
+        "v_addc_co_u32_e64 %5, %9, %5, 0, %9\n\t"
+        "v_addc_co_u32_e64 %6, %10, %6, 0, %10\n\t"
+        "v_addc_co_u32_e64 %7, %11, %7, 0, %11"
+        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "=&s"(k0),
+          "=&s"(k1), "=&s"(k2), "=&s"(k3)
+        : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
+}
+__device__ __forceinline__ void mac2(uint64_t &a0, uint64_t &a1, uint32_t &c0, uint32_t &c1, uint32_t A,
+                                     uint32_t b0, uint32_t b1) {
+    uint64_t k0, k1;
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %6, %8, %1\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
+        : "+v"(a0), "+v"(a1), "+v"(c0), "+v"(c1), "=&s"(k0), "=&s"(k1)
+        : "v"(A), "v"(b0), "v"(b1));
+}
+__device__ __forceinline__ void mac1(uint64_t &acc, uint32_t &cnt, uint32_t A, uint32_t b) {
+    uint64_t k;
+    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
+        "s_nop 1\n\t"
+        "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
+        : "+v"(acc), "+v"(cnt), "=&s"(k)
+        : "v"(A), "v"(b));
 }
 
 template <int NB, int NA>
@@ -126,9 +159,16 @@ __device__ __forceinline__ void bsgs_accumulate(BsgsAcc<NB, NA> &S, const uint32
 #pragma unroll
     for (int b = 0; b < NB; ++b) S.a0[b] += B[b];
 #pragma unroll
-    for (int a = 0; a < NA - 1; ++a)
+    for (int a = 0; a < NA - 1; ++a) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) mac_carry(S.m[a][b], S.c[a][b], A[a], B[b]);
+        for (int b = 0; b + 4 <= NB; b += 4)
+            mac4(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.c[a][b], S.c[a][b + 1], S.c[a][b + 2],
+                 S.c[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
+        if constexpr (NB % 4 >= 2)
+            mac2(S.m[a][NB / 4 * 4], S.m[a][NB / 4 * 4 + 1], S.c[a][NB / 4 * 4], S.c[a][NB / 4 * 4 + 1], A[a],
+                 B[NB / 4 * 4], B[NB / 4 * 4 + 1]);
+        if constexpr (NB % 2 == 1) mac1(S.m[a][NB - 1], S.c[a][NB - 1], A[a], B[NB - 1]);
+    }
 }
 
 template <int NB, int NA>
@@ -139,7 +179,7 @@ __device__ __forceinline__ void bsgs_one(BsgsAcc<NB, NA> &S, uint32_t id) {
 }
 
 template <int NB, int NA>
-__global__ __launch_bounds__(BLOCK) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids, uint64_t n,
+__global__ __launch_bounds__(BLOCK, NB * NA >= 24 ? 3 : 1) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids, uint64_t n,
                                                            uint32_t head, uint32_t T,
                                                            uint64_t *__restrict__ partials) {
     __shared__ uint64_t sm[WAVES * NB * NA];
@@ -155,8 +195,17 @@ __global__ __launch_bounds__(BLOCK) void k_encode_u32_bsgs(const uint32_t *__res
     const uint64_t h = head < n ? head : n;
     const uint64_t body = (n - h) >> 2;
     const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
-    for (uint64_t i = gtid; i < body; i += nthr) {
-        const uint4 w = v[i];
+    // Per-lane trip count + pointer walk (no 64-bit index compare in the
+    // loop); the next 16-byte load is issued before this iteration's
+    // arithmetic (3 waves/SIMD at this register count cannot hide it).
+    // The host guarantees body / nthr < 2^32.
+    const uint32_t iters = gtid < body ? (uint32_t)((body - gtid + nthr - 1) / nthr) : 0u;
+    const uint4 *__restrict__ p = v + gtid;
+    uint4 nxt = iters ? *p : make_uint4(0, 0, 0, 0);
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint4 w = nxt;
+        p += nthr;
+        if (it + 1 < iters) nxt = *p;
         const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -584,6 +633,7 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const uintptr_t a = (uintptr_t)ids;
     if (a & 3) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 4);
+    if (n >= (1ull << 40)) return QK_E_INVAL; // 4 TB of ids: beyond any HBM; keeps per-lane trip counts 32-bit
     // baby-step / giant-step for 9 <= T <= 32 (fewer modmuls per id); the
     // power chain otherwise
     if (T >= 9 && T <= 12)

@@ -197,7 +197,37 @@ __device__ __forceinline__ void mac_vcc(uint64_t &acc, uint32_t &cnt, uint32_t a
         : "+v"(acc), "+v"(cnt) : "v"(a), "v"(b) : "vcc");
 }
 
-template <int MINW, int CHN, int MAC = 0>
+__device__ __forceinline__ void mac_vcc_nop(uint64_t &acc, uint32_t &cnt, uint32_t a, uint32_t b) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(cnt) : "v"(a), "v"(b) : "vcc");
+}
+__device__ __forceinline__ void add_vcc(uint64_t &acc, uint32_t b) {
+    uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+    asm("v_add_co_u32_e32 %0, vcc, %0, %2\n\ts_nop 1\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(lo), "+v"(hi) : "v"(b) : "vcc");
+    acc = ((uint64_t)hi << 32) | lo;
+}
+
+// 4 MACs sharing A, carries in 4 distinct SGPR pairs: every v_addc reads a
+// carry written >= 3 VALU instructions earlier (>= 2 wait states, no s_nop).
+__device__ __forceinline__ void mac4(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t &c0,
+                                     uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t A, uint32_t b0,
+                                     uint32_t b1, uint32_t b2, uint32_t b3) {
+    uint64_t k0, k1, k2, k3;
+    asm("v_mad_u64_u32 %0, %8, %12, %13, %0\n\t"
+        "v_mad_u64_u32 %1, %9, %12, %14, %1\n\t"
+        "v_mad_u64_u32 %2, %10, %12, %15, %2\n\t"
+        "v_mad_u64_u32 %3, %11, %12, %16, %3\n\t"
+        "v_addc_co_u32_e64 %4, %8, %4, 0, %8\n\t"
+        "v_addc_co_u32_e64 %5, %9, %5, 0, %9\n\t"
+        "v_addc_co_u32_e64 %6, %10, %6, 0, %10\n\t"
+        "v_addc_co_u32_e64 %7, %11, %7, 0, %11"
+        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3),
+          "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3)
+        : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
+}
+
+template <int MINW, int CHN, int MAC = 0, int PF = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void k_bsgs2(const uint32_t *__restrict__ ids, uint64_t n,
                                                       uint64_t *__restrict__ partials) {
     __shared__ uint64_t sm[BLOCK / 64][T];
@@ -216,9 +246,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void k_bsgs2(const uint32_t *__restric
     const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     const uint64_t ng = (uint64_t)gridDim.x * BLOCK;
     const uint64_t units = n / CHN;
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (PF && g < units) nxt = reinterpret_cast<const uint4 *>(ids)[g];
     for (uint64_t u = g; u < units; u += ng) {
         uint32_t w[CHN];
-        if constexpr (CHN == 4) {
+        if constexpr (CHN == 4 && PF) {
+            const uint4 v = nxt;
+            if (u + ng < units) nxt = reinterpret_cast<const uint4 *>(ids)[u + ng];
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else if constexpr (CHN == 4) {
             const uint4 v = reinterpret_cast<const uint4 *>(ids)[u];
             w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
         } else if constexpr (CHN == 2) {
@@ -246,12 +282,24 @@ __global__ __launch_bounds__(BLOCK, MINW) void k_bsgs2(const uint32_t *__restric
                 }
             }
 #pragma unroll
-            for (int b = 0; b < 8; ++b) acc0[b] += B[b];
+            for (int b = 0; b < 8; ++b) {
+                if constexpr (MAC == 4) add_vcc(acc0[b], B[b]);
+                else acc0[b] += B[b];
+            }
+            if constexpr (MAC == 5) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int b = 0; b < 8; b += 4)
+                        mac4(acc[a][b], acc[a][b + 1], acc[a][b + 2], acc[a][b + 3], cnt[a][b], cnt[a][b + 1],
+                             cnt[a][b + 2], cnt[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            } else
 #pragma unroll
             for (int a = 0; a < 3; ++a)
 #pragma unroll
                 for (int b = 0; b < 8; ++b) {
                     if constexpr (MAC == 0) mac_vcc(acc[a][b], cnt[a][b], A[a], B[b]);
+                    else if constexpr (MAC == 3 || MAC == 4) mac_vcc_nop(acc[a][b], cnt[a][b], A[a], B[b]);
                     else if constexpr (MAC == 1) mac_carry(acc[a][b], cnt[a][b], A[a], B[b]);
                     else {
                         // B = Bh*2^16 + Bl: A*Bl, A*Bh < 2^48, no carry for 2^16 ids per lane;
@@ -378,8 +426,8 @@ int main(int argc, char **argv) {
     CHK(hipDeviceSynchronize());
 
     std::vector<Var> vars = {
-        {"CH4_G1_W0", k_var<4, 1, 1>, 1}, {"BSGS2_C4", k_bsgs2<1, 4, 0>, 1}, {"BSGS3_SGPR_C4", k_bsgs2<1, 4, 1>, 1},
-        {"BSGS3_SGPR_C2", k_bsgs2<1, 2, 1>, 1}, {"BSGS4_SPLIT_C2", k_bsgs2<1, 2, 2>, 1}, {"BSGS4_SPLIT_C1", k_bsgs2<1, 1, 2>, 1},
+        {"BSGS2_C4", k_bsgs2<1, 4, 0>, 1}, {"BSGS2_C4_NOP", k_bsgs2<1, 4, 3>, 1}, {"BSGS_MAC4", k_bsgs2<1, 4, 5>, 1},
+        {"BSGS_PF", k_bsgs2<1, 4, 0, 1>, 1}, {"BSGS_MAC4_PF", k_bsgs2<1, 4, 5, 1>, 1}, {"BSGS_NOP_PF", k_bsgs2<1, 4, 3, 1>, 1},
     };
     uint32_t ref[T], got[T];
     std::vector<std::vector<float>> times(vars.size());
