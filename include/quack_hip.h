@@ -175,6 +175,39 @@ int qk_u32_encode_host(qk_ctx *ctx, const uint32_t *h_ids, size_t n, qk_u32 *q);
 int qk_u64_encode_host(qk_ctx *ctx, const uint64_t *h_ids, size_t n, qk_u64 *q);
 
 /* ------------------------------------------------------------------------
+ * Packet batches: identifier extraction fused in front of the encode
+ * (SURVEY.md §8f rank 2).  Replaces the sniff loop of sidekick.rs:76-124 for
+ * a batch of captured buffers: per packet, in order,
+ *   skip unless sll_pkttype is PACKET_HOST/PACKET_OTHERHOST      (:78-80)
+ *   skip unless sll_protocol == htons(ETH_P_IP)                    (:81-84)
+ *   skip unless buf[23] == IPPROTO_UDP      (buffer.rs:80-83)      (:85-88)
+ *   dst ip buf[30..34] == my_ipv4 -> reset the quACK               (:92-96)
+ *   skip unless the capture length == QK_BUFFER_SIZE               (:99-102)
+ *   insert the big-endian u32 at byte QK_ID_OFFSET (buffer.rs:99-106)
+ * Buffers are `stride`-byte records (the reference reads QK_BUFFER_SIZE = 67
+ * bytes per packet) in device memory; meta may be NULL (all packets incoming
+ * IPv4 of full length).  my_ipv4 may be NULL (no packet resets).
+ * ---------------------------------------------------------------------- */
+#define QK_ID_OFFSET 63u
+#define QK_BUFFER_SIZE 67u
+typedef struct qk_pkt_meta {
+    uint8_t pkttype;      /* sockaddr_ll.sll_pkttype */
+    uint8_t reserved;
+    uint16_t protocol_be; /* sockaddr_ll.sll_protocol (network byte order, as stored) */
+    uint32_t len;         /* bytes returned by recvfrom */
+} qk_pkt_meta;
+typedef struct qk_pkt_stats {
+    uint64_t inserted;    /* inserts that reached the final state (after the last reset) */
+    uint64_t discarded;   /* inserts wiped by a later reset in the same batch */
+    uint64_t resets;
+    uint64_t filtered;    /* packets skipped by the filters */
+    int64_t last_reset_index; /* -1 if no reset */
+} qk_pkt_stats;
+int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
+                                 const qk_pkt_meta *d_meta, const uint8_t my_ipv4[4], qk_u32 *q,
+                                 qk_pkt_stats *stats, void *stream);
+
+/* ------------------------------------------------------------------------
  * Decode-missing root test.  Replaces media_client.rs:306-313:
  *   for id in log { if arithmetic::eval(&coeffs, id).value() == 0 { hit } }
  * Hit positions (indices into the log) are returned ascending (log order);

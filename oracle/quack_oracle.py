@@ -246,3 +246,49 @@ def root_test_u32_np(coeffs, log: np.ndarray, chunk: int = 1 << 22) -> np.ndarra
         r = (r + cs[d - 1]) % p
         hits.append(np.nonzero(r == 0)[0].astype(np.int64) + s)
     return np.concatenate(hits) if hits else np.zeros(0, dtype=np.int64)
+
+
+# --------------------------------------------------------------------------
+# Sniff loop over a batch of captured packets (sidekick/src/sidekick.rs:76-124,
+# buffer.rs:6-7,80-106), applied literally, packet by packet.
+# --------------------------------------------------------------------------
+ID_OFFSET = 63
+BUFFER_SIZE = ID_OFFSET + 4
+PACKET_HOST, PACKET_OTHERHOST, PACKET_OUTGOING = 0, 3, 4
+ETH_P_IP_BE = 0x0008  # (libc::ETH_P_IP as u16).to_be() read as a little-endian u16
+IPPROTO_UDP = 17
+
+
+def sniff_batch(q: "OracleQuack", bufs, pkttype=None, protocol_be=None, lens=None, my_ipv4=None):
+    """Apply the sniff loop to records bufs[i] (uint8 rows).  Returns
+    (q, stats) where q may be a fresh sketch if a reset happened."""
+    stats = {"inserted": 0, "discarded": 0, "resets": 0, "filtered": 0, "last_reset_index": -1}
+    n = len(bufs)
+    for i in range(n):
+        buf = bufs[i]
+        pt = PACKET_HOST if pkttype is None else int(pkttype[i])
+        proto = ETH_P_IP_BE if protocol_be is None else int(protocol_be[i])
+        ln = BUFFER_SIZE if lens is None else int(lens[i])
+        if pt not in (PACKET_HOST, PACKET_OTHERHOST):      # :78-80
+            stats["filtered"] += 1
+            continue
+        if proto != ETH_P_IP_BE:                           # :81-84
+            stats["filtered"] += 1
+            continue
+        if int(buf[23]) != IPPROTO_UDP:                    # :85-88
+            stats["filtered"] += 1
+            continue
+        if my_ipv4 is not None and [int(b) for b in buf[30:34]] == list(my_ipv4):  # :92-96
+            stats["discarded"] += stats["inserted"]
+            stats["inserted"] = 0
+            stats["resets"] += 1
+            stats["last_reset_index"] = i
+            q = OracleQuack(q.threshold, q.bits)
+            continue
+        if ln != BUFFER_SIZE:                              # :99-102
+            stats["filtered"] += 1
+            continue
+        ident = int.from_bytes(bytes(int(b) for b in buf[ID_OFFSET:ID_OFFSET + 4]), "big")  # buffer.rs:99-106
+        q.insert(ident)
+        stats["inserted"] += 1
+    return q, stats

@@ -83,6 +83,7 @@ SIGNATURES = {
     "qk_u64_root_test_device": (C.c_int, [vp, u64p, C.c_uint32, vp, sz, C.c_int, C.c_uint64, u64p, sz, szp, vp]),
     "qk_u32_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
     "qk_u64_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
+    "qk_u32_encode_packets_device": (C.c_int, [vp, vp, sz, sz, vp, vp, vp, vp, vp]),
     "qk_fill_splitmix_u32": (C.c_int, [vp, vp, sz, C.c_uint64, C.c_uint64, vp]),
     "qk_fill_splitmix_u64": (C.c_int, [vp, vp, sz, C.c_uint64, C.c_uint64, vp]),
 }

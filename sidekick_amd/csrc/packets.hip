@@ -1,0 +1,253 @@
+// packets.hip — packet-batch identifier extraction fused in front of the
+// encode.
+//
+// Replaces, for a batch of captured packets, the per-packet sniff loop of
+// sidekick/src/sidekick.rs:76-124:
+//     if Direction::Incoming != addr.sll_pkttype.into() { continue }      (:78-80)
+//     if addr.sll_protocol != ETH_P_IP.to_be()          { continue }      (:81-84)
+//     if !UdpParser::is_udp(&buf)  /* buf[23] == 17 */  { continue }      (:85-88)
+//     if parse_dst_ip(&buf) == my_ipv4_addr { sc.reset(); continue }      (:92-96)
+//     if n != BUFFER_SIZE                               { continue }      (:99-102)
+//     sc.insert_packet(parse_identifier(&buf))  /* BE u32 at byte 63 */   (:103-115)
+// (buffer.rs:6-7,80-83,88-90,99-106).
+//
+// Pass 1 (k_pkt_extract): each workgroup owns a contiguous chunk of packets
+// and walks it in tiles of 256 records staged into LDS with coalesced 16-byte
+// loads (records are `stride` bytes, 67 in the reference, so a lane's fields
+// are unaligned).  Each lane classifies one record and writes its id (0 for a
+// skipped packet: x = 0 adds nothing to any power sum) to a compact u32
+// array, so pass 2 is the ordinary encode over that array from the last reset
+// on.  Per-chunk bookkeeping (last reset, inserts after it, last insert) is
+// combined on the host in chunk order.  The pass reads every record byte once:
+// it is HBM-bound (~67 B per packet), not VALU-bound.
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "ctx.h"
+#include "field.h"
+
+namespace qk {
+
+constexpr int PK_BLOCK = 256;
+constexpr uint32_t PK_UDP = 17;
+
+struct ChunkStat {       // per workgroup chunk, written by lane 0
+    int64_t last_reset;  // absolute packet index of the last reset in the chunk, -1 if none
+    int64_t last_insert; // absolute index of the last insert (after last_reset), -1 if none
+    uint64_t inserts;    // inserts after last_reset (all inserts if no reset)
+    uint64_t resets;     // resets in the chunk
+    uint64_t all_inserts; // inserts in the chunk, before or after resets
+};
+
+__device__ __forceinline__ uint8_t lds_byte(const uint8_t *t, uint32_t off) { return t[off]; }
+
+__global__ __launch_bounds__(PK_BLOCK) void k_pkt_extract(const uint8_t *__restrict__ bufs, uint64_t n,
+                                                          uint32_t stride, const qk_pkt_meta *__restrict__ meta,
+                                                          uint32_t my_ip_le, int check_reset, uint64_t chunk,
+                                                          uint32_t *__restrict__ ids_out, ChunkStat *stats) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    __shared__ int64_t s_reset[PK_BLOCK / 64], s_insert[PK_BLOCK / 64];
+    __shared__ uint64_t s_cnt[PK_BLOCK / 64], s_nres[PK_BLOCK / 64], s_nins[PK_BLOCK / 64];
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
+    const uintptr_t base_addr = (uintptr_t)bufs;
+    const uint64_t total_bytes = n * (uint64_t)stride;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+    // chunk-level state, kept by thread 0 while walking the tiles in order
+    int64_t blk_reset = -1;   // last reset seen so far
+    uint64_t blk_cnt = 0;     // inserts after blk_reset so far
+    int64_t blk_insert = -1;  // last insert after blk_reset
+    uint64_t blk_nres = 0, blk_nins = 0;
+
+    for (uint64_t p0 = c0; p0 < c1; p0 += PK_BLOCK) {
+        const uint64_t np = (c1 - p0) < PK_BLOCK ? (c1 - p0) : PK_BLOCK;
+        // byte range of this tile, widened to 16-byte alignment of the absolute address
+        const uint64_t b_lo = p0 * stride, b_hi = (p0 + np) * stride;
+        const uint64_t a_lo = ((base_addr + b_lo) & ~(uintptr_t)15) - base_addr;  // may be "negative" (wraps)
+        const uint64_t a_hi = ((base_addr + b_hi + 15) & ~(uintptr_t)15) - base_addr;
+        const uint32_t nvec = (uint32_t)((a_hi - a_lo) / 16);
+        __syncthreads(); // previous tile fully consumed
+        for (uint32_t v = threadIdx.x; v < nvec; v += PK_BLOCK) {
+            const uint64_t off = a_lo + 16ull * v;     // relative to bufs (mod 2^64)
+            // whole 16-byte vector inside [0, total_bytes)?  (off < total as unsigned also rejects
+            // the wrapped "negative" head)
+            if (off < total_bytes && off + 16 <= total_bytes) {
+                *reinterpret_cast<uint4 *>(tile + 16 * v) = *reinterpret_cast<const uint4 *>(bufs + off);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const uint64_t o = off + k;
+                    tile[16 * v + k] = o < total_bytes ? bufs[o] : 0;
+                }
+            }
+        }
+        __syncthreads();
+        // classify one record per lane
+        uint32_t cls = 0, id = 0; // 0 skip, 1 insert, 2 reset
+        const uint64_t pi = p0 + threadIdx.x;
+        if (threadIdx.x < np) {
+            const uint32_t r = (uint32_t)(b_lo - a_lo) + threadIdx.x * stride; // record offset in tile
+            qk_pkt_meta m;
+            if (meta) m = meta[pi];
+            else { m.pkttype = 0; m.protocol_be = 0x0008; m.len = (uint32_t)QK_BUFFER_SIZE; }
+            const bool incoming = m.pkttype == 0 || m.pkttype == 3;   // PACKET_HOST | PACKET_OTHERHOST
+            const bool ip = m.protocol_be == 0x0008;                   // ETH_P_IP (0x0800) in network order
+            const bool udp = lds_byte(tile, r + 23) == PK_UDP;
+            if (incoming && ip && udp) {
+                const uint32_t dst = (uint32_t)lds_byte(tile, r + 30) | ((uint32_t)lds_byte(tile, r + 31) << 8) |
+                                     ((uint32_t)lds_byte(tile, r + 32) << 16) | ((uint32_t)lds_byte(tile, r + 33) << 24);
+                if (check_reset && dst == my_ip_le) cls = 2;
+                else if (m.len == (uint32_t)QK_BUFFER_SIZE) {
+                    cls = 1;
+                    id = ((uint32_t)lds_byte(tile, r + QK_ID_OFFSET) << 24) |
+                         ((uint32_t)lds_byte(tile, r + QK_ID_OFFSET + 1) << 16) |
+                         ((uint32_t)lds_byte(tile, r + QK_ID_OFFSET + 2) << 8) |
+                         (uint32_t)lds_byte(tile, r + QK_ID_OFFSET + 3);
+                }
+            }
+            ids_out[pi] = cls == 1 ? id : 0u;
+        }
+        // tile bookkeeping: last reset in tile, inserts after it, last insert
+        const unsigned long long rmask = __ballot(cls == 2);
+        const unsigned long long imask = __ballot(cls == 1);
+        if (lane == 0) {
+            int64_t wr = -1, wi = -1;
+            uint64_t wc;
+            if (rmask) {
+                const int hb = 63 - __clzll(rmask);
+                wr = (int64_t)(p0 + wave * 64 + hb);
+                const unsigned long long after = hb == 63 ? 0ull : (imask & (~0ull << (hb + 1)));
+                wc = __popcll(after);
+            } else {
+                wc = __popcll(imask);
+            }
+            if (imask) wi = (int64_t)(p0 + wave * 64 + 63 - __clzll(imask));
+            s_reset[wave] = wr;
+            s_insert[wave] = wi;
+            s_cnt[wave] = wc;
+            s_nres[wave] = __popcll(rmask);
+            s_nins[wave] = __popcll(imask);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 0; w < PK_BLOCK / 64; ++w) { // waves in packet order
+                blk_nres += s_nres[w];
+                blk_nins += s_nins[w];
+                if (s_reset[w] >= 0) { blk_reset = s_reset[w]; blk_cnt = s_cnt[w]; blk_insert = -1; }
+                else blk_cnt += s_cnt[w];
+                if (s_insert[w] > blk_reset) blk_insert = s_insert[w] > blk_insert ? s_insert[w] : blk_insert;
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        ChunkStat st;
+        st.last_reset = blk_reset;
+        st.last_insert = blk_insert;
+        st.inserts = blk_cnt;
+        st.resets = blk_nres;
+        st.all_inserts = blk_nins;
+        stats[blockIdx.x] = st;
+    }
+}
+
+} // namespace qk
+
+using namespace qk;
+
+extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
+                                            const qk_pkt_meta *d_meta, const uint8_t my_ipv4[4], qk_u32 *q,
+                                            qk_pkt_stats *out_stats, void *stream) {
+    if (!ctx || !q || (n && !d_bufs)) return QK_E_INVAL;
+    if (stride < QK_BUFFER_SIZE || stride > 512) return QK_E_INVAL; // one LDS tile = 256 records
+    const uint32_t t = q->threshold;
+    if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    qk_pkt_stats st = {0, 0, 0, 0, -1};
+    if (n == 0) {
+        if (out_stats) *out_stats = st;
+        return QK_OK;
+    }
+    if (!is_device_ptr(d_bufs) || (d_meta && !is_device_ptr(d_meta))) return QK_E_INVAL;
+    const uint32_t my_ip_le = my_ipv4 ? ((uint32_t)my_ipv4[0] | ((uint32_t)my_ipv4[1] << 8) |
+                                         ((uint32_t)my_ipv4[2] << 16) | ((uint32_t)my_ipv4[3] << 24))
+                                      : 0u;
+    const int check_reset = my_ipv4 != nullptr; // no own address given: nothing resets
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = pick_stream(ctx, stream);
+
+    // chunking: >= 4 tiles per workgroup, enough workgroups to cover the chip
+    const uint64_t tiles = (n + PK_BLOCK - 1) / PK_BLOCK;
+    uint64_t tiles_per_chunk = std::max<uint64_t>(4, (tiles + (uint64_t)ctx->num_cus * 4 - 1) / ((uint64_t)ctx->num_cus * 4));
+    const uint64_t chunk = tiles_per_chunk * PK_BLOCK;
+    const uint32_t nchunks = (uint32_t)((n + chunk - 1) / chunk);
+
+    // device scratch: compact ids (n u32) + chunk stats
+    uint32_t *d_ids = nullptr;
+    ChunkStat *d_stats = nullptr;
+    if (hipMallocAsync((void **)&d_ids, n * sizeof(uint32_t), s) != hipSuccess) return QK_E_NOMEM;
+    if (hipMallocAsync((void **)&d_stats, nchunks * sizeof(ChunkStat), s) != hipSuccess) {
+        (void)hipFreeAsync(d_ids, s);
+        return QK_E_NOMEM;
+    }
+    const size_t lds = (size_t)PK_BLOCK * stride + 32;
+    hipLaunchKernelGGL(k_pkt_extract, dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs, (uint64_t)n, (uint32_t)stride,
+                       d_meta, my_ip_le, check_reset, chunk, d_ids, d_stats);
+    int rc = QK_OK;
+    if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+    std::vector<ChunkStat> hs(nchunks);
+    if (!rc && hipMemcpyAsync(hs.data(), d_stats, nchunks * sizeof(ChunkStat), hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = QK_E_HIP;
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = QK_E_HIP;
+    if (!rc) {
+        // combine chunks in packet order: the state after the last reset wins
+        int64_t last_reset = -1, last_insert = -1;
+        uint64_t inserts = 0, resets = 0, all_inserts = 0;
+        for (const ChunkStat &c : hs) {
+            resets += c.resets;
+            all_inserts += c.all_inserts;
+            if (c.last_reset >= 0) { last_reset = c.last_reset; inserts = c.inserts; last_insert = -1; }
+            else inserts += c.inserts;
+            if (c.last_insert > last_reset && c.last_insert > last_insert) last_insert = c.last_insert;
+        }
+        st.resets = resets;
+        st.last_reset_index = last_reset;
+        st.inserted = inserts;
+        st.discarded = all_inserts - inserts;
+        // encode ids after the last reset (skipped packets are 0 and add nothing)
+        const uint64_t from = (uint64_t)(last_reset + 1);
+        qk_u32 *tmp = (qk_u32 *)malloc(qk_u32_size(t));
+        if (!tmp) rc = QK_E_NOMEM;
+        else {
+            qk_u32_init(tmp, t);
+            if (from < n) rc = launch_encode_u32(ctx, d_ids + from, n - from, t, ctx->d_small, s);
+            if (!rc && from < n) {
+                const size_t w = qk_u32_partial_words(t);
+                if (hipMemcpyAsync(ctx->h_small, ctx->d_small, w * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess)
+                    rc = QK_E_HIP;
+                else {
+                    ctx->h_small[t] = inserts; // count = inserts, not array length
+                    uint32_t last_id = 0;
+                    if (last_insert >= 0 &&
+                        hipMemcpy(&last_id, d_ids + last_insert, 4, hipMemcpyDeviceToHost) != hipSuccess)
+                        rc = QK_E_HIP;
+                    if (!rc) rc = qk_u32_merge_partial(tmp, ctx->h_small, last_insert >= 0, last_id);
+                }
+            }
+            if (!rc) {
+                if (last_reset >= 0) qk_u32_init(q, t); // Sidekick::reset (sidekick.rs:47-50)
+                rc = qk_u32_merge(q, tmp);
+            }
+            free(tmp);
+        }
+    }
+    (void)hipFreeAsync(d_ids, s);
+    (void)hipFreeAsync(d_stats, s);
+    (void)hipStreamSynchronize(s);
+    st.filtered = n - st.inserted - st.discarded - st.resets;
+    if (out_stats) *out_stats = st;
+    return rc;
+}

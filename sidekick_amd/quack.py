@@ -359,6 +359,40 @@ class PowerSumQuackU64(_PowerSumQuack):
 # --------------------------------------------------------------------------
 # Low-level async encode (bench / multi-GPU): partial vectors on the device
 # --------------------------------------------------------------------------
+class PktMeta(C.Structure):
+    _fields_ = [("pkttype", C.c_uint8), ("reserved", C.c_uint8), ("protocol_be", C.c_uint16), ("len", C.c_uint32)]
+
+
+class PktStats(C.Structure):
+    _fields_ = [("inserted", C.c_uint64), ("discarded", C.c_uint64), ("resets", C.c_uint64),
+                ("filtered", C.c_uint64), ("last_reset_index", C.c_int64)]
+
+
+def encode_packets(q: "PowerSumQuackU32", bufs, stride: int = 67, meta=None, my_ipv4=None,
+                   ctx: Context | None = None) -> dict:
+    """Sniff-loop batch (sidekick.rs:76-124) on the GPU: `bufs` is a CUDA
+    uint8 tensor of n*stride bytes (records), `meta` an optional CUDA tensor
+    of n 8-byte qk_pkt_meta records (int64 view), `my_ipv4` 4 ints or None.
+    Updates q in place (reset if a packet to my_ipv4 is seen); returns stats."""
+    import torch
+    if not (isinstance(bufs, torch.Tensor) and bufs.is_cuda and bufs.dtype == torch.uint8 and bufs.is_contiguous()):
+        raise TypeError("bufs must be a contiguous CUDA uint8 tensor")
+    n = bufs.numel() // stride
+    dev = bufs.device.index if bufs.device.index is not None else torch.cuda.current_device()
+    ctx = ctx or get_context(dev)
+    mptr = None
+    if meta is not None:
+        if not (meta.is_cuda and meta.is_contiguous() and meta.numel() * meta.element_size() == 8 * n):
+            raise ValueError("meta must be a contiguous CUDA tensor of n 8-byte records")
+        mptr = meta.data_ptr()
+    ip = (C.c_uint8 * 4)(*my_ipv4) if my_ipv4 is not None else None
+    st = PktStats()
+    check(lib().qk_u32_encode_packets_device(ctx.handle, bufs.data_ptr(), n, stride, mptr, ip, q._buf,
+                                              C.byref(st), torch.cuda.current_stream(dev).cuda_stream),
+          "encode_packets")
+    return {k: getattr(st, k) for k, _ in PktStats._fields_}
+
+
 def partial_words(threshold: int, bits: int = 32) -> int:
     return int(getattr(lib(), f"qk_u{bits}_partial_words")(threshold))
 

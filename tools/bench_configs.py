@@ -146,6 +146,34 @@ def run_host(args, ctx):
     emit({"config": "raw H2D copy, pinned (torch)", "GBps": 4 * n / (time.perf_counter() - t0) / 1e9})
 
 
+def run_packets(args, ctx):
+    """Sniff-loop batch: n 67-byte captured records in HBM -> quACK (t=32)."""
+    from sidekick_amd.quack import encode_packets
+    n, stride = int(args.npkts), 67
+    raw = torch.empty(n * stride, dtype=torch.uint8, device=DEV)
+    # synthetic records: random bytes, UDP at byte 23, foreign dst ip, no resets
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    raw.random_(0, 256, generator=g)
+    rec = raw.view(n, stride)
+    rec[:, 23] = 17
+    rec[:, 30] = 192
+    q = sk.PowerSumQuackU32(32)
+    encode_packets(q, raw, stride=stride, my_ipv4=(10, 0, 2, 1))   # warm
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(args.steps):
+        q = sk.PowerSumQuackU32(32)
+        t0 = time.perf_counter()
+        st = encode_packets(q, raw, stride=stride, my_ipv4=(10, 0, 2, 1))
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    tm = float(np.median(times))
+    emit({"config": "sniff-loop batch: 67-byte records in HBM -> extract + encode u32 t=32", "n_packets": n,
+          "packets_per_s": n / tm, "record_GBps": n * stride / tm / 1e9, "frac_hbm_8TBs": n * stride / tm / 8e12,
+          "inserted": st["inserted"], "seconds": tm})
+
+
 def run_sweep(args, ctx):
     n = int(args.nsweep)
     ids = torch.empty(n, dtype=torch.int32, device=DEV)
@@ -157,7 +185,8 @@ def run_sweep(args, ctx):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep"])
+    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "packets"])
+    ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--n64", type=float, default=1e9)
     ap.add_argument("--ndec", type=float, default=1e8)
@@ -169,7 +198,8 @@ def main():
     args = ap.parse_args()
     ctx = sk.get_context(0)
     for w in args.what:
-        {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep}[w](args, ctx)
+        {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep,
+         "packets": run_packets}[w](args, ctx)
         torch.cuda.empty_cache()
 
 
