@@ -208,6 +208,32 @@ int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, s
                                  qk_pkt_stats *stats, void *stream);
 
 /* ------------------------------------------------------------------------
+ * Segmented multi-flow encode: one quACK per flow.
+ * ---------------------------------------------------------------------- */
+/* AddrKey of sidekick_multi.rs:13 / buffer.rs:91-95:
+ * [src ip (4), src port (2), dst ip (4), dst port (2)], bytes as on the wire. */
+typedef struct qk_flow_key {
+    uint8_t addr[12];
+} qk_flow_key;
+/* SidekickMulti over a packet batch (sidekick_multi.rs:65-90,101-143): every
+ * Insert goes to its AddrKey's quACK (created on first use).  Output: the
+ * batch's flows in ascending key order, keys[i] and sketches record i
+ * (qk_u32_size(threshold) bytes each, ready for qk_u32_merge into the
+ * caller's table).  my_addr = own dst ip:port (6 bytes) or NULL.  A Reset
+ * packet (dst ip:port == my_addr) only clears an existing table entry with
+ * its own key, which can never hold inserts, so it changes no output; it is
+ * counted in stats.  cap < flows -> QK_E_CAPACITY with *n_flows set. */
+int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
+                               const qk_pkt_meta *d_meta, const uint8_t my_addr[6], uint32_t threshold,
+                               qk_flow_key *keys, uint8_t *sketches, size_t cap, size_t *n_flows,
+                               qk_pkt_stats *stats, void *stream);
+/* The segmented primitive: ids already grouped by flow (device array,
+ * segment g = [offsets[g], offsets[g+1]), host offsets, stream order within a
+ * segment) -> nseg sketches (qk_u32_size(threshold) bytes each). */
+int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *offsets, size_t nseg,
+                                  uint32_t threshold, uint8_t *sketches, void *stream);
+
+/* ------------------------------------------------------------------------
  * Decode-missing root test.  Replaces media_client.rs:306-313:
  *   for id in log { if arithmetic::eval(&coeffs, id).value() == 0 { hit } }
  * Hit positions (indices into the log) are returned ascending (log order);

@@ -292,3 +292,36 @@ def sniff_batch(q: "OracleQuack", bufs, pkttype=None, protocol_be=None, lens=Non
         q.insert(ident)
         stats["inserted"] += 1
     return q, stats
+
+
+def addr_key(buf) -> bytes:
+    """UdpParser::parse_addr_key (buffer.rs:91-95)."""
+    b = [int(v) for v in buf]
+    return bytes([b[26], b[27], b[28], b[29], b[34], b[35], b[30], b[31], b[32], b[33], b[36], b[37]])
+
+
+def sniff_multi_batch(table: dict, threshold: int, bufs, pkttype=None, protocol_be=None, lens=None, my_addr=None):
+    """SidekickMulti over a batch (sidekick_multi.rs:101-143 process_one_packet,
+    :65-90 insert, :59-63 reset), literally.  table: AddrKey -> OracleQuack."""
+    stats = {"inserted": 0, "resets": 0, "filtered": 0}
+    for i in range(len(bufs)):
+        buf = bufs[i]
+        pt = PACKET_HOST if pkttype is None else int(pkttype[i])
+        proto = ETH_P_IP_BE if protocol_be is None else int(protocol_be[i])
+        ln = BUFFER_SIZE if lens is None else int(lens[i])
+        if pt not in (PACKET_HOST, PACKET_OTHERHOST) or proto != ETH_P_IP_BE or int(buf[23]) != IPPROTO_UDP:
+            stats["filtered"] += 1
+            continue
+        key = addr_key(buf)
+        if my_addr is not None and list(key[6:12]) == list(my_addr):
+            stats["resets"] += 1
+            if key in table:
+                table[key] = OracleQuack(threshold)
+            continue
+        if ln != BUFFER_SIZE:
+            stats["filtered"] += 1
+            continue
+        ident = int.from_bytes(bytes(int(b) for b in buf[ID_OFFSET:ID_OFFSET + 4]), "big")
+        table.setdefault(key, OracleQuack(threshold)).insert(ident)
+        stats["inserted"] += 1
+    return table, stats

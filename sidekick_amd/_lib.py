@@ -84,6 +84,8 @@ SIGNATURES = {
     "qk_u32_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
     "qk_u64_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
     "qk_u32_encode_packets_device": (C.c_int, [vp, vp, sz, sz, vp, vp, vp, vp, vp]),
+    "qk_u32_encode_flows_device": (C.c_int, [vp, vp, sz, sz, vp, vp, C.c_uint32, vp, vp, sz, szp, vp, vp]),
+    "qk_u32_encode_segments_device": (C.c_int, [vp, vp, u64p, sz, C.c_uint32, vp, vp]),
     "qk_fill_splitmix_u32": (C.c_int, [vp, vp, sz, C.c_uint64, C.c_uint64, vp]),
     "qk_fill_splitmix_u64": (C.c_int, [vp, vp, sz, C.c_uint64, C.c_uint64, vp]),
 }

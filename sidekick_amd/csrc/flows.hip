@@ -1,0 +1,416 @@
+// flows.hip — segmented multi-flow encode.
+//
+// Replaces, for a batch, SidekickMulti's per-packet flow table
+// (sidekick/src/sidekick_multi.rs:36,65-90,101-143):
+//     match process_one_packet(n, &buf, &addr, my_addr) {
+//         Insert { addr_key, id } => senders.entry(addr_key).or_insert(new(t)).insert(id),
+//         Reset  { addr_key }     => if let Some(q) = senders.get_mut(&addr_key) { *q = new(t) },
+//         Skip => {} }
+// with AddrKey = [src ip(4), src port(2), dst ip(4), dst port(2)] = buf[26..30],
+// buf[34..36], buf[30..34], buf[36..38] (buffer.rs:91-95).  A Reset targets the
+// key of a packet whose dst ip:port IS the proxy's own address, and an Insert
+// needs dst ip:port != own address, so a reset can never hit a key that holds
+// inserts: within a batch resets are no-ops on the produced table (counted in
+// the stats).  The caller merges the batch table into its own with
+// qk_u32_merge, flow by flow.
+//
+// Device pipeline:
+//   1. k_flow_extract   LDS-staged records -> (key_hi = src ip:port, key_lo =
+//                       dst ip:port, id) per packet; filtered packets get an
+//                       out-of-range key and sort last.
+//   2. two stable radix sorts (hipCUB/rocPRIM, 49-bit keys: lo, then hi) ->
+//      packet order within each flow is preserved (last_value = last id).
+//   3. segment heads -> work items of <= 64 Ki ids per workgroup.
+//   4. k_seg_encode<G,K>  power chains per id, block reduction, one integer
+//      atomicAdd per (flow, power) per work item (order-independent, exact).
+// The CSR primitive qk_u32_encode_segments_device runs step 4 directly on
+// caller-grouped ids.
+#include <string.h>
+
+#include <algorithm>
+#include <hipcub/hipcub.hpp>
+#include <vector>
+
+#include "ctx.h"
+#include "field.h"
+#include "records.h"
+
+namespace qk {
+
+constexpr int SG_BLOCK = 256;
+constexpr int SG_WAVES = SG_BLOCK / 64;
+constexpr uint64_t KEY_INVALID = 1ull << 48; // above every 48-bit ip:port
+constexpr uint32_t SEG_CHUNK = 1u << 16;     // ids per work item
+
+struct SegItem {
+    uint32_t seg;
+    uint32_t pad;
+    uint64_t lo, hi; // [lo, hi) in the grouped id array
+};
+
+__device__ __forceinline__ uint64_t sg_shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = __shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// lane j of a G-group: start = x^(j+1), step = x^G (canonical)
+template <int G>
+__device__ __forceinline__ void sg_group_powers(uint32_t x, int j, uint32_t &start, uint32_t &step) {
+    uint32_t b = x, r = 1;
+    const uint32_t e = (uint32_t)j + 1;
+#pragma unroll
+    for (int bit = 0; (1 << bit) <= G; ++bit) {
+        const uint32_t rb = mul32_lazy(r, b);
+        r = ((e >> bit) & 1) ? rb : r;
+        if ((1 << bit) < G) b = mul32_lazy(b, b);
+    }
+    start = r;
+    step = canon32(b);
+}
+
+template <int G, int K>
+__global__ __launch_bounds__(SG_BLOCK) void k_seg_encode(const uint32_t *__restrict__ ids,
+                                                         const SegItem *__restrict__ items, uint32_t T,
+                                                         unsigned long long *__restrict__ acc_out) {
+    __shared__ uint64_t sm[SG_WAVES * G * K];
+    const SegItem it = items[blockIdx.x];
+    uint64_t acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0;
+    const int j = threadIdx.x % G;
+    for (uint64_t i = it.lo + threadIdx.x / G; i < it.hi; i += SG_BLOCK / G) {
+        const uint32_t x = canon32(ids[i]);
+        uint32_t start, step;
+        if constexpr (G == 1) { start = x; step = x; }
+        else sg_group_powers<G>(x, j, start, step);
+        const uint32_t step5 = times5_32(step);
+        uint64_t t = start;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc[k] += t;
+            if (k + 1 < K) t = tstep32p(t, step, step5, 0u);
+        }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uint64_t v = fold64_32(acc[k]);
+#pragma unroll
+        for (int off = 32; off >= G; off >>= 1) v += sg_shfl_xor_u64(v, off);
+        if (lane < G) sm[wave * (G * K) + lane + k * G] = v;
+    }
+    __syncthreads();
+    for (uint32_t m = threadIdx.x; m < T; m += SG_BLOCK) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int w = 0; w < SG_WAVES; ++w) s += sm[w * (G * K) + m];   // < 2^40
+        atomicAdd(&acc_out[(size_t)it.seg * T + m], (unsigned long long)fold64_32(s));
+    }
+}
+
+__global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
+                                                           uint32_t stride, const qk_pkt_meta *__restrict__ meta,
+                                                           uint64_t my_key_lo, uint64_t *__restrict__ key_hi,
+                                                           uint64_t *__restrict__ key_lo,
+                                                           uint32_t *__restrict__ ids,
+                                                           uint32_t *__restrict__ order,
+                                                           unsigned long long *__restrict__ counters) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    const uint64_t p0 = (uint64_t)blockIdx.x * REC_TILE;
+    const uint64_t np = n - p0 < (uint64_t)REC_TILE ? n - p0 : (uint64_t)REC_TILE;
+    const uint32_t r0 = stage_records(bufs, n, stride, p0, np, tile);
+    __syncthreads();
+    if (threadIdx.x >= np) return;
+    const uint64_t i = p0 + threadIdx.x;
+    const uint8_t *rec = tile + r0 + threadIdx.x * stride;
+    const qk_pkt_meta m = record_meta(meta, i);
+    uint64_t kh = KEY_INVALID, kl = KEY_INVALID;
+    uint32_t id = 0;
+    int cls = 0; // 0 skip, 1 insert, 2 reset
+    if (record_is_incoming_udp(m, rec)) {
+        // AddrKey, packed big-endian so numeric order == byte order
+        const uint64_t src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
+                             ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];
+        const uint64_t dst = ((uint64_t)rec[30] << 40) | ((uint64_t)rec[31] << 32) | ((uint64_t)rec[32] << 24) |
+                             ((uint64_t)rec[33] << 16) | ((uint64_t)rec[36] << 8) | (uint64_t)rec[37];
+        if (dst == my_key_lo) cls = 2;
+        else if (m.len == QK_BUFFER_SIZE) {
+            cls = 1;
+            kh = src;
+            kl = dst;
+            id = record_identifier(rec);
+        }
+    }
+    key_hi[i] = kh;
+    key_lo[i] = kl;
+    ids[i] = id;
+    order[i] = (uint32_t)i;
+    if (cls == 1) atomicAdd(&counters[0], 1ull);
+    if (cls == 2) atomicAdd(&counters[1], 1ull);
+}
+
+template <typename T, typename I>
+__global__ void k_gather(const T *__restrict__ src, const I *__restrict__ idx, T *__restrict__ dst, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[idx[i]];
+}
+
+__global__ void k_heads(const uint64_t *__restrict__ kh, const uint64_t *__restrict__ kl, uint64_t n,
+                        uint8_t *__restrict__ flag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        flag[i] = kh[i] != KEY_INVALID && (i == 0 || kh[i] != kh[i - 1] || kl[i] != kl[i - 1]);
+}
+
+// per segment: key and last id (segment end = next head or nvalid)
+__global__ void k_seg_info(const uint64_t *__restrict__ kh, const uint64_t *__restrict__ kl,
+                           const uint32_t *__restrict__ ids, const uint32_t *__restrict__ starts, uint32_t nseg,
+                           uint64_t nvalid, uint64_t *__restrict__ info) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const uint64_t b = starts[s], e = s + 1 < nseg ? starts[s + 1] : nvalid;
+    info[4 * s + 0] = kh[b];
+    info[4 * s + 1] = kl[b];
+    info[4 * s + 2] = e - b;
+    info[4 * s + 3] = ids[e - 1];
+}
+
+// (G, K) for a threshold: smallest G with ceil(T/G) <= 32, K = ceil(T/G) rounded to a supported size
+static void seg_choose(uint32_t T, int &G, int &K) {
+    G = 1;
+    while ((T + G - 1) / G > 32u) G *= 2;
+    const uint32_t kneed = (T + G - 1) / G;
+    static const int ks[] = {4, 8, 16, 20, 24, 32};
+    K = 32;
+    for (int k : ks)
+        if ((uint32_t)k >= kneed) { K = k; break; }
+}
+
+template <int G, int K>
+static int seg_launch_gk(const uint32_t *ids, const SegItem *items, uint32_t nitems, uint32_t T,
+                         unsigned long long *acc, hipStream_t s) {
+    hipLaunchKernelGGL((k_seg_encode<G, K>), dim3(nitems), dim3(SG_BLOCK), 0, s, ids, items, T, acc);
+    return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
+}
+
+template <int G>
+static int seg_launch_g(int K, const uint32_t *ids, const SegItem *items, uint32_t nitems, uint32_t T,
+                        unsigned long long *acc, hipStream_t s) {
+    switch (K) {
+    case 4: return seg_launch_gk<G, 4>(ids, items, nitems, T, acc, s);
+    case 8: return seg_launch_gk<G, 8>(ids, items, nitems, T, acc, s);
+    case 16: return seg_launch_gk<G, 16>(ids, items, nitems, T, acc, s);
+    case 20: return seg_launch_gk<G, 20>(ids, items, nitems, T, acc, s);
+    case 24: return seg_launch_gk<G, 24>(ids, items, nitems, T, acc, s);
+    default: return seg_launch_gk<G, 32>(ids, items, nitems, T, acc, s);
+    }
+}
+
+// Segmented encode of a grouped id array (CSR offsets on the host) into a
+// device accumulator [nseg][T] (u64, zeroed here).
+static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const std::vector<uint64_t> &offs, uint32_t T,
+                      unsigned long long *d_acc, hipStream_t s) {
+    const size_t nseg = offs.size() - 1;
+    std::vector<SegItem> items;
+    for (size_t g = 0; g < nseg; ++g)
+        for (uint64_t lo = offs[g]; lo < offs[g + 1]; lo += SEG_CHUNK)
+            items.push_back({(uint32_t)g, 0u, lo, std::min<uint64_t>(lo + SEG_CHUNK, offs[g + 1])});
+    QK_HIP_TRY(hipMemsetAsync(d_acc, 0, nseg * T * sizeof(uint64_t), s));
+    if (items.empty()) return QK_OK;
+    SegItem *d_items = nullptr;
+    QK_HIP_TRY(hipMallocAsync((void **)&d_items, items.size() * sizeof(SegItem), s));
+    int rc = QK_OK;
+    if (hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(SegItem), hipMemcpyHostToDevice, s) != hipSuccess)
+        rc = QK_E_HIP;
+    if (!rc) {
+        int G, K;
+        seg_choose(T, G, K);
+        const uint32_t ni = (uint32_t)items.size();
+        hipEvent_t e0 = prof_begin(ctx, s);
+        switch (G) {
+        case 1: rc = seg_launch_g<1>(K, d_ids, d_items, ni, T, d_acc, s); break;
+        case 2: rc = seg_launch_g<2>(K, d_ids, d_items, ni, T, d_acc, s); break;
+        case 4: rc = seg_launch_g<4>(K, d_ids, d_items, ni, T, d_acc, s); break;
+        case 8: rc = seg_launch_g<8>(K, d_ids, d_items, ni, T, d_acc, s); break;
+        case 16: rc = seg_launch_g<16>(K, d_ids, d_items, ni, T, d_acc, s); break;
+        case 32: rc = seg_launch_g<32>(K, d_ids, d_items, ni, T, d_acc, s); break;
+        default: rc = QK_E_THRESHOLD;
+        }
+        prof_end(ctx, s, e0);
+    }
+    // the host vector `items` must outlive the async copy
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = QK_E_HIP;
+    (void)hipFreeAsync(d_items, s);
+    return rc;
+}
+
+} // namespace qk
+
+using namespace qk;
+
+extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *offsets,
+                                             size_t nseg, uint32_t threshold, uint8_t *sketches, void *stream) {
+    if (!ctx || !offsets || (nseg && !sketches)) return QK_E_INVAL;
+    if (threshold == 0 || threshold > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if (nseg == 0) return QK_OK;
+    std::vector<uint64_t> offs(offsets, offsets + nseg + 1);
+    for (size_t g = 0; g < nseg; ++g)
+        if (offs[g + 1] < offs[g]) return QK_E_INVAL;
+    const uint64_t n = offs[nseg] - offs[0];
+    if (n && (!d_ids || !is_device_ptr(d_ids))) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = pick_stream(ctx, stream);
+    const uint32_t T = threshold;
+    unsigned long long *d_acc = nullptr;
+    QK_HIP_TRY(hipMallocAsync((void **)&d_acc, nseg * T * sizeof(uint64_t), s));
+    int rc = seg_encode(ctx, d_ids, offs, T, d_acc, s);
+    std::vector<uint64_t> acc(nseg * T);
+    std::vector<uint32_t> last(nseg, 0);
+    if (!rc && hipMemcpyAsync(acc.data(), d_acc, acc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = QK_E_HIP;
+    for (size_t i = 0; !rc && i < nseg; ++i)
+        if (offs[i + 1] > offs[i] &&
+            hipMemcpyAsync(&last[i], d_ids + offs[i + 1] - 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+            rc = QK_E_HIP;
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = QK_E_HIP;
+    (void)hipFreeAsync(d_acc, s);
+    (void)hipStreamSynchronize(s);
+    if (rc) return rc;
+    const size_t rec = qk_u32_size(T);
+    for (size_t i = 0; i < nseg; ++i) {
+        qk_u32 *q = (qk_u32 *)(sketches + i * rec);
+        qk_u32_init(q, T);
+        for (uint32_t m = 0; m < T; ++m) q->power_sums[m] = canon32(fold64_32(acc[i * T + m]));
+        q->count = (uint32_t)(offs[i + 1] - offs[i]);
+        if (offs[i + 1] > offs[i]) { q->has_last = 1; q->last_value = last[i]; }
+    }
+    return QK_OK;
+}
+
+extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
+                                          const qk_pkt_meta *d_meta, const uint8_t my_addr[6], uint32_t threshold,
+                                          qk_flow_key *keys, uint8_t *sketches, size_t cap, size_t *n_flows,
+                                          qk_pkt_stats *stats, void *stream) {
+    if (!ctx || !n_flows || (n && !d_bufs)) return QK_E_INVAL;
+    if (stride < QK_BUFFER_SIZE || stride > 512) return QK_E_INVAL;
+    if (threshold == 0 || threshold > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
+    if (n >= (1ull << 32)) return QK_E_INVAL; // packet indices are u32
+    *n_flows = 0;
+    qk_pkt_stats st = {0, 0, 0, 0, -1};
+    if (n == 0) {
+        if (stats) *stats = st;
+        return QK_OK;
+    }
+    if (!is_device_ptr(d_bufs) || (d_meta && !is_device_ptr(d_meta))) return QK_E_INVAL;
+    uint64_t my_key = ~0ull; // no own address: no packet is a reset
+    if (my_addr)
+        my_key = ((uint64_t)my_addr[0] << 40) | ((uint64_t)my_addr[1] << 32) | ((uint64_t)my_addr[2] << 24) |
+                 ((uint64_t)my_addr[3] << 16) | ((uint64_t)my_addr[4] << 8) | (uint64_t)my_addr[5];
+    std::lock_guard<std::mutex> g(ctx->mu);
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = pick_stream(ctx, stream);
+    const uint32_t T = threshold;
+
+    // device scratch: keys (2 x 2 x u64), ids (2 x u32), order (2 x u32), flags, heads, counters
+    uint64_t *kh = nullptr, *kl = nullptr, *kh2 = nullptr, *kl2 = nullptr;
+    uint32_t *ids = nullptr, *ids2 = nullptr, *ord = nullptr, *ord2 = nullptr, *heads = nullptr;
+    uint8_t *flag = nullptr;
+    unsigned long long *counters = nullptr, *acc = nullptr;
+    void *temp = nullptr;
+    uint64_t *info = nullptr;
+    int rc = QK_OK;
+    auto A = [&](void **p, size_t b) {
+        if (!rc && hipMallocAsync(p, b ? b : 8, s) != hipSuccess) rc = QK_E_NOMEM;
+    };
+    A((void **)&kh, n * 8); A((void **)&kl, n * 8); A((void **)&kh2, n * 8); A((void **)&kl2, n * 8);
+    A((void **)&ids, n * 4); A((void **)&ids2, n * 4); A((void **)&ord, n * 4); A((void **)&ord2, n * 4);
+    A((void **)&heads, n * 4); A((void **)&flag, n); A((void **)&counters, 4 * 8);
+    if (!rc && hipMemsetAsync(counters, 0, 4 * 8, s) != hipSuccess) rc = QK_E_HIP;
+    const uint32_t ntiles = (uint32_t)((n + REC_TILE - 1) / REC_TILE);
+    if (!rc) {
+        hipLaunchKernelGGL(k_flow_extract, dim3(ntiles), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s, d_bufs,
+                           (uint64_t)n, (uint32_t)stride, d_meta, my_key, kh, kl, ids, ord, counters);
+        if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+    }
+    // stable LSD sort: by dst ip:port, then by src ip:port (49-bit keys)
+    size_t tb1 = 0, tb2 = 0;
+    if (!rc && hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, kl, kl2, ord, ord2, (uint32_t)n, 0, 49, s) != hipSuccess)
+        rc = QK_E_HIP;
+    if (!rc && hipcub::DeviceSelect::Flagged(nullptr, tb2, hipcub::CountingInputIterator<uint32_t>(0), flag, heads,
+                                             (uint32_t *)(counters + 2), (int64_t)n, s) != hipSuccess)
+        rc = QK_E_HIP;
+    A(&temp, std::max(tb1, tb2));
+    const uint32_t gb = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 8);
+    if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb1, kl, kl2, ord, ord2, (uint32_t)n, 0, 49, s) != hipSuccess)
+        rc = QK_E_HIP;
+    if (!rc) hipLaunchKernelGGL((k_gather<uint64_t, uint32_t>), dim3(gb), dim3(256), 0, s, kh, ord2, kh2, (uint64_t)n);
+    if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb1, kh2, kh, ord2, ord, (uint32_t)n, 0, 49, s) != hipSuccess)
+        rc = QK_E_HIP;
+    // now kh = sorted key_hi, ord = final packet order; gather key_lo and ids
+    if (!rc) {
+        hipLaunchKernelGGL((k_gather<uint64_t, uint32_t>), dim3(gb), dim3(256), 0, s, kl, ord, kl2, (uint64_t)n);
+        hipLaunchKernelGGL((k_gather<uint32_t, uint32_t>), dim3(gb), dim3(256), 0, s, ids, ord, ids2, (uint64_t)n);
+        hipLaunchKernelGGL(k_heads, dim3(gb), dim3(256), 0, s, kh, kl2, (uint64_t)n, flag);
+        if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+    }
+    if (!rc && hipcub::DeviceSelect::Flagged(temp, tb2, hipcub::CountingInputIterator<uint32_t>(0), flag, heads,
+                                             (uint32_t *)(counters + 2), (int64_t)n, s) != hipSuccess)
+        rc = QK_E_HIP;
+    uint64_t hc[3] = {0, 0, 0};
+    if (!rc && (hipMemcpyAsync(hc, counters, 24, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess))
+        rc = QK_E_HIP;
+    const uint64_t inserted = hc[0], resets = hc[1];
+    const uint32_t nseg = (uint32_t)(hc[2] & 0xFFFFFFFFu);
+    if (!rc) {
+        st.inserted = inserted;
+        st.resets = resets;
+        st.filtered = n - inserted - resets;
+        *n_flows = nseg;
+        if (nseg > cap || (nseg && (!keys || !sketches))) rc = QK_E_CAPACITY;
+    }
+    if (!rc && nseg) {
+        std::vector<uint32_t> hs(nseg);
+        A((void **)&info, (size_t)nseg * 32);
+        A((void **)&acc, (size_t)nseg * T * 8);
+        if (!rc) hipLaunchKernelGGL(k_seg_info, dim3((nseg + 255) / 256), dim3(256), 0, s, kh, kl2, ids2, heads, nseg,
+                                    inserted, info);
+        std::vector<uint64_t> hinfo((size_t)nseg * 4);
+        if (!rc && (hipMemcpyAsync(hs.data(), heads, nseg * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipMemcpyAsync(hinfo.data(), info, (size_t)nseg * 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess))
+            rc = QK_E_HIP;
+        std::vector<uint64_t> offs(nseg + 1);
+        for (uint32_t i = 0; i < nseg; ++i) offs[i] = hs[i];
+        offs[nseg] = inserted;
+        if (!rc) rc = seg_encode(ctx, ids2, offs, T, acc, s);
+        std::vector<uint64_t> hacc((size_t)nseg * T);
+        if (!rc && (hipMemcpyAsync(hacc.data(), acc, hacc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess))
+            rc = QK_E_HIP;
+        if (!rc) {
+            const size_t rec = qk_u32_size(T);
+            for (uint32_t i = 0; i < nseg; ++i) {
+                const uint64_t khv = hinfo[4 * i], klv = hinfo[4 * i + 1];
+                uint8_t *k = keys[i].addr;
+                k[0] = (uint8_t)(khv >> 40); k[1] = (uint8_t)(khv >> 32); k[2] = (uint8_t)(khv >> 24);
+                k[3] = (uint8_t)(khv >> 16); k[4] = (uint8_t)(khv >> 8); k[5] = (uint8_t)khv;
+                k[6] = (uint8_t)(klv >> 40); k[7] = (uint8_t)(klv >> 32); k[8] = (uint8_t)(klv >> 24);
+                k[9] = (uint8_t)(klv >> 16); k[10] = (uint8_t)(klv >> 8); k[11] = (uint8_t)klv;
+                qk_u32 *q = (qk_u32 *)(sketches + i * rec);
+                qk_u32_init(q, T);
+                for (uint32_t m = 0; m < T; ++m) q->power_sums[m] = canon32(fold64_32(hacc[(size_t)i * T + m]));
+                q->count = (uint32_t)hinfo[4 * i + 2];
+                q->has_last = 1;
+                q->last_value = (uint32_t)hinfo[4 * i + 3];
+            }
+        }
+    }
+    for (void *p : {(void *)kh, (void *)kl, (void *)kh2, (void *)kl2, (void *)ids, (void *)ids2, (void *)ord,
+                    (void *)ord2, (void *)heads, (void *)flag, (void *)counters, temp, (void *)info, (void *)acc})
+        if (p) (void)hipFreeAsync(p, s);
+    (void)hipStreamSynchronize(s);
+    if (stats) *stats = st;
+    return rc;
+}

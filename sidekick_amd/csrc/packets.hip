@@ -27,11 +27,11 @@
 
 #include "ctx.h"
 #include "field.h"
+#include "records.h"
 
 namespace qk {
 
-constexpr int PK_BLOCK = 256;
-constexpr uint32_t PK_UDP = 17;
+constexpr int PK_BLOCK = REC_TILE;
 
 struct ChunkStat {       // per workgroup chunk, written by lane 0
     int64_t last_reset;  // absolute packet index of the last reset in the chunk, -1 if none
@@ -40,8 +40,6 @@ struct ChunkStat {       // per workgroup chunk, written by lane 0
     uint64_t resets;     // resets in the chunk
     uint64_t all_inserts; // inserts in the chunk, before or after resets
 };
-
-__device__ __forceinline__ uint8_t lds_byte(const uint8_t *t, uint32_t off) { return t[off]; }
 
 __global__ __launch_bounds__(PK_BLOCK) void k_pkt_extract(const uint8_t *__restrict__ bufs, uint64_t n,
                                                           uint32_t stride, const qk_pkt_meta *__restrict__ meta,
@@ -52,8 +50,6 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_extract(const uint8_t *__restr
     __shared__ uint64_t s_cnt[PK_BLOCK / 64], s_nres[PK_BLOCK / 64], s_nins[PK_BLOCK / 64];
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
-    const uintptr_t base_addr = (uintptr_t)bufs;
-    const uint64_t total_bytes = n * (uint64_t)stride;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
     // chunk-level state, kept by thread 0 while walking the tiles in order
@@ -64,48 +60,22 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_extract(const uint8_t *__restr
 
     for (uint64_t p0 = c0; p0 < c1; p0 += PK_BLOCK) {
         const uint64_t np = (c1 - p0) < PK_BLOCK ? (c1 - p0) : PK_BLOCK;
-        // byte range of this tile, widened to 16-byte alignment of the absolute address
-        const uint64_t b_lo = p0 * stride, b_hi = (p0 + np) * stride;
-        const uint64_t a_lo = ((base_addr + b_lo) & ~(uintptr_t)15) - base_addr;  // may be "negative" (wraps)
-        const uint64_t a_hi = ((base_addr + b_hi + 15) & ~(uintptr_t)15) - base_addr;
-        const uint32_t nvec = (uint32_t)((a_hi - a_lo) / 16);
         __syncthreads(); // previous tile fully consumed
-        for (uint32_t v = threadIdx.x; v < nvec; v += PK_BLOCK) {
-            const uint64_t off = a_lo + 16ull * v;     // relative to bufs (mod 2^64)
-            // whole 16-byte vector inside [0, total_bytes)?  (off < total as unsigned also rejects
-            // the wrapped "negative" head)
-            if (off < total_bytes && off + 16 <= total_bytes) {
-                *reinterpret_cast<uint4 *>(tile + 16 * v) = *reinterpret_cast<const uint4 *>(bufs + off);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint64_t o = off + k;
-                    tile[16 * v + k] = o < total_bytes ? bufs[o] : 0;
-                }
-            }
-        }
+        const uint32_t r0 = stage_records(bufs, n, stride, p0, np, tile);
         __syncthreads();
         // classify one record per lane
         uint32_t cls = 0, id = 0; // 0 skip, 1 insert, 2 reset
         const uint64_t pi = p0 + threadIdx.x;
         if (threadIdx.x < np) {
-            const uint32_t r = (uint32_t)(b_lo - a_lo) + threadIdx.x * stride; // record offset in tile
-            qk_pkt_meta m;
-            if (meta) m = meta[pi];
-            else { m.pkttype = 0; m.protocol_be = 0x0008; m.len = (uint32_t)QK_BUFFER_SIZE; }
-            const bool incoming = m.pkttype == 0 || m.pkttype == 3;   // PACKET_HOST | PACKET_OTHERHOST
-            const bool ip = m.protocol_be == 0x0008;                   // ETH_P_IP (0x0800) in network order
-            const bool udp = lds_byte(tile, r + 23) == PK_UDP;
-            if (incoming && ip && udp) {
-                const uint32_t dst = (uint32_t)lds_byte(tile, r + 30) | ((uint32_t)lds_byte(tile, r + 31) << 8) |
-                                     ((uint32_t)lds_byte(tile, r + 32) << 16) | ((uint32_t)lds_byte(tile, r + 33) << 24);
+            const uint8_t *rec = tile + r0 + threadIdx.x * stride;
+            const qk_pkt_meta m = record_meta(meta, pi);
+            if (record_is_incoming_udp(m, rec)) {
+                const uint32_t dst = (uint32_t)rec[30] | ((uint32_t)rec[31] << 8) | ((uint32_t)rec[32] << 16) |
+                                     ((uint32_t)rec[33] << 24);
                 if (check_reset && dst == my_ip_le) cls = 2;
                 else if (m.len == (uint32_t)QK_BUFFER_SIZE) {
                     cls = 1;
-                    id = ((uint32_t)lds_byte(tile, r + QK_ID_OFFSET) << 24) |
-                         ((uint32_t)lds_byte(tile, r + QK_ID_OFFSET + 1) << 16) |
-                         ((uint32_t)lds_byte(tile, r + QK_ID_OFFSET + 2) << 8) |
-                         (uint32_t)lds_byte(tile, r + QK_ID_OFFSET + 3);
+                    id = record_identifier(rec);
                 }
             }
             ids_out[pi] = cls == 1 ? id : 0u;

@@ -34,7 +34,7 @@ from ._lib import (P32, P64, QK_E_CAPACITY, QuackError, check, lib)
 
 __all__ = [
     "PowerSumQuackU32", "PowerSumQuackU64", "ModularInteger", "CoefficientVector",
-    "arithmetic", "Context", "get_context", "device_count",
+    "arithmetic", "Context", "get_context", "device_count", "FlowQuacks",
 ]
 
 
@@ -391,6 +391,98 @@ def encode_packets(q: "PowerSumQuackU32", bufs, stride: int = 67, meta=None, my_
                                               C.byref(st), torch.cuda.current_stream(dev).cuda_stream),
           "encode_packets")
     return {k: getattr(st, k) for k, _ in PktStats._fields_}
+
+
+class FlowKey(C.Structure):
+    _fields_ = [("addr", C.c_uint8 * 12)]
+
+
+def encode_segments(ids, offsets, threshold: int, ctx: Context | None = None) -> list:
+    """Segmented encode: `ids` a CUDA u32 tensor grouped by flow, `offsets`
+    nseg+1 ints (CSR).  Returns one PowerSumQuackU32 per segment."""
+    ptr, n, dev, stream = _device_array(ids, 32)
+    ctx = ctx or get_context(dev)
+    offs = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+    nseg = len(offs) - 1
+    rec = lib().qk_u32_size(threshold)
+    out = C.create_string_buffer(max(nseg, 1) * rec)
+    check(lib().qk_u32_encode_segments_device(ctx.handle, ptr, offs.ctypes.data_as(C.POINTER(C.c_uint64)), nseg,
+                                               threshold, out, stream), "encode_segments")
+    res = []
+    for i in range(nseg):
+        q = PowerSumQuackU32.__new__(PowerSumQuackU32)
+        q._t = threshold
+        q._buf = C.create_string_buffer(out.raw[i * rec:(i + 1) * rec], rec)
+        res.append(q)
+    return res
+
+
+class FlowQuacks:
+    """SidekickMulti's flow table, HashMap<AddrKey, PowerSumQuackU32>
+    (sidekick_multi.rs:22-37,57-90), with a GPU batch entry point.
+    Keys are the 12-byte AddrKey (bytes)."""
+
+    def __init__(self, threshold: int):
+        self.threshold = int(threshold)
+        self._senders: dict = {}
+
+    # per-packet host path (sidekick_multi.rs:65-90)
+    def insert(self, addr_key: bytes, sidekick_id: int) -> "PowerSumQuackU32":
+        q = self._senders.get(bytes(addr_key))
+        if q is None:
+            q = self._senders[bytes(addr_key)] = PowerSumQuackU32(self.threshold)
+        q.insert(sidekick_id)
+        return q
+
+    # sidekick_multi.rs:59-63: only an existing entry is reset
+    def reset(self, addr_key: bytes) -> None:
+        if bytes(addr_key) in self._senders:
+            self._senders[bytes(addr_key)] = PowerSumQuackU32(self.threshold)
+
+    def quack(self, addr_key: bytes):
+        q = self._senders.get(bytes(addr_key))
+        return q.clone() if q is not None else None
+
+    def senders(self) -> dict:
+        return self._senders
+
+    def insert_packets(self, bufs, stride: int = 67, meta=None, my_addr=None, ctx: Context | None = None) -> dict:
+        """Batch of captured records (CUDA uint8 tensor) through the GPU:
+        extract, group by AddrKey, encode per flow, merge into the table."""
+        import torch
+        if not (isinstance(bufs, torch.Tensor) and bufs.is_cuda and bufs.dtype == torch.uint8):
+            raise TypeError("bufs must be a CUDA uint8 tensor")
+        n = bufs.numel() // stride
+        dev = bufs.device.index if bufs.device.index is not None else torch.cuda.current_device()
+        ctx = ctx or get_context(dev)
+        mptr = meta.data_ptr() if meta is not None else None
+        addr = (C.c_uint8 * 6)(*my_addr) if my_addr is not None else None
+        rec = lib().qk_u32_size(self.threshold)
+        cap = 1024
+        while True:
+            keys = (FlowKey * cap)()
+            sk = C.create_string_buffer(cap * rec)
+            nf = C.c_size_t()
+            st = PktStats()
+            rc = lib().qk_u32_encode_flows_device(ctx.handle, bufs.data_ptr(), n, stride, mptr, addr, self.threshold,
+                                                  keys, sk, cap, C.byref(nf), C.byref(st),
+                                                  torch.cuda.current_stream(dev).cuda_stream)
+            if rc == QK_E_CAPACITY:
+                cap = nf.value
+                continue
+            check(rc, "encode_flows")
+            break
+        for i in range(nf.value):
+            key = bytes(keys[i].addr)
+            q = PowerSumQuackU32.__new__(PowerSumQuackU32)
+            q._t = self.threshold
+            q._buf = C.create_string_buffer(sk.raw[i * rec:(i + 1) * rec], rec)
+            old = self._senders.get(key)
+            if old is None:
+                self._senders[key] = q
+            else:
+                old.merge(q)
+        return {k: getattr(st, k) for k, _ in PktStats._fields_}
 
 
 def partial_words(threshold: int, bits: int = 32) -> int:

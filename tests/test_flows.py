@@ -1,0 +1,107 @@
+"""Segmented multi-flow encode vs the oracle's
+literal SidekickMulti restatement (sidekick_multi.rs:65-90,101-143)."""
+import numpy as np
+import pytest
+
+from oracle import coracle, quack_oracle as qo
+
+MY_ADDR = (10, 0, 2, 1, 0x1F, 0x90)   # own dst ip:port (6 bytes)
+META_DT = np.dtype([("pkttype", "u1"), ("reserved", "u1"), ("protocol_be", "<u2"), ("len", "<u4")])
+
+
+def make_flows(n, nflows, seed, stride=67, p_filter=0.1, p_reset=0.01, skew=False):
+    rng = np.random.default_rng(seed)
+    bufs = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
+    bufs[:, 23] = 17
+    flows = rng.integers(0, 256, size=(nflows, 12), dtype=np.uint8)
+    flows[:, 6:12] = (192, 168, 0, 9, 0x11, 0x5C)   # dst side differs from MY_ADDR ...
+    flows[: nflows // 2, 9] = rng.integers(0, 256, size=nflows // 2)  # ... and varies for half the flows
+    if skew:
+        f = np.minimum(rng.zipf(1.5, size=n) - 1, nflows - 1)
+    else:
+        f = rng.integers(0, nflows, size=n)
+    key = flows[f]
+    bufs[:, 26:30] = key[:, 0:4]
+    bufs[:, 34:36] = key[:, 4:6]
+    bufs[:, 30:34] = key[:, 6:10]
+    bufs[:, 36:38] = key[:, 10:12]
+    r = rng.random(n)
+    rs = r < p_reset
+    bufs[rs, 30:34] = MY_ADDR[:4]
+    bufs[rs, 36:38] = MY_ADDR[4:]
+    meta = np.zeros(n, dtype=META_DT)
+    meta["protocol_be"] = 0x0008
+    meta["len"] = 67
+    k = (r >= p_reset) & (r < p_reset + p_filter)
+    kind = rng.integers(0, 4, size=n)
+    meta["pkttype"][k & (kind == 0)] = 4
+    meta["protocol_be"][k & (kind == 1)] = 0xDD86
+    bufs[k & (kind == 2), 23] = 6
+    meta["len"][k & (kind == 3)] = 40
+    return bufs, meta
+
+
+def vector_flows(bufs, meta, my_addr=MY_ADDR):
+    """Vectorised SidekickMulti (checked against the oracle below):
+    {key: ids in packet order}."""
+    inc = (meta["pkttype"] == 0) | (meta["pkttype"] == 3)
+    ok = inc & (meta["protocol_be"] == 0x0008) & (bufs[:, 23] == 17)
+    keys = np.concatenate([bufs[:, 26:30], bufs[:, 34:36], bufs[:, 30:34], bufs[:, 36:38]], axis=1)
+    rst = ok & np.all(keys[:, 6:12] == np.array(my_addr, dtype=np.uint8), axis=1) if my_addr else np.zeros(len(bufs), bool)
+    ins = ok & ~rst & (meta["len"] == 67)
+    idb = bufs[:, 63:67].astype(np.uint32)
+    ids = (idb[:, 0] << 24) | (idb[:, 1] << 16) | (idb[:, 2] << 8) | idb[:, 3]
+    out = {}
+    for i in np.nonzero(ins)[0]:
+        out.setdefault(bytes(keys[i]), []).append(int(ids[i]))
+    return out, int(rst.sum())
+
+
+def test_vector_flows_matches_oracle():
+    bufs, meta = make_flows(3000, 7, seed=1, p_reset=0.05, p_filter=0.2)
+    table, st = qo.sniff_multi_batch({}, 8, bufs, meta["pkttype"], meta["protocol_be"], meta["len"], MY_ADDR)
+    flows, nres = vector_flows(bufs, meta)
+    assert set(table) == set(flows) and st["resets"] == nres
+    for k, ids in flows.items():
+        w = qo.OracleQuack(8)
+        w.insert_all(ids)
+        assert table[k].power_sums == w.power_sums and table[k].count == len(ids) and table[k].last_value == ids[-1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,nflows,t,skew", [(1, 1, 32, False), (1000, 3, 32, False), (70_000, 40, 16, False),
+                                             (200_000, 5000, 32, False), (300_000, 64, 80, True),
+                                             (150_000, 2, 20, False)])
+def test_gpu_flows_vs_oracle(n, nflows, t, skew):
+    import torch
+    import sidekick_amd as sk
+    bufs, meta = make_flows(n, nflows, seed=n + t, skew=skew)
+    table = sk.FlowQuacks(t)
+    pre_key = None
+    flows, nres = vector_flows(bufs, meta)
+    if flows:                                # pre-existing entry merges with the batch
+        pre_key = sorted(flows)[0]
+        table.insert(pre_key, 424242)
+    st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
+                              meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
+    assert st["resets"] == nres and st["inserted"] == sum(len(v) for v in flows.values())
+    assert set(table.senders()) == set(flows)
+    for k, ids in flows.items():
+        q = table.senders()[k]
+        want_ids = ([424242] if k == pre_key else []) + ids
+        assert q.power_sums() == coracle.encode_u32(np.array(want_ids, dtype=np.uint32), t), k.hex()
+        assert q.count() == len(want_ids) and q.last_value() == ids[-1]
+
+
+@pytest.mark.gpu
+def test_gpu_segments_primitive():
+    import torch
+    from sidekick_amd.quack import encode_segments
+    ids = coracle.splitmix_u32(0xF10, 400_000)
+    offs = [0, 0, 1, 5, 70_000, 70_000, 200_003, 400_000]   # empty, tiny, > one 64 Ki work item
+    qs = encode_segments(torch.from_numpy(ids.view(np.int32)).cuda(), offs, 32)
+    assert len(qs) == len(offs) - 1
+    for g, q in enumerate(qs):
+        seg = ids[offs[g]:offs[g + 1]]
+        assert q.power_sums() == coracle.encode_u32(seg, 32)
+        assert q.count() == len(seg) and q.last_value() == (int(seg[-1]) if len(seg) else None)
