@@ -1,0 +1,111 @@
+"""Caller-side decode loop with the reset protocol (media_client.rs:205-325):
+sender -> lossy proxy (quACK over bincode, resets) -> QuackReceiver, checked
+action by action against an independent restatement on the oracle's
+arithmetic.  CPU runs use the per-packet host path; the GPU run forces the
+batch encode / root-test paths (batch_min = 1)."""
+import random
+
+import pytest
+
+import sidekick_amd as sk
+from sidekick_amd.receiver import QuackReceiver
+from oracle import quack_oracle as qo
+
+
+class OracleReceiver:
+    """media_client.rs:205-325 restated on oracle.OracleQuack."""
+
+    def __init__(self, t, debounce=0.1):
+        self.t, self.debounce = t, debounce
+        self.my = qo.OracleQuack(t)
+        self.log, self.last_reset = [], None
+
+    def on_quack(self, q: "qo.OracleQuack", now):
+        if q.last_value == self.my.last_value:
+            return [], False
+        idx = next((i for i, (_, v) in enumerate(self.log) if v == q.last_value), None)
+        if idx is not None:
+            for _, v in self.log[: idx + 1]:
+                self.my.insert(v)
+        r0, r1, r2 = idx is None, self.my.count < q.count, self.my.count > q.count + self.t
+        if r0 or r1 or r2:
+            if self.last_reset is None or now > self.last_reset + self.debounce:
+                self.my, self.log, self.last_reset = qo.OracleQuack(self.t), [], now
+                return [], True
+            return [], False
+        self.last_reset = None
+        diff = self.my.clone()
+        diff.sub_assign(q)
+        if diff.count == 0:
+            del self.log[: idx + 1]
+            return [], False
+        c = diff.to_coeffs()
+        miss = []
+        for s, v in self.log:
+            if v == diff.last_value:
+                break
+            if qo.poly_eval(c, v, qo.P32) == 0:
+                miss.append((s, v))
+        del self.log[: idx + 1]
+        for _, v in miss:
+            self.my.remove(v)
+        return [s for s, _ in miss], False
+
+
+def simulate(t, n_pkts, loss, seed, batch_min, reorder_every=0):
+    rnd = random.Random(seed)
+    rx, orx = QuackReceiver(t, batch_min=batch_min), OracleReceiver(t)
+    proxy = sk.PowerSumQuackU32(t)
+    seq, now, sent, stats = 0, 0.0, [], {"retx": 0, "resets": 0, "quacks": 0}
+    pending = []   # (seqno, id) queued to send (new + retransmissions)
+    for step in range(n_pkts):
+        seq += 1
+        pending.append((seq, rnd.getrandbits(32)))
+        while pending:
+            s, v = pending.pop(0)
+            rx.on_send(s, v)
+            orx.log.append((s, v))
+            if rnd.random() >= loss:
+                proxy.insert(v)
+        now += 0.003
+        if step % 25 == 24:
+            wire = proxy.serialize()                      # sidekick.rs:187 / media_client.rs:227
+            q = sk.PowerSumQuackU32.deserialize(wire)
+            oq = qo.OracleQuack(t)
+            oq.power_sums, oq.count, oq.last_value = q.power_sums(), q.count(), q.last_value()
+            if reorder_every and (step // 25) % reorder_every == reorder_every - 1:
+                q.insert(0xDEADBEEF)                      # a quACK whose last_value is not in the log
+                oq.insert(0xDEADBEEF)
+            act = rx.on_quack(q, now)
+            want_retx, want_reset = orx.on_quack(oq, now)
+            assert act.retransmit == want_retx and act.send_reset == want_reset, step
+            assert rx.my_quack.power_sums() == orx.my.power_sums and len(rx.seqno_ids) == len(orx.log)
+            stats["quacks"] += 1
+            stats["retx"] += len(act.retransmit)
+            if act.send_reset:
+                stats["resets"] += 1
+                proxy = sk.PowerSumQuackU32(t)           # the proxy resets on the [0] datagram
+            for s in act.retransmit:
+                pending.append((s, rnd.getrandbits(32)))
+    return stats
+
+
+@pytest.mark.parametrize("loss,reorder", [(0.0, 0), (0.03, 0), (0.2, 0), (0.03, 3)])
+def test_receiver_matches_media_client_host_path(loss, reorder):
+    st = simulate(t=8, n_pkts=1500, loss=loss, seed=int(loss * 100) + reorder, batch_min=1 << 30,
+                  reorder_every=reorder)
+    if loss == 0:
+        assert st["retx"] == 0 and st["resets"] == 0
+    if loss == 0.03 and not reorder:
+        assert st["retx"] > 0
+    if loss == 0.2:
+        assert st["resets"] > 0          # 25-packet windows with > 8 losses exceed the threshold
+    if reorder:
+        assert st["resets"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("loss", [0.03, 0.2])
+def test_receiver_matches_media_client_gpu_path(loss):
+    st = simulate(t=16, n_pkts=1200, loss=loss, seed=7, batch_min=1)
+    assert st["quacks"] > 0
