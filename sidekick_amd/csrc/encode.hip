@@ -362,16 +362,22 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u32(const uint64_t *__restri
 }
 
 // ------------------------------------------------------------------ u64
-// 96-bit lazy accumulators: lo (u64) + hi (u32 carry count).
+// t-form chain over p64 (field.h tstep64): per power eight v_mad_u64_u32 and
+// a 96-bit accumulate (three carry-chained 32-bit adds, no folding).
 template <int K>
 __device__ __forceinline__ void chain64(uint64_t (&lo)[K], uint32_t (&hi)[K], uint64_t start, uint64_t step) {
-    uint64_t y = start;
+    // start: any value < 2^64 (t-form with th = 0); step canonical
+    const uint64_t step59 = mul64(step, C64);
+    const uint32_t x0 = (uint32_t)step, x1 = (uint32_t)(step >> 32);
+    const uint32_t y0 = (uint32_t)step59, y1 = (uint32_t)(step59 >> 32);
+    uint32_t t0 = (uint32_t)start, t1 = (uint32_t)(start >> 32), th = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint64_t s = lo[k] + y;
-        hi[k] += (s < y) ? 1u : 0u;
+        const uint64_t tl = ((uint64_t)t1 << 32) | t0;
+        const uint64_t s = lo[k] + tl;
+        hi[k] += th + (s < tl ? 1u : 0u);   // < 60 per add
         lo[k] = s;
-        if (k + 1 < K) y = mul64_lazy(y, step);
+        if (k + 1 < K) tstep64(t0, t1, th, x0, x1, y0, y1);
     }
 }
 
@@ -386,7 +392,7 @@ __device__ __forceinline__ void group_powers64(uint64_t x, int j, uint64_t &star
         if ((1 << bit) < G) b = mul64_lazy(b, b);
     }
     start = r;
-    step = b;
+    step = canon64(b); // the t-form chain needs a canonical step
 }
 
 // u64 partials: two 32-bit limbs per power, stored [2m + limb][block].
@@ -433,12 +439,12 @@ __global__ __launch_bounds__(BLOCK) void k_encode_u64_g1(const uint64_t *__restr
     const ulonglong2 *__restrict__ v = reinterpret_cast<const ulonglong2 *>(ids + h);
     for (uint64_t i = gtid; i < body; i += nthr) {
         const ulonglong2 w = v[i];
-        chain64<K>(lo, hi, w.x, w.x);
-        chain64<K>(lo, hi, w.y, w.y);
+        chain64<K>(lo, hi, w.x, canon64(w.x));
+        chain64<K>(lo, hi, w.y, canon64(w.y));
     }
     const uint64_t tail0 = h + (body << 1);
-    if (gtid < h) chain64<K>(lo, hi, ids[gtid], ids[gtid]);
-    if (gtid < n - tail0) chain64<K>(lo, hi, ids[tail0 + gtid], ids[tail0 + gtid]);
+    if (gtid < h) chain64<K>(lo, hi, ids[gtid], canon64(ids[gtid]));
+    if (gtid < n - tail0) chain64<K>(lo, hi, ids[tail0 + gtid], canon64(ids[tail0 + gtid]));
     block_store64<1, K>(lo, hi, T, partials, sm);
 }
 

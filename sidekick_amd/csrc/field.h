@@ -170,6 +170,27 @@ QK_HD uint64_t mad64_lazy(uint64_t a, uint64_t b, uint64_t c) {
     return (uint64_t)u + C64 * (uint64_t)(u >> 64);
 }
 
+// ---- u64 "t-form": v = t0 + t1*2^32 + th*2^64 with th <= 59 ---------------
+// With x = (x1:x0) and x59 = 59x mod p = (y1:y0) canonical (<= p-1), one step
+// v <- v*x is P = (t1:t0)*x + th*x59 <= (2^64-1)(p-1) + 59(p-1) = (p-1)(2^64+58)
+// < 2^128, then v' = P_L + 59*P_H < 60*2^64 (th' <= 59), congruent because
+// th*x59 == th*59x == th*2^64*x (mod p).  Eight v_mad_u64_u32 in 32-bit limbs;
+// every intermediate bound is noted (no carry can be lost).
+QK_HD void tstep64(uint32_t &t0, uint32_t &t1, uint32_t &th, uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1) {
+    const uint64_t c0 = (uint64_t)t0 * x0;                                   // < 2^64
+    const uint64_t c1 = (uint64_t)t1 * x0 + (c0 >> 32);                      // <= 2^64 - 2^32
+    const uint64_t c2 = (uint64_t)t0 * x1 + (uint32_t)c1;                    // <= 2^64 - 2^32
+    const uint64_t c3 = (uint64_t)t1 * x1 + (c1 >> 32) + (c2 >> 32);         // <= 2^64 - 1
+    const uint64_t d0 = (uint64_t)th * y0 + (uint32_t)c0;                    // < 2^38
+    const uint64_t d1 = (uint64_t)th * y1 + (uint32_t)c2 + (d0 >> 32);       // < 2^38
+    const uint64_t PH = c3 + (d1 >> 32);                                      // P < 2^128 => no wrap
+    const uint64_t e0 = (uint64_t)(uint32_t)PH * C64 + (uint32_t)d0;          // < 2^38
+    const uint64_t e1 = (uint64_t)(uint32_t)(PH >> 32) * C64 + (uint32_t)d1 + (e0 >> 32); // < 60*2^32
+    t0 = (uint32_t)e0;
+    t1 = (uint32_t)e1;
+    th = (uint32_t)(e1 >> 32);
+}
+
 // Fold a 96-bit lazy accumulator hi*2^64 + lo (hi < 2^32) to [0, 2^64).
 QK_HD uint64_t fold96_64(uint32_t hi, uint64_t lo) {
     unsigned __int128 t = (unsigned __int128)hi * C64 + lo;   // < 2^38 + 2^64

@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <initializer_list>
+
 #include "../../sidekick_amd/csrc/field.h"
 
 using namespace qk;
@@ -44,6 +46,15 @@ static void check_tstep(uint32_t lo, uint32_t hi, uint32_t x, uint32_t c) {
     EXPECT(h2 <= 5, "tstep hi bound lo=%u hi=%u x=%u c=%u -> hi=%u", lo, hi, x, c, h2);
     EXPECT(t2 % P32 == ((u128)t * x + c) % P32, "tstep congruence lo=%u hi=%u x=%u c=%u", lo, hi, x, c);
     EXPECT(tstep32p(t, x, x5, c) == t2, "tstep32p != tstep32");
+}
+
+static void check_tstep64(uint64_t lo, uint32_t hi, uint64_t x) {
+    const uint64_t x59 = mul64(x, C64);
+    uint32_t t0 = (uint32_t)lo, t1 = (uint32_t)(lo >> 32), th = hi;
+    tstep64(t0, t1, th, (uint32_t)x, (uint32_t)(x >> 32), (uint32_t)x59, (uint32_t)(x59 >> 32));
+    const u128 v = ((u128)hi << 64) + lo, v2 = ((u128)th << 64) + (((uint64_t)t1 << 32) | t0);
+    EXPECT(th <= 59, "tstep64 th bound hi=%u -> %u", hi, th);
+    EXPECT((uint64_t)(v2 % P64) == (uint64_t)(v % P64 * x % P64), "tstep64 congruence");
 }
 
 static void check_mulfold(uint32_t y, uint32_t x) {
@@ -96,6 +107,12 @@ static int run_check() {
         const uint32_t h = r32();
         EXPECT(canon64(fold96_64(h, a)) == (uint64_t)((((u128)h << 64) + a) % P64), "fold96_64 rnd");
     }
+    // u64 t-form step: edges of every operand, then random
+    for (uint64_t lo : e64)
+        for (uint32_t hi : {0u, 1u, 58u, 59u})
+            for (uint64_t x : std::initializer_list<uint64_t>{0, 1, 59, P64 - 1, P64 - 2, 1ull << 63, 0xFFFFFFFFull, 1ull << 32})
+                check_tstep64(lo, hi, x);
+    for (int i = 0; i < 1000000; ++i) check_tstep64(rnd(), r32() % 60, rnd() % P64);
     printf("field_check: %s (%d failures)\n", fails ? "FAIL" : "ok", fails);
     return fails ? 1 : 0;
 }
