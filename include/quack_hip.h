@@ -248,6 +248,19 @@ int qk_u32_root_test_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t d, con
 int qk_u64_root_test_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log,
                             size_t n, int stop_at_value, uint64_t stop_value, uint64_t *hits,
                             size_t cap, size_t *n_hits, void *stream);
+/* Shard form of the root test for a log cut into contiguous shards across
+ * ranks: as above on this shard, and *stop_index is set to the
+ * position of the first entry equal to stop_value in the shard, or n when
+ * there is none (or stop_at_value == 0).  The global result is the union of
+ * shard hits (offset by shard base) below the smallest shard_base+stop_index;
+ * sidekick_amd/dist.py: root_test_sharded does that merge with two small
+ * collectives. */
+int qk_u32_root_test_shard_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t d, const uint32_t *d_log,
+                                  size_t n, int stop_at_value, uint32_t stop_value, uint64_t *hits,
+                                  size_t cap, size_t *n_hits, uint64_t *stop_index, void *stream);
+int qk_u64_root_test_shard_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log,
+                                  size_t n, int stop_at_value, uint64_t stop_value, uint64_t *hits,
+                                  size_t cap, size_t *n_hits, uint64_t *stop_index, void *stream);
 /* decode_with_log on the device: to_coeffs(diff) on the host (O(t^2)), then
  * the root test over the device-resident log.  diff->count == 0 -> no hits;
  * diff->count > threshold -> QK_E_UNDECODABLE. */

@@ -81,6 +81,10 @@ SIGNATURES = {
     "qk_u64_encode_host": (C.c_int, [vp, vp, sz, vp]),
     "qk_u32_root_test_device": (C.c_int, [vp, u32p, C.c_uint32, vp, sz, C.c_int, C.c_uint32, u64p, sz, szp, vp]),
     "qk_u64_root_test_device": (C.c_int, [vp, u64p, C.c_uint32, vp, sz, C.c_int, C.c_uint64, u64p, sz, szp, vp]),
+    "qk_u32_root_test_shard_device": (C.c_int, [vp, u32p, C.c_uint32, vp, sz, C.c_int, C.c_uint32, u64p, sz, szp,
+                                                u64p, vp]),
+    "qk_u64_root_test_shard_device": (C.c_int, [vp, u64p, C.c_uint32, vp, sz, C.c_int, C.c_uint64, u64p, sz, szp,
+                                                u64p, vp]),
     "qk_u32_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
     "qk_u64_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
     "qk_u32_encode_packets_device": (C.c_int, [vp, vp, sz, sz, vp, vp, vp, vp, vp]),

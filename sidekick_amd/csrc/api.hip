@@ -194,10 +194,17 @@ static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t,
 
 template <typename T, typename Launch>
 static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop,
-                          T stop_value, uint64_t *hits, size_t cap, size_t *n_hits, void *stream, Launch launch) {
+                          T stop_value, uint64_t *hits, size_t cap, size_t *n_hits, void *stream, Launch launch,
+                          uint64_t *stop_index = nullptr) {
     if (!ctx || !n_hits || (d && !coeffs) || (n && !d_log)) return QK_E_INVAL;
     *n_hits = 0;
-    if (d == 0 || n == 0) return QK_OK; // P == 1 has no roots
+    if (stop_index) *stop_index = n;
+    if (n == 0) return QK_OK;
+    if (d == 0) {
+        if (!stop_index || !use_stop) return QK_OK; // P == 1 has no roots
+        // no roots, but a shard caller still needs the stop position: the
+        // degree-0 launch tests nothing and only records the stop (below)
+    }
     if (d > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
     if (!is_device_ptr(d_log)) return QK_E_INVAL;
     std::lock_guard<std::mutex> g(ctx->mu);
@@ -229,6 +236,7 @@ static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_l
         std::sort(h.begin(), h.end());
         size_t m = h.size();
         if (use_stop) m = (size_t)(std::lower_bound(h.begin(), h.end(), cnt[1]) - h.begin());
+        if (stop_index) *stop_index = use_stop ? std::min<uint64_t>(cnt[1], (uint64_t)n) : (uint64_t)n;
         *n_hits = m;
         if (m > cap || (m && !hits)) return QK_E_CAPACITY;
         std::copy(h.begin(), h.begin() + m, hits);
@@ -444,6 +452,22 @@ int qk_u64_root_test_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, con
                             void *stream) {
     return root_test_impl<uint64_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
                                     launch_root_test_u64);
+}
+
+int qk_u32_root_test_shard_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t d, const uint32_t *d_log, size_t n,
+                                  int stop_at_value, uint32_t stop_value, uint64_t *hits, size_t cap,
+                                  size_t *n_hits, uint64_t *stop_index, void *stream) {
+    if (!stop_index) return QK_E_INVAL;
+    return root_test_impl<uint32_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
+                                    launch_root_test_u32, stop_index);
+}
+
+int qk_u64_root_test_shard_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log, size_t n,
+                                  int stop_at_value, uint64_t stop_value, uint64_t *hits, size_t cap,
+                                  size_t *n_hits, uint64_t *stop_index, void *stream) {
+    if (!stop_index) return QK_E_INVAL;
+    return root_test_impl<uint64_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
+                                    launch_root_test_u64, stop_index);
 }
 
 int qk_u32_decode_device(qk_ctx *ctx, const qk_u32 *diff, const uint32_t *d_log, size_t n, int stop_at_last,

@@ -362,47 +362,150 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u32(const uint64_t *__restri
 }
 
 // ------------------------------------------------------------------ u64
-// t-form chain over p64 (field.h tstep64): per power eight v_mad_u64_u32 and
-// a 96-bit accumulate (three carry-chained 32-bit adds, no folding).
+// Power chain over p64 = 2^64 - 59, hand-scheduled (gfx950 ISA).  State:
+// t = t0 + t1*2^32 + th*2^64 (th <= 59; t0:t1 pinned in v[2:3] so the step can
+// address the halves of its 64-bit pairs).  One step, for a step value x < 2^64:
+//   V  = (t0:t1) + 59*th            v_mad_u64_u32; wraps past 2^64 only when
+//                                   V < 59*60, then V += 59 (2^64 == 59) exactly
+//   P  = V*x < 2^128                four v_mad_u64_u32:
+//        A = V.lo*x0, B = V.hi*x0 + A.hi, C = V.lo*x1 + B (carry cc),
+//        PH = V.hi*x1 + C.hi + cc*2^32, P_L = A.lo + C.lo*2^32
+//   t' = P_L + 59*PH  (< 60*2^64)   two v_mad_u64_u32: E = P_L + 59*PH.lo
+//                                   (carry ce), F = E.hi + ce*2^32 + 59*PH.hi;
+//                                   t0' = E.lo, t1' = F.lo, th' = F.hi
+// and the previous power's value is added into its 96-bit accumulator
+// (a0, a1, a2) with a carry chain in the same block: 7 multiplies + 14 simple
+// ops per power (the compiler's rendering of field.h tstep64 plus the
+// accumulate spends 8 multiplies and ~20 moves/adds/compares).  Every
+// VALU-written carry is read >= 2 wait states later (gfx950 VALU SGPR-write ->
+// VALU read hazard).
+#define QK_U64_STEP_ASM                                                                            \
+    "v_add_co_u32_e64 %[a0], %[sc], %[a0], v2\n\t"                                                   \
+    "v_mad_u64_u32 v[4:5], %[cw], %[th], 59, v[2:3]\n\t"                                             \
+    "v_mov_b32_e32 v11, 0\n\t"                                                                     \
+    "v_addc_co_u32_e64 %[a1], %[sc], %[a1], v3, %[sc]\n\t"                                           \
+    "v_cndmask_b32_e64 %[tmp], 0, 59, %[cw]\n\t"                                                     \
+    "v_add_u32_e32 v4, v4, %[tmp]\n\t"                                                               \
+    "v_addc_co_u32_e64 %[a2], %[cx], %[a2], %[th], %[sc]\n\t"                                        \
+    "v_mad_u64_u32 v[6:7], %[cx], v4, %[x0], 0\n\t"                                                  \
+    "v_mov_b32_e32 v10, v7\n\t"                                                                    \
+    "v_mad_u64_u32 v[8:9], %[cx], v5, %[x0], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[8:9], %[cc], v4, %[x1], v[8:9]\n\t"                                             \
+    "v_mov_b32_e32 v7, v8\n\t"                                                                     \
+    "v_mov_b32_e32 v10, v9\n\t"                                                                    \
+    "v_cndmask_b32_e64 v11, 0, 1, %[cc]\n\t"                                                         \
+    "v_mad_u64_u32 v[4:5], %[cx], v5, %[x1], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[2:3], %[ce], v4, 59, v[6:7]\n\t"                                                \
+    "v_mov_b32_e32 v8, v3\n\t"                                                                     \
+    "s_nop 0\n\t"                                                                                  \
+    "v_cndmask_b32_e64 v9, 0, 1, %[ce]\n\t"                                                          \
+    "v_mad_u64_u32 v[8:9], %[cx], v5, 59, v[8:9]\n\t"                                                \
+    "v_mov_b32_e32 v3, v8\n\t"                                                                     \
+    "v_mov_b32_e32 %[th], v9\n\t"
+
 template <int K>
-__device__ __forceinline__ void chain64(uint64_t (&lo)[K], uint32_t (&hi)[K], uint64_t start, uint64_t step) {
-    // start: any value < 2^64 (t-form with th = 0); step canonical
-    const uint64_t step59 = mul64(step, C64);
+__device__ __forceinline__ void chain64(uint32_t (&a0)[K], uint32_t (&a1)[K], uint32_t (&a2)[K], uint64_t start,
+                                        uint64_t step) {
+    // start, step: any values < 2^64 (t-form with th = 0)
+    uint64_t t = start;
+    uint32_t th = 0;
     const uint32_t x0 = (uint32_t)step, x1 = (uint32_t)(step >> 32);
-    const uint32_t y0 = (uint32_t)step59, y1 = (uint32_t)(step59 >> 32);
-    uint32_t t0 = (uint32_t)start, t1 = (uint32_t)(start >> 32), th = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint64_t tl = ((uint64_t)t1 << 32) | t0;
-        const uint64_t s = lo[k] + tl;
-        hi[k] += th + (s < tl ? 1u : 0u);   // < 60 per add
-        lo[k] = s;
-        if (k + 1 < K) tstep64(t0, t1, th, x0, x1, y0, y1);
+    for (int k = 0; k + 1 < K; ++k) {
+        uint64_t sc, cw, cx, cc, ce;
+        uint32_t tmp;
+        asm volatile(QK_U64_STEP_ASM
+                     : [a0] "+v"(a0[k]), [a1] "+v"(a1[k]), [a2] "+v"(a2[k]), "+{v[2:3]}"(t), [th] "+v"(th),
+                       [sc] "=&s"(sc), [cw] "=&s"(cw), [cx] "=&s"(cx), [cc] "=&s"(cc), [ce] "=&s"(ce),
+                       [tmp] "=&v"(tmp)
+                     : [x0] "v"(x0), [x1] "v"(x1)
+                     : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11");
     }
+    uint64_t sc, cx;
+    asm volatile("v_add_co_u32_e64 %[a0], %[sc], %[a0], v2\n\t"
+                 "s_nop 1\n\t"
+                 "v_addc_co_u32_e64 %[a1], %[sc], %[a1], v3, %[sc]\n\t"
+                 "s_nop 1\n\t"
+                 "v_addc_co_u32_e64 %[a2], %[cx], %[a2], %[th], %[sc]\n\t"
+                 : [a0] "+v"(a0[K - 1]), [a1] "+v"(a1[K - 1]), [a2] "+v"(a2[K - 1]), [sc] "=&s"(sc), [cx] "=&s"(cx)
+                 : "{v[2:3]}"(t), [th] "v"(th));
 }
 
+// (lo, hi) -> a 64-bit value through an opaque move, so the 32-bit
+// accumulators are not kept as zero-extended / shifted 64-bit pairs
+__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
+    uint64_t v;
+    asm volatile("v_mov_b32_e32 v12, %1\n\tv_mov_b32_e32 v13, %2" : "={v[12:13]}"(v) : "v"(lo), "v"(hi));
+    return v;
+}
+
+// t-form value -> a value < 2^64 congruent to it (chain starts and steps)
+__device__ __forceinline__ uint64_t vfold64(uint32_t t0, uint32_t t1, uint32_t th) {
+    const uint64_t t = ((uint64_t)t1 << 32) | t0;
+    const uint64_t v = t + (uint64_t)th * C64;
+    return v < t ? v + C64 : v; // wrapped: v < 59*60 and 2^64 == 59
+}
+
+// The step without an accumulate (chain setup): t <- t*x, t-form in/out.
+#define QK_U64_MUL_ASM                                                                             \
+    "v_mad_u64_u32 v[4:5], %[cw], %[th], 59, v[2:3]\n\t"                                             \
+    "v_mov_b32_e32 v11, 0\n\t"                                                                     \
+    "s_nop 0\n\t"                                                                                  \
+    "v_cndmask_b32_e64 %[tmp], 0, 59, %[cw]\n\t"                                                     \
+    "v_add_u32_e32 v4, v4, %[tmp]\n\t"                                                               \
+    "v_mad_u64_u32 v[6:7], %[cx], v4, %[x0], 0\n\t"                                                  \
+    "v_mov_b32_e32 v10, v7\n\t"                                                                    \
+    "v_mad_u64_u32 v[8:9], %[cx], v5, %[x0], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[8:9], %[cc], v4, %[x1], v[8:9]\n\t"                                             \
+    "v_mov_b32_e32 v7, v8\n\t"                                                                     \
+    "v_mov_b32_e32 v10, v9\n\t"                                                                    \
+    "v_cndmask_b32_e64 v11, 0, 1, %[cc]\n\t"                                                         \
+    "v_mad_u64_u32 v[4:5], %[cx], v5, %[x1], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[2:3], %[ce], v4, 59, v[6:7]\n\t"                                                \
+    "v_mov_b32_e32 v8, v3\n\t"                                                                     \
+    "s_nop 0\n\t"                                                                                  \
+    "v_cndmask_b32_e64 v9, 0, 1, %[ce]\n\t"                                                          \
+    "v_mad_u64_u32 v[8:9], %[cx], v5, 59, v[8:9]\n\t"                                                \
+    "v_mov_b32_e32 v3, v8\n\t"                                                                     \
+    "v_mov_b32_e32 %[th], v9\n\t"
+
+__device__ __forceinline__ void tmul64_asm(uint64_t &t, uint32_t &th, uint32_t x0, uint32_t x1) {
+    uint64_t cw, cx, cc, ce;
+    uint32_t tmp;
+    asm volatile(QK_U64_MUL_ASM
+                 : "+{v[2:3]}"(t), [th] "+v"(th), [cw] "=&s"(cw), [cx] "=&s"(cx), [cc] "=&s"(cc), [ce] "=&s"(ce),
+                   [tmp] "=&v"(tmp)
+                 : [x0] "v"(x0), [x1] "v"(x1)
+                 : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11");
+}
+
+// Lane j of a group of G starts at x^(j+1) and steps by x^G: x^2 .. x^G by
+// the same step, each folded below 2^64.
 template <int G>
 __device__ __forceinline__ void group_powers64(uint64_t x, int j, uint64_t &start, uint64_t &step) {
-    uint64_t b = x, r = 1;
-    const uint32_t e = (uint32_t)j + 1;
+    const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
+    uint64_t t = x;
+    uint32_t th = 0;
+    start = x;
+    step = x;
 #pragma unroll
-    for (int bit = 0; (1 << bit) <= G; ++bit) {
-        const uint64_t rb = mul64_lazy(r, b);
-        r = ((e >> bit) & 1) ? rb : r;
-        if ((1 << bit) < G) b = mul64_lazy(b, b);
+    for (int g = 1; g < G; ++g) {
+        tmul64_asm(t, th, x0, x1);
+        const uint64_t v = vfold64((uint32_t)t, (uint32_t)(t >> 32), th);
+        if (g == j) start = v;
+        step = v; // after the last iteration: x^G
     }
-    start = r;
-    step = canon64(b); // the t-form chain needs a canonical step
 }
 
 // u64 partials: two 32-bit limbs per power, stored [2m + limb][block].
 template <int G, int K>
-__device__ __forceinline__ void block_store64(const uint64_t (&lo)[K], const uint32_t (&hi)[K], uint32_t T,
-                                              uint64_t *partials, uint64_t *sm) {
+__device__ __forceinline__ void block_store64(const uint32_t (&a0)[K], const uint32_t (&a1)[K],
+                                              const uint32_t (&a2)[K], uint32_t T, uint64_t *partials,
+                                              uint64_t *sm) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint64_t f = fold96_64(hi[k], lo[k]);
+        const uint64_t f = fold96_64(a2[k], pack64(a0[k], a1[k]));
         uint64_t a = (uint32_t)f, b = f >> 32;
 #pragma unroll
         for (int off = 32; off >= G; off >>= 1) {
@@ -428,10 +531,9 @@ __global__ __launch_bounds__(BLOCK) void k_encode_u64_g1(const uint64_t *__restr
                                                          uint32_t head, uint32_t T,
                                                          uint64_t *__restrict__ partials) {
     __shared__ uint64_t sm[WAVES * 2 * K];
-    uint64_t lo[K];
-    uint32_t hi[K];
+    uint32_t a0[K], a1[K], a2[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) { lo[k] = 0; hi[k] = 0; }
+    for (int k = 0; k < K; ++k) { a0[k] = 0; a1[k] = 0; a2[k] = 0; }
     const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     const uint64_t nthr = (uint64_t)gridDim.x * BLOCK;
     const uint64_t h = head < n ? head : n;
@@ -439,13 +541,13 @@ __global__ __launch_bounds__(BLOCK) void k_encode_u64_g1(const uint64_t *__restr
     const ulonglong2 *__restrict__ v = reinterpret_cast<const ulonglong2 *>(ids + h);
     for (uint64_t i = gtid; i < body; i += nthr) {
         const ulonglong2 w = v[i];
-        chain64<K>(lo, hi, w.x, canon64(w.x));
-        chain64<K>(lo, hi, w.y, canon64(w.y));
+        chain64<K>(a0, a1, a2, w.x, w.x);
+        chain64<K>(a0, a1, a2, w.y, w.y);
     }
     const uint64_t tail0 = h + (body << 1);
-    if (gtid < h) chain64<K>(lo, hi, ids[gtid], canon64(ids[gtid]));
-    if (gtid < n - tail0) chain64<K>(lo, hi, ids[tail0 + gtid], canon64(ids[tail0 + gtid]));
-    block_store64<1, K>(lo, hi, T, partials, sm);
+    if (gtid < h) chain64<K>(a0, a1, a2, ids[gtid], ids[gtid]);
+    if (gtid < n - tail0) chain64<K>(a0, a1, a2, ids[tail0 + gtid], ids[tail0 + gtid]);
+    block_store64<1, K>(a0, a1, a2, T, partials, sm);
 }
 
 template <int G, int K>
@@ -454,19 +556,18 @@ __global__ __launch_bounds__(BLOCK) void k_encode_u64_gn(const uint64_t *__restr
                                                          uint64_t *__restrict__ partials) {
     (void)head;
     __shared__ uint64_t sm[WAVES * 2 * G * K];
-    uint64_t lo[K];
-    uint32_t hi[K];
+    uint32_t a0[K], a1[K], a2[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) { lo[k] = 0; hi[k] = 0; }
+    for (int k = 0; k < K; ++k) { a0[k] = 0; a1[k] = 0; a2[k] = 0; }
     const int j = threadIdx.x % G;
     const uint64_t grp = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) / G;
     const uint64_t ngrp = (uint64_t)gridDim.x * BLOCK / G;
     for (uint64_t i = grp; i < n; i += ngrp) {
         uint64_t start, step;
         group_powers64<G>(ids[i], j, start, step);
-        chain64<K>(lo, hi, start, step);
+        chain64<K>(a0, a1, a2, start, step);
     }
-    block_store64<G, K>(lo, hi, T, partials, sm);
+    block_store64<G, K>(a0, a1, a2, T, partials, sm);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restrict__ partials,
@@ -548,8 +649,8 @@ static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t
 // budget, then the smallest instantiated K >= ceil(T/G).
 static const int K32_G1[] = {1, 2, 4, 8, 12, 16, 20, 24, 28, 32};
 static const int K32_GN[] = {20, 24, 28, 32};
-static const int K64_G1[] = {1, 2, 4, 8, 12, 16, 20};
-static const int K64_GN[] = {12, 16, 20};
+static const int K64_G1[] = {1, 2, 4, 8, 12, 16, 20, 24, 32, 40};
+static const int K64_GN[] = {12, 16, 20, 24, 32, 40};
 
 template <int G, int K>
 static int enc32_gk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
@@ -612,12 +713,18 @@ static int enc64_g(qk_ctx *ctx, int K, const uint64_t *ids, size_t n, uint32_t h
         case 12: return enc64_gk<1, 12>(ctx, ids, n, head, T, out, acc, s);
         case 16: return enc64_gk<1, 16>(ctx, ids, n, head, T, out, acc, s);
         case 20: return enc64_gk<1, 20>(ctx, ids, n, head, T, out, acc, s);
+        case 24: return enc64_gk<1, 24>(ctx, ids, n, head, T, out, acc, s);
+        case 32: return enc64_gk<1, 32>(ctx, ids, n, head, T, out, acc, s);
+        case 40: return enc64_gk<1, 40>(ctx, ids, n, head, T, out, acc, s);
         }
     } else {
         switch (K) {
         case 12: return enc64_gk<G, 12>(ctx, ids, n, head, T, out, acc, s);
         case 16: return enc64_gk<G, 16>(ctx, ids, n, head, T, out, acc, s);
         case 20: return enc64_gk<G, 20>(ctx, ids, n, head, T, out, acc, s);
+        case 24: return enc64_gk<G, 24>(ctx, ids, n, head, T, out, acc, s);
+        case 32: return enc64_gk<G, 32>(ctx, ids, n, head, T, out, acc, s);
+        case 40: return enc64_gk<G, 40>(ctx, ids, n, head, T, out, acc, s);
         }
     }
     return QK_E_THRESHOLD;
@@ -673,7 +780,11 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     if (a & 7) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
     int G, K;
-    choose_gk(T, 20, K64_G1, 7, K64_GN, 3, G, K);
+    // K <= 40 accumulators per lane (120 VGPRs, 3 waves/SIMD) beat K <= 20 at
+    // 5 waves by needing fewer lanes per id (t = 80: 2 x (39 + 1) steps vs
+    // 4 x (19 + 3)); QK_TUNE_U64_KMAX overrides for measurements.
+    static const int kmax = [] { const char *e = getenv("QK_TUNE_U64_KMAX"); return e ? atoi(e) : 40; }();
+    choose_gk(T, kmax, K64_G1, 10, K64_GN, 6, G, K);
     switch (G) {
     case 1: return enc64_g<1>(ctx, K, ids, n, head, T, out, acc, s);
     case 2: return enc64_g<2>(ctx, K, ids, n, head, T, out, acc, s);

@@ -1,4 +1,4 @@
-"""Multi-GPU sharding of the encode path (one process per GPU).
+"""Multi-GPU sharding of the encode and decode paths (one process per GPU).
 
 The sketch is additive: S_k(A ⊎ B) = S_k(A) + S_k(B) mod p
 and counts add, so the id stream is cut into contiguous shards, one per rank,
@@ -9,6 +9,17 @@ the CPU tests) merges them on rank 0.  Partial words are canonical residues
 to 2^27 ranks cannot overflow; rank 0 folds the sum mod p.  last_value comes
 from the last non-empty shard, which rank 0 learns without communication
 (shards are contiguous and their sizes are known to every rank).
+
+Decode shards the same way: rank 0 turns the merged
+difference into coefficients (O(t^2), host), ONE broadcast ships
+[d, stop flag, stop value, c_1..c_d] to every rank, each rank root-tests its
+contiguous log shard on its own GPU (`root_test_shard`, which also reports
+where the stop value first occurs in the shard), ONE all-reduce(MIN) finds
+the global stop position (the caller's `break` at media_client.rs:307-309
+applies to the whole log), and the hit positions — offset by the shard base
+and cut at the global stop — are all-gathered (two small collectives: counts,
+then the padded positions).  Every rank returns the same ascending list,
+identical to the single-GPU root test of the whole log.
 """
 from __future__ import annotations
 
@@ -63,3 +74,68 @@ def reduce_partial_(partial_tensor, threshold: int, bits: int, dst: int = 0, gro
     import torch.distributed as dist
     k = reduce_words(threshold, bits)
     dist.reduce(partial_tensor[:k], dst=dst, op=dist.ReduceOp.SUM, group=group)
+
+
+def _coll_device(group=None):
+    """Device for collective buffers: CUDA for nccl (RCCL), CPU for gloo."""
+    import torch
+    import torch.distributed as dist
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+        else torch.device("cpu")
+
+
+def broadcast_coeffs(coeffs, stop_value, threshold: int, bits: int, src: int = 0, group=None):
+    """Ship rank src's (coefficients, stop value) to every rank: one broadcast
+    of t+3 words.  Other ranks pass coeffs=None.  u64 values travel as their
+    two's-complement int64 image."""
+    import torch
+    import torch.distributed as dist
+    dev = _coll_device(group)
+    buf = torch.zeros(threshold + 3, dtype=torch.int64, device=dev)
+    if dist.get_rank(group) == src:
+        w = np.zeros(threshold + 3, dtype=np.uint64)
+        w[0] = len(coeffs)
+        w[1] = 0 if stop_value is None else 1
+        w[2] = 0 if stop_value is None else int(stop_value)
+        w[3:3 + len(coeffs)] = [int(c) for c in coeffs]
+        buf.copy_(torch.from_numpy(w.view(np.int64)))
+    dist.broadcast(buf, src=src, group=group)
+    w = buf.cpu().numpy().view(np.uint64)
+    d = int(w[0])
+    mask = (1 << bits) - 1
+    coeffs = [int(c) & mask for c in w[3:3 + d]]
+    return coeffs, (int(w[2]) & mask if w[1] else None)
+
+
+def root_test_sharded(local_test, coeffs, log_shard, shard_start: int, stop_value=None, group=None) -> list:
+    """Global ascending hit positions of a root test over a log cut into
+    contiguous shards (this rank holds log[shard_start : shard_start+len]).
+
+    local_test(coeffs, log_shard, stop_value) -> (positions, stop_index) is
+    the shard root test — PowerSumQuackU32/U64.root_test_shard on the GPU."""
+    import torch
+    import torch.distributed as dist
+    dev = _coll_device(group)
+    pos, stop = local_test(coeffs, log_shard, stop_value)
+    n_local = len(log_shard)
+    big = np.iinfo(np.int64).max
+    g_stop = torch.tensor([shard_start + stop if stop < n_local else big], dtype=torch.int64, device=dev)
+    dist.all_reduce(g_stop, op=dist.ReduceOp.MIN, group=group)
+    cut = int(g_stop.item())
+    mine = [shard_start + p for p in pos if shard_start + p < cut]
+    world = dist.get_world_size(group)
+    cnt = torch.tensor([len(mine)], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    width = max(int(c.item()) for c in cnts)
+    if width == 0:
+        return []
+    pad = torch.full((width,), -1, dtype=torch.int64, device=dev)
+    if mine:
+        pad[: len(mine)] = torch.tensor(mine, dtype=torch.int64)
+    bufs = [torch.empty(width, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    out = []
+    for b, c in zip(bufs, cnts):
+        out.extend(int(v) for v in b[: int(c.item())].cpu().tolist())
+    return out

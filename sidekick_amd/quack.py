@@ -299,6 +299,15 @@ class _PowerSumQuack:
         """Positions (log order) of entries of `log` that are roots of
         `coeffs`; with stop_value, only positions before its first
         occurrence (media_client.rs:306-313)."""
+        return self._root_test(coeffs, log, stop_value, ctx, cap, shard=False)[0]
+
+    def root_test_shard(self, coeffs, log, stop_value=None, ctx: Context | None = None, cap: int = 1 << 16):
+        """root_test on one shard of a log: (positions, stop_index) where
+        stop_index is the first position equal to stop_value in this shard,
+        or len(log) (sidekick_amd.dist.root_test_sharded merges shards)."""
+        return self._root_test(coeffs, log, stop_value, ctx, cap, shard=True)
+
+    def _root_test(self, coeffs, log, stop_value, ctx, cap, shard):
         coeffs = list(coeffs)
         d = len(coeffs)
         carr = (self._ELEM * max(d, 1))(*coeffs)
@@ -311,16 +320,21 @@ class _PowerSumQuack:
             dev = _device_array(keep, self.BITS)
         ptr, n, dv, stream = dev
         ctx = ctx or get_context(dv)
+        stop_idx = C.c_uint64(n)
         while True:
             hits = (C.c_uint64 * max(cap, 1))()
             nh = C.c_size_t()
-            rc = self._f("root_test_device")(ctx.handle, carr, d, ptr, n, int(stop_value is not None),
-                                             int(stop_value or 0), hits, cap, C.byref(nh), stream)
+            args = (ctx.handle, carr, d, ptr, n, int(stop_value is not None), int(stop_value or 0), hits, cap,
+                    C.byref(nh))
+            if shard:
+                rc = self._f("root_test_shard_device")(*args, C.byref(stop_idx), stream)
+            else:
+                rc = self._f("root_test_device")(*args, stream)
             if rc == QK_E_CAPACITY:
                 cap = nh.value
                 continue
             check(rc, "root_test_device")
-            return [int(h) for h in hits[: nh.value]]
+            return [int(h) for h in hits[: nh.value]], int(stop_idx.value)
 
     def decode_with_log(self, log, ctx: Context | None = None) -> list:
         """quack's decode_with_log: the ids of `log` that are missing (every

@@ -75,3 +75,89 @@ def test_shard_cover():
             assert sum(c for _, c in parts) == n
             for (s0, c0), (s1, _) in zip(parts, parts[1:]):
                 assert s0 + c0 == s1
+
+
+# ---------------------------------------------------------------- sharded decode
+def _decode_case(bits, seed, n_total, n_drop, stop_at):
+    """Global log, a dropped subset, and the expected single-log answer."""
+    rng = np.random.default_rng(seed)
+    log = (qo.ids_u32 if bits == 32 else qo.ids_u64)(seed, n_total, 0)
+    log[rng.choice(n_total, 3, replace=False)] = log[rng.choice(n_total, 3, replace=False)]  # duplicates
+    drops = sorted(rng.choice(n_total, n_drop, replace=False).tolist())
+    p = qo.MOD[bits]
+    diff = qo.OracleQuack(32, bits)
+    for i in drops:
+        diff.insert(int(log[i]))
+    coeffs = diff.to_coeffs()
+    stop = None if stop_at is None else int(log[stop_at])
+    want = qo.root_test_indices(coeffs, log.tolist(), p, stop_value=stop)
+    return log, coeffs, stop, want
+
+
+def _oracle_shard_test(bits):
+    def run(coeffs, shard, stop):
+        vals = shard.tolist()
+        pos = qo.root_test_indices(coeffs, vals, qo.MOD[bits], stop_value=stop)
+        si = vals.index(stop) if stop is not None and stop in vals else len(vals)
+        return pos, si
+    return run
+
+
+def _decode_worker(rank, world, port, bits, seed, n_total, n_drop, stop_at, use_gpu, q):
+    import torch
+    from sidekick_amd import dist as skd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        log, coeffs, stop, want = _decode_case(bits, seed, n_total, n_drop, stop_at)
+        c, s = skd.broadcast_coeffs(coeffs if rank == 0 else None, stop if rank == 0 else None, 32, bits)
+        assert c == [int(v) for v in coeffs] and s == stop
+        start, cnt = skd.shard(n_total, rank, world)
+        shard = log[start:start + cnt]
+        if use_gpu:
+            import sidekick_amd as sk
+            qcls = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+            dev = torch.from_numpy(shard.view(np.int32 if bits == 32 else np.int64).copy()).cuda()
+            test = lambda cc, _sh, st: qcls(32).root_test_shard(cc, dev, stop_value=st)  # noqa: E731
+        else:
+            test = _oracle_shard_test(bits)
+        got = skd.root_test_sharded(test, c, shard, start, s)
+        q.put((rank, got == want, len(want)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_decode(world, bits, n_total, n_drop, stop_at, use_gpu, seed=0xDEC0):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_decode_worker,
+                         args=(r, world, port, bits, seed, n_total, n_drop, stop_at, use_gpu, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
+    return res[0][2]
+
+
+@pytest.mark.parametrize("world,bits,stop_at", [(2, 32, None), (2, 32, 1500), (3, 32, 200), (3, 64, 2500),
+                                                (2, 64, None)])
+def test_sharded_root_test_matches_single_log(world, bits, stop_at):
+    """SURVEY §8e decode sharding: broadcast coefficients, per-shard root
+    test with the stop position, MIN-reduce of the stop, all-gather of hits
+    == the single-log root test (media_client.rs:306-313)."""
+    nh = _run_decode(world, bits, 3000, 12, stop_at, use_gpu=False)
+    assert nh > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,stop_at", [(32, None), (32, 40_000), (64, 70_000)])
+def test_sharded_root_test_gpu_two_ranks(bits, stop_at):
+    """The same merge with each rank's shard tested by the gfx950 root test
+    (two processes on one GPU, gloo for the small collectives)."""
+    _run_decode(2, bits, 100_000, 20, stop_at, use_gpu=True)

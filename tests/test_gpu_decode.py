@@ -96,6 +96,29 @@ def test_stop_at_last_value():
     assert q.root_test(c, d, stop_value=int(log[5000])) == want
 
 
+def test_root_test_shard_reports_stop_index():
+    """qk_*_root_test_shard_device: the shard's hits (cut at its own stop)
+    plus the position of the first stop value (len when absent); d = 0 still
+    reports the stop.  Duplicated stop value -> first occurrence."""
+    log = coracle.splitmix_u32(45, 20_000)
+    log[7000] = log[3000]
+    q = sk.PowerSumQuackU32(8)
+    for i in (10, 5000, 15000):
+        q.insert(int(log[i]))
+    c = q.to_coeffs()
+    d = dev(log)
+    assert q.root_test_shard(c, d) == ([10, 5000, 15000], len(log))
+    assert q.root_test_shard(c, d, stop_value=int(log[3000])) == ([10], 3000)
+    absent = next(v for v in range(1, 100) if v not in set(log.tolist()))
+    assert q.root_test_shard(c, d, stop_value=absent) == ([10, 5000, 15000], len(log))
+    assert q.root_test_shard([], d, stop_value=int(log[12345])) == ([], 12345)
+    assert q.root_test_shard([], d) == ([], len(log))
+    log64 = coracle.splitmix_u64(46, 5000)
+    q64 = sk.PowerSumQuackU64(4)
+    q64.insert(int(log64[100]))
+    assert q64.root_test_shard(q64.to_coeffs(), dev(log64, 64), stop_value=int(log64[4000])) == ([100], 4000)
+
+
 def test_many_hits_capacity_growth():
     # a log made mostly of roots: > the 4096 default device hit capacity
     roots = coracle.splitmix_u32(8, 4)

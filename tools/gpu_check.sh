@@ -22,9 +22,10 @@ for s in $STEPS; do
   case $s in
     ubench) step ubench 120 ./tools/ubench_int || exit 3 ;;
     smoke) step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
-    pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA ${PYTEST_ARGS:-}; rc=$?; ok_or_testfail $rc || exit 3 ;;
+    pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
     configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
+    configs20) QK_TUNE_U64_KMAX=20 step configs20 900 python3 -u tools/bench_configs.py u64 || exit 3 ;;
     prof)
       export TMPDIR=/tmp
       step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 1 --cpu-sample 0 || exit 3 ;;
