@@ -219,6 +219,22 @@ def main():
         }
         if not parity:
             log("PARITY FAILURE: GPU power sums differ from the CPU oracle on the sample prefix")
+        # all host cores of this process's share: the same loop,
+        # one partial per thread, merged; the same per-thread sample size
+        thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        thr = max(1, min(thr, 64))
+        mm = int(min(m * thr, cnt))
+        tc = time.perf_counter()
+        mt_S = coracle.encode_seed_mt(bits, args.seed, mm, t, thr, start=start)
+        mt_s = time.perf_counter() - tc
+        q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
+        q.insert_batch(ids[:mm])
+        out["cpu_baseline_all_cores"] = {
+            "value": mm / mt_s, "unit": "identifiers/s", "cores": thr, "kind": "port",
+            "sample": f"first {mm} ids of the same stream, {thr} threads x {mm // thr} ids, one partial sketch "
+                      f"per thread merged (oracle/quack_oracle.c qo_encode_seed_mt), {mt_s:.1f} s",
+            "parity_with_gpu": q.power_sums() == mt_S,
+        }
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

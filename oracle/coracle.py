@@ -36,6 +36,8 @@ def lib():
             "qo_encode_u32_seed": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u32p]),
             "qo_encode_u64": (None, [u64p, C.c_uint64, C.c_uint32, u64p]),
             "qo_encode_u64_seed": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
+            "qo_encode_seed_mt": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                            C.c_void_p]),
             "qo_to_coeffs_u32": (None, [u32p, C.c_uint32, u32p]),
             "qo_to_coeffs_u64": (None, [u64p, C.c_uint32, u64p]),
             "qo_eval_u32": (C.c_uint32, [u32p, C.c_uint32, C.c_uint32]),
@@ -77,6 +79,16 @@ def encode_u32(ids, t):
 def encode_u32_seed(seed, n, t, start=0):
     S = np.zeros(t, dtype=np.uint32)
     lib().qo_encode_u32_seed(seed, start, n, t, _p(S, C.c_uint32))
+    return [int(v) for v in S]
+
+
+def encode_seed_mt(bits, seed, n, t, threads, start=0):
+    """All-cores restatement (one partial per thread, merged): bench.py's
+    cpu_baseline_all_cores leg."""
+    S = np.zeros(t, dtype=np.uint32 if bits == 32 else np.uint64)
+    rc = lib().qo_encode_seed_mt(bits, seed, start, n, t, threads, S.ctypes.data)
+    if rc:
+        raise RuntimeError(f"qo_encode_seed_mt rc={rc}")
     return [int(v) for v in S]
 
 

@@ -21,8 +21,10 @@
  * Decode (media_client.rs:295-313): Newton's identities (to_coeffs) and the
  * Horner root test (arithmetic::eval(&coeffs, id).value() == 0).
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 
 #define QO_P32 4294967291u                 /* 2^32 - 5  */
 #define QO_P64 18446744073709551557ull     /* 2^64 - 59 */
@@ -159,4 +161,48 @@ uint64_t qo_root_test_u64(const uint64_t *c, uint32_t d, const uint64_t *log, ui
     for (uint64_t i = 0; i < n; ++i)
         if (qo_eval_u64(c, d, log[i]) == 0) { if (nh < cap) hits[nh] = (int64_t)i; ++nh; }
     return nh;
+}
+
+
+/* ---- all-cores CPU baseline: the same scalar insert loop on
+ * nthreads threads, one partial sketch per thread over a contiguous slice,
+ * merged at the end (the sketch is additive). */
+typedef struct {
+    uint64_t seed, start, n;
+    uint32_t t, bits;
+    void *S;
+} qo_job;
+
+static void *qo_worker(void *arg) {
+    qo_job *j = (qo_job *)arg;
+    if (j->bits == 32) qo_encode_u32_seed(j->seed, j->start, j->n, j->t, (uint32_t *)j->S);
+    else qo_encode_u64_seed(j->seed, j->start, j->n, j->t, (uint64_t *)j->S);
+    return 0;
+}
+
+/* returns 0 on success */
+int qo_encode_seed_mt(uint32_t bits, uint64_t seed, uint64_t start, uint64_t n, uint32_t t, uint32_t nthreads,
+                      void *S) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    qo_job job[256];
+    const size_t esz = bits == 32 ? 4 : 8;
+    uint8_t *parts = (uint8_t *)calloc((size_t)nthreads * t, esz);
+    if (!parts) return -1;
+    uint32_t started = 0;
+    for (uint32_t i = 0; i < nthreads; ++i, ++started) {
+        const uint64_t b = n * i / nthreads, e = n * (i + 1) / nthreads;
+        job[i] = (qo_job){seed, start + b, e - b, t, bits, parts + (size_t)i * t * esz};
+        if (pthread_create(&th[i], 0, qo_worker, &job[i])) break;
+    }
+    for (uint32_t i = 0; i < started; ++i) pthread_join(th[i], 0);
+    if (started < nthreads) { free(parts); return -2; }
+    for (uint32_t i = 0; i < nthreads; ++i)
+        for (uint32_t k = 0; k < t; ++k) {
+            if (bits == 32) ((uint32_t *)S)[k] = add32(((uint32_t *)S)[k], ((uint32_t *)parts)[(size_t)i * t + k]);
+            else ((uint64_t *)S)[k] = add64(((uint64_t *)S)[k], ((uint64_t *)parts)[(size_t)i * t + k]);
+        }
+    free(parts);
+    return 0;
 }

@@ -131,3 +131,12 @@ def test_stop_value_semantics():
     assert qo.root_test_indices(c, log, qo.P32) == [2, 4]
     assert qo.root_test_indices(c, log, qo.P32, stop_value=7) == [2]
     assert qo.root_test_indices(c, log, qo.P32, stop_value=5) == []
+
+
+def test_all_cores_restatement_matches_scalar():
+    """bench.py's all-cores CPU baseline (one partial per thread, merged)
+    equals the 1-core loop on the same stream."""
+    from oracle import coracle
+    for bits, n, t, thr in ((32, 100_003, 32, 7), (32, 5, 16, 8), (64, 20_001, 80, 3)):
+        one = (coracle.encode_u32_seed if bits == 32 else coracle.encode_u64_seed)(0xBEEF, n, t, start=11)
+        assert coracle.encode_seed_mt(bits, 0xBEEF, n, t, thr, start=11) == one

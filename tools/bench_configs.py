@@ -174,6 +174,48 @@ def run_packets(args, ctx):
           "inserted": st["inserted"], "seconds": tm})
 
 
+def run_flows(args, ctx):
+    """SidekickMulti batch (sidekick_multi.rs:101-143): n 67-byte records of F
+    flows in HBM -> one quACK per AddrKey (extract, radix-sort grouping,
+    segmented encode, keys + sketches copied to the host)."""
+    import ctypes as C
+    from sidekick_amd._lib import lib
+    from sidekick_amd.quack import FlowKey, PktStats
+    n, stride, t = int(args.npkts), 67, 32
+    raw = torch.empty(n * stride, dtype=torch.uint8, device=DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    raw.random_(0, 256, generator=g)
+    rec = raw.view(n, stride)
+    rec[:, 23] = 17
+    for nflows in (16, 10_000, 1_000_000):
+        f = torch.randint(0, nflows, (n,), device=DEV, generator=g, dtype=torch.int64)
+        for k in range(4):                       # src ip = flow id (LE bytes), fixed ports / dst
+            rec[:, 26 + k] = ((f >> (8 * k)) & 255).to(torch.uint8)
+        rec[:, 30:38] = torch.tensor([192, 168, 0, 9, 0x11, 0x5C, 0x1F, 0x90], dtype=torch.uint8, device=DEV)
+        cap = nflows
+        rsz = lib().qk_u32_size(t)
+        keys = (FlowKey * cap)()
+        sk_buf = C.create_string_buffer(cap * rsz)
+        times = []
+        for it in range(max(3, args.steps // 2) + 1):
+            nf, st = C.c_size_t(), PktStats()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rc = lib().qk_u32_encode_flows_device(ctx.handle, raw.data_ptr(), n, stride, None, None, t, keys, sk_buf,
+                                                  cap, C.byref(nf), C.byref(st), 0)
+            torch.cuda.synchronize()
+            if rc != 0:
+                raise RuntimeError(f"encode_flows rc={rc}")
+            if it:
+                times.append(time.perf_counter() - t0)
+        tm = float(np.median(times))
+        emit({"config": f"per-flow batch: {n} records of {nflows} flows -> one quACK per AddrKey, t={t}",
+              "n_packets": n, "flows": int(nf.value), "packets_per_s": n / tm, "record_GBps": n * stride / tm / 1e9,
+              "seconds": tm, "inserted": int(st.inserted)})
+        del f
+
+
 def run_sweep(args, ctx):
     n = int(args.nsweep)
     ids = torch.empty(n, dtype=torch.int32, device=DEV)
@@ -185,7 +227,7 @@ def run_sweep(args, ctx):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "packets"])
+    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "packets", "flows"])
     ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--n64", type=float, default=1e9)
@@ -199,7 +241,7 @@ def main():
     ctx = sk.get_context(0)
     for w in args.what:
         {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep,
-         "packets": run_packets}[w](args, ctx)
+         "packets": run_packets, "flows": run_flows}[w](args, ctx)
         torch.cuda.empty_cache()
 
 

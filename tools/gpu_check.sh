@@ -21,9 +21,14 @@ STEPS="${STEPS:-ubench smoke pytest bench prof}"
 for s in $STEPS; do
   case $s in
     ubench) step ubench 120 ./tools/ubench_int || exit 3 ;;
+    ubdep) step ubdep 300 ./tools/ubench_dep || exit 3 ;;
     smoke) step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
     pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
+    scgsweep)
+      for g in ${SCG_LIST:-0 1 2 3 4 5 6}; do
+        QK_TUNE_BSGS_SCG=$g step scg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 || exit 3
+      done ;;
     configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
     configs20) QK_TUNE_U64_KMAX=20 step configs20 900 python3 -u tools/bench_configs.py u64 || exit 3 ;;
     prof)
