@@ -223,7 +223,7 @@ def main():
         # one partial per thread, merged; the same per-thread sample size
         thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         thr = max(1, min(thr, 64))
-        mm = int(min(m * thr, cnt))
+        mm = int(min(m * thr // 3, cnt))  # ~1/3 of the 1-core sample per thread
         tc = time.perf_counter()
         mt_S = coracle.encode_seed_mt(bits, args.seed, mm, t, thr, start=start)
         mt_s = time.perf_counter() - tc

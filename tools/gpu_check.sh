@@ -40,6 +40,12 @@ for s in $STEPS; do
     pmcsq)
       export TMPDIR=/tmp
       step pmcsq 600 rocprofv3 --pmc ${PMC_SQ:-SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE} --output-format csv -d "$OUT/pmcsq" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
+    pmcab)  # SQ stall/issue counters for two BSGS variants (A/B), two counter passes each
+      export TMPDIR=/tmp
+      for g in ${SCG_AB:-0 6}; do
+        QK_TUNE_BSGS_SCG=$g step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
+        QK_TUNE_BSGS_SCG=$g step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
+      done ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;

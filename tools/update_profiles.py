@@ -23,7 +23,8 @@ def main(rnd: str, src: str = "gpurun_out", key: str = "u32_t32", n_ids: int = 1
     copies = {"prof/run_kernel_stats.csv": "encode_kernel_stats.csv",
               "pmc/run_counter_collection.csv": "encode_pmc_fetch_size.csv",
               "pmcsq/run_counter_collection.csv": "encode_pmc_sq.csv",
-              "ubench.log": "ubench_int.json", "tune.log": "tune_encode.json"}
+              "ubench.log": "ubench_int.json", "tune.log": "tune_encode.json", "ubdep.log": "ubench_dep.json",
+              "pytest.log": "pytest_gpu.log", "smoke.log": "smoke.log"}
     for a, b in copies.items():
         if os.path.exists(os.path.join(src, a)):
             shutil.copy(os.path.join(src, a), os.path.join(dst, b))
@@ -32,6 +33,14 @@ def main(rnd: str, src: str = "gpurun_out", key: str = "u32_t32", n_ids: int = 1
         lines = [l for l in open(bench) if l.startswith("{")]
         if lines:
             open(os.path.join(dst, "bench_n1.json"), "w").write(lines[-1])
+
+    # tools/bench_configs.py rows (configs*.log): one JSON object per line
+    rows = []
+    for name in sorted(os.listdir(src)):
+        if name.startswith("configs") and name.endswith(".log"):
+            rows += [l for l in open(os.path.join(src, name)) if l.startswith("{")]
+    if rows:
+        open(os.path.join(dst, "configs.jsonl"), "w").write("".join(rows))
 
     out = {}
     pmc = os.path.join(src, "pmc/run_counter_collection.csv")
