@@ -51,6 +51,20 @@ int ensure_scratch(qk_ctx *ctx, size_t bytes) {
     return QK_OK;
 }
 
+int ensure_flow(qk_ctx *ctx, int which, size_t bytes) {
+    if (bytes <= ctx->flow_bytes[which]) return QK_OK;
+    if (ctx->d_flow[which]) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->d_flow[which]);
+        ctx->d_flow[which] = nullptr;
+        ctx->flow_bytes[which] = 0;
+    }
+    const size_t sz = std::max(bytes + bytes / 8, (size_t)1 << 20); // headroom for growing batches
+    if (hipMalloc(&ctx->d_flow[which], sz) != hipSuccess) return QK_E_NOMEM;
+    ctx->flow_bytes[which] = sz;
+    return QK_OK;
+}
+
 int ensure_hits(qk_ctx *ctx, size_t cap) {
     if (cap <= ctx->hits_cap) return QK_OK;
     if (ctx->d_hits) {
@@ -303,6 +317,8 @@ void qk_ctx_destroy(qk_ctx *ctx) {
     if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
     if (ctx->d_scratch) hipFree(ctx->d_scratch);
     if (ctx->d_hits) hipFree(ctx->d_hits);
+    for (void *f : ctx->d_flow)
+        if (f) hipFree(f);
     if (ctx->d_small) hipFree(ctx->d_small);
     if (ctx->h_small) hipHostFree(ctx->h_small);
     if (ctx->stream) hipStreamDestroy(ctx->stream);

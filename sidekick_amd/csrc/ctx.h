@@ -22,6 +22,13 @@ struct qk_ctx {
     uint64_t *d_hits = nullptr;
     size_t hits_cap = 0;
 
+    // per-flow batches (flows.hip): per-packet arena (keys, ids, sort buffers)
+    // and per-flow arena (segment info, accumulators, work items); grow-only,
+    // reused across calls (a stream-ordered malloc/free of GBs per batch costs
+    // more than the whole pipeline)
+    void *d_flow[2] = {nullptr, nullptr};
+    size_t flow_bytes[2] = {0, 0};
+
     // host-input pipeline: pinned staging + device chunk buffers (2 slots)
     void *h_stage[2] = {nullptr, nullptr};
     void *d_stage[2] = {nullptr, nullptr};
@@ -61,6 +68,7 @@ int scratch_acquire(qk_ctx *ctx, hipStream_t s);
 int scratch_release(qk_ctx *ctx, hipStream_t s);
 int ensure_scratch(qk_ctx *ctx, size_t bytes);
 int ensure_hits(qk_ctx *ctx, size_t cap);
+int ensure_flow(qk_ctx *ctx, int which, size_t bytes);
 int ensure_stage(qk_ctx *ctx, size_t bytes);
 bool is_device_ptr(const void *p);
 hipEvent_t prof_begin(qk_ctx *ctx, hipStream_t s);

@@ -121,14 +121,14 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     const uint64_t np = n - p0 < (uint64_t)REC_TILE ? n - p0 : (uint64_t)REC_TILE;
     const uint32_t r0 = stage_records(bufs, n, stride, p0, np, tile);
     __syncthreads();
-    if (threadIdx.x >= np) return;
+    const bool valid = threadIdx.x < np;
     const uint64_t i = p0 + threadIdx.x;
     const uint8_t *rec = tile + r0 + threadIdx.x * stride;
-    const qk_pkt_meta m = record_meta(meta, i);
     uint64_t kh = KEY_INVALID, kl = KEY_INVALID;
     uint32_t id = 0;
     int cls = 0; // 0 skip, 1 insert, 2 reset
-    if (record_is_incoming_udp(m, rec)) {
+    const qk_pkt_meta m = valid ? record_meta(meta, i) : qk_pkt_meta{};
+    if (valid && record_is_incoming_udp(m, rec)) {
         // AddrKey, packed big-endian so numeric order == byte order
         const uint64_t src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
                              ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];
@@ -142,12 +142,19 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
             id = record_identifier(rec);
         }
     }
-    key_hi[i] = kh;
-    key_lo[i] = kl;
-    ids[i] = id;
-    order[i] = (uint32_t)i;
-    if (cls == 1) atomicAdd(&counters[0], 1ull);
-    if (cls == 2) atomicAdd(&counters[1], 1ull);
+    if (valid) {
+        key_hi[i] = kh;
+        key_lo[i] = kl;
+        ids[i] = id;
+        order[i] = (uint32_t)i;
+    }
+    // one atomic per workgroup (a per-packet atomic on one address
+    // serialises: 1.2 s per 1e8 packets)
+    const int ins = __syncthreads_count(cls == 1), rst = __syncthreads_count(cls == 2);
+    if (threadIdx.x == 0) {
+        if (ins) atomicAdd(&counters[0], (unsigned long long)ins);
+        if (rst) atomicAdd(&counters[1], (unsigned long long)rst);
+    }
 }
 
 template <typename T, typename I>
@@ -206,19 +213,41 @@ static int seg_launch_g(int K, const uint32_t *ids, const SegItem *items, uint32
     }
 }
 
-// Segmented encode of a grouped id array (CSR offsets on the host) into a
-// device accumulator [nseg][T] (u64, zeroed here).
-static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const std::vector<uint64_t> &offs, uint32_t T,
-                      unsigned long long *d_acc, hipStream_t s) {
-    const size_t nseg = offs.size() - 1;
+// Bump allocator over a ctx flow arena (256-byte aligned sub-buffers); with
+// base == nullptr it only measures.
+struct Carve {
+    char *base;
+    size_t off = 0;
+    template <typename T> T *take(size_t count) {
+        off = (off + 255) & ~(size_t)255;
+        T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
+        off += std::max<size_t>(count * sizeof(T), 8);
+        return p;
+    }
+};
+
+// last id of each non-empty segment
+__global__ void k_seg_last(const uint32_t *__restrict__ ids, const uint64_t *__restrict__ offs, uint64_t nseg,
+                           uint32_t *__restrict__ last) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nseg) last[i] = offs[i + 1] > offs[i] ? ids[offs[i + 1] - 1] : 0u;
+}
+
+static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs) {
     std::vector<SegItem> items;
-    for (size_t g = 0; g < nseg; ++g)
+    for (size_t g = 0; g + 1 < offs.size(); ++g)
         for (uint64_t lo = offs[g]; lo < offs[g + 1]; lo += SEG_CHUNK)
             items.push_back({(uint32_t)g, 0u, lo, std::min<uint64_t>(lo + SEG_CHUNK, offs[g + 1])});
+    return items;
+}
+
+// Segmented encode of a grouped id array (work items from seg_items) into a
+// device accumulator [nseg][T] (u64, zeroed here); d_items holds
+// items.size() entries.
+static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const std::vector<SegItem> &items, size_t nseg,
+                      uint32_t T, unsigned long long *d_acc, SegItem *d_items, hipStream_t s) {
     QK_HIP_TRY(hipMemsetAsync(d_acc, 0, nseg * T * sizeof(uint64_t), s));
     if (items.empty()) return QK_OK;
-    SegItem *d_items = nullptr;
-    QK_HIP_TRY(hipMallocAsync((void **)&d_items, items.size() * sizeof(SegItem), s));
     int rc = QK_OK;
     if (hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(SegItem), hipMemcpyHostToDevice, s) != hipSuccess)
         rc = QK_E_HIP;
@@ -240,7 +269,6 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const std::vector<uint
     }
     // the host vector `items` must outlive the async copy
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = QK_E_HIP;
-    (void)hipFreeAsync(d_items, s);
     return rc;
 }
 
@@ -262,20 +290,32 @@ extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids,
     QK_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = pick_stream(ctx, stream);
     const uint32_t T = threshold;
-    unsigned long long *d_acc = nullptr;
-    QK_HIP_TRY(hipMallocAsync((void **)&d_acc, nseg * T * sizeof(uint64_t), s));
-    int rc = seg_encode(ctx, d_ids, offs, T, d_acc, s);
+    const std::vector<SegItem> items = seg_items(offs);
+    Carve probe{nullptr};
+    probe.take<unsigned long long>(nseg * T);
+    probe.take<SegItem>(items.size());
+    probe.take<uint32_t>(nseg);
+    probe.take<uint64_t>(nseg + 1);
+    if (int e = ensure_flow(ctx, 1, probe.off)) return e;
+    Carve cv{(char *)ctx->d_flow[1]};
+    unsigned long long *d_acc = cv.take<unsigned long long>(nseg * T);
+    SegItem *d_items = cv.take<SegItem>(items.size());
+    uint32_t *d_last = cv.take<uint32_t>(nseg);
+    uint64_t *d_offs = cv.take<uint64_t>(nseg + 1);
+    int rc = seg_encode(ctx, d_ids, items, nseg, T, d_acc, d_items, s);
     std::vector<uint64_t> acc(nseg * T);
     std::vector<uint32_t> last(nseg, 0);
     if (!rc && hipMemcpyAsync(acc.data(), d_acc, acc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = QK_E_HIP;
-    for (size_t i = 0; !rc && i < nseg; ++i)
-        if (offs[i + 1] > offs[i] &&
-            hipMemcpyAsync(&last[i], d_ids + offs[i + 1] - 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
-            rc = QK_E_HIP;
+    if (!rc && hipMemcpyAsync(d_offs, offs.data(), (nseg + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+        rc = QK_E_HIP;
+    if (!rc) {
+        hipLaunchKernelGGL(k_seg_last, dim3((uint32_t)((nseg + 255) / 256)), dim3(256), 0, s, d_ids, d_offs,
+                           (uint64_t)nseg, d_last);
+        if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+    }
+    if (!rc && hipMemcpyAsync(last.data(), d_last, nseg * 4, hipMemcpyDeviceToHost, s) != hipSuccess) rc = QK_E_HIP;
     if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = QK_E_HIP;
-    (void)hipFreeAsync(d_acc, s);
-    (void)hipStreamSynchronize(s);
     if (rc) return rc;
     const size_t rec = qk_u32_size(T);
     for (size_t i = 0; i < nseg; ++i) {
@@ -312,21 +352,41 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     hipStream_t s = pick_stream(ctx, stream);
     const uint32_t T = threshold;
 
-    // device scratch: keys (2 x 2 x u64), ids (2 x u32), order (2 x u32), flags, heads, counters
+    // device scratch (ctx flow arena 0): keys (2 x 2 x u64), ids (2 x u32),
+    // order (2 x u32), flags, heads, counters, hipCUB temp storage
+    size_t tb1 = 0, tb2 = 0;
+    {
+        uint64_t *k0 = nullptr;
+        uint32_t *o0 = nullptr, *h0 = nullptr;
+        uint8_t *f0 = nullptr;
+        if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, k0, k0, o0, o0, (uint32_t)n, 0, 49, s) != hipSuccess ||
+            hipcub::DeviceSelect::Flagged(nullptr, tb2, hipcub::CountingInputIterator<uint32_t>(0), f0, h0, h0,
+                                          (int64_t)n, s) != hipSuccess)
+            return QK_E_HIP;
+    }
+    auto layout = [&](Carve &c, uint64_t *&kh, uint64_t *&kl, uint64_t *&kh2, uint64_t *&kl2, uint32_t *&ids,
+                      uint32_t *&ids2, uint32_t *&ord, uint32_t *&ord2, uint32_t *&heads, uint8_t *&flag,
+                      unsigned long long *&counters, void *&temp) {
+        kh = c.take<uint64_t>(n); kl = c.take<uint64_t>(n); kh2 = c.take<uint64_t>(n); kl2 = c.take<uint64_t>(n);
+        ids = c.take<uint32_t>(n); ids2 = c.take<uint32_t>(n); ord = c.take<uint32_t>(n); ord2 = c.take<uint32_t>(n);
+        heads = c.take<uint32_t>(n); flag = c.take<uint8_t>(n); counters = c.take<unsigned long long>(4);
+        temp = c.take<char>(std::max(tb1, tb2));
+    };
     uint64_t *kh = nullptr, *kl = nullptr, *kh2 = nullptr, *kl2 = nullptr;
     uint32_t *ids = nullptr, *ids2 = nullptr, *ord = nullptr, *ord2 = nullptr, *heads = nullptr;
     uint8_t *flag = nullptr;
     unsigned long long *counters = nullptr, *acc = nullptr;
     void *temp = nullptr;
     uint64_t *info = nullptr;
+    {
+        Carve probe{nullptr};
+        layout(probe, kh, kl, kh2, kl2, ids, ids2, ord, ord2, heads, flag, counters, temp);
+        if (int e = ensure_flow(ctx, 0, probe.off)) return e;
+        Carve cv{(char *)ctx->d_flow[0]};
+        layout(cv, kh, kl, kh2, kl2, ids, ids2, ord, ord2, heads, flag, counters, temp);
+    }
     int rc = QK_OK;
-    auto A = [&](void **p, size_t b) {
-        if (!rc && hipMallocAsync(p, b ? b : 8, s) != hipSuccess) rc = QK_E_NOMEM;
-    };
-    A((void **)&kh, n * 8); A((void **)&kl, n * 8); A((void **)&kh2, n * 8); A((void **)&kl2, n * 8);
-    A((void **)&ids, n * 4); A((void **)&ids2, n * 4); A((void **)&ord, n * 4); A((void **)&ord2, n * 4);
-    A((void **)&heads, n * 4); A((void **)&flag, n); A((void **)&counters, 4 * 8);
-    if (!rc && hipMemsetAsync(counters, 0, 4 * 8, s) != hipSuccess) rc = QK_E_HIP;
+    if (hipMemsetAsync(counters, 0, 4 * 8, s) != hipSuccess) rc = QK_E_HIP;
     const uint32_t ntiles = (uint32_t)((n + REC_TILE - 1) / REC_TILE);
     if (!rc) {
         hipLaunchKernelGGL(k_flow_extract, dim3(ntiles), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s, d_bufs,
@@ -334,13 +394,6 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
     }
     // stable LSD sort: by dst ip:port, then by src ip:port (49-bit keys)
-    size_t tb1 = 0, tb2 = 0;
-    if (!rc && hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, kl, kl2, ord, ord2, (uint32_t)n, 0, 49, s) != hipSuccess)
-        rc = QK_E_HIP;
-    if (!rc && hipcub::DeviceSelect::Flagged(nullptr, tb2, hipcub::CountingInputIterator<uint32_t>(0), flag, heads,
-                                             (uint32_t *)(counters + 2), (int64_t)n, s) != hipSuccess)
-        rc = QK_E_HIP;
-    A(&temp, std::max(tb1, tb2));
     const uint32_t gb = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 8);
     if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb1, kl, kl2, ord, ord2, (uint32_t)n, 0, 49, s) != hipSuccess)
         rc = QK_E_HIP;
@@ -372,8 +425,23 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     }
     if (!rc && nseg) {
         std::vector<uint32_t> hs(nseg);
-        A((void **)&info, (size_t)nseg * 32);
-        A((void **)&acc, (size_t)nseg * T * 8);
+        // per-flow arena 1 (arena 0 still holds the grouped ids): info, acc,
+        // work items (at most one per flow plus one per SEG_CHUNK ids)
+        const size_t items_max = (size_t)nseg + inserted / SEG_CHUNK + 1;
+        SegItem *d_items = nullptr;
+        {
+            Carve probe{nullptr};
+            probe.take<uint64_t>((size_t)nseg * 4);
+            probe.take<unsigned long long>((size_t)nseg * T);
+            probe.take<SegItem>(items_max);
+            rc = ensure_flow(ctx, 1, probe.off);
+        }
+        if (!rc) {
+            Carve cv{(char *)ctx->d_flow[1]};
+            info = cv.take<uint64_t>((size_t)nseg * 4);
+            acc = cv.take<unsigned long long>((size_t)nseg * T);
+            d_items = cv.take<SegItem>(items_max);
+        }
         if (!rc) hipLaunchKernelGGL(k_seg_info, dim3((nseg + 255) / 256), dim3(256), 0, s, kh, kl2, ids2, heads, nseg,
                                     inserted, info);
         std::vector<uint64_t> hinfo((size_t)nseg * 4);
@@ -384,7 +452,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         std::vector<uint64_t> offs(nseg + 1);
         for (uint32_t i = 0; i < nseg; ++i) offs[i] = hs[i];
         offs[nseg] = inserted;
-        if (!rc) rc = seg_encode(ctx, ids2, offs, T, acc, s);
+        const std::vector<SegItem> items = seg_items(offs);
+        if (!rc) rc = seg_encode(ctx, ids2, items, nseg, T, acc, d_items, s);
         std::vector<uint64_t> hacc((size_t)nseg * T);
         if (!rc && (hipMemcpyAsync(hacc.data(), acc, hacc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess))
@@ -407,10 +476,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             }
         }
     }
-    for (void *p : {(void *)kh, (void *)kl, (void *)kh2, (void *)kl2, (void *)ids, (void *)ids2, (void *)ord,
-                    (void *)ord2, (void *)heads, (void *)flag, (void *)counters, temp, (void *)info, (void *)acc})
-        if (p) (void)hipFreeAsync(p, s);
-    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s); // the arenas are reused by the next call
     if (stats) *stats = st;
     return rc;
 }

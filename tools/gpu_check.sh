@@ -40,6 +40,9 @@ for s in $STEPS; do
     pmcsq)
       export TMPDIR=/tmp
       step pmcsq 600 rocprofv3 --pmc ${PMC_SQ:-SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE} --output-format csv -d "$OUT/pmcsq" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
+    proflows)
+      export TMPDIR=/tmp
+      step proflows 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflows" -o run -- python3 "$ROOT/tools/bench_configs.py" flows packets --steps 4 || exit 3 ;;
     pmcab)  # SQ stall/issue counters for two BSGS variants (A/B), two counter passes each
       export TMPDIR=/tmp
       for g in ${SCG_AB:-0 6}; do
