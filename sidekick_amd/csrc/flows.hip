@@ -37,6 +37,9 @@
 
 namespace qk {
 
+static_assert(sizeof(qk_flow_key) == 12, "qk_flow_key is 12 packed bytes");
+static_assert(sizeof(qk_u32) == 16, "qk_u32 header is 4 words (k_flow_finalize writes it)");
+
 constexpr int SG_BLOCK = 256;
 constexpr int SG_WAVES = SG_BLOCK / 64;
 constexpr uint64_t KEY_INVALID = 1ull << 48; // above every 48-bit ip:port
@@ -180,6 +183,30 @@ __global__ void k_seg_info(const uint64_t *__restrict__ kh, const uint64_t *__re
     info[4 * s + 1] = kl[b];
     info[4 * s + 2] = e - b;
     info[4 * s + 3] = ids[e - 1];
+}
+
+// qk_u32 records (header + T canonical sums) and AddrKey bytes of every flow,
+// written on the device so the host receives exactly its output in two copies
+__global__ void k_flow_finalize(const unsigned long long *__restrict__ acc, const uint64_t *__restrict__ info,
+                                uint64_t nseg, uint32_t T, uint32_t *__restrict__ rec, uint8_t *__restrict__ keys) {
+    const uint64_t words = 4ull + T, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nseg * words; j += stride) {
+        const uint64_t i = j / words;
+        const uint32_t w = (uint32_t)(j - i * words);
+        uint32_t v;
+        if (w == 0) v = T;
+        else if (w == 1) v = (uint32_t)info[4 * i + 2];  // count
+        else if (w == 2) v = 1u;                          // has_last
+        else if (w == 3) v = (uint32_t)info[4 * i + 3];  // last_value
+        else v = canon32(fold64_32(acc[i * T + (w - 4)]));
+        rec[j] = v;
+    }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nseg * 12; j += stride) {
+        const uint64_t i = j / 12;
+        const uint32_t b = (uint32_t)(j - i * 12);
+        const uint64_t k = b < 6 ? info[4 * i] : info[4 * i + 1];
+        keys[j] = (uint8_t)(k >> (40 - 8 * (b % 6)));
+    }
 }
 
 // (G, K) for a threshold: smallest G with ceil(T/G) <= 32, K = ceil(T/G) rounded to a supported size
@@ -426,14 +453,20 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     if (!rc && nseg) {
         std::vector<uint32_t> hs(nseg);
         // per-flow arena 1 (arena 0 still holds the grouped ids): info, acc,
-        // work items (at most one per flow plus one per SEG_CHUNK ids)
+        // work items (at most one per flow plus one per SEG_CHUNK ids), and
+        // the output records and keys
         const size_t items_max = (size_t)nseg + inserted / SEG_CHUNK + 1;
+        const size_t rec = qk_u32_size(T);
         SegItem *d_items = nullptr;
+        uint32_t *d_rec = nullptr;
+        uint8_t *d_keys = nullptr;
         {
             Carve probe{nullptr};
             probe.take<uint64_t>((size_t)nseg * 4);
             probe.take<unsigned long long>((size_t)nseg * T);
             probe.take<SegItem>(items_max);
+            probe.take<uint8_t>((size_t)nseg * rec);
+            probe.take<uint8_t>((size_t)nseg * 12);
             rc = ensure_flow(ctx, 1, probe.off);
         }
         if (!rc) {
@@ -441,12 +474,12 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             info = cv.take<uint64_t>((size_t)nseg * 4);
             acc = cv.take<unsigned long long>((size_t)nseg * T);
             d_items = cv.take<SegItem>(items_max);
+            d_rec = (uint32_t *)cv.take<uint8_t>((size_t)nseg * rec);
+            d_keys = cv.take<uint8_t>((size_t)nseg * 12);
         }
         if (!rc) hipLaunchKernelGGL(k_seg_info, dim3((nseg + 255) / 256), dim3(256), 0, s, kh, kl2, ids2, heads, nseg,
                                     inserted, info);
-        std::vector<uint64_t> hinfo((size_t)nseg * 4);
         if (!rc && (hipMemcpyAsync(hs.data(), heads, nseg * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                    hipMemcpyAsync(hinfo.data(), info, (size_t)nseg * 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess))
             rc = QK_E_HIP;
         std::vector<uint64_t> offs(nseg + 1);
@@ -454,26 +487,14 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         offs[nseg] = inserted;
         const std::vector<SegItem> items = seg_items(offs);
         if (!rc) rc = seg_encode(ctx, ids2, items, nseg, T, acc, d_items, s);
-        std::vector<uint64_t> hacc((size_t)nseg * T);
-        if (!rc && (hipMemcpyAsync(hacc.data(), acc, hacc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                    hipStreamSynchronize(s) != hipSuccess))
-            rc = QK_E_HIP;
         if (!rc) {
-            const size_t rec = qk_u32_size(T);
-            for (uint32_t i = 0; i < nseg; ++i) {
-                const uint64_t khv = hinfo[4 * i], klv = hinfo[4 * i + 1];
-                uint8_t *k = keys[i].addr;
-                k[0] = (uint8_t)(khv >> 40); k[1] = (uint8_t)(khv >> 32); k[2] = (uint8_t)(khv >> 24);
-                k[3] = (uint8_t)(khv >> 16); k[4] = (uint8_t)(khv >> 8); k[5] = (uint8_t)khv;
-                k[6] = (uint8_t)(klv >> 40); k[7] = (uint8_t)(klv >> 32); k[8] = (uint8_t)(klv >> 24);
-                k[9] = (uint8_t)(klv >> 16); k[10] = (uint8_t)(klv >> 8); k[11] = (uint8_t)klv;
-                qk_u32 *q = (qk_u32 *)(sketches + i * rec);
-                qk_u32_init(q, T);
-                for (uint32_t m = 0; m < T; ++m) q->power_sums[m] = canon32(fold64_32(hacc[(size_t)i * T + m]));
-                q->count = (uint32_t)hinfo[4 * i + 2];
-                q->has_last = 1;
-                q->last_value = (uint32_t)hinfo[4 * i + 3];
-            }
+            const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nseg * (4 + T) + 255) / 256,
+                                                             (uint64_t)ctx->num_cus * 16);
+            hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info, (uint64_t)nseg, T, d_rec, d_keys);
+            if (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(sketches, d_rec, (size_t)nseg * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(keys, d_keys, (size_t)nseg * 12, hipMemcpyDeviceToHost, s) != hipSuccess)
+                rc = QK_E_HIP;
         }
     }
     (void)hipStreamSynchronize(s); // the arenas are reused by the next call
