@@ -1,0 +1,478 @@
+// bsgs.h — baby-step / giant-step u32 encode body for 9 <= t <= 32 (the
+// headline kernel).  Shared by encode.hip (product kernel)
+// and tools/tune_bsgs.hip (A/B harness), so the tuned code is the shipped code.
+//
+// Power m+1 = a*NB + b + 1 with B_b = x^(b+1) (b < NB) and A_a = x^(a*NB)
+// (a < NA; A_0 = 1), so S_{m+1} = sum_i A_a(x_i) * B_b(x_i): NB-1 + NA-2
+// lazy modmuls per id, then (NA-1)*NB 32x32->64 multiply-accumulates into
+// 64-bit accumulators whose wraps are counted (2^64 == 25 mod p), plus NB
+// 32-bit adds for the a = 0 row whose wraps are counted (2^32 == 5 mod p).
+//
+// Wrap counting, per accumulator group of four (template knobs):
+//   VALU form   v_mad_u64_u32 / v_add_co_u32 writes its carry to an SGPR pair,
+//               v_addc_co_u32 adds it into a per-lane 32-bit counter.  gfx950
+//               needs two wait states between a VALU SGPR write and a VALU
+//               carry-in read (hipcc pads with s_nop), so four ops with four
+//               distinct carry pairs are issued back to back first: every
+//               v_addc reads a carry written >= 3 VALU instructions earlier.
+//   SALU form   only the SUM over lanes of a power's wraps matters (the block
+//               reduction adds every lane), so the carry mask is counted per
+//               wave on the scalar unit (s_bcnt1 + s_add, issued beside the
+//               VALU stream).  Needs EXEC = all lanes at the op (wave-uniform
+//               control flow; lanes past their range feed id 0).
+//
+// Ids are not reduced mod p first: every product below is exact for any
+// 32-bit operand and x == id (mod p) either way.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "field.h"
+
+namespace qk {
+namespace bsgs {
+
+constexpr int BLOCK = 256;
+constexpr int WAVES = BLOCK / 64;
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = __shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ---- multiply-accumulate and add groups, carries counted ------------------
+// The carry masks live in explicitly named SGPR pairs, and consecutive groups
+// alternate between two disjoint sets (SET 0: s[40:47], SET 1: s[48:55]).
+// hipcc treats an inline-asm block's SGPR definitions conservatively and pads
+// "s_nop 0" between two blocks that define the same SGPRs; with disjoint sets
+// back to back it inserts none (8 nops per id before).  Inside a block every
+// VALU carry-in read is >= 3 VALU instructions after its write.
+#define QK_MAC4V(P0, P1, P2, P3)                                                                       \
+    "v_mad_u64_u32 %0, " P0 ", %8, %9, %0\n\t"                                                         \
+    "v_mad_u64_u32 %1, " P1 ", %8, %10, %1\n\t"                                                        \
+    "v_mad_u64_u32 %2, " P2 ", %8, %11, %2\n\t"                                                        \
+    "v_mad_u64_u32 %3, " P3 ", %8, %12, %3\n\t"                                                        \
+    "v_addc_co_u32_e64 %4, " P0 ", %4, 0, " P0 "\n\t"                                                  \
+    "v_addc_co_u32_e64 %5, " P1 ", %5, 0, " P1 "\n\t"                                                  \
+    "v_addc_co_u32_e64 %6, " P2 ", %6, 0, " P2 "\n\t"                                                  \
+    "v_addc_co_u32_e64 %7, " P3 ", %7, 0, " P3
+#define QK_MAC4S(P0, P1, P2, P3)                                                                       \
+    "v_mad_u64_u32 %0, " P0 ", %12, %13, %0\n\t"                                                       \
+    "v_mad_u64_u32 %1, " P1 ", %12, %14, %1\n\t"                                                       \
+    "v_mad_u64_u32 %2, " P2 ", %12, %15, %2\n\t"                                                       \
+    "v_mad_u64_u32 %3, " P3 ", %12, %16, %3\n\t"                                                       \
+    "s_bcnt1_i32_b64 %8, " P0 "\n\ts_add_u32 %4, %4, %8\n\t"                                           \
+    "s_bcnt1_i32_b64 %9, " P1 "\n\ts_add_u32 %5, %5, %9\n\t"                                           \
+    "s_bcnt1_i32_b64 %10, " P2 "\n\ts_add_u32 %6, %6, %10\n\t"                                         \
+    "s_bcnt1_i32_b64 %11, " P3 "\n\ts_add_u32 %7, %7, %11"
+#define QK_ADD4V(P0, P1, P2, P3)                                                                       \
+    "v_add_co_u32_e64 %0, " P0 ", %0, %8\n\t"                                                          \
+    "v_add_co_u32_e64 %1, " P1 ", %1, %9\n\t"                                                          \
+    "v_add_co_u32_e64 %2, " P2 ", %2, %10\n\t"                                                         \
+    "v_add_co_u32_e64 %3, " P3 ", %3, %11\n\t"                                                         \
+    "v_addc_co_u32_e64 %4, " P0 ", %4, 0, " P0 "\n\t"                                                  \
+    "v_addc_co_u32_e64 %5, " P1 ", %5, 0, " P1 "\n\t"                                                  \
+    "v_addc_co_u32_e64 %6, " P2 ", %6, 0, " P2 "\n\t"                                                  \
+    "v_addc_co_u32_e64 %7, " P3 ", %7, 0, " P3
+#define QK_ADD4S(P0, P1, P2, P3)                                                                       \
+    "v_add_co_u32_e64 %0, " P0 ", %0, %12\n\t"                                                         \
+    "v_add_co_u32_e64 %1, " P1 ", %1, %13\n\t"                                                         \
+    "v_add_co_u32_e64 %2, " P2 ", %2, %14\n\t"                                                         \
+    "v_add_co_u32_e64 %3, " P3 ", %3, %15\n\t"                                                         \
+    "s_bcnt1_i32_b64 %8, " P0 "\n\ts_add_u32 %4, %4, %8\n\t"                                           \
+    "s_bcnt1_i32_b64 %9, " P1 "\n\ts_add_u32 %5, %5, %9\n\t"                                           \
+    "s_bcnt1_i32_b64 %10, " P2 "\n\ts_add_u32 %6, %6, %10\n\t"                                         \
+    "s_bcnt1_i32_b64 %11, " P3 "\n\ts_add_u32 %7, %7, %11"
+#define QK_SET0 "s[40:41]", "s[42:43]", "s[44:45]", "s[46:47]"
+#define QK_SET1 "s[48:49]", "s[50:51]", "s[52:53]", "s[54:55]"
+#define QK_CLOB0 "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47"
+#define QK_CLOB1 "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55"
+#define QK_EXPAND(M, ...) M(__VA_ARGS__)
+
+// acc_j += A * b_j (64-bit), wraps counted per lane (c_j) or per wave (s_j)
+template <int SET>
+__device__ __forceinline__ void mac4v(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t &c0,
+                                      uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t A, uint32_t b0,
+                                      uint32_t b1, uint32_t b2, uint32_t b3) {
+    if constexpr (SET == 0)
+        asm(QK_EXPAND(QK_MAC4V, QK_SET0)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+            : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : QK_CLOB0);
+    else
+        asm(QK_EXPAND(QK_MAC4V, QK_SET1)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+            : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : QK_CLOB1);
+}
+template <int SET>
+__device__ __forceinline__ void mac4s(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t &s0,
+                                      uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t A, uint32_t b0,
+                                      uint32_t b1, uint32_t b2, uint32_t b3) {
+    uint32_t t0, t1, t2, t3;
+    if constexpr (SET == 0)
+        asm(QK_EXPAND(QK_MAC4S, QK_SET0)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
+              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+            : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : "scc", QK_CLOB0);
+    else
+        asm(QK_EXPAND(QK_MAC4S, QK_SET1)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
+              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+            : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : "scc", QK_CLOB1);
+}
+// lo_j += b_j (32-bit), wraps counted per lane (c_j) or per wave (s_j)
+template <int SET>
+__device__ __forceinline__ void add4v(uint32_t &l0, uint32_t &l1, uint32_t &l2, uint32_t &l3, uint32_t &c0,
+                                      uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t b0, uint32_t b1,
+                                      uint32_t b2, uint32_t b3) {
+    if constexpr (SET == 0)
+        asm(QK_EXPAND(QK_ADD4V, QK_SET0)
+            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+            : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : QK_CLOB0);
+    else
+        asm(QK_EXPAND(QK_ADD4V, QK_SET1)
+            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+            : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : QK_CLOB1);
+}
+template <int SET>
+__device__ __forceinline__ void add4s(uint32_t &l0, uint32_t &l1, uint32_t &l2, uint32_t &l3, uint32_t &s0,
+                                      uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t b0, uint32_t b1,
+                                      uint32_t b2, uint32_t b3) {
+    uint32_t t0, t1, t2, t3;
+    if constexpr (SET == 0)
+        asm(QK_EXPAND(QK_ADD4S, QK_SET0)
+            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
+              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+            : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : "scc", QK_CLOB0);
+    else
+        asm(QK_EXPAND(QK_ADD4S, QK_SET1)
+            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
+              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+            : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : "scc", QK_CLOB1);
+}
+// leftovers for NB % 4 != 0 (t = 17..24 uses NB = 6): compiler-allocated
+// carries with explicit wait states
+__device__ __forceinline__ void mac2v(uint64_t &a0, uint64_t &a1, uint32_t &c0, uint32_t &c1, uint32_t A,
+                                      uint32_t b0, uint32_t b1) {
+    uint64_t k0, k1;
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %6, %8, %1\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
+        : "+v"(a0), "+v"(a1), "+v"(c0), "+v"(c1), "=&s"(k0), "=&s"(k1)
+        : "v"(A), "v"(b0), "v"(b1));
+}
+__device__ __forceinline__ void add2v(uint32_t &l0, uint32_t &l1, uint32_t &c0, uint32_t &c1, uint32_t b0,
+                                      uint32_t b1) {
+    uint64_t k0, k1;
+    asm("v_add_co_u32_e64 %0, %4, %0, %6\n\t"
+        "v_add_co_u32_e64 %1, %5, %1, %7\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
+        : "+v"(l0), "+v"(l1), "+v"(c0), "+v"(c1), "=&s"(k0), "=&s"(k1)
+        : "v"(b0), "v"(b1));
+}
+
+// ---- a = 0 row as 64-bit multiply-adds: acc_j += b_j * 1 ------------------
+// acc < 2^64 for < 2^32 adds of 32-bit values, so no carry is counted: one
+// VALU per add (its carry-out is dead) instead of an add + add-with-carry pair
+// (both SGPR-writing VALU ops, ~4 SIMD cycles each on gfx950: tools/ubench_issue.hip).
+#define QK_ROW4M(P0, P1, P2, P3)                                                                       \
+    "v_mad_u64_u32 %0, " P0 ", %4, 1, %0\n\t"                                                          \
+    "v_mad_u64_u32 %1, " P1 ", %5, 1, %1\n\t"                                                          \
+    "v_mad_u64_u32 %2, " P2 ", %6, 1, %2\n\t"                                                          \
+    "v_mad_u64_u32 %3, " P3 ", %7, 1, %3"
+template <int SET>
+__device__ __forceinline__ void row4m(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t b0,
+                                      uint32_t b1, uint32_t b2, uint32_t b3) {
+    if constexpr (SET == 0)
+        asm(QK_EXPAND(QK_ROW4M, QK_SET0)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+            : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : QK_CLOB0);
+    else
+        asm(QK_EXPAND(QK_ROW4M, QK_SET1)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+            : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
+            : QK_CLOB1);
+}
+__device__ __forceinline__ void row2m(uint64_t &a0, uint64_t &a1, uint32_t b0, uint32_t b1) {
+    uint64_t k0, k1;
+    asm("v_mad_u64_u32 %0, %2, %4, 1, %0\n\t"
+        "v_mad_u64_u32 %1, %3, %5, 1, %1"
+        : "+v"(a0), "+v"(a1), "=&s"(k0), "=&s"(k1)
+        : "v"(b0), "v"(b1));
+}
+
+// ---- configuration ----------------------------------------------------------
+//  NB, NA  baby / giant steps (NB even)
+//  SG      the first SG 4-wide accumulator groups count their wraps on the
+//          scalar unit.  Group numbering: the a = 0 row's groups are
+//          g = 0 .. NB/4-1 (only when ROW0 == 0), MAC row a (1..NA-1) has
+//          g = a*(NB/4) + b/4.  NB % 4 leftovers always use the VALU form.
+//  ROW0    0: a = 0 row as 32-bit adds with counted wraps; 1: 64-bit mads
+//  FOLD    0: lazy fold with an SGPR-writing add (wrap = its carry, ORed on the
+//          scalar unit); 1: plain add, wraps caught by a per-lane minimum of
+//          the fold results (a wrapped fold leaves a value < 25, field.h)
+//  PAIR    interleave the power chains of two ids
+template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false>
+struct Cfg {
+    static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_;
+    static constexpr bool PAIR = PAIR_;
+    static_assert(NB % 2 == 0 && NA >= 2, "NB even, NA >= 2");
+};
+
+template <int NB, int NA>
+struct Acc {
+    uint32_t lo0[NB];         // a = 0 row (ROW0 == 0): sum of B_b mod 2^32
+    uint32_t c0[NB];          // ... its wraps (lane count, or wave total if scalar)
+    uint64_t r0[NB];          // a = 0 row (ROW0 == 1): sum of B_b, 64-bit
+    uint64_t m[NA - 1][NB];   // a >= 1: sum of A_a * B_b mod 2^64
+    uint32_t c[NA - 1][NB];   // ... its wraps (lane count, or wave total if scalar)
+};
+
+template <class C>
+__host__ __device__ constexpr bool scalar_group(int row, int b) {
+    return b / 4 * 4 + 4 <= C::NB && (row > 0 || C::ROW0 == 0) && row * (C::NB / 4) + b / 4 < C::SG;
+}
+
+// y * x (mod p) lazily, y, x < 2^32 -> r < 2^32 (FOLD == 1 form, see Cfg):
+// t = tl + 5 th (th <= 5) as in field.h mulfold32_fast, then r = tl + 5 th
+// mod 2^32.  If that add wrapped, r < 5 th <= 25; mn tracks the minimum so
+// the caller can redo the id exactly (probability ~25 / 2^32 per fold).
+__device__ __forceinline__ uint32_t mulfold32_min(uint32_t y, uint32_t x, uint32_t &mn) {
+    const uint64_t P = (uint64_t)y * x;
+    const uint32_t Ph = (uint32_t)(P >> 32);
+    const uint64_t Q = P + (uint64_t)Ph * C32;
+    const uint32_t tl = (uint32_t)Q, th = (uint32_t)(Q >> 32) - Ph;
+    const uint32_t r = tl + th * C32;
+    mn = r < mn ? r : mn;
+    return r;
+}
+
+// powers of one id; returns nonzero if a lazy fold may have wrapped (the
+// caller then recomputes exactly)
+template <class C>
+__device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], uint32_t (&A)[C::NA - 1]) {
+    constexpr int NB = C::NB, NA = C::NA;
+    B[0] = id;
+    if constexpr (C::FOLD == 0) {
+        uint32_t wrapped = 0;
+#pragma unroll
+        for (int b = 1; b < NB; ++b) B[b] = mulfold32_fast(B[b - 1], B[0], wrapped);
+        A[0] = B[NB - 1];
+#pragma unroll
+        for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_fast(A[a - 1], A[0], wrapped);
+        return wrapped;
+    } else {
+        uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+        for (int b = 1; b < NB; ++b) B[b] = mulfold32_min(B[b - 1], B[0], mn);
+        A[0] = B[NB - 1];
+#pragma unroll
+        for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_min(A[a - 1], A[0], mn);
+        return mn < 25u;
+    }
+}
+template <class C>
+__device__ __forceinline__ void powers_exact(uint32_t (&B)[C::NB], uint32_t (&A)[C::NA - 1]) {
+#pragma unroll
+    for (int b = 1; b < C::NB; ++b) B[b] = mulfold32_exact(B[b - 1], B[0]);
+    A[0] = B[C::NB - 1];
+#pragma unroll
+    for (int a = 1; a < C::NA - 1; ++a) A[a] = mulfold32_exact(A[a - 1], A[0]);
+}
+
+// Groups are issued in the order row 0, row 1, ... and alternate carry-SGPR
+// sets (group index parity), so no two adjacent blocks share SGPRs.
+template <class C>
+__device__ __forceinline__ void accumulate(Acc<C::NB, C::NA> &S, const uint32_t (&B)[C::NB],
+                                           const uint32_t (&A)[C::NA - 1]) {
+    constexpr int NB = C::NB, NA = C::NA;
+#pragma unroll
+    for (int b = 0; b + 4 <= NB; b += 4) {
+        const bool s0 = (b / 4) % 2 == 0;
+        if constexpr (C::ROW0 == 1) {
+            if (s0) row4m<0>(S.r0[b], S.r0[b + 1], S.r0[b + 2], S.r0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            else row4m<1>(S.r0[b], S.r0[b + 1], S.r0[b + 2], S.r0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+        } else if (scalar_group<C>(0, b)) {
+            if (s0)
+                add4s<0>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            else
+                add4s<1>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+        } else {
+            if (s0)
+                add4v<0>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            else
+                add4v<1>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+        }
+    }
+    if constexpr (NB % 4 == 2) {
+        if constexpr (C::ROW0 == 1) row2m(S.r0[NB - 2], S.r0[NB - 1], B[NB - 2], B[NB - 1]);
+        else add2v(S.lo0[NB - 2], S.lo0[NB - 1], S.c0[NB - 2], S.c0[NB - 1], B[NB - 2], B[NB - 1]);
+    }
+#pragma unroll
+    for (int a = 0; a < NA - 1; ++a) {
+#pragma unroll
+        for (int b = 0; b + 4 <= NB; b += 4) {
+            const int g = (a + 1) * (NB / 4) + b / 4;   // group index: parity picks the SGPR set
+            if (scalar_group<C>(a + 1, b)) {
+                if (g % 2 == 0)
+                    mac4s<0>(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.c[a][b], S.c[a][b + 1],
+                             S.c[a][b + 2], S.c[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
+                else
+                    mac4s<1>(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.c[a][b], S.c[a][b + 1],
+                             S.c[a][b + 2], S.c[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            } else {
+                if (g % 2 == 0)
+                    mac4v<0>(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.c[a][b], S.c[a][b + 1],
+                             S.c[a][b + 2], S.c[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
+                else
+                    mac4v<1>(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.c[a][b], S.c[a][b + 1],
+                             S.c[a][b + 2], S.c[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            }
+        }
+        if constexpr (NB % 4 == 2)
+            mac2v(S.m[a][NB - 2], S.m[a][NB - 1], S.c[a][NB - 2], S.c[a][NB - 1], A[a], B[NB - 2], B[NB - 1]);
+    }
+}
+
+template <class C>
+__device__ __forceinline__ void one(Acc<C::NB, C::NA> &S, uint32_t id) {
+    uint32_t B[C::NB], A[C::NA - 1];
+    const uint32_t w = powers<C>(id, B, A);
+    if (__builtin_expect(__any(w), 0)) {
+        if (w) powers_exact<C>(B, A);
+    }
+    accumulate<C>(S, B, A);
+}
+
+// two ids at once: their power chains are independent straight-line code, so
+// the compiler interleaves them (ILP for the dependent modmul chains)
+template <class C>
+__device__ __forceinline__ void two(Acc<C::NB, C::NA> &S, uint32_t id0, uint32_t id1) {
+    uint32_t B0[C::NB], A0[C::NA - 1], B1[C::NB], A1[C::NA - 1];
+    const uint32_t w0 = powers<C>(id0, B0, A0);
+    const uint32_t w1 = powers<C>(id1, B1, A1);
+    if (__builtin_expect(__any(w0 | w1), 0)) {
+        if (w0) powers_exact<C>(B0, A0);
+        if (w1) powers_exact<C>(B1, A1);
+    }
+    accumulate<C>(S, B0, A0);
+    accumulate<C>(S, B1, A1);
+}
+
+template <class C>
+__device__ __forceinline__ void four(Acc<C::NB, C::NA> &S, uint4 w) {
+    if constexpr (C::PAIR) {
+        two<C>(S, w.x, w.y);
+        two<C>(S, w.z, w.w);
+    } else {
+        one<C>(S, w.x);
+        one<C>(S, w.y);
+        one<C>(S, w.z);
+        one<C>(S, w.w);
+    }
+}
+
+// The kernel body: grid-stride over 16-byte groups of ids (+ unaligned head
+// and tail), then lane partials -> wave butterfly -> LDS -> one partial per
+// (power, block) stored [power][block].
+//
+// Every lane of a wave runs the wave's trip count (lane 0 has the largest):
+// lanes past their range feed id 0, whose powers are all 0, so EXEC is full
+// at every scalar-counted op.  The loop is split: while every lane of the
+// wave still has a next group, the prefetch is unconditional; the last <= 2
+// trips take the masked form.  Per-lane 32-bit trip counts (the host
+// guarantees body / nthr < 2^32).
+template <class C>
+__device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
+                                     uint64_t *__restrict__ partials) {
+    constexpr int NB = C::NB, NA = C::NA;
+    __shared__ uint64_t sm[WAVES * NB * NA];
+    Acc<NB, NA> S;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        S.lo0[b] = 0;
+        S.c0[b] = 0;
+        S.r0[b] = 0;
+#pragma unroll
+        for (int a = 0; a < NA - 1; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; }
+    }
+    const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t nbody = (n - h) >> 2;
+    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
+    const uint32_t iters = gtid < nbody ? (uint32_t)((nbody - gtid + nthr - 1) / nthr) : 0u;
+    const uint32_t tmax = (uint32_t)__builtin_amdgcn_readfirstlane(iters);           // lane 0: most trips
+    const uint32_t tmin = (uint32_t)__builtin_amdgcn_readlane((int)iters, 63);       // lane 63: fewest
+    const uint4 *__restrict__ p = v + gtid;
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (iters) nxt = *p;
+    uint32_t it = 0;
+    for (; it + 1 < tmin; ++it) {
+        const uint4 w = nxt;
+        p += nthr;
+        nxt = *p;
+        four<C>(S, w);
+    }
+    for (; it < tmax; ++it) {
+        const uint4 w = nxt;
+        p += nthr;
+        nxt = make_uint4(0, 0, 0, 0);
+        if (it + 1 < iters) nxt = *p;
+        four<C>(S, w);
+    }
+    const uint64_t tail0 = h + (nbody << 2);
+    one<C>(S, gtid < h ? ids[gtid] : 0u);
+    one<C>(S, gtid < n - tail0 ? ids[tail0 + gtid] : 0u);
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            // value = lo + c * W with W = 2^32 == 5 (a = 0) or 2^64 == 25 (a > 0);
+            // a scalar-counted c is the wave's total, added once (by lane 0)
+            const bool sc = scalar_group<C>(a, b);
+            const uint32_t c = a == 0 ? S.c0[b] : S.c[a - 1][b];
+            const uint32_t cl = sc ? (lane == 0 ? c : 0u) : c;
+            uint64_t x;
+            if (a == 0) {
+                if constexpr (C::ROW0 == 1) x = S.r0[b];
+                else x = (uint64_t)S.lo0[b] + (uint64_t)cl * 5u;                      // < 6*2^32
+            } else {
+                x = (uint64_t)fold64_32(S.m[a - 1][b]) + fold64_32((uint64_t)cl * 25u);
+            }
+            x = fold64_32(x);                                                         // < 2^32
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) x += shfl_xor_u64(x, off);        // < 2^38
+            if (lane == 0) sm[wave * (NB * NA) + a * NB + b] = x;
+        }
+    }
+    __syncthreads();
+    for (uint32_t m = threadIdx.x; m < T; m += BLOCK) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) s += sm[w * (NB * NA) + m];
+        partials[(size_t)m * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+} // namespace bsgs
+} // namespace qk

@@ -21,6 +21,18 @@
 // of 4 B/id is ~5% of the roofline at t = 32.
 #include "ctx.h"
 #include "field.h"
+#include "bsgs.h"
+
+// scalar-counted wrap groups of the t = 25..32 BSGS kernel (tools/tune_bsgs.hip)
+#ifndef QK_BSGS_SG_T32
+#define QK_BSGS_SG_T32 8
+#endif
+#ifndef QK_BSGS_ROW0
+#define QK_BSGS_ROW0 1
+#endif
+#ifndef QK_BSGS_FOLD
+#define QK_BSGS_FOLD 1
+#endif
 
 namespace qk {
 
@@ -72,236 +84,15 @@ __device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
     }
 }
 
-// ---- baby-step / giant-step encode for t <= 32 ---------
-// power m+1 = a*NB + b + 1 with B_b = x^(b+1) (b < NB) and A_a = x^(a*NB)
-// (a < NA; A_0 = 1), so S_{m+1} = sum_i A_a(x_i) * B_b(x_i): NB-1 + NA-2
-// lazy modmuls per id, then (NA-1)*NB 32x32->64 multiply-accumulates into
-// 64-bit accumulators whose wraps are counted (2^64 == 25 mod p), plus NB
-// plain adds for the a = 0 row.
-// MACs: v_mad_u64_u32 acc += A*B with the carry-out in an SGPR pair, then
-// v_addc_co_u32 adds that carry into a 32-bit wrap counter.  gfx950 needs two
-// wait states between a VALU SGPR/VCC write and a VALU carry-in read of it
-// (hipcc pads the same pattern with s_nop), so MACs are issued in groups of
-// four with four distinct carry pairs: each v_addc is >= 3 VALU instructions
-// after the v_mad_u64_u32 whose carry it reads.
-__device__ __forceinline__ void mac4(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t &c0,
-                                     uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t A, uint32_t b0,
-                                     uint32_t b1, uint32_t b2, uint32_t b3) {
-    uint64_t k0, k1, k2, k3;
-    asm("v_mad_u64_u32 %0, %8, %12, %13, %0\n\t"
-        "v_mad_u64_u32 %1, %9, %12, %14, %1\n\t"
-        "v_mad_u64_u32 %2, %10, %12, %15, %2\n\t"
-        "v_mad_u64_u32 %3, %11, %12, %16, %3\n\t"
-        "v_addc_co_u32_e64 %4, %8, %4, 0, %8\n\t"
-        "v_addc_co_u32_e64 %5, %9, %5, 0, %9\n\t"
-        "v_addc_co_u32_e64 %6, %10, %6, 0, %10\n\t"
-        "v_addc_co_u32_e64 %7, %11, %7, 0, %11"
-        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "=&s"(k0),
-          "=&s"(k1), "=&s"(k2), "=&s"(k3)
-        : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
-}
-__device__ __forceinline__ void mac2(uint64_t &a0, uint64_t &a1, uint32_t &c0, uint32_t &c1, uint32_t A,
-                                     uint32_t b0, uint32_t b1) {
-    uint64_t k0, k1;
-    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
-        "v_mad_u64_u32 %1, %5, %6, %8, %1\n\t"
-        "s_nop 0\n\t"
-        "v_addc_co_u32_e64 %2, %4, %2, 0, %4\n\t"
-        "v_addc_co_u32_e64 %3, %5, %3, 0, %5"
-        : "+v"(a0), "+v"(a1), "+v"(c0), "+v"(c1), "=&s"(k0), "=&s"(k1)
-        : "v"(A), "v"(b0), "v"(b1));
-}
-__device__ __forceinline__ void mac1(uint64_t &acc, uint32_t &cnt, uint32_t A, uint32_t b) {
-    uint64_t k;
-    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-        "s_nop 1\n\t"
-        "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
-        : "+v"(acc), "+v"(cnt), "=&s"(k)
-        : "v"(A), "v"(b));
-}
-
-// Scalar-carry MACs: only the SUM over lanes of a power's
-// wraps matters (the block reduction adds every lane anyway), so the carry
-// mask of each v_mad_u64_u32 is counted per wave on the scalar unit
-// (s_bcnt1 + s_add, issued beside the VALU stream) instead of a per-lane
-// v_addc into a VGPR counter.  Callers keep EXEC = all lanes (inactive lanes'
-// carry bits are not guaranteed zero): wave-uniform control flow only.  A
-// VALU SGPR write read by SALU needs no wait states.
-__device__ __forceinline__ void mac4s(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t &s0,
-                                      uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t A, uint32_t b0,
-                                      uint32_t b1, uint32_t b2, uint32_t b3) {
-    uint64_t k0, k1, k2, k3;
-    uint32_t t0, t1, t2, t3;
-    asm("v_mad_u64_u32 %0, %8, %16, %17, %0\n\t"
-        "v_mad_u64_u32 %1, %9, %16, %18, %1\n\t"
-        "v_mad_u64_u32 %2, %10, %16, %19, %2\n\t"
-        "v_mad_u64_u32 %3, %11, %16, %20, %3\n\t"
-        "s_bcnt1_i32_b64 %12, %8\n\ts_add_u32 %4, %4, %12\n\t"
-        "s_bcnt1_i32_b64 %13, %9\n\ts_add_u32 %5, %5, %13\n\t"
-        "s_bcnt1_i32_b64 %14, %10\n\ts_add_u32 %6, %6, %14\n\t"
-        "s_bcnt1_i32_b64 %15, %11\n\ts_add_u32 %7, %7, %15"
-        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(k0), "=&s"(k1),
-          "=&s"(k2), "=&s"(k3), "=&s"(t0), "=&s"(t1), "=&s"(t2), "=&s"(t3)
-        : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
-        : "scc");
-}
-template <int NB, int NA>
-struct BsgsAcc {
-    uint64_t a0[NB];          // a = 0 row: sum of B_b
-    uint64_t m[NA - 1][NB];   // a >= 1: sum of A_a * B_b mod 2^64
-    uint32_t c[NA - 1][NB];   // ... and its wrap count (per lane, VGPR)
-    uint32_t cs[NA - 1][NB];  // ... or the wave's wrap total (SGPR), scalar-counted groups
-};
-
-// powers of one id; returns nonzero if a lazy fold wrapped (then B/A are
-// recomputed exactly by the caller)
-template <int NB, int NA>
-__device__ __forceinline__ uint32_t bsgs_powers(uint32_t id, uint32_t (&B)[NB], uint32_t (&A)[NA > 1 ? NA - 1 : 1]) {
-    uint32_t wrapped = 0;
-    B[0] = canon32(id);
-#pragma unroll
-    for (int b = 1; b < NB; ++b) B[b] = mulfold32_fast(B[b - 1], B[0], wrapped);
-    if constexpr (NA > 1) {
-        A[0] = B[NB - 1];
-#pragma unroll
-        for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_fast(A[a - 1], A[0], wrapped);
-    }
-    return wrapped;
-}
-template <int NB, int NA>
-__device__ __forceinline__ void bsgs_powers_exact(uint32_t (&B)[NB], uint32_t (&A)[NA > 1 ? NA - 1 : 1]) {
-#pragma unroll
-    for (int b = 1; b < NB; ++b) B[b] = mulfold32_exact(B[b - 1], B[0]);
-    if constexpr (NA > 1) {
-        A[0] = B[NB - 1];
-#pragma unroll
-        for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_exact(A[a - 1], A[0]);
-    }
-}
-
-// MAC groups (row a, 4 consecutive b) are numbered g = a * (NB / 4) + b / 4;
-// the first SCG of them count their wraps per wave on the scalar unit
-// (S.c = wave totals), the rest per lane with v_addc (S.c = lane counts).
-// SCG balances VALU against SALU issue.  NB % 4 leftovers
-// always use the VALU form.
-template <int NB, int NA, int SCG>
-__device__ __forceinline__ void bsgs_accumulate_mix(BsgsAcc<NB, NA> &S, const uint32_t (&B)[NB],
-                                                    const uint32_t (&A)[NA > 1 ? NA - 1 : 1]) {
-#pragma unroll
-    for (int b = 0; b < NB; ++b) S.a0[b] += B[b];
-#pragma unroll
-    for (int a = 0; a < NA - 1; ++a) {
-#pragma unroll
-        for (int b = 0; b + 4 <= NB; b += 4) {
-            if (a * (NB / 4) + b / 4 < SCG)
-                mac4s(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.cs[a][b], S.cs[a][b + 1],
-                      S.cs[a][b + 2], S.cs[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
-            else
-                mac4(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.c[a][b], S.c[a][b + 1],
-                     S.c[a][b + 2], S.c[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
-        }
-        if constexpr (NB % 4 >= 2)
-            mac2(S.m[a][NB / 4 * 4], S.m[a][NB / 4 * 4 + 1], S.c[a][NB / 4 * 4], S.c[a][NB / 4 * 4 + 1], A[a],
-                 B[NB / 4 * 4], B[NB / 4 * 4 + 1]);
-        if constexpr (NB % 2 == 1) mac1(S.m[a][NB - 1], S.c[a][NB - 1], A[a], B[NB - 1]);
-    }
-}
-// is the (a, b) wrap count a per-wave (scalar) total?
-template <int NB, int SCG>
-__host__ __device__ constexpr bool bsgs_scalar(int a, int b) {
-    return b / 4 * 4 + 4 <= NB && a * (NB / 4) + b / 4 < SCG;
-}
-
-template <int NB, int NA, int SCG>
-__device__ __forceinline__ void bsgs_one(BsgsAcc<NB, NA> &S, uint32_t id) {
-    uint32_t B[NB], A[NA > 1 ? NA - 1 : 1];
-    if (bsgs_powers<NB, NA>(id, B, A)) bsgs_powers_exact<NB, NA>(B, A);
-    bsgs_accumulate_mix<NB, NA, SCG>(S, B, A);
-}
-
-template <int NB, int NA, int SCG>
-__global__ __launch_bounds__(BLOCK, NB * NA >= 24 ? 3 : 1) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids, uint64_t n,
-                                                           uint32_t head, uint32_t T,
-                                                           uint64_t *__restrict__ partials) {
-    __shared__ uint64_t sm[WAVES * NB * NA];
-    BsgsAcc<NB, NA> S;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        S.a0[b] = 0;
-#pragma unroll
-        for (int a = 0; a < NA - 1; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; S.cs[a][b] = 0; }
-    }
-    const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const uint64_t nthr = (uint64_t)gridDim.x * BLOCK;
-    const uint64_t h = head < n ? head : n;
-    const uint64_t body = (n - h) >> 2;
-    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
-    // Per-lane trip count + pointer walk (no 64-bit index compare in the
-    // loop); the next 16-byte load is issued before this iteration's
-    // arithmetic (3 waves/SIMD at this register count cannot hide it).
-    // The host guarantees body / nthr < 2^32.
-    const uint32_t iters = gtid < body ? (uint32_t)((body - gtid + nthr - 1) / nthr) : 0u;
-    // SC: every lane runs the wave's trip count (lane 0 has the largest) so
-    // EXEC is full at the scalar-counted MACs; a lane past its range feeds
-    // id 0, whose powers are all 0.
-    constexpr bool SC = SCG > 0;
-    const uint32_t trips = SC ? (uint32_t)__builtin_amdgcn_readfirstlane(iters) : iters;
-    const uint4 *__restrict__ p = v + gtid;
-    uint4 nxt = iters ? *p : make_uint4(0, 0, 0, 0);
-    for (uint32_t it = 0; it < trips; ++it) {
-        const uint4 w = nxt;
-        p += nthr;
-        if constexpr (SC) { // branch-free: lanes past their range load v[0] and drop it
-            const uint32_t m = it + 1 < iters ? ~0u : 0u;
-            const uint4 t = *(m ? p : v);
-            nxt = make_uint4(t.x & m, t.y & m, t.z & m, t.w & m);
-        } else if (it + 1 < iters) nxt = *p;
-        const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            uint32_t B[NB], A[NA > 1 ? NA - 1 : 1];
-            const uint32_t wrapped = bsgs_powers<NB, NA>(wv[c], B, A);
-            if (__builtin_expect(__any(wrapped), 0)) {
-                if (wrapped) bsgs_powers_exact<NB, NA>(B, A);
-            }
-            bsgs_accumulate_mix<NB, NA, SCG>(S, B, A);
-        }
-    }
-    const uint64_t tail0 = h + (body << 2);
-    if constexpr (SC) { // wave-uniform: lanes without a head/tail id feed 0
-        if (h) bsgs_one<NB, NA, SCG>(S, gtid < h ? ids[gtid] : 0u);
-        if (n > tail0) bsgs_one<NB, NA, SCG>(S, gtid < n - tail0 ? ids[tail0 + gtid] : 0u);
-    } else {
-        if (gtid < h) bsgs_one<NB, NA, SCG>(S, ids[gtid]);
-        if (gtid < n - tail0) bsgs_one<NB, NA, SCG>(S, ids[tail0 + gtid]);
-    }
-
-    // lane partials -> wave butterfly -> LDS -> one partial per (power, block)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            uint64_t x;
-            if (a == 0) x = fold64_32(S.a0[b]);
-            else { // m + c*2^64, 2^64 == 25 (mod p); c*25 < 2^37
-                // SC: c is the wave's total, added once (by lane 0)
-                const uint32_t c = bsgs_scalar<NB, SCG>(a - 1, b) ? (lane == 0 ? S.cs[a - 1][b] : 0u) : S.c[a - 1][b];
-                x = (uint64_t)fold64_32(S.m[a - 1][b]) + fold64_32((uint64_t)c * 25u);
-            }
-            x = fold64_32(x);                                  // < 2^32
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) x += shfl_xor_u64(x, off); // < 2^38
-            if (lane == 0) sm[wave * (NB * NA) + a * NB + b] = x;
-        }
-    }
-    __syncthreads();
-    for (uint32_t m = threadIdx.x; m < T; m += BLOCK) {
-        uint64_t s = 0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) s += sm[w * (NB * NA) + m];
-        partials[(size_t)m * gridDim.x + blockIdx.x] = s;
-    }
+// ---- baby-step / giant-step encode for 9 <= t <= 32 (bsgs.h)
+// waves per SIMD the register budget is sized for (tools/tune_bsgs.hip: 5 for
+// (8,4) beat 4 by 2-3 %; its three spilled VGPRs live outside the loop)
+template <int NB, int NA, int SG>
+__global__ __launch_bounds__(BLOCK, (NB * NA >= 32 ? 5 : 4)) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids,
+                                                                                  uint64_t n, uint32_t head,
+                                                                                  uint32_t T,
+                                                                                  uint64_t *__restrict__ partials) {
+    bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD>>(ids, n, head, T, partials);
 }
 
 // lane j of a G-group: start = x^(j+1), step = x^G (square-and-multiply).
@@ -807,29 +598,33 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     if (n >= (1ull << 40)) return QK_E_INVAL; // 4 TB of ids: beyond any HBM; keeps per-lane trip counts 32-bit
     // baby-step / giant-step for 9 <= T <= 32 (fewer modmuls per id); the
     // power chain otherwise
-    // Scalar-carry BSGS groups keep per-wave 32-bit wrap totals: a wave sees
-    // at most 256 * trips carries per power, so trips must stay < 2^24 — true
-    // for any n < 2^40 at the default grid; a tiny override grid over a huge n
-    // takes the all-VALU form.  QK_TUNE_BSGS_SCG=g overrides the number of
-    // scalar-counted MAC groups (measurements).
-    static const int scg_env = [] { const char *e = getenv("QK_TUNE_BSGS_SCG"); return e ? atoi(e) : -1; }();
-    const bool sc_ok = !(ctx->grid_override && n / (4ull * BLOCK * ctx->grid_override) >= (1ull << 24) - 2);
-    auto scg = [&](int dflt) { return sc_ok ? (scg_env >= 0 ? scg_env : dflt) : 0; };
+    // Scalar-counted BSGS groups (bsgs.h) keep per-wave 32-bit wrap totals: a
+    // wave sees at most 64 * (4 * trips + 2) wraps per accumulator, so trips
+    // must stay < 2^24 - 1 — true for any n < 2^40 at >= 1 workgroup per CU;
+    // a tiny override grid over a huge n takes the all-VALU form.
+    // QK_TUNE_BSGS_SG=g overrides the number of scalar-counted groups
+    // (measurements; tools/tune_bsgs.hip).
+    static const int sg_env = [] { const char *e = getenv("QK_TUNE_BSGS_SG"); return e ? atoi(e) : -1; }();
+    const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
+    const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
+    auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
 #define QK_BSGS(NB_, NA_, G_)                                                                        \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)
-    if (T >= 9 && T <= 12) return scg(0) ? QK_BSGS(4, 3, 2) : QK_BSGS(4, 3, 0);
-    if (T >= 13 && T <= 16) return scg(0) ? QK_BSGS(4, 4, 3) : QK_BSGS(4, 4, 0);
-    if (T >= 17 && T <= 24) return scg(0) ? QK_BSGS(6, 4, 3) : QK_BSGS(6, 4, 0);
+    if (T >= 9 && T <= 12) return sg(3) ? QK_BSGS(4, 3, 3) : QK_BSGS(4, 3, 0);
+    if (T >= 13 && T <= 16) return sg(4) ? QK_BSGS(4, 4, 4) : QK_BSGS(4, 4, 0);
+    if (T >= 17 && T <= 24) return sg(4) ? QK_BSGS(6, 4, 4) : QK_BSGS(6, 4, 0);
     if (T >= 25 && T <= 32) {
-        switch (scg(0)) {
+        switch (sg(QK_BSGS_SG_T32)) {
         case 0: return QK_BSGS(8, 4, 0);
         case 1: return QK_BSGS(8, 4, 1);
         case 2: return QK_BSGS(8, 4, 2);
         case 3: return QK_BSGS(8, 4, 3);
         case 4: return QK_BSGS(8, 4, 4);
         case 5: return QK_BSGS(8, 4, 5);
-        default: return QK_BSGS(8, 4, 6);
+        case 6: return QK_BSGS(8, 4, 6);
+        case 7: return QK_BSGS(8, 4, 7);
+        default: return QK_BSGS(8, 4, 8);
         }
     }
 #undef QK_BSGS

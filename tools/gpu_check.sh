@@ -22,12 +22,13 @@ for s in $STEPS; do
   case $s in
     ubench) step ubench 120 ./tools/ubench_int || exit 3 ;;
     ubdep) step ubdep 300 ./tools/ubench_dep || exit 3 ;;
+    ubissue) step ubissue 300 ./tools/ubench_issue || exit 3 ;;
     smoke) step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
     pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
-    scgsweep)
-      for g in ${SCG_LIST:-0 1 2 3 4 5 6}; do
-        QK_TUNE_BSGS_SCG=$g step scg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 || exit 3
+    sgsweep)
+      for g in ${SG_LIST:-0 2 4 6 8}; do
+        QK_TUNE_BSGS_SG=$g step sg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 || exit 3
       done ;;
     configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
     configs20) QK_TUNE_U64_KMAX=20 step configs20 900 python3 -u tools/bench_configs.py u64 || exit 3 ;;
@@ -36,6 +37,7 @@ for s in $STEPS; do
       step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 1 --cpu-sample 0 || exit 3 ;;
     dist2) step dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --ids-per-gpu 2e8 --dist-backend gloo || exit 3 ;;
     tune) step tune 600 ./tools/tune_encode ${TUNE_ARGS:-} || exit 3 ;;
+    tunebsgs) step tunebsgs 600 ./tools/tune_bsgs ${TUNE_ARGS:-} || exit 3 ;;
     listctr) step listctr 120 rocprofv3 -L || true ;;
     pmcsq)
       export TMPDIR=/tmp
@@ -45,9 +47,9 @@ for s in $STEPS; do
       step proflows 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflows" -o run -- python3 "$ROOT/tools/bench_configs.py" flows packets --steps 4 || exit 3 ;;
     pmcab)  # SQ stall/issue counters for two BSGS variants (A/B), two counter passes each
       export TMPDIR=/tmp
-      for g in ${SCG_AB:-0 6}; do
-        QK_TUNE_BSGS_SCG=$g step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
-        QK_TUNE_BSGS_SCG=$g step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
+      for g in ${SG_AB:-0 8}; do
+        QK_TUNE_BSGS_SG=$g step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
+        QK_TUNE_BSGS_SG=$g step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
       done ;;
     pmc)
       export TMPDIR=/tmp
