@@ -41,7 +41,7 @@ for s in $STEPS; do
     listctr) step listctr 120 rocprofv3 -L || true ;;
     pmcsq)
       export TMPDIR=/tmp
-      step pmcsq 600 rocprofv3 --pmc ${PMC_SQ:-SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE} --output-format csv -d "$OUT/pmcsq" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
+      step pmcsq 600 rocprofv3 --pmc ${PMC_SQ:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE} --output-format csv -d "$OUT/pmcsq" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
     proflows)
       export TMPDIR=/tmp
       step proflows 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflows" -o run -- python3 "$ROOT/tools/bench_configs.py" flows packets --steps 4 || exit 3 ;;

@@ -207,13 +207,15 @@ int main(int argc, char **argv) {
 
     // SG counts row-0 groups (0-1) only when ROW0 == 0; with ROW0 == 1 the
     // scalar groups start at the first MAC group (g = 2)
-    std::vector<Var> vars = {{"r1f1_sg8", k_sg<8, 1, 1>},
-                             {"r1f1_sg8_w5", k_sg<8, 1, 1, false, 5>},
-                             {"r1f1_sg7", k_sg<7, 1, 1>},
-                             {"r0f1_sg8", k_sg<8, 0, 1>},
-                             {"r0f1_sg7", k_sg<7, 0, 1>},
-                             {"r0f1_sg6", k_sg<6, 0, 1>},
-                             {"r0f1_sg8_w5", k_sg<8, 0, 1, false, 5>}};
+    // round-1 measurements: legacy 3.13 ms; row 0 as mads +
+    // min-tracked folds + all MAC wraps scalar (r1f1_sg8) 2.73 ms at 4 waves,
+    // 2.67 ms at 5 waves; burst-free interleaved scalar counting 3.12 ms;
+    // compiler-scheduled popcounts spill SGPRs.  Ablations (wrong sums): no
+    // scalar counting 2.58 ms, no MACs 1.69 ms.
+    std::vector<Var> vars = {{"legacy", k_legacy},
+                             {"r0f0_sg8_w3", k_sg<8, 0, 0>},
+                             {"r1f1_sg8_w4", k_sg<8, 1, 1, false, 4>},
+                             {"r1f1_sg8_w5", k_sg<8, 1, 1, false, 5>}};
     uint32_t ref[T], got[T];
     std::vector<std::vector<float>> times(vars.size());
     std::vector<double> mhz(vars.size(), 0.0);

@@ -24,6 +24,7 @@ def main(rnd: str, src: str = "gpurun_out", key: str = "u32_t32", n_ids: int = 1
               "pmc/run_counter_collection.csv": "encode_pmc_fetch_size.csv",
               "pmcsq/run_counter_collection.csv": "encode_pmc_sq.csv",
               "ubench.log": "ubench_int.json", "tune.log": "tune_encode.json", "ubdep.log": "ubench_dep.json",
+              "tunebsgs.log": "tune_bsgs.json", "ubissue.log": "ubench_issue.json",
               "pytest.log": "pytest_gpu.log", "smoke.log": "smoke.log"}
     for a, b in copies.items():
         if os.path.exists(os.path.join(src, a)):
