@@ -43,11 +43,14 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
 
 // ---- multiply-accumulate and add groups, carries counted ------------------
 // The carry masks live in explicitly named SGPR pairs, and consecutive groups
-// alternate between two disjoint sets (SET 0: s[40:47], SET 1: s[48:55]).
-// hipcc treats an inline-asm block's SGPR definitions conservatively and pads
-// "s_nop 0" between two blocks that define the same SGPRs; with disjoint sets
-// back to back it inserts none (8 nops per id before).  Inside a block every
-// VALU carry-in read is >= 3 VALU instructions after its write.
+// alternate between two disjoint sets (SET 0: s[40:47] + temp s56, SET 1:
+// s[48:55] + temp s57).  hipcc treats an inline-asm block's SGPR definitions
+// conservatively and pads "s_nop 0" between two blocks that define the same
+// SGPRs (8 nops per id with compiler-allocated pairs; 3-5 remain at blocks
+// with "+s" operands — one fused asm statement per id measured no faster).
+// The blocks are volatile so the compiler keeps them in this alternating
+// order.  Inside a block every VALU carry-in read is >= 3 VALU instructions
+// after its write.
 #define QK_MAC4V(P0, P1, P2, P3)                                                                       \
     "v_mad_u64_u32 %0, " P0 ", %8, %9, %0\n\t"                                                         \
     "v_mad_u64_u32 %1, " P1 ", %8, %10, %1\n\t"                                                        \
@@ -57,15 +60,15 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     "v_addc_co_u32_e64 %5, " P1 ", %5, 0, " P1 "\n\t"                                                  \
     "v_addc_co_u32_e64 %6, " P2 ", %6, 0, " P2 "\n\t"                                                  \
     "v_addc_co_u32_e64 %7, " P3 ", %7, 0, " P3
-#define QK_MAC4S(P0, P1, P2, P3)                                                                       \
-    "v_mad_u64_u32 %0, " P0 ", %12, %13, %0\n\t"                                                       \
-    "v_mad_u64_u32 %1, " P1 ", %12, %14, %1\n\t"                                                       \
-    "v_mad_u64_u32 %2, " P2 ", %12, %15, %2\n\t"                                                       \
-    "v_mad_u64_u32 %3, " P3 ", %12, %16, %3\n\t"                                                       \
-    "s_bcnt1_i32_b64 %8, " P0 "\n\ts_add_u32 %4, %4, %8\n\t"                                           \
-    "s_bcnt1_i32_b64 %9, " P1 "\n\ts_add_u32 %5, %5, %9\n\t"                                           \
-    "s_bcnt1_i32_b64 %10, " P2 "\n\ts_add_u32 %6, %6, %10\n\t"                                         \
-    "s_bcnt1_i32_b64 %11, " P3 "\n\ts_add_u32 %7, %7, %11"
+#define QK_MAC4S(P0, P1, P2, P3, T)                                                                       \
+    "v_mad_u64_u32 %0, " P0 ", %8, %9, %0\n\t"                                                         \
+    "v_mad_u64_u32 %1, " P1 ", %8, %10, %1\n\t"                                                        \
+    "v_mad_u64_u32 %2, " P2 ", %8, %11, %2\n\t"                                                        \
+    "v_mad_u64_u32 %3, " P3 ", %8, %12, %3\n\t"                                                        \
+    "s_bcnt1_i32_b64 " T ", " P0 "\n\ts_add_u32 %4, %4, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P1 "\n\ts_add_u32 %5, %5, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %6, %6, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P3 "\n\ts_add_u32 %7, %7, " T
 #define QK_ADD4V(P0, P1, P2, P3)                                                                       \
     "v_add_co_u32_e64 %0, " P0 ", %0, %8\n\t"                                                          \
     "v_add_co_u32_e64 %1, " P1 ", %1, %9\n\t"                                                          \
@@ -75,17 +78,20 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     "v_addc_co_u32_e64 %5, " P1 ", %5, 0, " P1 "\n\t"                                                  \
     "v_addc_co_u32_e64 %6, " P2 ", %6, 0, " P2 "\n\t"                                                  \
     "v_addc_co_u32_e64 %7, " P3 ", %7, 0, " P3
-#define QK_ADD4S(P0, P1, P2, P3)                                                                       \
-    "v_add_co_u32_e64 %0, " P0 ", %0, %12\n\t"                                                         \
-    "v_add_co_u32_e64 %1, " P1 ", %1, %13\n\t"                                                         \
-    "v_add_co_u32_e64 %2, " P2 ", %2, %14\n\t"                                                         \
-    "v_add_co_u32_e64 %3, " P3 ", %3, %15\n\t"                                                         \
-    "s_bcnt1_i32_b64 %8, " P0 "\n\ts_add_u32 %4, %4, %8\n\t"                                           \
-    "s_bcnt1_i32_b64 %9, " P1 "\n\ts_add_u32 %5, %5, %9\n\t"                                           \
-    "s_bcnt1_i32_b64 %10, " P2 "\n\ts_add_u32 %6, %6, %10\n\t"                                         \
-    "s_bcnt1_i32_b64 %11, " P3 "\n\ts_add_u32 %7, %7, %11"
+#define QK_ADD4S(P0, P1, P2, P3, T)                                                                       \
+    "v_add_co_u32_e64 %0, " P0 ", %0, %8\n\t"                                                          \
+    "v_add_co_u32_e64 %1, " P1 ", %1, %9\n\t"                                                          \
+    "v_add_co_u32_e64 %2, " P2 ", %2, %10\n\t"                                                         \
+    "v_add_co_u32_e64 %3, " P3 ", %3, %11\n\t"                                                         \
+    "s_bcnt1_i32_b64 " T ", " P0 "\n\ts_add_u32 %4, %4, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P1 "\n\ts_add_u32 %5, %5, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %6, %6, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P3 "\n\ts_add_u32 %7, %7, " T
 #define QK_SET0 "s[40:41]", "s[42:43]", "s[44:45]", "s[46:47]"
 #define QK_SET1 "s[48:49]", "s[50:51]", "s[52:53]", "s[54:55]"
+// scalar-form temps: one per set, so adjacent blocks never share a definition
+#define QK_SET0T QK_SET0, "s56"
+#define QK_SET1T QK_SET1, "s57"
 #define QK_CLOB0 "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47"
 #define QK_CLOB1 "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55"
 #define QK_EXPAND(M, ...) M(__VA_ARGS__)
@@ -96,12 +102,12 @@ __device__ __forceinline__ void mac4v(uint64_t &a0, uint64_t &a1, uint64_t &a2, 
                                       uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t A, uint32_t b0,
                                       uint32_t b1, uint32_t b2, uint32_t b3) {
     if constexpr (SET == 0)
-        asm(QK_EXPAND(QK_MAC4V, QK_SET0)
+        asm volatile(QK_EXPAND(QK_MAC4V, QK_SET0)
             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
             : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
             : QK_CLOB0);
     else
-        asm(QK_EXPAND(QK_MAC4V, QK_SET1)
+        asm volatile(QK_EXPAND(QK_MAC4V, QK_SET1)
             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
             : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
             : QK_CLOB1);
@@ -110,19 +116,16 @@ template <int SET>
 __device__ __forceinline__ void mac4s(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t &s0,
                                       uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t A, uint32_t b0,
                                       uint32_t b1, uint32_t b2, uint32_t b3) {
-    uint32_t t0, t1, t2, t3;
     if constexpr (SET == 0)
-        asm(QK_EXPAND(QK_MAC4S, QK_SET0)
-            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
-              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+        asm volatile(QK_EXPAND(QK_MAC4S, QK_SET0T)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3)
             : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
-            : "scc", QK_CLOB0);
+            : "scc", "s56", QK_CLOB0);
     else
-        asm(QK_EXPAND(QK_MAC4S, QK_SET1)
-            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
-              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+        asm volatile(QK_EXPAND(QK_MAC4S, QK_SET1T)
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3)
             : "v"(A), "v"(b0), "v"(b1), "v"(b2), "v"(b3)
-            : "scc", QK_CLOB1);
+            : "scc", "s57", QK_CLOB1);
 }
 // lo_j += b_j (32-bit), wraps counted per lane (c_j) or per wave (s_j)
 template <int SET>
@@ -130,12 +133,12 @@ __device__ __forceinline__ void add4v(uint32_t &l0, uint32_t &l1, uint32_t &l2, 
                                       uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t b0, uint32_t b1,
                                       uint32_t b2, uint32_t b3) {
     if constexpr (SET == 0)
-        asm(QK_EXPAND(QK_ADD4V, QK_SET0)
+        asm volatile(QK_EXPAND(QK_ADD4V, QK_SET0)
             : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
             : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
             : QK_CLOB0);
     else
-        asm(QK_EXPAND(QK_ADD4V, QK_SET1)
+        asm volatile(QK_EXPAND(QK_ADD4V, QK_SET1)
             : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
             : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
             : QK_CLOB1);
@@ -144,19 +147,16 @@ template <int SET>
 __device__ __forceinline__ void add4s(uint32_t &l0, uint32_t &l1, uint32_t &l2, uint32_t &l3, uint32_t &s0,
                                       uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t b0, uint32_t b1,
                                       uint32_t b2, uint32_t b3) {
-    uint32_t t0, t1, t2, t3;
     if constexpr (SET == 0)
-        asm(QK_EXPAND(QK_ADD4S, QK_SET0)
-            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
-              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+        asm volatile(QK_EXPAND(QK_ADD4S, QK_SET0T)
+            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3)
             : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
-            : "scc", QK_CLOB0);
+            : "scc", "s56", QK_CLOB0);
     else
-        asm(QK_EXPAND(QK_ADD4S, QK_SET1)
-            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "=&s"(t0),
-              "=&s"(t1), "=&s"(t2), "=&s"(t3)
+        asm volatile(QK_EXPAND(QK_ADD4S, QK_SET1T)
+            : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3)
             : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
-            : "scc", QK_CLOB1);
+            : "scc", "s57", QK_CLOB1);
 }
 // leftovers for NB % 4 != 0 (t = 17..24 uses NB = 6): compiler-allocated
 // carries with explicit wait states
@@ -196,12 +196,12 @@ template <int SET>
 __device__ __forceinline__ void row4m(uint64_t &a0, uint64_t &a1, uint64_t &a2, uint64_t &a3, uint32_t b0,
                                       uint32_t b1, uint32_t b2, uint32_t b3) {
     if constexpr (SET == 0)
-        asm(QK_EXPAND(QK_ROW4M, QK_SET0)
+        asm volatile(QK_EXPAND(QK_ROW4M, QK_SET0)
             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
             : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
             : QK_CLOB0);
     else
-        asm(QK_EXPAND(QK_ROW4M, QK_SET1)
+        asm volatile(QK_EXPAND(QK_ROW4M, QK_SET1)
             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
             : "v"(b0), "v"(b1), "v"(b2), "v"(b3)
             : QK_CLOB1);
@@ -244,20 +244,6 @@ struct Acc {
 template <class C>
 __host__ __device__ constexpr bool scalar_group(int row, int b) {
     return b / 4 * 4 + 4 <= C::NB && (row > 0 || C::ROW0 == 0) && row * (C::NB / 4) + b / 4 < C::SG;
-}
-
-// y * x (mod p) lazily, y, x < 2^32 -> r < 2^32 (FOLD == 1 form, see Cfg):
-// t = tl + 5 th (th <= 5) as in field.h mulfold32_fast, then r = tl + 5 th
-// mod 2^32.  If that add wrapped, r < 5 th <= 25; mn tracks the minimum so
-// the caller can redo the id exactly (probability ~25 / 2^32 per fold).
-__device__ __forceinline__ uint32_t mulfold32_min(uint32_t y, uint32_t x, uint32_t &mn) {
-    const uint64_t P = (uint64_t)y * x;
-    const uint32_t Ph = (uint32_t)(P >> 32);
-    const uint64_t Q = P + (uint64_t)Ph * C32;
-    const uint32_t tl = (uint32_t)Q, th = (uint32_t)(Q >> 32) - Ph;
-    const uint32_t r = tl + th * C32;
-    mn = r < mn ? r : mn;
-    return r;
 }
 
 // powers of one id; returns nonzero if a lazy fold may have wrapped (the

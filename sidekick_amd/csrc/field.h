@@ -99,6 +99,21 @@ QK_HD uint32_t mulfold32_exact(uint32_t y, uint32_t x) {
     return r;
 }
 
+// The BSGS kernels' lazy product (bsgs.h): the same t = tl + 5 th, then
+// r = tl + 5 th mod 2^32 with no carry handling.  If that add wrapped, the
+// true sum is r + 2^32 with r < 5 th <= 25, so the caller tracks mn = min(r)
+// over an id's products and redoes the id exactly when mn < 25 (probability
+// ~25 / 2^32 per product; a legitimately small r only costs a redo).
+QK_HD uint32_t mulfold32_min(uint32_t y, uint32_t x, uint32_t &mn) {
+    const uint64_t P = (uint64_t)y * x;
+    const uint32_t Ph = (uint32_t)(P >> 32);
+    const uint64_t Q = P + (uint64_t)Ph * C32;
+    const uint32_t tl = (uint32_t)Q, th = (uint32_t)(Q >> 32) - Ph;
+    const uint32_t r = tl + th * C32;
+    mn = r < mn ? r : mn;
+    return r;
+}
+
 // 5x mod p for canonical x (x5 in the step above)
 QK_HD uint32_t times5_32(uint32_t x) {
     const uint64_t v = (uint64_t)x * C32;                   // < 5*2^32

@@ -66,6 +66,13 @@ static void check_mulfold(uint32_t y, uint32_t x) {
     if (!w) EXPECT(f == e, "fast != exact without wrap y=%u x=%u", y, x);
     EXPECT(canon32(mul32_lazy(y, x)) == ref_mul32(y, x), "mul32_lazy y=%u x=%u", y, x);
     EXPECT(canon32(mad32_lazy(y, x, 7)) == (uint32_t)(((u128)y * x + 7) % P32), "mad32_lazy");
+    // min-tracked form (bsgs.h FOLD == 1): a wrap always leaves r < 25, and
+    // any r >= 25 is the exact lazy product
+    uint32_t mn = 0xFFFFFFFFu;
+    const uint32_t m = mulfold32_min(y, x, mn);
+    EXPECT(mn == m, "mulfold32_min tracks its result");
+    if (w) EXPECT(m < 25, "wrapped fold left r=%u >= 25 (y=%u x=%u)", m, y, x);
+    if (m >= 25) EXPECT(m == e, "min form != exact with r >= 25 y=%u x=%u", y, x);
 }
 
 static int run_check() {

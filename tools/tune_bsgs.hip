@@ -210,7 +210,8 @@ int main(int argc, char **argv) {
     // round-1 measurements: legacy 3.13 ms; row 0 as mads +
     // min-tracked folds + all MAC wraps scalar (r1f1_sg8) 2.73 ms at 4 waves,
     // 2.67 ms at 5 waves; burst-free interleaved scalar counting 3.12 ms;
-    // compiler-scheduled popcounts spill SGPRs.  Ablations (wrong sums): no
+    // compiler-scheduled popcounts spill SGPRs; the whole accumulate as one
+    // asm statement (no asm-boundary nops) 2.71 vs 2.71 ms.  Ablations (wrong sums): no
     // scalar counting 2.58 ms, no MACs 1.69 ms.
     std::vector<Var> vars = {{"legacy", k_legacy},
                              {"r0f0_sg8_w3", k_sg<8, 0, 0>},
