@@ -44,6 +44,7 @@ def lib():
             "qo_eval_u64": (C.c_uint64, [u64p, C.c_uint32, C.c_uint64]),
             "qo_root_test_u32": (C.c_uint64, [u32p, C.c_uint32, u32p, C.c_uint64, i64p, C.c_uint64]),
             "qo_root_test_u64": (C.c_uint64, [u64p, C.c_uint32, u64p, C.c_uint64, i64p, C.c_uint64]),
+            "qo_bench_construct": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -90,6 +91,14 @@ def encode_seed_mt(bits, seed, n, t, threads, start=0):
     if rc:
         raise RuntimeError(f"qo_encode_seed_mt rc={rc}")
     return [int(v) for v in S]
+
+
+def bench_construct(bits, seed, n, t, trials):
+    """Reference-shape CPU microbenchmark: mean ns per id over `trials`
+    construct-and-insert-n-ids runs (BASELINE.md's `-e 1000` rows)."""
+    sink = C.c_uint64()
+    ns = lib().qo_bench_construct(bits, seed, n, t, trials, C.byref(sink))
+    return ns / max(1, n * trials)
 
 
 def encode_u64(ids, t):

@@ -21,10 +21,13 @@
  * Decode (media_client.rs:295-313): Newton's identities (to_coeffs) and the
  * Horner root test (arithmetic::eval(&coeffs, id).value() == 0).
  */
+#define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
 #include <stdint.h>
 #include <stddef.h>
 #include <stdlib.h>
+#include <string.h>
+#include <time.h>
 
 #define QO_P32 4294967291u                 /* 2^32 - 5  */
 #define QO_P64 18446744073709551557ull     /* 2^64 - 59 */
@@ -205,4 +208,38 @@ int qo_encode_seed_mt(uint32_t bits, uint64_t seed, uint64_t start, uint64_t n, 
         }
     free(parts);
     return 0;
+}
+
+/* ---- reference-shape microbenchmark (BASELINE.md "Reference-shape row"):
+ * the shape of the quack crate's `benchmark_construct` runs quoted there
+ * (`-e 1000`, per-trial time / ids): each trial draws n fresh ids, then
+ * times constructing an empty sketch of threshold t and inserting them.
+ * Returns the summed timed nanoseconds; the folded sketches go to *sink so
+ * the work cannot be elided.  The crate itself is absent (parity unpinned),
+ * so this times the restatement's insert loop, not the crate. */
+static uint64_t qo_now_ns(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+uint64_t qo_bench_construct(uint32_t bits, uint64_t seed, uint64_t n, uint32_t t, uint32_t trials, uint64_t *sink) {
+    const size_t esz = bits == 32 ? 4 : 8;
+    void *ids = malloc(n ? n * esz : 1), *S = malloc(t ? t * esz : 1);
+    if (!ids || !S || t == 0) { free(ids); free(S); return 0; }
+    uint64_t total = 0, fold = 0;
+    for (uint32_t r = 0; r < trials; ++r) {
+        if (bits == 32) qo_splitmix_u32(seed, (uint64_t)r * n, n, (uint32_t *)ids);
+        else qo_splitmix_u64(seed, (uint64_t)r * n, n, (uint64_t *)ids);
+        const uint64_t t0 = qo_now_ns();
+        memset(S, 0, t * esz);
+        if (bits == 32) qo_encode_u32((const uint32_t *)ids, n, t, (uint32_t *)S);
+        else qo_encode_u64((const uint64_t *)ids, n, t, (uint64_t *)S);
+        total += qo_now_ns() - t0;
+        fold ^= bits == 32 ? ((uint32_t *)S)[t - 1] : ((uint64_t *)S)[t - 1];
+    }
+    if (sink) *sink = fold;
+    free(ids);
+    free(S);
+    return total;
 }

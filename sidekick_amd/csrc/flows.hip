@@ -20,9 +20,13 @@
 //                       out-of-range key and sort last.
 //   2. two stable radix sorts (hipCUB/rocPRIM, 49-bit keys: lo, then hi) ->
 //      packet order within each flow is preserved (last_value = last id).
-//   3. segment heads -> work items of <= 64 Ki ids per workgroup.
-//   4. k_seg_encode<G,K>  power chains per id, block reduction, one integer
-//      atomicAdd per (flow, power) per work item (order-independent, exact).
+//   3. segment heads -> per-flow offsets; flows of > SMALL_SEG ids (or any
+//      flow when T > 32) -> work items of <= 64 Ki ids per workgroup.
+//   4. k_seg_small<Cfg>   one lane per small flow: baby-step/giant-step per id
+//      (bsgs.h) with the whole flow in that lane's registers, one plain store
+//      per (flow, power); k_seg_encode<G,K> for the work items: power chains
+//      per id, block reduction, one integer atomicAdd per (flow, power) per
+//      work item (order-independent, exact).
 // The CSR primitive qk_u32_encode_segments_device runs step 4 directly on
 // caller-grouped ids.
 #include <string.h>
@@ -31,6 +35,7 @@
 #include <hipcub/hipcub.hpp>
 #include <vector>
 
+#include "bsgs.h"
 #include "ctx.h"
 #include "field.h"
 #include "records.h"
@@ -110,6 +115,63 @@ __global__ __launch_bounds__(SG_BLOCK) void k_seg_encode(const uint32_t *__restr
         for (int w = 0; w < SG_WAVES; ++w) s += sm[w * (G * K) + m];   // < 2^40
         atomicAdd(&acc_out[(size_t)it.seg * T + m], (unsigned long long)fold64_32(s));
     }
+}
+
+// ---- small flows (the many-flow case) ---------------------------------------
+// A flow of <= SMALL_SEG ids is encoded by ONE lane: the whole flow stays in
+// that lane's registers, so there is no cross-lane reduction and no atomic
+// (the lane owns its flow's accumulator row).  Per id it runs the headline
+// kernel's baby-step/giant-step work (bsgs.h) with per-lane wrap counters —
+// the lanes of a wave belong to different flows, so the wave-level scalar
+// count of the headline kernel would mix them.  Flows above SMALL_SEG keep
+// the work-item kernel above (a long flow in one lane would stall its wave).
+constexpr uint64_t SMALL_SEG = 4096;
+
+template <class C>
+__global__ __launch_bounds__(SG_BLOCK) void k_seg_small(const uint32_t *__restrict__ ids,
+                                                        const uint64_t *__restrict__ offs, uint32_t nseg,
+                                                        uint32_t T, unsigned long long *__restrict__ acc_out) {
+    const uint32_t g = blockIdx.x * SG_BLOCK + threadIdx.x;
+    if (g >= nseg) return;
+    const uint64_t b = offs[g], e = offs[g + 1];
+    if (e - b > SMALL_SEG) return;   // a work-item flow
+    bsgs::Acc<C::NB, C::NA> S;
+#pragma unroll
+    for (int j = 0; j < C::NB; ++j) {
+        S.lo0[j] = 0;
+        S.c0[j] = 0;
+        S.r0[j] = 0;
+#pragma unroll
+        for (int a = 0; a < C::NA - 1; ++a) { S.m[a][j] = 0; S.c[a][j] = 0; }
+    }
+    for (uint64_t i = b; i < e; ++i) bsgs::one<C>(S, ids[i]);
+    // power a*NB + j + 1: a = 0 row is a 64-bit sum; a >= 1 is m + c * 2^64,
+    // 2^64 == 25 (mod p)
+#pragma unroll
+    for (int a = 0; a < C::NA; ++a) {
+#pragma unroll
+        for (int j = 0; j < C::NB; ++j) {
+            const uint32_t m = (uint32_t)(a * C::NB + j);
+            if (m < T) {
+                const uint64_t v = a == 0 ? (uint64_t)fold64_32(S.r0[j])
+                                          : (uint64_t)fold64_32(S.m[a - 1][j]) +
+                                                fold64_32((uint64_t)S.c[a - 1][j] * 25u);
+                acc_out[(size_t)g * T + m] = fold64_32(v);
+            }
+        }
+    }
+}
+
+// per-lane (VALU) wrap counters: SG = 0
+static int seg_small_launch(uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
+                            unsigned long long *acc, hipStream_t s) {
+    const dim3 grid((nseg + SG_BLOCK - 1) / SG_BLOCK), block(SG_BLOCK);
+    if (T <= 8) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<4, 2, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
+    else if (T <= 12) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<4, 3, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
+    else if (T <= 16) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<4, 4, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
+    else if (T <= 24) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<6, 4, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
+    else hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<8, 4, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
+    return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
 }
 
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
@@ -260,21 +322,35 @@ __global__ void k_seg_last(const uint32_t *__restrict__ ids, const uint64_t *__r
     if (i < nseg) last[i] = offs[i + 1] > offs[i] ? ids[offs[i + 1] - 1] : 0u;
 }
 
-static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs) {
+// work items of the flows k_seg_small does not take: every flow when T > 32,
+// else the flows of more than SMALL_SEG ids
+static bool small_ok(uint32_t T) { return T <= 32; }
+static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs, uint32_t T) {
     std::vector<SegItem> items;
-    for (size_t g = 0; g + 1 < offs.size(); ++g)
+    for (size_t g = 0; g + 1 < offs.size(); ++g) {
+        if (small_ok(T) && offs[g + 1] - offs[g] <= SMALL_SEG) continue;
         for (uint64_t lo = offs[g]; lo < offs[g + 1]; lo += SEG_CHUNK)
             items.push_back({(uint32_t)g, 0u, lo, std::min<uint64_t>(lo + SEG_CHUNK, offs[g + 1])});
+    }
     return items;
 }
 
-// Segmented encode of a grouped id array (work items from seg_items) into a
-// device accumulator [nseg][T] (u64, zeroed here); d_items holds
-// items.size() entries.
-static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const std::vector<SegItem> &items, size_t nseg,
-                      uint32_t T, unsigned long long *d_acc, SegItem *d_items, hipStream_t s) {
+// Segmented encode of a grouped id array into a device accumulator [nseg][T]
+// (u64, zeroed here): the small flows by k_seg_small (d_offs: the nseg + 1
+// offsets on the device), the rest by the work items from seg_items (d_items
+// holds items.size() entries).
+static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs,
+                      const std::vector<SegItem> &items, size_t nseg, uint32_t T, unsigned long long *d_acc,
+                      SegItem *d_items, hipStream_t s) {
     QK_HIP_TRY(hipMemsetAsync(d_acc, 0, nseg * T * sizeof(uint64_t), s));
-    if (items.empty()) return QK_OK;
+    if (small_ok(T) && nseg) {
+        hipEvent_t e0 = prof_begin(ctx, s);
+        const int rs = seg_small_launch(T, d_ids, d_offs, (uint32_t)nseg, d_acc, s);
+        prof_end(ctx, s, e0);
+        if (rs) return rs;
+    }
+    // the caller's host offsets / items vectors must outlive their async copies
+    if (items.empty()) return hipStreamSynchronize(s) == hipSuccess ? QK_OK : QK_E_HIP;
     int rc = QK_OK;
     if (hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(SegItem), hipMemcpyHostToDevice, s) != hipSuccess)
         rc = QK_E_HIP;
@@ -317,7 +393,7 @@ extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids,
     QK_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = pick_stream(ctx, stream);
     const uint32_t T = threshold;
-    const std::vector<SegItem> items = seg_items(offs);
+    const std::vector<SegItem> items = seg_items(offs, T);
     Carve probe{nullptr};
     probe.take<unsigned long long>(nseg * T);
     probe.take<SegItem>(items.size());
@@ -329,12 +405,12 @@ extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids,
     SegItem *d_items = cv.take<SegItem>(items.size());
     uint32_t *d_last = cv.take<uint32_t>(nseg);
     uint64_t *d_offs = cv.take<uint64_t>(nseg + 1);
-    int rc = seg_encode(ctx, d_ids, items, nseg, T, d_acc, d_items, s);
+    int rc = QK_OK;
+    if (hipMemcpyAsync(d_offs, offs.data(), (nseg + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = QK_E_HIP;
+    if (!rc) rc = seg_encode(ctx, d_ids, d_offs, items, nseg, T, d_acc, d_items, s);
     std::vector<uint64_t> acc(nseg * T);
     std::vector<uint32_t> last(nseg, 0);
     if (!rc && hipMemcpyAsync(acc.data(), d_acc, acc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
-        rc = QK_E_HIP;
-    if (!rc && hipMemcpyAsync(d_offs, offs.data(), (nseg + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
         rc = QK_E_HIP;
     if (!rc) {
         hipLaunchKernelGGL(k_seg_last, dim3((uint32_t)((nseg + 255) / 256)), dim3(256), 0, s, d_ids, d_offs,
@@ -458,6 +534,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const size_t items_max = (size_t)nseg + inserted / SEG_CHUNK + 1;
         const size_t rec = qk_u32_size(T);
         SegItem *d_items = nullptr;
+        uint64_t *d_offs = nullptr;
         uint32_t *d_rec = nullptr;
         uint8_t *d_keys = nullptr;
         {
@@ -467,6 +544,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             probe.take<SegItem>(items_max);
             probe.take<uint8_t>((size_t)nseg * rec);
             probe.take<uint8_t>((size_t)nseg * 12);
+            probe.take<uint64_t>((size_t)nseg + 1);
             rc = ensure_flow(ctx, 1, probe.off);
         }
         if (!rc) {
@@ -476,6 +554,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             d_items = cv.take<SegItem>(items_max);
             d_rec = (uint32_t *)cv.take<uint8_t>((size_t)nseg * rec);
             d_keys = cv.take<uint8_t>((size_t)nseg * 12);
+            d_offs = cv.take<uint64_t>((size_t)nseg + 1);
         }
         if (!rc) hipLaunchKernelGGL(k_seg_info, dim3((nseg + 255) / 256), dim3(256), 0, s, kh, kl2, ids2, heads, nseg,
                                     inserted, info);
@@ -485,8 +564,10 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         std::vector<uint64_t> offs(nseg + 1);
         for (uint32_t i = 0; i < nseg; ++i) offs[i] = hs[i];
         offs[nseg] = inserted;
-        const std::vector<SegItem> items = seg_items(offs);
-        if (!rc) rc = seg_encode(ctx, ids2, items, nseg, T, acc, d_items, s);
+        const std::vector<SegItem> items = seg_items(offs, T);
+        if (!rc && hipMemcpyAsync(d_offs, offs.data(), ((size_t)nseg + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+            rc = QK_E_HIP;
+        if (!rc) rc = seg_encode(ctx, ids2, d_offs, items, nseg, T, acc, d_items, s);
         if (!rc) {
             const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nseg * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);

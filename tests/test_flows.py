@@ -105,3 +105,30 @@ def test_gpu_segments_primitive():
         seg = ids[offs[g]:offs[g + 1]]
         assert q.power_sums() == coracle.encode_u32(seg, 32)
         assert q.count() == len(seg) and q.last_value() == (int(seg[-1]) if len(seg) else None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t", [1, 5, 8, 9, 12, 13, 16, 17, 24, 25, 32, 33, 80])
+def test_gpu_many_small_segments(golden, t):
+    """Lane-per-segment kernel (segments <= 4096 ids, t <= 32) beside the
+    work-item path (longer segments, t > 32): thousands of ragged segments,
+    the 4096/4097 boundary, and lazy-fold wrap ids inside short segments."""
+    import torch
+    from sidekick_amd.quack import encode_segments
+    rng = np.random.default_rng(t)
+    lens = rng.integers(0, 200, size=3000)
+    lens[::97] = 0
+    lens[5], lens[6], lens[7], lens[8] = 4096, 4097, 1, 70_000
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ids = coracle.splitmix_u32(0x5E6 + t, int(offs[-1]))
+    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4"
+    wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
+    for j, g in enumerate((10, 11, 5, 6, 2999)):     # first/middle/last id of a segment
+        if lens[g]:
+            ids[offs[g] + (j % 3) * (lens[g] - 1) // 2] = wraps[j % len(wraps)]
+    qs = encode_segments(torch.from_numpy(ids.view(np.int32)).cuda(), offs.tolist(), t)
+    assert len(qs) == len(lens)
+    for g, q in enumerate(qs):
+        seg = ids[offs[g]:offs[g + 1]]
+        assert q.power_sums() == coracle.encode_u32(seg, t), (g, len(seg))
+        assert q.count() == len(seg) and q.last_value() == (int(seg[-1]) if len(seg) else None)

@@ -140,3 +140,12 @@ def test_all_cores_restatement_matches_scalar():
     for bits, n, t, thr in ((32, 100_003, 32, 7), (32, 5, 16, 8), (64, 20_001, 80, 3)):
         one = (coracle.encode_u32_seed if bits == 32 else coracle.encode_u64_seed)(0xBEEF, n, t, start=11)
         assert coracle.encode_seed_mt(bits, 0xBEEF, n, t, thr, start=11) == one
+
+
+def test_bench_construct_runs():
+    """Reference-shape microbenchmark leg (tools/bench_configs.py micro)."""
+    from oracle import coracle
+    for bits in (32, 64):
+        ns = coracle.bench_construct(bits, 7, 1000, 16, 3)
+        assert 0 < ns < 1e6
+    assert coracle.bench_construct(32, 7, 1000, 0, 3) == 0

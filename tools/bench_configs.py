@@ -7,6 +7,9 @@
   host     encode 1e9 u32 ids at t=32 starting from HOST memory (pinned and
            pageable): the PCIe-inclusive rate the sniffer-fed path sees
   sweep    encode rate vs threshold t (u32)
+  packets  sniff-loop batch: 67-byte records in HBM -> one quACK
+  flows    per-flow batch: records of 16 / 1e4 / 1e6 flows -> one quACK each
+  micro    reference-shape rows (1000 ids x 100 trials) and configs[0]
 
 Each prints one JSON line per measurement.  Kernel times come from HIP events
 on the launch stream (qk_ctx_set_profiling); wall times from perf_counter
@@ -216,6 +219,61 @@ def run_flows(args, ctx):
         del f
 
 
+# published quack-crate encode ns/id, 1000 ids per trial, 1 Xeon core
+# (zip:nsdi24/quack/threshold_vs_encode_time/{32,64}.txt)
+PUBLISHED_NS = {(32, 10): 34, (32, 20): 75, (32, 30): 117, (32, 40): 161, (32, 80): 327,
+                (64, 30): 167, (64, 40): 227, (64, 80): 461}
+
+
+def run_micro(args, ctx):
+    """Reference-shape rows: 1000 ids x 100 trials per
+    threshold, CPU restatement beside the published crate numbers and the GPU
+    doing the same tiny job (launch-latency bound at this size), then
+    configs[0] (1e6 u32 ids, t=16) on both."""
+    from oracle import coracle
+    n, trials = 1000, 100
+    rows = [(32, t) for t in (10, 16, 20, 30, 32, 40, 80)] + [(64, t) for t in (30, 40, 80)]
+    for bits, t in rows:
+        seed = 0xB0 + t + bits
+        cpu_ns = coracle.bench_construct(bits, seed, n, t, trials)
+        dt = torch.int32 if bits == 32 else torch.int64
+        ids = torch.empty(n * trials, dtype=dt, device=DEV)
+        fill_splitmix(ctx, ids, seed, bits=bits)
+        cls = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+        q = cls(t)
+        q.insert_batch(ids[:n])                          # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for r in range(trials):
+            q = cls(t)
+            q.insert_batch(ids[r * n:(r + 1) * n])        # returns after the sketch is on the host
+        gpu_ns = (time.perf_counter() - t0) / (n * trials) * 1e9
+        last = ids[(trials - 1) * n:].cpu().numpy()
+        want = (coracle.encode_u32(last.view(np.uint32), t) if bits == 32
+                else coracle.encode_u64(last.view(np.uint64), t))
+        emit({"config": f"reference-shape construct u{bits} t={t}: {n} ids x {trials} trials",
+              "published_crate_ns_per_id": PUBLISHED_NS.get((bits, t)), "cpu_port_ns_per_id": round(cpu_ns, 2),
+              "gpu_ns_per_id": round(gpu_ns, 2), "parity": q.power_sums() == want})
+    # configs[0]: 1e6 u32 ids, t = 16
+    m, t, seed = 1_000_000, 16, 0x5EED0001
+    d = torch.empty(m, dtype=torch.int32, device=DEV)
+    fill_splitmix(ctx, d, seed)
+    wall, kern = time_encode(ctx, d, t, 32, max(10, args.steps))
+    h = d.cpu().numpy().view(np.uint32)
+    times = []
+    for _ in range(5):
+        q = sk.PowerSumQuackU32(t)
+        t0 = time.perf_counter()
+        q.insert_batch(h)
+        times.append(time.perf_counter() - t0)
+    tc = time.perf_counter()
+    S = coracle.encode_u32_seed(seed, m, t)
+    cs = time.perf_counter() - tc
+    emit({"config": "configs[0]: encode 1e6 u32 ids t=16", "n": m, "gpu_device_resident_ids_per_s": m / wall,
+          "gpu_kernel_ids_per_s": m / kern, "gpu_from_pageable_host_ids_per_s": m / min(times),
+          "cpu_port_1core_ids_per_s": m / cs, "parity": q.power_sums() == S})
+
+
 def run_sweep(args, ctx):
     n = int(args.nsweep)
     ids = torch.empty(n, dtype=torch.int32, device=DEV)
@@ -227,7 +285,7 @@ def run_sweep(args, ctx):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "packets", "flows"])
+    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "packets", "flows", "micro"])
     ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--n64", type=float, default=1e9)
@@ -241,7 +299,7 @@ def main():
     ctx = sk.get_context(0)
     for w in args.what:
         {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep,
-         "packets": run_packets, "flows": run_flows}[w](args, ctx)
+         "packets": run_packets, "flows": run_flows, "micro": run_micro}[w](args, ctx)
         torch.cuda.empty_cache()
 
 

@@ -25,6 +25,7 @@ def main(rnd: str, src: str = "gpurun_out", key: str = "u32_t32", n_ids: int = 1
               "pmcsq/run_counter_collection.csv": "encode_pmc_sq.csv",
               "ubench.log": "ubench_int.json", "tune.log": "tune_encode.json", "ubdep.log": "ubench_dep.json",
               "tunebsgs.log": "tune_bsgs.json", "ubissue.log": "ubench_issue.json",
+              "proflows/run_kernel_stats.csv": "flows_packets_kernel_stats.csv",
               "pytest.log": "pytest_gpu.log", "smoke.log": "smoke.log"}
     for a, b in copies.items():
         if os.path.exists(os.path.join(src, a)):
@@ -40,8 +41,16 @@ def main(rnd: str, src: str = "gpurun_out", key: str = "u32_t32", n_ids: int = 1
     for name in sorted(os.listdir(src)):
         if name.startswith("configs") and name.endswith(".log"):
             rows += [l for l in open(os.path.join(src, name)) if l.startswith("{")]
-    if rows:
-        open(os.path.join(dst, "configs.jsonl"), "w").write("".join(rows))
+    if rows:   # merged by "config": a partial run refreshes its own rows only
+        path = os.path.join(dst, "configs.jsonl")
+        merged = collections.OrderedDict()
+        if os.path.exists(path):
+            for l in open(path):
+                if l.startswith("{"):
+                    merged[json.loads(l)["config"]] = l
+        for l in rows:
+            merged[json.loads(l)["config"]] = l
+        open(path, "w").write("".join(merged.values()))
 
     out = {}
     pmc = os.path.join(src, "pmc/run_counter_collection.csv")
