@@ -22,12 +22,14 @@ struct qk_ctx {
     uint64_t *d_hits = nullptr;
     size_t hits_cap = 0;
 
-    // per-flow batches (flows.hip): per-packet arena (keys, ids, sort buffers)
-    // and per-flow arena (segment info, accumulators, work items); grow-only,
-    // reused across calls (a stream-ordered malloc/free of GBs per batch costs
-    // more than the whole pipeline)
-    void *d_flow[2] = {nullptr, nullptr};
-    size_t flow_bytes[2] = {0, 0};
+    // per-flow batches (flows.hip): per-packet arena (slots, ids, sort
+    // buffers), per-flow arena (segment info, accumulators, work items) and
+    // the flow hash table; grow-only, reused across calls (a stream-ordered
+    // malloc/free of GBs per batch costs more than the whole pipeline).
+    // flow_hint: distinct flows of the previous batch (sizes the table).
+    void *d_flow[3] = {nullptr, nullptr, nullptr};
+    size_t flow_bytes[3] = {0, 0, 0};
+    size_t flow_hint = 0;
 
     // host-input pipeline: pinned staging + device chunk buffers (2 slots)
     void *h_stage[2] = {nullptr, nullptr};

@@ -15,13 +15,17 @@
 // qk_u32_merge, flow by flow.
 //
 // Device pipeline:
-//   1. k_flow_extract   LDS-staged records -> (key_hi = src ip:port, key_lo =
-//                       dst ip:port, id) per packet; filtered packets get an
-//                       out-of-range key and sort last.
-//   2. two stable radix sorts (hipCUB/rocPRIM, 49-bit keys: lo, then hi) ->
-//      packet order within each flow is preserved (last_value = last id).
-//   3. segment heads -> per-flow offsets; flows of > SMALL_SEG ids (or any
-//      flow when T > 32) -> work items of <= 64 Ki ids per workgroup.
+//   1. k_flow_extract   LDS-staged records -> per packet the filters and, for
+//                       an Insert, its flow's slot in a device hash table
+//                       (packets of a tile that share a flow elect one leader
+//                       in LDS, which probes / inserts once); writes slot + id.
+//   2. the occupied slots (DeviceSelect) sorted by AddrKey (two stable 48-bit
+//      radix sorts of the flows only) -> rank of each flow = output order.
+//   3. per packet slot -> rank; one stable radix sort of (rank, id) pairs over
+//      bit_width(flows) bits (1 pass for <= 256 flows) groups the ids by flow
+//      with packet order preserved (last_value = last id); offsets from the
+//      rank changes.  Flows of > SMALL_SEG ids (or any flow when T > 32) ->
+//      work items of <= 64 Ki ids per workgroup.
 //   4. k_seg_small<Cfg>   one lane per small flow: baby-step/giant-step per id
 //      (bsgs.h) with the whole flow in that lane's registers, one plain store
 //      per (flow, power); k_seg_encode<G,K> for the work items: power chains
@@ -47,7 +51,6 @@ static_assert(sizeof(qk_u32) == 16, "qk_u32 header is 4 words (k_flow_finalize w
 
 constexpr int SG_BLOCK = 256;
 constexpr int SG_WAVES = SG_BLOCK / 64;
-constexpr uint64_t KEY_INVALID = 1ull << 48; // above every 48-bit ip:port
 constexpr uint32_t SEG_CHUNK = 1u << 16;     // ids per work item
 
 struct SegItem {
@@ -174,77 +177,197 @@ static int seg_small_launch(uint32_t T, const uint32_t *ids, const uint64_t *d_o
     return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
 }
 
+// ---- flow table --------------------------------------------------------------
+// Open addressing with linear probing over C = 2^k slots of two words:
+//   w0 = (src + 1) | (dst >> 33) << 49   0 = empty
+//   w1 = (dst & (2^33 - 1)) | 1 << 40     0 = not yet set
+// (src, dst = the 48-bit big-endian ip:port halves of the AddrKey).  Each word
+// goes 0 -> final value exactly once, by CAS, so any nonzero value read (cached
+// or not) is final and a 0 is resolved by the CAS itself.  A lane whose key
+// matches w0 sets w1 itself if it is still 0, so no lane ever waits for
+// another (no intra-wave spin hazard): the slot belongs to the key whose w1
+// lands first, and every lane decides on final values only, so all lanes of
+// one key stop at the same slot.
+struct alignas(16) FlowSlot {
+    uint64_t w0, w1;
+};
+constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;
+constexpr uint64_t FT_OVERFLOW = 1;   // counters[3] flag
+
+__device__ __forceinline__ uint64_t ft_w0(uint64_t src, uint64_t dst) { return (src + 1) | ((dst >> 33) << 49); }
+__device__ __forceinline__ uint64_t ft_w1(uint64_t dst) { return (dst & ((1ull << 33) - 1)) | (1ull << 40); }
+__device__ __forceinline__ uint64_t ft_src(const FlowSlot &e) { return (e.w0 & ((1ull << 49) - 1)) - 1; }
+__device__ __forceinline__ uint64_t ft_dst(const FlowSlot &e) { return ((e.w0 >> 49) << 33) | (e.w1 & ((1ull << 33) - 1)); }
+__device__ __forceinline__ uint32_t ft_hash(uint64_t src, uint64_t dst) {
+    uint64_t z = src * 0x9E3779B97F4A7C15ull ^ (dst + 0x632BE59BD9B4E019ull) * 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 31;
+    z *= 0x94D049BB133111EBull;
+    return (uint32_t)(z >> 32);
+}
+// value of a write-once word, setting it to `want` if still 0
+__device__ __forceinline__ uint64_t ft_settle(uint64_t *w, uint64_t want) {
+    const uint64_t v = *w;
+    if (v != 0) return v;
+    const uint64_t o = atomicCAS((unsigned long long *)w, 0ull, (unsigned long long)want);
+    return o == 0 ? want : o;
+}
+
+// slot of (src, dst), inserting it if absent; SLOT_NONE (and a flag) when the
+// probe limit is reached
+__device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t probe_limit, uint64_t src,
+                                      uint64_t dst, unsigned long long *counters) {
+    const uint64_t a0 = ft_w0(src, dst), a1 = ft_w1(dst);
+    uint32_t slot = ft_hash(src, dst) & mask;
+    for (uint32_t probe = 0; probe < probe_limit; ++probe, slot = (slot + 1) & mask) {
+        const FlowSlot e = tab[slot];                  // one 16-byte read: the common cases
+        if (e.w0 == a0 && e.w1 == a1) return slot;
+        if (e.w0 != 0 && (e.w0 != a0 || e.w1 != 0)) continue;
+        if (ft_settle(&tab[slot].w0, a0) != a0) continue;
+        const uint64_t v = tab[slot].w1;
+        if (v == a1) return slot;
+        if (v != 0) continue;
+        const uint64_t o = atomicCAS((unsigned long long *)&tab[slot].w1, 0ull, (unsigned long long)a1);
+        if (o == 0) {
+            atomicAdd(&counters[2], 1ull);   // this key owns the slot
+            return slot;
+        }
+        if (o == a1) return slot;
+    }
+    atomicOr(&counters[3], (unsigned long long)FT_OVERFLOW);
+    return SLOT_NONE;
+}
+
+// Per packet: the SidekickMulti filters (records.h) and, for an Insert, its
+// flow's table slot.  Packets of one tile that share a flow elect a leader in
+// LDS first (one table probe per flow per tile: with few flows the table
+// lines are not hammered by every packet).  Writes slot (SLOT_NONE if not an
+// Insert) and id per packet; counters: [0] inserts, [1] resets, [2] distinct
+// flows, [3] flags.
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
                                                            uint32_t stride, const qk_pkt_meta *__restrict__ meta,
-                                                           uint64_t my_key_lo, uint64_t *__restrict__ key_hi,
-                                                           uint64_t *__restrict__ key_lo,
+                                                           uint64_t my_key_lo, uint64_t chunk,
+                                                           FlowSlot *__restrict__ tab, uint32_t mask,
+                                                           uint32_t probe_limit, uint32_t *__restrict__ slots,
                                                            uint32_t *__restrict__ ids,
-                                                           uint32_t *__restrict__ order,
                                                            unsigned long long *__restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
-    const uint64_t p0 = (uint64_t)blockIdx.x * REC_TILE;
-    const uint64_t np = n - p0 < (uint64_t)REC_TILE ? n - p0 : (uint64_t)REC_TILE;
-    const uint32_t r0 = stage_records(bufs, n, stride, p0, np, tile);
-    __syncthreads();
-    const bool valid = threadIdx.x < np;
-    const uint64_t i = p0 + threadIdx.x;
-    const uint8_t *rec = tile + r0 + threadIdx.x * stride;
-    uint64_t kh = KEY_INVALID, kl = KEY_INVALID;
-    uint32_t id = 0;
-    int cls = 0; // 0 skip, 1 insert, 2 reset
-    const qk_pkt_meta m = valid ? record_meta(meta, i) : qk_pkt_meta{};
-    if (valid && record_is_incoming_udp(m, rec)) {
-        // AddrKey, packed big-endian so numeric order == byte order
-        const uint64_t src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
-                             ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];
-        const uint64_t dst = ((uint64_t)rec[30] << 40) | ((uint64_t)rec[31] << 32) | ((uint64_t)rec[32] << 24) |
-                             ((uint64_t)rec[33] << 16) | ((uint64_t)rec[36] << 8) | (uint64_t)rec[37];
-        if (dst == my_key_lo) cls = 2;
-        else if (m.len == QK_BUFFER_SIZE) {
-            cls = 1;
-            kh = src;
-            kl = dst;
-            id = record_identifier(rec);
+    constexpr uint32_t LH = 2 * REC_TILE;                // LDS election table
+    __shared__ uint64_t l_src[REC_TILE], l_dst[REC_TILE];
+    __shared__ uint32_t l_lead[LH];
+    __shared__ uint32_t l_slot[REC_TILE];
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
+    uint64_t n_ins = 0, n_rst = 0;   // thread 0's running totals
+    for (uint64_t p0 = c0; p0 < c1; p0 += REC_TILE) {
+        const uint64_t np = c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE;
+        __syncthreads();   // previous tile fully consumed
+        const uint32_t r0 = stage_records(bufs, n, stride, p0, np, tile);
+        for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
+        __syncthreads();
+        const bool valid = threadIdx.x < np;
+        const uint64_t i = p0 + threadIdx.x;
+        const uint8_t *rec = tile + r0 + threadIdx.x * stride;
+        uint64_t src = 0, dst = 0;
+        uint32_t id = 0;
+        int cls = 0; // 0 skip, 1 insert, 2 reset
+        const qk_pkt_meta m = valid ? record_meta(meta, i) : qk_pkt_meta{};
+        if (valid && record_is_incoming_udp(m, rec)) {
+            // AddrKey halves, big-endian so numeric order == byte order
+            src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
+                  ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];
+            dst = ((uint64_t)rec[30] << 40) | ((uint64_t)rec[31] << 32) | ((uint64_t)rec[32] << 24) |
+                  ((uint64_t)rec[33] << 16) | ((uint64_t)rec[36] << 8) | (uint64_t)rec[37];
+            if (dst == my_key_lo) cls = 2;
+            else if (m.len == QK_BUFFER_SIZE) {
+                cls = 1;
+                id = record_identifier(rec);
+            }
         }
-    }
-    if (valid) {
-        key_hi[i] = kh;
-        key_lo[i] = kl;
-        ids[i] = id;
-        order[i] = (uint32_t)i;
+        l_src[threadIdx.x] = src;
+        l_dst[threadIdx.x] = dst;
+        __syncthreads();
+        // packets of this tile that share a flow elect one leader
+        uint32_t lead = SLOT_NONE;
+        if (cls == 1) {
+            uint32_t h = ft_hash(src, dst) & (LH - 1);
+            for (;;) {   // at most REC_TILE claims in LH slots: terminates
+                const uint32_t o = atomicCAS(&l_lead[h], SLOT_NONE, threadIdx.x);
+                if (o == SLOT_NONE) { lead = threadIdx.x; break; }
+                if (l_src[o] == src && l_dst[o] == dst) { lead = o; break; }
+                h = (h + 1) & (LH - 1);
+            }
+            if (lead == threadIdx.x)
+                l_slot[threadIdx.x] = ft_find_or_insert(tab, mask, probe_limit, src, dst, counters);
+        }
+        __syncthreads();
+        if (valid) {
+            slots[i] = cls == 1 ? l_slot[lead] : SLOT_NONE;
+            ids[i] = id;
+        }
+        const int ins = __syncthreads_count(cls == 1), rst = __syncthreads_count(cls == 2);
+        n_ins += (uint64_t)ins;
+        n_rst += (uint64_t)rst;
     }
     // one atomic per workgroup (a per-packet atomic on one address
     // serialises: 1.2 s per 1e8 packets)
-    const int ins = __syncthreads_count(cls == 1), rst = __syncthreads_count(cls == 2);
     if (threadIdx.x == 0) {
-        if (ins) atomicAdd(&counters[0], (unsigned long long)ins);
-        if (rst) atomicAdd(&counters[1], (unsigned long long)rst);
+        if (n_ins) atomicAdd(&counters[0], (unsigned long long)n_ins);
+        if (n_rst) atomicAdd(&counters[1], (unsigned long long)n_rst);
     }
 }
 
-template <typename T, typename I>
-__global__ void k_gather(const T *__restrict__ src, const I *__restrict__ idx, T *__restrict__ dst, uint64_t n) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        dst[i] = src[idx[i]];
+struct SlotUsed {
+    const FlowSlot *tab;
+    __device__ bool operator()(uint32_t s) const { return tab[s].w0 != 0; }
+};
+
+// the AddrKey halves of listed slots (either output may be null)
+__global__ void k_slot_keys(const FlowSlot *__restrict__ tab, const uint32_t *__restrict__ slot, uint32_t nf,
+                            uint64_t *__restrict__ dst_key, uint64_t *__restrict__ src_key) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nf) return;
+    const FlowSlot e = tab[slot[r]];
+    if (dst_key) dst_key[r] = ft_dst(e);
+    if (src_key) src_key[r] = ft_src(e);
 }
 
-__global__ void k_heads(const uint64_t *__restrict__ kh, const uint64_t *__restrict__ kl, uint64_t n,
-                        uint8_t *__restrict__ flag) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        flag[i] = kh[i] != KEY_INVALID && (i == 0 || kh[i] != kh[i - 1] || kl[i] != kl[i - 1]);
+// flows in ascending AddrKey order: rank r <-> slot; info[4r] = src, [4r+1] = dst
+__global__ void k_slot_rank(const FlowSlot *__restrict__ tab, const uint32_t *__restrict__ slot_of_rank, uint32_t nf,
+                            uint32_t *__restrict__ rank_of_slot, uint64_t *__restrict__ info) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nf) return;
+    const uint32_t s = slot_of_rank[r];
+    const FlowSlot e = tab[s];
+    rank_of_slot[s] = r;
+    info[4 * (uint64_t)r + 0] = ft_src(e);
+    info[4 * (uint64_t)r + 1] = ft_dst(e);
 }
 
-// per segment: key and last id (segment end = next head or nvalid)
-__global__ void k_seg_info(const uint64_t *__restrict__ kh, const uint64_t *__restrict__ kl,
-                           const uint32_t *__restrict__ ids, const uint32_t *__restrict__ starts, uint32_t nseg,
-                           uint64_t nvalid, uint64_t *__restrict__ info) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg) return;
-    const uint64_t b = starts[s], e = s + 1 < nseg ? starts[s + 1] : nvalid;
-    info[4 * s + 0] = kh[b];
-    info[4 * s + 1] = kl[b];
-    info[4 * s + 2] = e - b;
-    info[4 * s + 3] = ids[e - 1];
+// per packet, in place: slot -> flow rank (non-inserts -> nf, sorting last)
+__global__ void k_slot_to_rank(uint32_t *__restrict__ key, const uint32_t *__restrict__ rank_of_slot, uint64_t n,
+                               uint32_t nf) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = key[i];
+        key[i] = s == SLOT_NONE ? nf : rank_of_slot[s];
+    }
+}
+
+// segment starts of the rank-sorted packets (every rank 0..nf-1 occurs)
+__global__ void k_rank_offsets(const uint32_t *__restrict__ key, uint64_t ninserted, uint32_t nf,
+                               uint64_t *__restrict__ offs) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ninserted;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        if (i == 0 || key[i] != key[i - 1]) offs[key[i]] = i;
+    if (blockIdx.x == 0 && threadIdx.x == 0) offs[nf] = ninserted;
+}
+
+// info[4r+2] = count, [4r+3] = last id of flow r
+__global__ void k_flow_counts(const uint64_t *__restrict__ offs, const uint32_t *__restrict__ ids, uint32_t nf,
+                              uint64_t *__restrict__ info) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nf) return;
+    info[4 * (uint64_t)r + 2] = offs[r + 1] - offs[r];
+    info[4 * (uint64_t)r + 3] = ids[offs[r + 1] - 1];
 }
 
 // qk_u32 records (header + T canonical sums) and AddrKey bytes of every flow,
@@ -375,6 +498,13 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
     return rc;
 }
 
+static uint64_t next_pow2(uint64_t v) {
+    uint64_t c = 1;
+    while (c < v) c <<= 1;
+    return c;
+}
+static int bit_width32(uint32_t v) { return v ? 32 - __builtin_clz(v) : 0; }
+
 } // namespace qk
 
 using namespace qk;
@@ -455,126 +585,168 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     hipStream_t s = pick_stream(ctx, stream);
     const uint32_t T = threshold;
 
-    // device scratch (ctx flow arena 0): keys (2 x 2 x u64), ids (2 x u32),
-    // order (2 x u32), flags, heads, counters, hipCUB temp storage
-    size_t tb1 = 0, tb2 = 0;
+    // device scratch.  Arena 0, per packet: slot/rank key, id, their sorted
+    // copies (16 B per packet), counters, hipCUB temp storage.  Arena 2: the
+    // flow table (C slots) and slot -> rank.  Arena 1, per flow: see below.
+    const uint64_t cmax = std::min<uint64_t>(next_pow2(2 * (uint64_t)n + 2), 1ull << 31);
+    uint64_t C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(4096, 4 * (uint64_t)ctx->flow_hint)));
+    size_t tb = 0;
     {
-        uint64_t *k0 = nullptr;
-        uint32_t *o0 = nullptr, *h0 = nullptr;
-        uint8_t *f0 = nullptr;
-        if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, k0, k0, o0, o0, (uint32_t)n, 0, 49, s) != hipSuccess ||
-            hipcub::DeviceSelect::Flagged(nullptr, tb2, hipcub::CountingInputIterator<uint32_t>(0), f0, h0, h0,
-                                          (int64_t)n, s) != hipSuccess)
+        uint32_t *u = nullptr;
+        uint64_t *k = nullptr;
+        size_t b = 0;
+        for (int bits = 1; bits <= 32; ++bits) {   // the per-packet sort runs over bit_width(flows) bits
+            if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, u, u, u, u, (uint32_t)n, 0, bits, s) != hipSuccess)
+                return QK_E_HIP;
+            tb = std::max(tb, b);
+        }
+        if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, k, u, u, (uint32_t)n, 0, 48, s) != hipSuccess)
             return QK_E_HIP;
+        tb = std::max(tb, b);
+        if (hipcub::DeviceSelect::If(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), u, u, (int64_t)cmax,
+                                     SlotUsed{nullptr}, s) != hipSuccess)
+            return QK_E_HIP;
+        tb = std::max(tb, b);
     }
-    auto layout = [&](Carve &c, uint64_t *&kh, uint64_t *&kl, uint64_t *&kh2, uint64_t *&kl2, uint32_t *&ids,
-                      uint32_t *&ids2, uint32_t *&ord, uint32_t *&ord2, uint32_t *&heads, uint8_t *&flag,
-                      unsigned long long *&counters, void *&temp) {
-        kh = c.take<uint64_t>(n); kl = c.take<uint64_t>(n); kh2 = c.take<uint64_t>(n); kl2 = c.take<uint64_t>(n);
-        ids = c.take<uint32_t>(n); ids2 = c.take<uint32_t>(n); ord = c.take<uint32_t>(n); ord2 = c.take<uint32_t>(n);
-        heads = c.take<uint32_t>(n); flag = c.take<uint8_t>(n); counters = c.take<unsigned long long>(4);
-        temp = c.take<char>(std::max(tb1, tb2));
-    };
-    uint64_t *kh = nullptr, *kl = nullptr, *kh2 = nullptr, *kl2 = nullptr;
-    uint32_t *ids = nullptr, *ids2 = nullptr, *ord = nullptr, *ord2 = nullptr, *heads = nullptr;
-    uint8_t *flag = nullptr;
+    uint32_t *slots = nullptr, *ids = nullptr, *key_s = nullptr, *id_s = nullptr;
     unsigned long long *counters = nullptr, *acc = nullptr;
     void *temp = nullptr;
-    uint64_t *info = nullptr;
+    auto layout0 = [&](Carve &c) {
+        slots = c.take<uint32_t>(n); ids = c.take<uint32_t>(n); key_s = c.take<uint32_t>(n); id_s = c.take<uint32_t>(n);
+        counters = c.take<unsigned long long>(4);
+        temp = c.take<char>(tb);
+    };
     {
         Carve probe{nullptr};
-        layout(probe, kh, kl, kh2, kl2, ids, ids2, ord, ord2, heads, flag, counters, temp);
+        layout0(probe);
         if (int e = ensure_flow(ctx, 0, probe.off)) return e;
         Carve cv{(char *)ctx->d_flow[0]};
-        layout(cv, kh, kl, kh2, kl2, ids, ids2, ord, ord2, heads, flag, counters, temp);
+        layout0(cv);
     }
+    // pass 1: filters + flow table; a table that overflows its probe limit is
+    // regrown and the pass rerun (the next batch starts from this size)
     int rc = QK_OK;
-    if (hipMemsetAsync(counters, 0, 4 * 8, s) != hipSuccess) rc = QK_E_HIP;
-    const uint32_t ntiles = (uint32_t)((n + REC_TILE - 1) / REC_TILE);
-    if (!rc) {
-        hipLaunchKernelGGL(k_flow_extract, dim3(ntiles), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s, d_bufs,
-                           (uint64_t)n, (uint32_t)stride, d_meta, my_key, kh, kl, ids, ord, counters);
-        if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+    FlowSlot *tab = nullptr;
+    uint32_t *rank_of_slot = nullptr;
+    uint64_t hc[4] = {0, 0, 0, 0};
+    // >= 4 tiles per workgroup, enough workgroups to cover the chip
+    const uint64_t ntiles = (n + REC_TILE - 1) / REC_TILE;
+    const uint64_t tiles_per_chunk =
+        std::max<uint64_t>(4, (ntiles + (uint64_t)ctx->num_cus * 4 - 1) / ((uint64_t)ctx->num_cus * 4));
+    const uint64_t chunk = tiles_per_chunk * REC_TILE;
+    const uint32_t nchunks = (uint32_t)((n + chunk - 1) / chunk);
+    for (;;) {
+        {
+            Carve probe{nullptr};
+            probe.take<FlowSlot>(C);
+            probe.take<uint32_t>(C);
+            if (int e = ensure_flow(ctx, 2, probe.off)) return e;
+            Carve cv{(char *)ctx->d_flow[2]};
+            tab = cv.take<FlowSlot>(C);
+            rank_of_slot = cv.take<uint32_t>(C);
+        }
+        if (hipMemsetAsync(tab, 0, C * sizeof(FlowSlot), s) != hipSuccess ||
+            hipMemsetAsync(counters, 0, 4 * 8, s) != hipSuccess) {
+            rc = QK_E_HIP;
+            break;
+        }
+        const uint32_t probe_limit = C == cmax ? (uint32_t)C : 256u;
+        hipLaunchKernelGGL(k_flow_extract, dim3(nchunks), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s, d_bufs,
+                           (uint64_t)n, (uint32_t)stride, d_meta, my_key, chunk, tab, (uint32_t)(C - 1), probe_limit,
+                           slots, ids, counters);
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(hc, counters, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            rc = QK_E_HIP;
+            break;
+        }
+        if (!(hc[3] & FT_OVERFLOW)) break;
+        if (C == cmax) { rc = QK_E_NOMEM; break; }   // > 2^31 flows: no table size left
+        C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(16 * C, 4 * hc[2])));
     }
-    // stable LSD sort: by dst ip:port, then by src ip:port (49-bit keys)
-    const uint32_t gb = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 8);
-    if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb1, kl, kl2, ord, ord2, (uint32_t)n, 0, 49, s) != hipSuccess)
-        rc = QK_E_HIP;
-    if (!rc) hipLaunchKernelGGL((k_gather<uint64_t, uint32_t>), dim3(gb), dim3(256), 0, s, kh, ord2, kh2, (uint64_t)n);
-    if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb1, kh2, kh, ord2, ord, (uint32_t)n, 0, 49, s) != hipSuccess)
-        rc = QK_E_HIP;
-    // now kh = sorted key_hi, ord = final packet order; gather key_lo and ids
-    if (!rc) {
-        hipLaunchKernelGGL((k_gather<uint64_t, uint32_t>), dim3(gb), dim3(256), 0, s, kl, ord, kl2, (uint64_t)n);
-        hipLaunchKernelGGL((k_gather<uint32_t, uint32_t>), dim3(gb), dim3(256), 0, s, ids, ord, ids2, (uint64_t)n);
-        hipLaunchKernelGGL(k_heads, dim3(gb), dim3(256), 0, s, kh, kl2, (uint64_t)n, flag);
-        if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
-    }
-    if (!rc && hipcub::DeviceSelect::Flagged(temp, tb2, hipcub::CountingInputIterator<uint32_t>(0), flag, heads,
-                                             (uint32_t *)(counters + 2), (int64_t)n, s) != hipSuccess)
-        rc = QK_E_HIP;
-    uint64_t hc[3] = {0, 0, 0};
-    if (!rc && (hipMemcpyAsync(hc, counters, 24, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess))
-        rc = QK_E_HIP;
     const uint64_t inserted = hc[0], resets = hc[1];
-    const uint32_t nseg = (uint32_t)(hc[2] & 0xFFFFFFFFu);
+    const uint32_t nf = (uint32_t)hc[2];
     if (!rc) {
+        ctx->flow_hint = nf;
         st.inserted = inserted;
         st.resets = resets;
         st.filtered = n - inserted - resets;
-        *n_flows = nseg;
-        if (nseg > cap || (nseg && (!keys || !sketches))) rc = QK_E_CAPACITY;
+        *n_flows = nf;
+        if (nf > cap || (nf && (!keys || !sketches))) rc = QK_E_CAPACITY;
     }
-    if (!rc && nseg) {
-        std::vector<uint32_t> hs(nseg);
-        // per-flow arena 1 (arena 0 still holds the grouped ids): info, acc,
-        // work items (at most one per flow plus one per SEG_CHUNK ids), and
-        // the output records and keys
-        const size_t items_max = (size_t)nseg + inserted / SEG_CHUNK + 1;
+    if (!rc && nf) {
+        // per-flow arena 1: info, acc, work items (at most one per flow plus
+        // one per SEG_CHUNK ids), output records and keys, offsets, and the
+        // flow-key sort buffers
+        const size_t items_max = (size_t)nf + inserted / SEG_CHUNK + 1;
         const size_t rec = qk_u32_size(T);
+        uint64_t *info = nullptr, *d_offs = nullptr, *kd = nullptr, *kd2 = nullptr, *ks = nullptr, *ks2 = nullptr;
         SegItem *d_items = nullptr;
-        uint64_t *d_offs = nullptr;
-        uint32_t *d_rec = nullptr;
+        uint32_t *d_rec = nullptr, *used = nullptr, *sl2 = nullptr, *sl3 = nullptr, *nsel = nullptr;
         uint8_t *d_keys = nullptr;
+        auto layout1 = [&](Carve &c) {
+            info = c.take<uint64_t>((size_t)nf * 4);
+            acc = c.take<unsigned long long>((size_t)nf * T);
+            d_items = c.take<SegItem>(items_max);
+            d_rec = (uint32_t *)c.take<uint8_t>((size_t)nf * rec);
+            d_keys = c.take<uint8_t>((size_t)nf * 12);
+            d_offs = c.take<uint64_t>((size_t)nf + 1);
+            kd = c.take<uint64_t>(nf); kd2 = c.take<uint64_t>(nf); ks = c.take<uint64_t>(nf); ks2 = c.take<uint64_t>(nf);
+            used = c.take<uint32_t>(nf); sl2 = c.take<uint32_t>(nf); sl3 = c.take<uint32_t>(nf);
+            nsel = c.take<uint32_t>(1);
+        };
         {
             Carve probe{nullptr};
-            probe.take<uint64_t>((size_t)nseg * 4);
-            probe.take<unsigned long long>((size_t)nseg * T);
-            probe.take<SegItem>(items_max);
-            probe.take<uint8_t>((size_t)nseg * rec);
-            probe.take<uint8_t>((size_t)nseg * 12);
-            probe.take<uint64_t>((size_t)nseg + 1);
+            layout1(probe);
             rc = ensure_flow(ctx, 1, probe.off);
         }
         if (!rc) {
             Carve cv{(char *)ctx->d_flow[1]};
-            info = cv.take<uint64_t>((size_t)nseg * 4);
-            acc = cv.take<unsigned long long>((size_t)nseg * T);
-            d_items = cv.take<SegItem>(items_max);
-            d_rec = (uint32_t *)cv.take<uint8_t>((size_t)nseg * rec);
-            d_keys = cv.take<uint8_t>((size_t)nseg * 12);
-            d_offs = cv.take<uint64_t>((size_t)nseg + 1);
+            layout1(cv);
         }
-        if (!rc) hipLaunchKernelGGL(k_seg_info, dim3((nseg + 255) / 256), dim3(256), 0, s, kh, kl2, ids2, heads, nseg,
-                                    inserted, info);
-        if (!rc && (hipMemcpyAsync(hs.data(), heads, nseg * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        const uint32_t fblocks = (nf + 255) / 256;
+        const uint32_t gb = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 8);
+        // flows in ascending AddrKey order: stable LSD sort of the occupied
+        // slots by dst, then by src (48-bit halves)
+        if (!rc && hipcub::DeviceSelect::If(temp, tb, hipcub::CountingInputIterator<uint32_t>(0), used, nsel,
+                                            (int64_t)C, SlotUsed{tab}, s) != hipSuccess)
+            rc = QK_E_HIP;
+        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s, tab, used, nf, kd, (uint64_t *)nullptr);
+        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, kd, kd2, used, sl2, nf, 0, 48, s) != hipSuccess)
+            rc = QK_E_HIP;
+        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s, tab, sl2, nf, (uint64_t *)nullptr, ks);
+        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, ks, ks2, sl2, sl3, nf, 0, 48, s) != hipSuccess)
+            rc = QK_E_HIP;
+        // packets: slot -> rank, stable sort by rank (packet order kept within
+        // each flow, so last_value is the flow's last packet)
+        if (!rc) {
+            hipLaunchKernelGGL(k_slot_rank, dim3(fblocks), dim3(256), 0, s, tab, sl3, nf, rank_of_slot, info);
+            hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, (uint64_t)n, nf);
+            if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+        }
+        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n, 0,
+                                                      bit_width32(nf), s) != hipSuccess)
+            rc = QK_E_HIP;
+        if (!rc) {
+            const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
+            hipLaunchKernelGGL(k_rank_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted, nf, d_offs);
+            hipLaunchKernelGGL(k_flow_counts, dim3(fblocks), dim3(256), 0, s, d_offs, id_s, nf, info);
+            if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+        }
+        std::vector<uint64_t> offs((size_t)nf + 1);
+        uint32_t hsel = 0;
+        if (!rc && (hipMemcpyAsync(offs.data(), d_offs, ((size_t)nf + 1) * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipMemcpyAsync(&hsel, nsel, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess))
             rc = QK_E_HIP;
-        std::vector<uint64_t> offs(nseg + 1);
-        for (uint32_t i = 0; i < nseg; ++i) offs[i] = hs[i];
-        offs[nseg] = inserted;
-        const std::vector<SegItem> items = seg_items(offs, T);
-        if (!rc && hipMemcpyAsync(d_offs, offs.data(), ((size_t)nseg + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-            rc = QK_E_HIP;
-        if (!rc) rc = seg_encode(ctx, ids2, d_offs, items, nseg, T, acc, d_items, s);
+        if (!rc && hsel != nf) rc = QK_E_HIP;   // every occupied slot holds exactly one flow
+        if (!rc) rc = seg_encode(ctx, id_s, d_offs, seg_items(offs, T), nf, T, acc, d_items, s);
         if (!rc) {
-            const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nseg * (4 + T) + 255) / 256,
+            const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nf * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);
-            hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info, (uint64_t)nseg, T, d_rec, d_keys);
+            hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info, (uint64_t)nf, T, d_rec, d_keys);
             if (hipGetLastError() != hipSuccess ||
-                hipMemcpyAsync(sketches, d_rec, (size_t)nseg * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipMemcpyAsync(keys, d_keys, (size_t)nseg * 12, hipMemcpyDeviceToHost, s) != hipSuccess)
+                hipMemcpyAsync(sketches, d_rec, (size_t)nf * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(keys, d_keys, (size_t)nf * 12, hipMemcpyDeviceToHost, s) != hipSuccess)
                 rc = QK_E_HIP;
         }
     }

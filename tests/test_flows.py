@@ -9,13 +9,15 @@ MY_ADDR = (10, 0, 2, 1, 0x1F, 0x90)   # own dst ip:port (6 bytes)
 META_DT = np.dtype([("pkttype", "u1"), ("reserved", "u1"), ("protocol_be", "<u2"), ("len", "<u4")])
 
 
-def make_flows(n, nflows, seed, stride=67, p_filter=0.1, p_reset=0.01, skew=False):
+def make_flows(n, nflows, seed, stride=67, p_filter=0.1, p_reset=0.01, skew=False, flows=None):
     rng = np.random.default_rng(seed)
     bufs = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
     bufs[:, 23] = 17
-    flows = rng.integers(0, 256, size=(nflows, 12), dtype=np.uint8)
-    flows[:, 6:12] = (192, 168, 0, 9, 0x11, 0x5C)   # dst side differs from MY_ADDR ...
-    flows[: nflows // 2, 9] = rng.integers(0, 256, size=nflows // 2)  # ... and varies for half the flows
+    if flows is None:
+        flows = rng.integers(0, 256, size=(nflows, 12), dtype=np.uint8)
+        flows[:, 6:12] = (192, 168, 0, 9, 0x11, 0x5C)   # dst side differs from MY_ADDR ...
+        flows[: nflows // 2, 9] = rng.integers(0, 256, size=nflows // 2)  # ... and varies for half the flows
+    nflows = len(flows)
     if skew:
         f = np.minimum(rng.zipf(1.5, size=n) - 1, nflows - 1)
     else:
@@ -132,3 +134,41 @@ def test_gpu_many_small_segments(golden, t):
         seg = ids[offs[g]:offs[g + 1]]
         assert q.power_sums() == coracle.encode_u32(seg, t), (g, len(seg))
         assert q.count() == len(seg) and q.last_value() == (int(seg[-1]) if len(seg) else None)
+
+
+def check_flows_table(table, flows, t):
+    assert set(table.senders()) == set(flows)
+    for k, ids in flows.items():
+        q = table.senders()[k]
+        assert q.power_sums() == coracle.encode_u32(np.array(ids, dtype=np.uint32), t), k.hex()
+        assert q.count() == len(ids) and q.last_value() == ids[-1]
+
+
+@pytest.mark.gpu
+def test_gpu_flows_edge_keys_and_table_growth():
+    """AddrKeys at the ends of the key space (all-zero / all-0xFF halves, the
+    table's packed-word edge cases), then a batch of 60 000 distinct flows
+    right after a one-flow batch: the device flow table, sized from the
+    previous batch, overflows its probe limit and is regrown."""
+    import torch
+    import sidekick_amd as sk
+    rng = np.random.default_rng(99)
+    flows = rng.integers(0, 256, size=(40, 12), dtype=np.uint8)
+    flows[0] = 0xFF
+    flows[1] = 0
+    flows[2, :6], flows[2, 6:] = 0xFF, 0
+    flows[3, :6], flows[3, 6:] = 0, 0xFF
+    flows[4, :6], flows[4, 6:] = 0xFF, (0xFF, 0xFF, 0xFF, 0xFE, 0xFF, 0xFF)
+    for n, fl in ((50_000, flows), (1000, flows[:1]), (400_000, None)):
+        if fl is None:
+            fl = rng.integers(0, 256, size=(60_000, 12), dtype=np.uint8)
+        bufs, meta = make_flows(n, 0, seed=n, flows=fl, p_reset=0.0)
+        want, _ = vector_flows(bufs, meta)
+        table = sk.FlowQuacks(16)
+        st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
+                                  meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
+        assert st["inserted"] == sum(len(v) for v in want.values())
+        check_flows_table(table, want, 16)
+        assert list(table.senders()) == sorted(want)     # the C ABI returns flows in ascending AddrKey order
+        if fl is not flows and len(fl) > 1000:
+            assert len(want) > 50_000
