@@ -258,12 +258,18 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
     uint64_t n_ins = 0, n_rst = 0;   // thread 0's running totals
+    const bool pipe = stage_pipelined(stride, REC_TILE);
+    TileStage st;
+    if (pipe && c0 < c1) stage_issue(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
     for (uint64_t p0 = c0; p0 < c1; p0 += REC_TILE) {
         const uint64_t np = c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE;
         __syncthreads();   // previous tile fully consumed
-        const uint32_t r0 = stage_records(bufs, n, stride, p0, np, tile);
+        const uint32_t r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records(bufs, n, stride, p0, np, tile);
         for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
         __syncthreads();
+        if (pipe && p0 + REC_TILE < c1)   // next tile's loads fly while this one is classified
+            stage_issue(bufs, n, stride, p0 + REC_TILE,
+                        c1 - p0 - REC_TILE < (uint64_t)REC_TILE ? c1 - p0 - REC_TILE : REC_TILE, st);
         const bool valid = threadIdx.x < np;
         const uint64_t i = p0 + threadIdx.x;
         const uint8_t *rec = tile + r0 + threadIdx.x * stride;
@@ -650,7 +656,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             rc = QK_E_HIP;
             break;
         }
-        const uint32_t probe_limit = C == cmax ? (uint32_t)C : 256u;
+        const uint32_t probe_limit = C == cmax ? (uint32_t)C : 64u;   // load <= 1/4 when sized from the hint
         hipLaunchKernelGGL(k_flow_extract, dim3(nchunks), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s, d_bufs,
                            (uint64_t)n, (uint32_t)stride, d_meta, my_key, chunk, tab, (uint32_t)(C - 1), probe_limit,
                            slots, ids, counters);

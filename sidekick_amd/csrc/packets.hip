@@ -58,11 +58,16 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_extract(const uint8_t *__restr
     int64_t blk_insert = -1;  // last insert after blk_reset
     uint64_t blk_nres = 0, blk_nins = 0;
 
+    const bool pipe = stage_pipelined(stride, PK_BLOCK);
+    TileStage st;
+    if (pipe && c0 < c1) stage_issue(bufs, n, stride, c0, c1 - c0 < PK_BLOCK ? c1 - c0 : PK_BLOCK, st);
     for (uint64_t p0 = c0; p0 < c1; p0 += PK_BLOCK) {
         const uint64_t np = (c1 - p0) < PK_BLOCK ? (c1 - p0) : PK_BLOCK;
         __syncthreads(); // previous tile fully consumed
-        const uint32_t r0 = stage_records(bufs, n, stride, p0, np, tile);
+        const uint32_t r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records(bufs, n, stride, p0, np, tile);
         __syncthreads();
+        if (pipe && p0 + PK_BLOCK < c1)   // next tile's loads fly while this one is classified
+            stage_issue(bufs, n, stride, p0 + PK_BLOCK, c1 - p0 - PK_BLOCK < PK_BLOCK ? c1 - p0 - PK_BLOCK : PK_BLOCK, st);
         // classify one record per lane
         uint32_t cls = 0, id = 0; // 0 skip, 1 insert, 2 reset
         const uint64_t pi = p0 + threadIdx.x;
@@ -154,14 +159,12 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     const uint64_t chunk = tiles_per_chunk * PK_BLOCK;
     const uint32_t nchunks = (uint32_t)((n + chunk - 1) / chunk);
 
-    // device scratch: compact ids (n u32) + chunk stats
-    uint32_t *d_ids = nullptr;
-    ChunkStat *d_stats = nullptr;
-    if (hipMallocAsync((void **)&d_ids, n * sizeof(uint32_t), s) != hipSuccess) return QK_E_NOMEM;
-    if (hipMallocAsync((void **)&d_stats, nchunks * sizeof(ChunkStat), s) != hipSuccess) {
-        (void)hipFreeAsync(d_ids, s);
-        return QK_E_NOMEM;
-    }
+    // device scratch in the context's per-packet arena (grow-only, shared with
+    // the flow batches under ctx->mu): compact ids (n u32) + chunk stats
+    const size_t ids_bytes = ((size_t)n * sizeof(uint32_t) + 255) & ~(size_t)255;
+    if (int e = ensure_flow(ctx, 0, ids_bytes + (size_t)nchunks * sizeof(ChunkStat))) return e;
+    uint32_t *d_ids = (uint32_t *)ctx->d_flow[0];
+    ChunkStat *d_stats = (ChunkStat *)((char *)ctx->d_flow[0] + ids_bytes);
     const size_t lds = (size_t)PK_BLOCK * stride + 32;
     hipLaunchKernelGGL(k_pkt_extract, dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs, (uint64_t)n, (uint32_t)stride,
                        d_meta, my_ip_le, check_reset, chunk, d_ids, d_stats);
@@ -195,16 +198,15 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
             if (from < n) rc = launch_encode_u32(ctx, d_ids + from, n - from, t, ctx->d_small, s);
             if (!rc && from < n) {
                 const size_t w = qk_u32_partial_words(t);
+                uint32_t last_id = 0;   // fetched with the partial: one synchronisation
                 if (hipMemcpyAsync(ctx->h_small, ctx->d_small, w * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    (last_insert >= 0 &&
+                     hipMemcpyAsync(&last_id, d_ids + last_insert, 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
                     hipStreamSynchronize(s) != hipSuccess)
                     rc = QK_E_HIP;
                 else {
                     ctx->h_small[t] = inserts; // count = inserts, not array length
-                    uint32_t last_id = 0;
-                    if (last_insert >= 0 &&
-                        hipMemcpy(&last_id, d_ids + last_insert, 4, hipMemcpyDeviceToHost) != hipSuccess)
-                        rc = QK_E_HIP;
-                    if (!rc) rc = qk_u32_merge_partial(tmp, ctx->h_small, last_insert >= 0, last_id);
+                    rc = qk_u32_merge_partial(tmp, ctx->h_small, last_insert >= 0, last_id);
                 }
             }
             if (!rc) {
@@ -214,9 +216,7 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
             free(tmp);
         }
     }
-    (void)hipFreeAsync(d_ids, s);
-    (void)hipFreeAsync(d_stats, s);
-    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s); // the arena is reused by the next call
     st.filtered = n - st.inserted - st.discarded - st.resets;
     if (out_stats) *out_stats = st;
     return rc;

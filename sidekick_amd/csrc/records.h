@@ -25,19 +25,108 @@ __device__ __forceinline__ uint32_t stage_records(const uint8_t *__restrict__ bu
     const uint64_t a_lo = ((base + b_lo) & ~(uintptr_t)15) - base;  // may wrap below 0 (mod 2^64)
     const uint64_t a_hi = ((base + b_hi + 15) & ~(uintptr_t)15) - base;
     const uint32_t nvec = (uint32_t)((a_hi - a_lo) / 16);
-    for (uint32_t v = threadIdx.x; v < nvec; v += blockDim.x) {
-        const uint64_t off = a_lo + 16ull * v; // relative to bufs, mod 2^64
-        if (off < total && off + 16 <= total) {
-            *reinterpret_cast<uint4 *>(tile + 16 * v) = *reinterpret_cast<const uint4 *>(bufs + off);
-        } else {
+    // STAGE_V loads in flight per lane before any LDS write (a load -> wait ->
+    // write loop would pay one HBM round trip per 16 bytes); 5 covers a
+    // 256 x 67 B tile in one round
+    // (loads are unconditional, from an aligned in-range fallback address when
+    // a vector is partial or past the tile, so none waits inside a branch;
+    // total >= 67 bytes, so the first aligned vector is in range)
+    constexpr int STAGE_V = 5;
+    const uint64_t safe = ((base + 15) & ~(uintptr_t)15) - base;
+    for (uint32_t v0 = 0; v0 < nvec; v0 += STAGE_V * blockDim.x) {
+        uint4 r[STAGE_V];
+        bool ok[STAGE_V];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const uint64_t o = off + k; // a wrapped head offset comes back into range exactly
-                tile[16 * v + k] = o < total ? bufs[o] : 0;
+        for (int k = 0; k < STAGE_V; ++k) {
+            const uint32_t v = v0 + k * blockDim.x + threadIdx.x;
+            const uint64_t off = a_lo + 16ull * v; // relative to bufs, mod 2^64
+            ok[k] = v < nvec && off < total && off + 16 <= total;
+            r[k] = *reinterpret_cast<const uint4 *>(bufs + (ok[k] ? off : safe));
+        }
+        // pin the loads here (otherwise each is sunk into its store's branch
+        // and waited for alone)
+#pragma unroll
+        for (int k = 0; k < STAGE_V; ++k) asm volatile("" : "+v"(r[k].x), "+v"(r[k].y), "+v"(r[k].z), "+v"(r[k].w));
+#pragma unroll
+        for (int k = 0; k < STAGE_V; ++k) {
+            const uint32_t v = v0 + k * blockDim.x + threadIdx.x;
+            if (v >= nvec) continue;
+            if (ok[k]) {
+                *reinterpret_cast<uint4 *>(tile + 16 * v) = r[k];
+            } else {
+                const uint64_t off = a_lo + 16ull * v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) {
+                    const uint64_t o = off + b; // a wrapped head offset comes back into range exactly
+                    tile[16 * v + b] = o < total ? bufs[o] : 0;
+                }
             }
         }
     }
     return (uint32_t)(b_lo - a_lo);
+}
+
+// Software-pipelined form for tiles of at most STAGE_V 16-byte vectors per
+// lane (stride <= 79 at 256 records): stage_issue() starts a tile's loads into
+// registers, stage_commit() writes them to LDS.  A kernel issues tile k+1
+// right after committing tile k and classifies tile k meanwhile, so each
+// tile's HBM latency hides behind the previous tile's work.
+constexpr int STAGE_VEC = 5;
+struct TileStage {
+    uint4 r[STAGE_VEC];
+    uint32_t ok;     // bit k: vector k is fully in range (else the byte path)
+    uint32_t nvec;
+    uint64_t a_lo;
+    uint32_t r0;
+};
+
+__device__ __forceinline__ bool stage_pipelined(uint32_t stride, uint32_t threads) {
+    return ((uint64_t)REC_TILE * stride + 15) / 16 + 1 <= (uint64_t)STAGE_VEC * threads;
+}
+
+__device__ __forceinline__ void stage_issue(const uint8_t *__restrict__ bufs, uint64_t n, uint32_t stride,
+                                            uint64_t p0, uint64_t np, TileStage &st) {
+    const uintptr_t base = (uintptr_t)bufs;
+    const uint64_t total = n * (uint64_t)stride;
+    const uint64_t b_lo = p0 * stride, b_hi = (p0 + np) * stride;
+    st.a_lo = ((base + b_lo) & ~(uintptr_t)15) - base;
+    const uint64_t a_hi = ((base + b_hi + 15) & ~(uintptr_t)15) - base;
+    st.nvec = (uint32_t)((a_hi - st.a_lo) / 16);
+    st.r0 = (uint32_t)(b_lo - st.a_lo);
+    const uint64_t safe = ((base + 15) & ~(uintptr_t)15) - base;   // in range: total >= 67
+    st.ok = 0;
+#pragma unroll
+    for (int k = 0; k < STAGE_VEC; ++k) {
+        const uint32_t v = k * blockDim.x + threadIdx.x;
+        const uint64_t off = st.a_lo + 16ull * v;
+        const bool ok = v < st.nvec && off < total && off + 16 <= total;
+        st.ok |= (uint32_t)ok << k;
+        st.r[k] = *reinterpret_cast<const uint4 *>(bufs + (ok ? off : safe));
+    }
+}
+
+__device__ __forceinline__ uint32_t stage_commit(const uint8_t *__restrict__ bufs, uint64_t n, uint32_t stride,
+                                                 TileStage &st, uint8_t *tile) {
+    const uint64_t total = n * (uint64_t)stride;
+#pragma unroll
+    for (int k = 0; k < STAGE_VEC; ++k)   // the loads complete here, not inside a branch below
+        asm volatile("" : "+v"(st.r[k].x), "+v"(st.r[k].y), "+v"(st.r[k].z), "+v"(st.r[k].w));
+#pragma unroll
+    for (int k = 0; k < STAGE_VEC; ++k) {
+        const uint32_t v = k * blockDim.x + threadIdx.x;
+        if (v >= st.nvec) continue;
+        if ((st.ok >> k) & 1) {
+            *reinterpret_cast<uint4 *>(tile + 16 * v) = st.r[k];
+        } else {
+            const uint64_t off = st.a_lo + 16ull * v;
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const uint64_t o = off + b;
+                tile[16 * v + b] = o < total ? bufs[o] : 0;
+            }
+        }
+    }
+    return st.r0;
 }
 
 __device__ __forceinline__ qk_pkt_meta record_meta(const qk_pkt_meta *__restrict__ meta, uint64_t i) {
