@@ -385,9 +385,13 @@ __device__ __forceinline__ void four(Acc<C::NB, C::NA> &S, uint4 w) {
 // wave still has a next group, the prefetch is unconditional; the last <= 2
 // trips take the masked form.  Per-lane 32-bit trip counts (the host
 // guarantees body / nthr < 2^32).
-template <class C>
-__device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
-                                     uint64_t *__restrict__ partials) {
+// body_gen: the ids are walked by `nthr` threads of which this is `gtid`
+// (the whole grid for the headline kernel, one workgroup for a flow's work
+// item); out(m, s) receives the workgroup's sum for power m + 1 (< 2^40) in
+// thread m.
+template <class C, class Out>
+__device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
+                                         uint64_t gtid, uint64_t nthr, Out out) {
     constexpr int NB = C::NB, NA = C::NA;
     __shared__ uint64_t sm[WAVES * NB * NA];
     Acc<NB, NA> S;
@@ -399,8 +403,6 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
 #pragma unroll
         for (int a = 0; a < NA - 1; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; }
     }
-    const uint64_t gtid = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const uint64_t nthr = (uint64_t)gridDim.x * BLOCK;
     const uint64_t h = head < n ? head : n;
     const uint64_t nbody = (n - h) >> 2;
     const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
@@ -456,8 +458,17 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
         uint64_t s = 0;
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) s += sm[w * (NB * NA) + m];
-        partials[(size_t)m * gridDim.x + blockIdx.x] = s;
+        out(m, s);
     }
+}
+
+// the headline kernel's form: grid-stride, one partial per (power, block)
+// stored [power][block]
+template <class C>
+__device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
+                                     uint64_t *__restrict__ partials) {
+    body_gen<C>(ids, n, head, T, (uint64_t)blockIdx.x * BLOCK + threadIdx.x, (uint64_t)gridDim.x * BLOCK,
+                [=](uint32_t m, uint64_t s) { partials[(size_t)m * gridDim.x + blockIdx.x] = s; });
 }
 
 } // namespace bsgs

@@ -120,6 +120,24 @@ __global__ __launch_bounds__(SG_BLOCK) void k_seg_encode(const uint32_t *__restr
     }
 }
 
+// Work items of 9 <= T <= 32: one workgroup walks its item [lo, hi) with the
+// headline kernel's baby-step/giant-step body (bsgs.h).  All lanes of the
+// workgroup belong to one flow, so the wave-level scalar wrap counts stay
+// valid; the workgroup's sums go to the flow's accumulator row by atomicAdd.
+template <int NB, int NA, int SG>
+__global__ __launch_bounds__(bsgs::BLOCK, (NB * NA >= 32 ? 5 : 4)) void k_seg_bsgs(
+    const uint32_t *__restrict__ ids, const SegItem *__restrict__ items, uint32_t T,
+    unsigned long long *__restrict__ acc_out) {
+    const SegItem it = items[blockIdx.x];
+    const uint32_t *p = ids + it.lo;
+    const uint32_t head = (uint32_t)(((16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u) >> 2);   // ids to 16-B alignment
+    unsigned long long *row = acc_out + (size_t)it.seg * T;
+    bsgs::body_gen<bsgs::Cfg<NB, NA, SG>>(p, it.hi - it.lo, head, T, threadIdx.x, (uint64_t)bsgs::BLOCK,
+                                          [=](uint32_t m, uint64_t s) {
+                                              atomicAdd(&row[m], (unsigned long long)fold64_32(s));
+                                          });
+}
+
 // ---- small flows (the many-flow case) ---------------------------------------
 // A flow of <= SMALL_SEG ids is encoded by ONE lane: the whole flow stays in
 // that lane's registers, so there is no cross-lane reduction and no atomic
@@ -488,7 +506,17 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
         seg_choose(T, G, K);
         const uint32_t ni = (uint32_t)items.size();
         hipEvent_t e0 = prof_begin(ctx, s);
+        const dim3 grid(ni), block(bsgs::BLOCK);
+        if (T >= 9 && T <= 32) {   // same configurations as the headline encode
+            if (T <= 12) hipLaunchKernelGGL((k_seg_bsgs<4, 3, 3>), grid, block, 0, s, d_ids, d_items, T, d_acc);
+            else if (T <= 16) hipLaunchKernelGGL((k_seg_bsgs<4, 4, 4>), grid, block, 0, s, d_ids, d_items, T, d_acc);
+            else if (T <= 24) hipLaunchKernelGGL((k_seg_bsgs<6, 4, 4>), grid, block, 0, s, d_ids, d_items, T, d_acc);
+            else hipLaunchKernelGGL((k_seg_bsgs<8, 4, 8>), grid, block, 0, s, d_ids, d_items, T, d_acc);
+            rc = hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
+            G = 0;
+        }
         switch (G) {
+        case 0: break;
         case 1: rc = seg_launch_g<1>(K, d_ids, d_items, ni, T, d_acc, s); break;
         case 2: rc = seg_launch_g<2>(K, d_ids, d_items, ni, T, d_acc, s); break;
         case 4: rc = seg_launch_g<4>(K, d_ids, d_items, ni, T, d_acc, s); break;
