@@ -235,8 +235,11 @@ __device__ __forceinline__ uint64_t ft_settle(uint64_t *w, uint64_t want) {
 __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t probe_limit, uint64_t src,
                                       uint64_t dst, unsigned long long *counters) {
     const uint64_t a0 = ft_w0(src, dst), a1 = ft_w1(dst);
+    // slot `mask` (all ones) is never used: SLOT_NONE then sorts after every
+    // slot on the low log2(C) bits (the by-slot grouping sort)
     uint32_t slot = ft_hash(src, dst) & mask;
-    for (uint32_t probe = 0; probe < probe_limit; ++probe, slot = (slot + 1) & mask) {
+    if (slot == mask) slot = 0;
+    for (uint32_t probe = 0; probe < probe_limit; ++probe, slot = slot + 1 == mask ? 0 : slot + 1) {
         const FlowSlot e = tab[slot];                  // one 16-byte read: the common cases
         if (e.w0 == a0 && e.w1 == a1) return slot;
         if (e.w0 != 0 && (e.w0 != a0 || e.w1 != 0)) continue;
@@ -367,6 +370,34 @@ __global__ void k_slot_rank(const FlowSlot *__restrict__ tab, const uint32_t *__
     info[4 * (uint64_t)r + 1] = ft_dst(e);
 }
 
+// by-slot grouping: pos_of_slot[used[p]] = p (segments are in slot order)
+__global__ void k_slot_pos(const uint32_t *__restrict__ used, uint32_t nf, uint32_t *__restrict__ pos_of_slot) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < nf) pos_of_slot[used[p]] = p;
+}
+
+// by-slot grouping: output rank r -> segment perm[r]; info[4r] = src, [4r+1] = dst
+__global__ void k_rank_perm(const FlowSlot *__restrict__ tab, const uint32_t *__restrict__ slot_of_rank, uint32_t nf,
+                            const uint32_t *__restrict__ pos_of_slot, uint32_t *__restrict__ perm,
+                            uint64_t *__restrict__ info) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nf) return;
+    const uint32_t s = slot_of_rank[r];
+    const FlowSlot e = tab[s];
+    perm[r] = pos_of_slot[s];
+    info[4 * (uint64_t)r + 0] = ft_src(e);
+    info[4 * (uint64_t)r + 1] = ft_dst(e);
+}
+
+// by-slot grouping: segment starts of the slot-sorted packets
+__global__ void k_slot_offsets(const uint32_t *__restrict__ key, uint64_t ninserted,
+                               const uint32_t *__restrict__ pos_of_slot, uint32_t nf, uint64_t *__restrict__ offs) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ninserted;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        if (i == 0 || key[i] != key[i - 1]) offs[pos_of_slot[key[i]]] = i;
+    if (blockIdx.x == 0 && threadIdx.x == 0) offs[nf] = ninserted;
+}
+
 // per packet, in place: slot -> flow rank (non-inserts -> nf, sorting last)
 __global__ void k_slot_to_rank(uint32_t *__restrict__ key, const uint32_t *__restrict__ rank_of_slot, uint64_t n,
                                uint32_t nf) {
@@ -385,19 +416,21 @@ __global__ void k_rank_offsets(const uint32_t *__restrict__ key, uint64_t ninser
     if (blockIdx.x == 0 && threadIdx.x == 0) offs[nf] = ninserted;
 }
 
-// info[4r+2] = count, [4r+3] = last id of flow r
+// info[4r+2] = count, [4r+3] = last id of flow r (segment perm[r], or r)
 __global__ void k_flow_counts(const uint64_t *__restrict__ offs, const uint32_t *__restrict__ ids, uint32_t nf,
-                              uint64_t *__restrict__ info) {
+                              const uint32_t *__restrict__ perm, uint64_t *__restrict__ info) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nf) return;
-    info[4 * (uint64_t)r + 2] = offs[r + 1] - offs[r];
-    info[4 * (uint64_t)r + 3] = ids[offs[r + 1] - 1];
+    const uint32_t g = perm ? perm[r] : r;
+    info[4 * (uint64_t)r + 2] = offs[g + 1] - offs[g];
+    info[4 * (uint64_t)r + 3] = ids[offs[g + 1] - 1];
 }
 
 // qk_u32 records (header + T canonical sums) and AddrKey bytes of every flow,
 // written on the device so the host receives exactly its output in two copies
 __global__ void k_flow_finalize(const unsigned long long *__restrict__ acc, const uint64_t *__restrict__ info,
-                                uint64_t nseg, uint32_t T, uint32_t *__restrict__ rec, uint8_t *__restrict__ keys) {
+                                const uint32_t *__restrict__ perm, uint64_t nseg, uint32_t T,
+                                uint32_t *__restrict__ rec, uint8_t *__restrict__ keys) {
     const uint64_t words = 4ull + T, stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nseg * words; j += stride) {
         const uint64_t i = j / words;
@@ -407,7 +440,7 @@ __global__ void k_flow_finalize(const unsigned long long *__restrict__ acc, cons
         else if (w == 1) v = (uint32_t)info[4 * i + 2];  // count
         else if (w == 2) v = 1u;                          // has_last
         else if (w == 3) v = (uint32_t)info[4 * i + 3];  // last_value
-        else v = canon32(fold64_32(acc[i * T + (w - 4)]));
+        else v = canon32(fold64_32(acc[(perm ? (uint64_t)perm[i] : i) * T + (w - 4)]));
         rec[j] = v;
     }
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nseg * 12; j += stride) {
@@ -684,7 +717,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             rc = QK_E_HIP;
             break;
         }
-        const uint32_t probe_limit = C == cmax ? (uint32_t)C : 64u;   // load <= 1/4 when sized from the hint
+        const uint32_t probe_limit = C == cmax ? (uint32_t)C - 1 : 64u;   // load <= 1/4 when sized from the hint
         hipLaunchKernelGGL(k_flow_extract, dim3(nchunks), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s, d_bufs,
                            (uint64_t)n, (uint32_t)stride, d_meta, my_key, chunk, tab, (uint32_t)(C - 1), probe_limit,
                            slots, ids, counters);
@@ -715,7 +748,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const size_t rec = qk_u32_size(T);
         uint64_t *info = nullptr, *d_offs = nullptr, *kd = nullptr, *kd2 = nullptr, *ks = nullptr, *ks2 = nullptr;
         SegItem *d_items = nullptr;
-        uint32_t *d_rec = nullptr, *used = nullptr, *sl2 = nullptr, *sl3 = nullptr, *nsel = nullptr;
+        uint32_t *d_rec = nullptr, *used = nullptr, *sl2 = nullptr, *sl3 = nullptr, *nsel = nullptr, *perm = nullptr;
         uint8_t *d_keys = nullptr;
         auto layout1 = [&](Carve &c) {
             info = c.take<uint64_t>((size_t)nf * 4);
@@ -726,6 +759,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             d_offs = c.take<uint64_t>((size_t)nf + 1);
             kd = c.take<uint64_t>(nf); kd2 = c.take<uint64_t>(nf); ks = c.take<uint64_t>(nf); ks2 = c.take<uint64_t>(nf);
             used = c.take<uint32_t>(nf); sl2 = c.take<uint32_t>(nf); sl3 = c.take<uint32_t>(nf);
+            perm = c.take<uint32_t>(nf);
             nsel = c.take<uint32_t>(1);
         };
         {
@@ -750,21 +784,41 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s, tab, sl2, nf, (uint64_t *)nullptr, ks);
         if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, ks, ks2, sl2, sl3, nf, 0, 48, s) != hipSuccess)
             rc = QK_E_HIP;
-        // packets: slot -> rank, stable sort by rank (packet order kept within
-        // each flow, so last_value is the flow's last packet)
-        if (!rc) {
+        // packets: one stable radix sort groups the ids by flow with packet
+        // order kept (last_value = the flow's last packet).  By rank (slot ->
+        // rank remap per packet, bit_width(flows) bits) or, when the table's
+        // log2(C) bits need no more 8-bit passes, directly by slot (no remap;
+        // segments come out in slot order and perm maps rank -> segment).
+        const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
+        const bool by_slot = (cbits + 7) / 8 <= (fbits + 7) / 8;
+        const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
+        if (!rc && by_slot) {
+            hipLaunchKernelGGL(k_slot_pos, dim3(fblocks), dim3(256), 0, s, used, nf, rank_of_slot);
+            hipLaunchKernelGGL(k_rank_perm, dim3(fblocks), dim3(256), 0, s, tab, sl3, nf, rank_of_slot, perm, info);
+            if (hipGetLastError() != hipSuccess ||
+                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n, 0, cbits, s) !=
+                    hipSuccess)
+                rc = QK_E_HIP;
+            if (!rc) {
+                hipLaunchKernelGGL(k_slot_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted,
+                                   rank_of_slot, nf, d_offs);
+                hipLaunchKernelGGL(k_flow_counts, dim3(fblocks), dim3(256), 0, s, d_offs, id_s, nf, perm, info);
+                if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+            }
+        } else if (!rc) {
             hipLaunchKernelGGL(k_slot_rank, dim3(fblocks), dim3(256), 0, s, tab, sl3, nf, rank_of_slot, info);
             hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, (uint64_t)n, nf);
-            if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
-        }
-        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n, 0,
-                                                      bit_width32(nf), s) != hipSuccess)
-            rc = QK_E_HIP;
-        if (!rc) {
-            const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
-            hipLaunchKernelGGL(k_rank_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted, nf, d_offs);
-            hipLaunchKernelGGL(k_flow_counts, dim3(fblocks), dim3(256), 0, s, d_offs, id_s, nf, info);
-            if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+            if (hipGetLastError() != hipSuccess ||
+                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n, 0, fbits, s) !=
+                    hipSuccess)
+                rc = QK_E_HIP;
+            if (!rc) {
+                hipLaunchKernelGGL(k_rank_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted, nf,
+                                   d_offs);
+                hipLaunchKernelGGL(k_flow_counts, dim3(fblocks), dim3(256), 0, s, d_offs, id_s, nf,
+                                   (const uint32_t *)nullptr, info);
+                if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+            }
         }
         std::vector<uint64_t> offs((size_t)nf + 1);
         uint32_t hsel = 0;
@@ -777,7 +831,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         if (!rc) {
             const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nf * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);
-            hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info, (uint64_t)nf, T, d_rec, d_keys);
+            hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info,
+                               by_slot ? (const uint32_t *)perm : nullptr, (uint64_t)nf, T, d_rec, d_keys);
             if (hipGetLastError() != hipSuccess ||
                 hipMemcpyAsync(sketches, d_rec, (size_t)nf * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipMemcpyAsync(keys, d_keys, (size_t)nf * 12, hipMemcpyDeviceToHost, s) != hipSuccess)

@@ -172,3 +172,22 @@ def test_gpu_flows_edge_keys_and_table_growth():
         assert list(table.senders()) == sorted(want)     # the C ABI returns flows in ascending AddrKey order
         if fl is not flows and len(fl) > 1000:
             assert len(want) > 50_000
+
+
+@pytest.mark.gpu
+def test_gpu_flows_group_by_slot_and_by_rank():
+    """The grouping sort runs by table slot when log2(table size) needs no more
+    radix passes than bit_width(flows) (10 000 flows, table sized from the
+    previous batch: 16 vs 14 bits), else by flow rank (16 flows: 12 vs 5
+    bits).  Both must give the oracle's tables, in ascending key order."""
+    import torch
+    import sidekick_amd as sk
+    for nflows, seed in ((10_000, 1), (10_000, 2), (16, 3), (10_000, 4)):
+        bufs, meta = make_flows(200_000, nflows, seed=seed, p_reset=0.02)
+        want, nres = vector_flows(bufs, meta)
+        table = sk.FlowQuacks(24)
+        st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
+                                  meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
+        assert st["resets"] == nres
+        check_flows_table(table, want, 24)
+        assert list(table.senders()) == sorted(want)
