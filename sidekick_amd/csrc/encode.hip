@@ -611,6 +611,7 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
 #define QK_BSGS(NB_, NA_, G_)                                                                        \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)
+    if (T >= 5 && T <= 8 && sg(1)) return QK_BSGS(4, 2, 1);
     if (T >= 9 && T <= 12) return sg(3) ? QK_BSGS(4, 3, 3) : QK_BSGS(4, 3, 0);
     if (T >= 13 && T <= 16) return sg(4) ? QK_BSGS(4, 4, 4) : QK_BSGS(4, 4, 0);
     if (T >= 17 && T <= 24) return sg(4) ? QK_BSGS(6, 4, 4) : QK_BSGS(6, 4, 0);
