@@ -632,6 +632,8 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     // form would spill, so a grid too small for scalar counts takes the chain
     if (T >= 33 && T <= 40 && sg(10)) return QK_BSGS(8, 5, 10);
     if (T >= 41 && T <= 48 && sg(12)) return QK_BSGS(8, 6, 12);
+    if (T >= 49 && T <= 56 && sg(14)) return QK_BSGS(8, 7, 14);
+    if (T >= 57 && T <= 64 && sg(16)) return QK_BSGS(8, 8, 16);
 #undef QK_BSGS
     int G, K;
     choose_gk(T, 32, K32_G1, 10, K32_GN, 4, G, K);

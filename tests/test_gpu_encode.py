@@ -57,7 +57,7 @@ def test_golden_streams(golden):
         assert q.count() == s["n"]
 
 
-U32_TS = list(range(1, 34)) + [36, 40, 41, 47, 48, 49, 64, 65, 80, 100, 128, 129, 256, 300, 513, 1024]
+U32_TS = list(range(1, 34)) + [36, 40, 41, 47, 48, 49, 55, 56, 57, 63, 64, 65, 80, 100, 128, 129, 256, 300, 513, 1024]
 U64_TS = [1, 2, 3, 5, 8, 12, 16, 19, 20, 21, 32, 40, 64, 80, 81, 160, 300, 1024]
 
 
@@ -233,12 +233,12 @@ def test_full_size_u64_properties():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("t", [5, 8, 9, 12, 13, 16, 17, 20, 24, 25, 31, 32, 33, 37, 40, 41, 44, 48])
+@pytest.mark.parametrize("t", [5, 8, 9, 12, 13, 16, 17, 20, 24, 25, 31, 32, 33, 37, 40, 41, 44, 48, 49, 56, 57, 64])
 def test_bsgs_rare_wrap_branch(golden, t):
     """Ids whose lazy folds wrap (prob ~2.6e-8 per id) force the exact
     recompute branch of the baby-step/giant-step kernel: alone in a wave,
     several in one wave, and in the unaligned head/tail (scalar path)."""
-    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4" if t <= 32 else "8x5" if t <= 40 else "8x6"
+    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4" if t <= 32 else "8x5" if t <= 40 else "8x6" if t <= 48 else "8x7" if t <= 56 else "8x8"
     wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
     ids = coracle.splitmix_u32(0xF00D + t, 20_003)
     ids[100] = wraps[0]                      # one lane of one wave
