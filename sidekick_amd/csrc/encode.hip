@@ -88,7 +88,7 @@ __device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
 // waves per SIMD the register budget is sized for (tools/tune_bsgs.hip: 5 for
 // (8,4) beat 4 by 2-3 %; its three spilled VGPRs live outside the loop)
 template <int NB, int NA, int SG>
-__global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 40 ? 3 : 4)) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids,
+__global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB * NA > 40 ? 3 : 4)) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids,
                                                                                   uint64_t n, uint32_t head,
                                                                                   uint32_t T,
                                                                                   uint64_t *__restrict__ partials) {
@@ -634,6 +634,7 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     if (T >= 41 && T <= 48 && sg(12)) return QK_BSGS(8, 6, 12);
     if (T >= 49 && T <= 56 && sg(14)) return QK_BSGS(8, 7, 14);
     if (T >= 57 && T <= 64 && sg(16)) return QK_BSGS(8, 8, 16);
+    if (T >= 65 && T <= 80 && sg(16)) return QK_BSGS(8, 10, 16);
 #undef QK_BSGS
     int G, K;
     choose_gk(T, 32, K32_G1, 10, K32_GN, 4, G, K);

@@ -120,12 +120,12 @@ __global__ __launch_bounds__(SG_BLOCK) void k_seg_encode(const uint32_t *__restr
     }
 }
 
-// Work items of 5 <= T <= 64: one workgroup walks its item [lo, hi) with the
+// Work items of 5 <= T <= 80: one workgroup walks its item [lo, hi) with the
 // headline kernel's baby-step/giant-step body (bsgs.h).  All lanes of the
 // workgroup belong to one flow, so the wave-level scalar wrap counts stay
 // valid; the workgroup's sums go to the flow's accumulator row by atomicAdd.
 template <int NB, int NA, int SG>
-__global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 40 ? 3 : 4)) void k_seg_bsgs(
+__global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB * NA > 40 ? 3 : 4)) void k_seg_bsgs(
     const uint32_t *__restrict__ ids, const SegItem *__restrict__ items, uint32_t T,
     unsigned long long *__restrict__ acc_out) {
     const SegItem it = items[blockIdx.x];
@@ -540,7 +540,7 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
         const uint32_t ni = (uint32_t)items.size();
         hipEvent_t e0 = prof_begin(ctx, s);
         const dim3 grid(ni), block(bsgs::BLOCK);
-        if (T >= 5 && T <= 64) {   // same configurations as the headline encode
+        if (T >= 5 && T <= 80) {   // same configurations as the headline encode
             if (T <= 8) hipLaunchKernelGGL((k_seg_bsgs<4, 2, 1>), grid, block, 0, s, d_ids, d_items, T, d_acc);
             else if (T <= 12) hipLaunchKernelGGL((k_seg_bsgs<4, 3, 3>), grid, block, 0, s, d_ids, d_items, T, d_acc);
             else if (T <= 16) hipLaunchKernelGGL((k_seg_bsgs<4, 4, 4>), grid, block, 0, s, d_ids, d_items, T, d_acc);
@@ -549,7 +549,8 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
             else if (T <= 40) hipLaunchKernelGGL((k_seg_bsgs<8, 5, 10>), grid, block, 0, s, d_ids, d_items, T, d_acc);
             else if (T <= 48) hipLaunchKernelGGL((k_seg_bsgs<8, 6, 12>), grid, block, 0, s, d_ids, d_items, T, d_acc);
             else if (T <= 56) hipLaunchKernelGGL((k_seg_bsgs<8, 7, 14>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else hipLaunchKernelGGL((k_seg_bsgs<8, 8, 16>), grid, block, 0, s, d_ids, d_items, T, d_acc);
+            else if (T <= 64) hipLaunchKernelGGL((k_seg_bsgs<8, 8, 16>), grid, block, 0, s, d_ids, d_items, T, d_acc);
+            else hipLaunchKernelGGL((k_seg_bsgs<8, 10, 16>), grid, block, 0, s, d_ids, d_items, T, d_acc);
             rc = hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
             G = 0;
         }

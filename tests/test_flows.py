@@ -110,7 +110,7 @@ def test_gpu_segments_primitive():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("t", [1, 5, 8, 9, 12, 13, 16, 17, 24, 25, 32, 33, 40, 48, 56, 64, 65, 80])
+@pytest.mark.parametrize("t", [1, 5, 8, 9, 12, 13, 16, 17, 24, 25, 32, 33, 40, 48, 56, 64, 65, 80, 81])
 def test_gpu_many_small_segments(golden, t):
     """Lane-per-segment kernel (segments <= 4096 ids, t <= 32) beside the
     work-item path (longer segments, t > 32): thousands of ragged segments,
@@ -124,7 +124,7 @@ def test_gpu_many_small_segments(golden, t):
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     ids = coracle.splitmix_u32(0x5E6 + t, int(offs[-1]))
     cfg = ("4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4" if t <= 32
-           else "8x5" if t <= 40 else "8x6" if t <= 48 else "8x7" if t <= 56 else "8x8")
+           else "8x5" if t <= 40 else "8x6" if t <= 48 else "8x7" if t <= 56 else "8x8" if t <= 64 else "8x10")
     wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
     for j, g in enumerate((10, 11, 5, 6, 2999)):     # first/middle/last id of a segment
         if lens[g]:

@@ -233,12 +233,12 @@ def test_full_size_u64_properties():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("t", [5, 8, 9, 12, 13, 16, 17, 20, 24, 25, 31, 32, 33, 37, 40, 41, 44, 48, 49, 56, 57, 64])
+@pytest.mark.parametrize("t", [5, 8, 9, 12, 13, 16, 17, 20, 24, 25, 31, 32, 33, 37, 40, 41, 44, 48, 49, 56, 57, 64, 65, 72, 80])
 def test_bsgs_rare_wrap_branch(golden, t):
     """Ids whose lazy folds wrap (prob ~2.6e-8 per id) force the exact
     recompute branch of the baby-step/giant-step kernel: alone in a wave,
     several in one wave, and in the unaligned head/tail (scalar path)."""
-    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4" if t <= 32 else "8x5" if t <= 40 else "8x6" if t <= 48 else "8x7" if t <= 56 else "8x8"
+    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4" if t <= 32 else "8x5" if t <= 40 else "8x6" if t <= 48 else "8x7" if t <= 56 else "8x8" if t <= 64 else "8x10"
     wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
     ids = coracle.splitmix_u32(0xF00D + t, 20_003)
     ids[100] = wraps[0]                      # one lane of one wave
