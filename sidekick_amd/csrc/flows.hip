@@ -230,10 +230,10 @@ __device__ __forceinline__ uint64_t ft_settle(uint64_t *w, uint64_t want) {
     return o == 0 ? want : o;
 }
 
-// slot of (src, dst), inserting it if absent; SLOT_NONE (and a flag) when the
-// probe limit is reached
+// slot of (src, dst), inserting it if absent (++created when this call made
+// the flow); SLOT_NONE (and a flag) when the probe limit is reached
 __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t probe_limit, uint64_t src,
-                                      uint64_t dst, unsigned long long *counters) {
+                                      uint64_t dst, unsigned long long *counters, uint32_t &created) {
     const uint64_t a0 = ft_w0(src, dst), a1 = ft_w1(dst);
     // slot `mask` (all ones) is never used: SLOT_NONE then sorts after every
     // slot on the low log2(C) bits (the by-slot grouping sort)
@@ -249,7 +249,7 @@ __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t pro
         if (v != 0) continue;
         const uint64_t o = atomicCAS((unsigned long long *)&tab[slot].w1, 0ull, (unsigned long long)a1);
         if (o == 0) {
-            atomicAdd(&counters[2], 1ull);   // this key owns the slot
+            ++created;   // this key owns the slot (summed per workgroup by the caller)
             return slot;
         }
         if (o == a1) return slot;
@@ -279,6 +279,11 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
     uint64_t n_ins = 0, n_rst = 0;   // thread 0's running totals
+    // flows this thread created; summed in LDS and added with one atomic per
+    // workgroup (a per-flow atomic on one counter serialises at 1e6 flows)
+    __shared__ uint32_t l_new;
+    uint32_t n_new = 0;
+    if (threadIdx.x == 0) l_new = 0;
     const bool pipe = stage_pipelined(stride, REC_TILE);
     TileStage st;
     if (pipe && c0 < c1) stage_issue(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
@@ -324,7 +329,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
                 h = (h + 1) & (LH - 1);
             }
             if (lead == threadIdx.x)
-                l_slot[threadIdx.x] = ft_find_or_insert(tab, mask, probe_limit, src, dst, counters);
+                l_slot[threadIdx.x] = ft_find_or_insert(tab, mask, probe_limit, src, dst, counters, n_new);
         }
         __syncthreads();
         if (valid) {
@@ -335,11 +340,14 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
         n_ins += (uint64_t)ins;
         n_rst += (uint64_t)rst;
     }
+    if (n_new) atomicAdd(&l_new, n_new);
+    __syncthreads();
     // one atomic per workgroup (a per-packet atomic on one address
     // serialises: 1.2 s per 1e8 packets)
     if (threadIdx.x == 0) {
         if (n_ins) atomicAdd(&counters[0], (unsigned long long)n_ins);
         if (n_rst) atomicAdd(&counters[1], (unsigned long long)n_rst);
+        if (l_new) atomicAdd(&counters[2], (unsigned long long)l_new);
     }
 }
 
