@@ -115,7 +115,9 @@ uint64_t qk_u64_eval(const uint64_t *coeffs, uint32_t d, uint64_t x);
 size_t qk_u32_serialized_size(const qk_u32 *q);
 int qk_u32_serialize(const qk_u32 *q, uint8_t *buf, size_t cap, size_t *len);
 /* Reads the threshold from the bytes; *threshold_out lets the caller size q
- * first (call with q == NULL). */
+ * first (call with q == NULL), then qk_*_init(q, threshold) and call again:
+ * q->threshold must equal the serialized threshold (else QK_E_MISMATCH and q
+ * is untouched). */
 int qk_u32_deserialize(const uint8_t *buf, size_t len, qk_u32 *q, uint32_t *threshold_out);
 size_t qk_u64_serialized_size(const qk_u64 *q);
 int qk_u64_serialize(const qk_u64 *q, uint8_t *buf, size_t cap, size_t *len);
@@ -220,9 +222,12 @@ typedef struct qk_flow_key {
  * batch's flows in ascending key order, keys[i] and sketches record i
  * (qk_u32_size(threshold) bytes each, ready for qk_u32_merge into the
  * caller's table).  my_addr = own dst ip:port (6 bytes) or NULL.  A Reset
- * packet (dst ip:port == my_addr) only clears an existing table entry with
- * its own key, which can never hold inserts, so it changes no output; it is
- * counted in stats.  cap < flows -> QK_E_CAPACITY with *n_flows set. */
+ * packet (dst ip:port == my_addr) wipes EVERY flow, as the sniff loops do
+ * (`senders = HashMap::new()`, sidekick_multi.rs:205,265): the output holds
+ * only the inserts after the batch's last reset, stats.discarded counts the
+ * inserts before it, stats.last_reset_index is its position, and a caller
+ * with stats.resets > 0 must clear its own table before merging the output.
+ * cap < flows -> QK_E_CAPACITY with *n_flows set. */
 int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
                                const qk_pkt_meta *d_meta, const uint8_t my_addr[6], uint32_t threshold,
                                qk_flow_key *keys, uint8_t *sketches, size_t cap, size_t *n_flows,

@@ -301,9 +301,13 @@ def addr_key(buf) -> bytes:
 
 
 def sniff_multi_batch(table: dict, threshold: int, bufs, pkttype=None, protocol_be=None, lens=None, my_addr=None):
-    """SidekickMulti over a batch (sidekick_multi.rs:101-143 process_one_packet,
-    :65-90 insert, :59-63 reset), literally.  table: AddrKey -> OracleQuack."""
-    stats = {"inserted": 0, "resets": 0, "filtered": 0}
+    """The SidekickMulti sniff loop over a batch, literally:
+    process_one_packet (sidekick_multi.rs:101-143), Insert -> SidekickMulti::
+    insert (:65-90), Reset -> `senders = HashMap::new()` (:205 in
+    start_sidekick_multi, :265 in start_sidekick_multi_frequency_pkts: every
+    flow is wiped, not only the reset key's entry).  table: AddrKey ->
+    OracleQuack, updated in place."""
+    stats = {"inserted": 0, "discarded": 0, "resets": 0, "filtered": 0, "last_reset_index": -1}
     for i in range(len(bufs)):
         buf = bufs[i]
         pt = PACKET_HOST if pkttype is None else int(pkttype[i])
@@ -315,8 +319,10 @@ def sniff_multi_batch(table: dict, threshold: int, bufs, pkttype=None, protocol_
         key = addr_key(buf)
         if my_addr is not None and list(key[6:12]) == list(my_addr):
             stats["resets"] += 1
-            if key in table:
-                table[key] = OracleQuack(threshold)
+            stats["discarded"] += stats["inserted"]
+            stats["inserted"] = 0
+            stats["last_reset_index"] = i
+            table.clear()
             continue
         if ln != BUFFER_SIZE:
             stats["filtered"] += 1

@@ -4,21 +4,25 @@
 // (sidekick/src/sidekick_multi.rs:36,65-90,101-143):
 //     match process_one_packet(n, &buf, &addr, my_addr) {
 //         Insert { addr_key, id } => senders.entry(addr_key).or_insert(new(t)).insert(id),
-//         Reset  { addr_key }     => if let Some(q) = senders.get_mut(&addr_key) { *q = new(t) },
+//         Reset  { .. }           => senders = HashMap::new(),          (:205, :265)
 //         Skip => {} }
 // with AddrKey = [src ip(4), src port(2), dst ip(4), dst port(2)] = buf[26..30],
-// buf[34..36], buf[30..34], buf[36..38] (buffer.rs:91-95).  A Reset targets the
-// key of a packet whose dst ip:port IS the proxy's own address, and an Insert
-// needs dst ip:port != own address, so a reset can never hit a key that holds
-// inserts: within a batch resets are no-ops on the produced table (counted in
-// the stats).  The caller merges the batch table into its own with
-// qk_u32_merge, flow by flow.
+// buf[34..36], buf[30..34], buf[36..38] (buffer.rs:91-95).  A Reset (a packet
+// whose dst ip:port IS the proxy's own address) wipes EVERY flow — the sniff
+// loops replace the whole map, they do not call SidekickMulti::reset — so the
+// batch's table is the inserts after its last reset, and the caller clears
+// its own table before merging when stats.resets > 0.  The caller merges the
+// batch table into its own with qk_u32_merge, flow by flow.
 //
 // Device pipeline:
 //   1. k_flow_extract   LDS-staged records -> per packet the filters and, for
 //                       an Insert, its flow's slot in a device hash table
 //                       (packets of a tile that share a flow elect one leader
-//                       in LDS, which probes / inserts once); writes slot + id.
+//                       in LDS, which probes / inserts once); writes slot + id
+//                       and the batch's last reset position.  A batch with a
+//                       reset reruns the pass over the packets after it with
+//                       an empty table (resets are rare: one per receiver
+//                       request, media_client.rs:272).
 //   2. the occupied slots (DeviceSelect) sorted by AddrKey (two stable 48-bit
 //      radix sorts of the flows only) -> rank of each flow = output order.
 //   3. per packet slot -> rank; one stable radix sort of (rank, id) pairs over
@@ -263,7 +267,7 @@ __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t pro
 // LDS first (one table probe per flow per tile: with few flows the table
 // lines are not hammered by every packet).  Writes slot (SLOT_NONE if not an
 // Insert) and id per packet; counters: [0] inserts, [1] resets, [2] distinct
-// flows, [3] flags.
+// flows, [3] flags, [4] 1 + the position of the last reset (0: none).
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
                                                            uint32_t stride, const qk_pkt_meta *__restrict__ meta,
                                                            uint64_t my_key_lo, uint64_t chunk,
@@ -279,6 +283,9 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
     uint64_t n_ins = 0, n_rst = 0;   // thread 0's running totals
+    uint64_t my_rst = 0;             // 1 + this thread's last reset position (0: none)
+    __shared__ unsigned long long l_rst;
+    if (threadIdx.x == 0) l_rst = 0;
     // flows this thread created; summed in LDS and added with one atomic per
     // workgroup (a per-flow atomic on one counter serialises at 1e6 flows)
     __shared__ uint32_t l_new;
@@ -309,8 +316,10 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
                   ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];
             dst = ((uint64_t)rec[30] << 40) | ((uint64_t)rec[31] << 32) | ((uint64_t)rec[32] << 24) |
                   ((uint64_t)rec[33] << 16) | ((uint64_t)rec[36] << 8) | (uint64_t)rec[37];
-            if (dst == my_key_lo) cls = 2;
-            else if (m.len == QK_BUFFER_SIZE) {
+            if (dst == my_key_lo) {
+                cls = 2;
+                my_rst = i + 1;
+            } else if (m.len == QK_BUFFER_SIZE) {
                 cls = 1;
                 id = record_identifier(rec);
             }
@@ -341,6 +350,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
         n_rst += (uint64_t)rst;
     }
     if (n_new) atomicAdd(&l_new, n_new);
+    if (my_rst) atomicMax(&l_rst, (unsigned long long)my_rst);
     __syncthreads();
     // one atomic per workgroup (a per-packet atomic on one address
     // serialises: 1.2 s per 1e8 packets)
@@ -348,6 +358,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
         if (n_ins) atomicAdd(&counters[0], (unsigned long long)n_ins);
         if (n_rst) atomicAdd(&counters[1], (unsigned long long)n_rst);
         if (l_new) atomicAdd(&counters[2], (unsigned long long)l_new);
+        if (l_rst) atomicMax(&counters[4], l_rst);
     }
 }
 
@@ -694,7 +705,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     void *temp = nullptr;
     auto layout0 = [&](Carve &c) {
         slots = c.take<uint32_t>(n); ids = c.take<uint32_t>(n); key_s = c.take<uint32_t>(n); id_s = c.take<uint32_t>(n);
-        counters = c.take<unsigned long long>(4);
+        counters = c.take<unsigned long long>(5);
         temp = c.take<char>(tb);
     };
     {
@@ -704,53 +715,67 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         Carve cv{(char *)ctx->d_flow[0]};
         layout0(cv);
     }
-    // pass 1: filters + flow table; a table that overflows its probe limit is
-    // regrown and the pass rerun (the next batch starts from this size)
+    // pass 1: filters + flow table over packets [p_from, n); a table that
+    // overflows its probe limit is regrown and the pass rerun (the next batch
+    // starts from this size).  When the batch holds a reset, every flow made
+    // before it is wiped (sidekick_multi.rs:205,265): the pass reruns over the
+    // packets after the last reset with an empty table.
     int rc = QK_OK;
     FlowSlot *tab = nullptr;
     uint32_t *rank_of_slot = nullptr;
-    uint64_t hc[4] = {0, 0, 0, 0};
-    // >= 4 tiles per workgroup, enough workgroups to cover the chip
-    const uint64_t ntiles = (n + REC_TILE - 1) / REC_TILE;
-    const uint64_t tiles_per_chunk =
-        std::max<uint64_t>(4, (ntiles + (uint64_t)ctx->num_cus * 4 - 1) / ((uint64_t)ctx->num_cus * 4));
-    const uint64_t chunk = tiles_per_chunk * REC_TILE;
-    const uint32_t nchunks = (uint32_t)((n + chunk - 1) / chunk);
-    for (;;) {
-        {
-            Carve probe{nullptr};
-            probe.take<FlowSlot>(C);
-            probe.take<uint32_t>(C);
-            if (int e = ensure_flow(ctx, 2, probe.off)) return e;
-            Carve cv{(char *)ctx->d_flow[2]};
-            tab = cv.take<FlowSlot>(C);
-            rank_of_slot = cv.take<uint32_t>(C);
+    uint64_t hc[5] = {0, 0, 0, 0, 0};
+    auto pass1 = [&](uint64_t p_from) -> int {
+        const uint64_t pn = n - p_from;
+        const uint8_t *pb = d_bufs + p_from * stride;
+        const qk_pkt_meta *pm = d_meta ? d_meta + p_from : nullptr;
+        // >= 4 tiles per workgroup, enough workgroups to cover the chip
+        const uint64_t ntiles = (pn + REC_TILE - 1) / REC_TILE;
+        const uint64_t tiles_per_chunk =
+            std::max<uint64_t>(4, (ntiles + (uint64_t)ctx->num_cus * 4 - 1) / ((uint64_t)ctx->num_cus * 4));
+        const uint64_t chunk = tiles_per_chunk * REC_TILE;
+        const uint32_t nchunks = (uint32_t)std::max<uint64_t>(1, (pn + chunk - 1) / chunk);
+        for (;;) {
+            {
+                Carve probe{nullptr};
+                probe.take<FlowSlot>(C);
+                probe.take<uint32_t>(C);
+                if (int e = ensure_flow(ctx, 2, probe.off)) return e;
+                Carve cv{(char *)ctx->d_flow[2]};
+                tab = cv.take<FlowSlot>(C);
+                rank_of_slot = cv.take<uint32_t>(C);
+            }
+            if (hipMemsetAsync(tab, 0, C * sizeof(FlowSlot), s) != hipSuccess ||
+                hipMemsetAsync(counters, 0, 5 * 8, s) != hipSuccess)
+                return QK_E_HIP;
+            const uint32_t probe_limit = C == cmax ? (uint32_t)C - 1 : 64u;   // load <= 1/4 when sized from the hint
+            if (pn)
+                hipLaunchKernelGGL(k_flow_extract, dim3(nchunks), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
+                                   pb, pn, (uint32_t)stride, pm, my_key, chunk, tab, (uint32_t)(C - 1), probe_limit,
+                                   slots, ids, counters);
+            if (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(hc, counters, 40, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return QK_E_HIP;
+            if (!(hc[3] & FT_OVERFLOW)) return QK_OK;
+            if (C == cmax) return QK_E_NOMEM;   // > 2^31 flows: no table size left
+            C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(16 * C, 4 * hc[2])));
         }
-        if (hipMemsetAsync(tab, 0, C * sizeof(FlowSlot), s) != hipSuccess ||
-            hipMemsetAsync(counters, 0, 4 * 8, s) != hipSuccess) {
-            rc = QK_E_HIP;
-            break;
-        }
-        const uint32_t probe_limit = C == cmax ? (uint32_t)C - 1 : 64u;   // load <= 1/4 when sized from the hint
-        hipLaunchKernelGGL(k_flow_extract, dim3(nchunks), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s, d_bufs,
-                           (uint64_t)n, (uint32_t)stride, d_meta, my_key, chunk, tab, (uint32_t)(C - 1), probe_limit,
-                           slots, ids, counters);
-        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(hc, counters, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-            rc = QK_E_HIP;
-            break;
-        }
-        if (!(hc[3] & FT_OVERFLOW)) break;
-        if (C == cmax) { rc = QK_E_NOMEM; break; }   // > 2^31 flows: no table size left
-        C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(16 * C, 4 * hc[2])));
+    };
+    rc = pass1(0);
+    const uint64_t all_inserts = hc[0], resets = hc[1];
+    if (!rc && hc[4]) {
+        st.last_reset_index = (int64_t)hc[4] - 1;
+        rc = pass1(hc[4]);   // the packets after the last reset (no reset among them)
     }
-    const uint64_t inserted = hc[0], resets = hc[1];
+    const uint64_t n_eff = n - (uint64_t)(st.last_reset_index + 1);
+    const uint64_t inserted = hc[0];
     const uint32_t nf = (uint32_t)hc[2];
     if (!rc) {
         ctx->flow_hint = nf;
         st.inserted = inserted;
+        st.discarded = all_inserts - inserted;
         st.resets = resets;
-        st.filtered = n - inserted - resets;
+        st.filtered = n - all_inserts - resets;
         *n_flows = nf;
         if (nf > cap || (nf && (!keys || !sketches))) rc = QK_E_CAPACITY;
     }
@@ -786,7 +811,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             layout1(cv);
         }
         const uint32_t fblocks = (nf + 255) / 256;
-        const uint32_t gb = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 8);
+        const uint32_t gb = (uint32_t)std::min<uint64_t>((n_eff + 255) / 256, (uint64_t)ctx->num_cus * 8);
         // flows in ascending AddrKey order: stable LSD sort of the occupied
         // slots by dst, then by src (48-bit halves)
         if (!rc && hipcub::DeviceSelect::If(temp, tb, hipcub::CountingInputIterator<uint32_t>(0), used, nsel,
@@ -810,7 +835,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             hipLaunchKernelGGL(k_slot_pos, dim3(fblocks), dim3(256), 0, s, used, nf, rank_of_slot);
             hipLaunchKernelGGL(k_rank_perm, dim3(fblocks), dim3(256), 0, s, tab, sl3, nf, rank_of_slot, perm, info);
             if (hipGetLastError() != hipSuccess ||
-                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n, 0, cbits, s) !=
+                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, cbits, s) !=
                     hipSuccess)
                 rc = QK_E_HIP;
             if (!rc) {
@@ -821,9 +846,9 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             }
         } else if (!rc) {
             hipLaunchKernelGGL(k_slot_rank, dim3(fblocks), dim3(256), 0, s, tab, sl3, nf, rank_of_slot, info);
-            hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, (uint64_t)n, nf);
+            hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, n_eff, nf);
             if (hipGetLastError() != hipSuccess ||
-                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n, 0, fbits, s) !=
+                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, fbits, s) !=
                     hipSuccess)
                 rc = QK_E_HIP;
             if (!rc) {

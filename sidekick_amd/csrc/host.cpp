@@ -35,6 +35,9 @@ int deser(const uint8_t *buf, size_t len, Q *q, uint32_t *t_out, T modulus) {
     const size_t need = body + 1 + (tag ? sizeof(T) : 0) + 4;
     if (len != need) return QK_E_FORMAT;
     if (!q) return QK_OK;
+    // q must have been initialised for this threshold (qk_*_init(q, t) sizes
+    // its power_sums): a smaller sketch would be overrun
+    if (q->threshold != (uint32_t)t) return QK_E_MISMATCH;
     for (uint64_t k = 0; k < t; ++k) {
         const T v = (T)get_le(buf + 8 + sizeof(T) * k, sizeof(T));
         if (v >= modulus) return QK_E_FORMAT; // ModularInteger values are canonical

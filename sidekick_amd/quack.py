@@ -448,7 +448,9 @@ class FlowQuacks:
         q.insert(sidekick_id)
         return q
 
-    # sidekick_multi.rs:59-63: only an existing entry is reset
+    # SidekickMulti::reset (sidekick_multi.rs:59-63): only an existing entry is
+    # reset.  The sniff loops never call it — a Reset packet replaces the whole
+    # map (:205, :265), which insert_packets does.
     def reset(self, addr_key: bytes) -> None:
         if bytes(addr_key) in self._senders:
             self._senders[bytes(addr_key)] = PowerSumQuackU32(self.threshold)
@@ -464,12 +466,16 @@ class FlowQuacks:
         """Batch of captured records (CUDA uint8 tensor) through the GPU:
         extract, group by AddrKey, encode per flow, merge into the table."""
         import torch
-        if not (isinstance(bufs, torch.Tensor) and bufs.is_cuda and bufs.dtype == torch.uint8):
-            raise TypeError("bufs must be a CUDA uint8 tensor")
+        if not (isinstance(bufs, torch.Tensor) and bufs.is_cuda and bufs.dtype == torch.uint8 and bufs.is_contiguous()):
+            raise TypeError("bufs must be a contiguous CUDA uint8 tensor")
         n = bufs.numel() // stride
         dev = bufs.device.index if bufs.device.index is not None else torch.cuda.current_device()
         ctx = ctx or get_context(dev)
-        mptr = meta.data_ptr() if meta is not None else None
+        mptr = None
+        if meta is not None:
+            if not (meta.is_cuda and meta.is_contiguous() and meta.numel() * meta.element_size() == 8 * n):
+                raise ValueError("meta must be a contiguous CUDA tensor of n 8-byte records")
+            mptr = meta.data_ptr()
         addr = (C.c_uint8 * 6)(*my_addr) if my_addr is not None else None
         rec = lib().qk_u32_size(self.threshold)
         cap = 1024
@@ -486,6 +492,10 @@ class FlowQuacks:
                 continue
             check(rc, "encode_flows")
             break
+        if st.resets:
+            # a Reset wipes every flow (`senders = HashMap::new()`,
+            # sidekick_multi.rs:205,265); the batch output is what follows it
+            self._senders = {}
         for i in range(nf.value):
             key = bytes(keys[i].addr)
             q = PowerSumQuackU32.__new__(PowerSumQuackU32)

@@ -84,7 +84,8 @@ class QuackReceiver:
             self._insert_prefix(last_index)
         reset0 = last_index is None                                                 # :257-261
         reset1 = self.my_quack.count() < quack.count()
-        reset2 = self.my_quack.count() > quack.count() + self.threshold
+        # `quack.count() + threshold as u32` is u32 arithmetic (wraps in a release build)
+        reset2 = self.my_quack.count() > (quack.count() + self.threshold) & 0xFFFFFFFF
         if reset0 or reset1 or reset2:
             should = self.last_quack_reset is None or now > self.last_quack_reset + self.reset_debounce_s
             act.reset_reason = (reset0, reset1, reset2)

@@ -9,7 +9,10 @@ MY_ADDR = (10, 0, 2, 1, 0x1F, 0x90)   # own dst ip:port (6 bytes)
 META_DT = np.dtype([("pkttype", "u1"), ("reserved", "u1"), ("protocol_be", "<u2"), ("len", "<u4")])
 
 
-def make_flows(n, nflows, seed, stride=67, p_filter=0.1, p_reset=0.01, skew=False, flows=None):
+def make_flows(n, nflows, seed, stride=67, p_filter=0.1, p_reset=0.01, skew=False, flows=None, reset_until=0.5):
+    """n records over nflows AddrKeys; resets (packets to MY_ADDR) only in the
+    first reset_until fraction, so the flows after the last reset — the only
+    ones a Reset leaves (sidekick_multi.rs:205,265) — hold most packets."""
     rng = np.random.default_rng(seed)
     bufs = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
     bufs[:, 23] = 17
@@ -28,7 +31,7 @@ def make_flows(n, nflows, seed, stride=67, p_filter=0.1, p_reset=0.01, skew=Fals
     bufs[:, 30:34] = key[:, 6:10]
     bufs[:, 36:38] = key[:, 10:12]
     r = rng.random(n)
-    rs = r < p_reset
+    rs = (r < p_reset) & (np.arange(n) < int(reset_until * n))
     bufs[rs, 30:34] = MY_ADDR[:4]
     bufs[rs, 36:38] = MY_ADDR[4:]
     meta = np.zeros(n, dtype=META_DT)
@@ -44,30 +47,59 @@ def make_flows(n, nflows, seed, stride=67, p_filter=0.1, p_reset=0.01, skew=Fals
 
 
 def vector_flows(bufs, meta, my_addr=MY_ADDR):
-    """Vectorised SidekickMulti (checked against the oracle below):
-    {key: ids in packet order}."""
+    """Vectorised SidekickMulti sniff loop (checked against the oracle below):
+    ({key: ids in packet order after the last reset}, resets, last reset
+    position or -1)."""
     inc = (meta["pkttype"] == 0) | (meta["pkttype"] == 3)
     ok = inc & (meta["protocol_be"] == 0x0008) & (bufs[:, 23] == 17)
     keys = np.concatenate([bufs[:, 26:30], bufs[:, 34:36], bufs[:, 30:34], bufs[:, 36:38]], axis=1)
     rst = ok & np.all(keys[:, 6:12] == np.array(my_addr, dtype=np.uint8), axis=1) if my_addr else np.zeros(len(bufs), bool)
     ins = ok & ~rst & (meta["len"] == 67)
+    last_reset = int(np.nonzero(rst)[0][-1]) if rst.any() else -1
     idb = bufs[:, 63:67].astype(np.uint32)
     ids = (idb[:, 0] << 24) | (idb[:, 1] << 16) | (idb[:, 2] << 8) | idb[:, 3]
     out = {}
-    for i in np.nonzero(ins)[0]:
+    for i in np.nonzero(ins[last_reset + 1:])[0] + last_reset + 1:
         out.setdefault(bytes(keys[i]), []).append(int(ids[i]))
-    return out, int(rst.sum())
+    return out, int(rst.sum()), last_reset
 
 
-def test_vector_flows_matches_oracle():
-    bufs, meta = make_flows(3000, 7, seed=1, p_reset=0.05, p_filter=0.2)
-    table, st = qo.sniff_multi_batch({}, 8, bufs, meta["pkttype"], meta["protocol_be"], meta["len"], MY_ADDR)
-    flows, nres = vector_flows(bufs, meta)
-    assert set(table) == set(flows) and st["resets"] == nres
+@pytest.mark.parametrize("reset_until", [0.0, 0.5, 1.0])
+def test_vector_flows_matches_oracle(reset_until):
+    bufs, meta = make_flows(3000, 7, seed=1, p_reset=0.05, p_filter=0.2, reset_until=reset_until)
+    pre = qo.OracleQuack(8)
+    pre.insert(7)
+    table = {b"\x01" * 12: pre}            # the caller's table before the batch
+    table, st = qo.sniff_multi_batch(table, 8, bufs, meta["pkttype"], meta["protocol_be"], meta["len"], MY_ADDR)
+    flows, nres, last_reset = vector_flows(bufs, meta)
+    assert st["resets"] == nres and st["last_reset_index"] == last_reset
+    assert st["inserted"] == sum(len(v) for v in flows.values())
+    if nres:                                 # a Reset wiped the caller's flow too
+        assert set(table) == set(flows)
+    else:
+        assert set(table) == set(flows) | {b"\x01" * 12}
     for k, ids in flows.items():
         w = qo.OracleQuack(8)
         w.insert_all(ids)
         assert table[k].power_sums == w.power_sums and table[k].count == len(ids) and table[k].last_value == ids[-1]
+
+
+def test_sniff_multi_reset_wipes_every_flow():
+    """sidekick_multi.rs:205: a Reset packet replaces the whole map, so a flow
+    whose packets all came before it is gone, and a flow seen on both sides
+    restarts from the packets after it."""
+    bufs, meta = make_flows(40, 2, seed=5, p_reset=0.0, p_filter=0.0)
+    k0, k1 = sorted({qo.addr_key(b) for b in bufs})
+    bufs[20, 30:34] = MY_ADDR[:4]
+    bufs[20, 36:38] = MY_ADDR[4:]
+    table, st = qo.sniff_multi_batch({}, 4, bufs, meta["pkttype"], meta["protocol_be"], meta["len"], MY_ADDR)
+    assert st["resets"] == 1 and st["last_reset_index"] == 20
+    after = {}
+    for b in bufs[21:]:
+        after.setdefault(qo.addr_key(b), []).append(int.from_bytes(bytes(b[63:67]), "big"))
+    assert set(table) == set(after) and st["inserted"] == 19 and st["discarded"] == 20
+    for k, ids in after.items():
+        assert table[k].count == len(ids) and table[k].last_value == ids[-1]
 
 
 @pytest.mark.gpu
@@ -77,20 +109,25 @@ def test_vector_flows_matches_oracle():
 def test_gpu_flows_vs_oracle(n, nflows, t, skew):
     import torch
     import sidekick_amd as sk
-    bufs, meta = make_flows(n, nflows, seed=n + t, skew=skew)
+    bufs, meta = make_flows(n, nflows, seed=n + t, skew=skew, reset_until=0.3 if n % 2 else 0.0)
     table = sk.FlowQuacks(t)
     pre_key = None
-    flows, nres = vector_flows(bufs, meta)
-    if flows:                                # pre-existing entry merges with the batch
+    flows, nres, last_reset = vector_flows(bufs, meta)
+    if flows:                                # pre-existing entry merges with the batch (or is wiped by a reset)
         pre_key = sorted(flows)[0]
         table.insert(pre_key, 424242)
     st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
                               meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
     assert st["resets"] == nres and st["inserted"] == sum(len(v) for v in flows.values())
+    assert st["last_reset_index"] == last_reset
+    _, ost = qo.sniff_multi_batch({}, t, bufs[: min(n, 5000)], meta["pkttype"], meta["protocol_be"], meta["len"],
+                                  MY_ADDR) if n <= 5000 else (None, None)
+    if ost is not None:
+        assert ost == st
     assert set(table.senders()) == set(flows)
     for k, ids in flows.items():
         q = table.senders()[k]
-        want_ids = ([424242] if k == pre_key else []) + ids
+        want_ids = ([424242] if k == pre_key and nres == 0 else []) + ids
         assert q.power_sums() == coracle.encode_u32(np.array(want_ids, dtype=np.uint32), t), k.hex()
         assert q.count() == len(want_ids) and q.last_value() == ids[-1]
 
@@ -164,7 +201,7 @@ def test_gpu_flows_edge_keys_and_table_growth():
         if fl is None:
             fl = rng.integers(0, 256, size=(60_000, 12), dtype=np.uint8)
         bufs, meta = make_flows(n, 0, seed=n, flows=fl, p_reset=0.0)
-        want, _ = vector_flows(bufs, meta)
+        want, _, _ = vector_flows(bufs, meta)
         table = sk.FlowQuacks(16)
         st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
                                   meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
@@ -185,10 +222,43 @@ def test_gpu_flows_group_by_slot_and_by_rank():
     import sidekick_amd as sk
     for nflows, seed in ((10_000, 1), (10_000, 2), (16, 3), (10_000, 4)):
         bufs, meta = make_flows(200_000, nflows, seed=seed, p_reset=0.02)
-        want, nres = vector_flows(bufs, meta)
+        want, nres, _ = vector_flows(bufs, meta)
         table = sk.FlowQuacks(24)
         st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
                                   meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
         assert st["resets"] == nres
         check_flows_table(table, want, 24)
         assert list(table.senders()) == sorted(want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["first", "middle", "last", "none"])
+def test_gpu_flows_reset_wipes_table(where):
+    """A Reset anywhere in the batch wipes every flow made before it, the
+    caller's existing table included (sidekick_multi.rs:205,265); a reset as
+    the last packet leaves an empty table.  Stats match the literal loop."""
+    import torch
+    import sidekick_amd as sk
+    n = 3000
+    bufs, meta = make_flows(n, 12, seed=77, p_reset=0.0)
+    pos = {"first": 0, "middle": n // 2, "last": n - 1, "none": None}[where]
+    if pos is not None:
+        bufs[pos, 30:34] = MY_ADDR[:4]
+        bufs[pos, 36:38] = MY_ADDR[4:]
+        meta["pkttype"][pos], meta["protocol_be"][pos] = 0, 0x0008
+        bufs[pos, 23] = 17
+    otab = {b"\x02" * 12: qo.OracleQuack(32)}
+    otab, ost = qo.sniff_multi_batch(otab, 32, bufs, meta["pkttype"], meta["protocol_be"], meta["len"], MY_ADDR)
+    table = sk.FlowQuacks(32)
+    table.insert(b"\x02" * 12, 5)
+    st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
+                              meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
+    assert st == ost
+    assert set(table.senders()) == set(otab)
+    for k, q in otab.items():
+        g = table.senders()[k]
+        if k == b"\x02" * 12:
+            continue
+        assert g.power_sums() == q.power_sums and g.count() == q.count and g.last_value() == q.last_value
+    if where == "last":
+        assert table.senders() == {}

@@ -27,7 +27,8 @@ class OracleReceiver:
         if idx is not None:
             for _, v in self.log[: idx + 1]:
                 self.my.insert(v)
-        r0, r1, r2 = idx is None, self.my.count < q.count, self.my.count > q.count + self.t
+        # `quack.count() + threshold as u32` is u32 arithmetic (media_client.rs:260)
+        r0, r1, r2 = idx is None, self.my.count < q.count, self.my.count > (q.count + self.t) & 0xFFFFFFFF
         if r0 or r1 or r2:
             if self.last_reset is None or now > self.last_reset + self.debounce:
                 self.my, self.log, self.last_reset = qo.OracleQuack(self.t), [], now
@@ -109,3 +110,31 @@ def test_receiver_matches_media_client_host_path(loss, reorder):
 def test_receiver_matches_media_client_gpu_path(loss):
     st = simulate(t=16, n_pkts=1200, loss=loss, seed=7, batch_min=1)
     assert st["quacks"] > 0
+
+
+def _with_count(q, count):
+    """The same sketch with its wrapping u32 count set (bincode image: the
+    count is the trailing u32)."""
+    wire = bytearray(q.serialize())
+    wire[-4:] = int(count).to_bytes(4, "little")
+    return sk.PowerSumQuackU32.deserialize(bytes(wire))
+
+
+def test_receiver_reset2_wraps_like_u32():
+    """reset2 = my.count() > quack.count() + threshold in u32 (media_client.rs:260):
+    near 2^32 the sum wraps, and the receiver resets where unbounded
+    arithmetic would not."""
+    t = 8
+    rx, orx = QuackReceiver(t, batch_min=1 << 30), OracleReceiver(t)
+    rx.my_quack = _with_count(sk.PowerSumQuackU32(t), 0xFFFFFFFE)
+    orx.my.count = 0xFFFFFFFE
+    rx.on_send(1, 77)
+    orx.log.append((1, 77))
+    q = sk.PowerSumQuackU32(t)
+    q.insert(77)
+    q = _with_count(q, 0xFFFFFFFD)
+    oq = qo.OracleQuack(t)
+    oq.power_sums, oq.count, oq.last_value = q.power_sums(), q.count(), q.last_value()
+    act = rx.on_quack(q, 1.0)
+    assert orx.on_quack(oq, 1.0) == (act.retransmit, act.send_reset)
+    assert act.send_reset and act.reset_reason == (False, False, True)
