@@ -7,7 +7,10 @@ t=32 on one MI355X, ids already resident in HBM.  One step = one pass of the
 encode path over the GPU's batch: the encode kernel + finalize kernel, and,
 for N > 1, the single RCCL sum-reduce of the partial power-sum vectors to
 rank 0 (weak scaling: every GPU owns a fixed 1e9-id shard of one global
-stream).
+stream).  For N > 1 the data path is the library's native communicator
+(qk_u32_encode_sharded_async: encode + ONE ncclReduce over xGMI, comm.hip);
+torch.distributed (gloo) only carries the control plane — the RCCL unique
+id, the barriers around the timed region and the max-over-ranks time.
 
     python bench.py [--gpus N --steps K --warmup W --n IDS_PER_GPU --t 32 --bits 32]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -64,8 +67,12 @@ def main():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     ap.add_argument("--cpu-sample", type=float, default=1e8, help="ids for the CPU baseline (0 disables)")
     ap.add_argument("--grid", type=int, default=0, help="override workgroups per launch")
-    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
-                    help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse several ranks on one GPU")
+    ap.add_argument("--comm", action="store_true",
+                    help="at N = 1 too, run each step through the native communicator (a world-1 ncclReduce)")
+    ap.add_argument("--dist-backend", default="rccl", choices=("rccl", "gloo"),
+                    help="rccl: the native communicator (RCCL over xGMI, one GPU per rank) for real runs; gloo: "
+                         "the same shard/reduce protocol over torch.distributed CPU tensors, only to rehearse "
+                         "several ranks on one GPU")
     args = ap.parse_args()
 
     import numpy as np
@@ -84,17 +91,21 @@ def main():
     ndev = torch.cuda.device_count()
     dev_index = local % ndev  # == local on a real node (one process per GPU)
     torch.cuda.set_device(dev_index)
+    comm = None
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")          # control plane only
+        if args.dist_backend == "rccl":
+            comm = skd.Comm.from_process_group(dev_index)
+    elif args.comm:
+        comm = skd.Comm.create([dev_index])
 
     n = int(args.ids_per_gpu)
     t, bits = args.t, args.bits
     n_total = n * world
     start, cnt = skd.shard(n_total, rank, world)
-    ctx = sk.get_context(dev_index)
+    # the context that runs the encode: the communicator's own for the native
+    # multi-GPU path (profiling and the grid knob must reach that one)
+    ctx = comm.context(0) if comm is not None else sk.get_context(dev_index)
     if args.grid:
         ctx.set_grid(args.grid)
 
@@ -105,14 +116,14 @@ def main():
     torch.cuda.synchronize()
 
     def step():
+        if comm is not None:
+            comm.encode_sharded_async([ids], t, bits=bits, root=0)   # encode + one ncclReduce (comm.hip)
+            return
         encode_device_async(ctx, ids, t, partial, bits=bits)
-        if world > 1:
-            if args.dist_backend == "nccl":
-                skd.reduce_partial_(partial, t, bits, dst=0)      # one RCCL reduce of t+1 words
-            else:
-                host = partial.cpu()                              # rehearsal only (gloo is CPU)
-                skd.reduce_partial_(host, t, bits, dst=0)
-                partial.copy_(host)
+        if world > 1:                                                 # gloo rehearsal (CPU tensors)
+            host = partial.cpu()
+            skd.reduce_partial_(host, t, bits, dst=0)
+            partial.copy_(host)
 
     for _ in range(args.warmup):
         step()
@@ -134,17 +145,22 @@ def main():
     ctx.set_profiling(False)
     kern_ms, launches = ctx.kernel_stats()
     if world > 1:
-        el = torch.tensor([elapsed], dtype=torch.float64,
-                          device=f"cuda:{dev_index}" if args.dist_backend == "nccl" else "cpu")
+        el = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
     ms_per_step = elapsed / args.steps * 1e3
     kern_avg_ms = kern_ms / max(launches, 1)
 
     # result of the last step (rank 0 holds the reduced sum)
+    if comm is not None:
+        qres = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
+        comm.encode_sharded_wait(qres)
     part_host = partial.cpu().numpy().view(np.uint64)
     if rank == 0:
-        S, count = skd.fold_partial_sum(part_host, t, bits)
+        if comm is not None:
+            S, count = qres.power_sums(), qres.count()
+        else:
+            S, count = skd.fold_partial_sum(part_host, t, bits)
         log(f"encode result: count={count} S[0..3]={S[:3]}")
         import hashlib
         digest = hashlib.sha256((",".join(str(v) for v in S) + f"|{count}").encode()).hexdigest()[:16]
@@ -152,6 +168,8 @@ def main():
     if rank != 0:
         if world > 1:
             dist.barrier()
+            if comm is not None:
+                comm.close()
             dist.destroy_process_group()
         return
 
@@ -176,7 +194,9 @@ def main():
         "data": "synthetic: splitmix64 uniform ids generated in HBM (seeded), no host copies in the timed region",
         "config": {
             "workload": f"encode {n:.0e} u{bits} ids per GPU at t={t}, device-resident"
-                        + ("" if world == 1 else f", {world} contiguous shards + one RCCL reduce"),
+                        + ("" if world == 1 else
+                           f", {world} contiguous shards + one RCCL reduce (native qk_comm)" if comm is not None else
+                           f", {world} contiguous shards + one gloo reduce (rehearsal)"),
             "ids_per_gpu": cnt, "global_ids": n_total, "threshold": t, "bits": bits,
             "seed": hex(args.seed), "parallelism": f"shard{world}",
         },
@@ -236,8 +256,12 @@ def main():
             "parity_with_gpu": q.power_sums() == mt_S,
         }
     print(json.dumps(out), flush=True)
+    if comm is not None and world == 1:
+        comm.close()
     if world > 1:
         dist.barrier()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -22,6 +22,7 @@ QK_E_HIP = -6
 QK_E_NO_DEVICE = -7
 QK_E_NOMEM = -8
 QK_E_FORMAT = -9
+QK_E_COMM = -10
 
 P32 = 4294967291
 P64 = 18446744073709551557
@@ -31,6 +32,7 @@ u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
 u64p = C.POINTER(C.c_uint64)
 vp = C.c_void_p
+vpp = C.POINTER(C.c_void_p)
 sz = C.c_size_t
 szp = C.POINTER(C.c_size_t)
 
@@ -90,6 +92,21 @@ SIGNATURES = {
     "qk_u32_encode_packets_device": (C.c_int, [vp, vp, sz, sz, vp, vp, vp, vp, vp]),
     "qk_u32_encode_flows_device": (C.c_int, [vp, vp, sz, sz, vp, vp, C.c_uint32, vp, vp, sz, szp, vp, vp]),
     "qk_u32_encode_segments_device": (C.c_int, [vp, vp, u64p, sz, C.c_uint32, vp, vp]),
+    "qk_comm_unique_id": (C.c_int, [u8p]),
+    "qk_comm_create": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
+    "qk_comm_init_rank": (C.c_int, [u8p, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+    "qk_comm_destroy": (None, [vp]),
+    "qk_comm_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "qk_comm_context": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
+    "qk_comm_barrier": (C.c_int, [vp]),
+    "qk_u32_encode_sharded_async": (C.c_int, [vp, vpp, szp, C.c_uint32, C.c_int, vpp]),
+    "qk_u64_encode_sharded_async": (C.c_int, [vp, vpp, szp, C.c_uint32, C.c_int, vpp]),
+    "qk_u32_encode_sharded_wait": (C.c_int, [vp, vp]),
+    "qk_u64_encode_sharded_wait": (C.c_int, [vp, vp]),
+    "qk_u32_encode_sharded": (C.c_int, [vp, vpp, szp, vp, C.c_int, vpp]),
+    "qk_u64_encode_sharded": (C.c_int, [vp, vpp, szp, vp, C.c_int, vpp]),
+    "qk_u32_decode_sharded": (C.c_int, [vp, vp, C.c_int, vpp, szp, C.c_int, u64p, sz, szp, vpp]),
+    "qk_u64_decode_sharded": (C.c_int, [vp, vp, C.c_int, vpp, szp, C.c_int, u64p, sz, szp, vpp]),
     "qk_fill_splitmix_u32": (C.c_int, [vp, vp, sz, C.c_uint64, C.c_uint64, vp]),
     "qk_fill_splitmix_u64": (C.c_int, [vp, vp, sz, C.c_uint64, C.c_uint64, vp]),
 }

@@ -36,47 +36,49 @@ int scratch_release(qk_ctx *ctx, hipStream_t s) {
     return QK_OK;
 }
 
-int ensure_scratch(qk_ctx *ctx, size_t bytes) {
+// Grow-only device buffers use stream-ordered allocation: hipFree performs an
+// implicit hipDeviceSynchronize, which would stall every stream of the device
+// (the caller's unrelated work included) whenever a buffer grows.  The old
+// buffer is released with hipFreeAsync on the stream that needs the new one,
+// after that buffer's last user (ctx->scratch_ev for the encode scratch,
+// which async launches on any stream hand over; the flow arenas and the hit
+// buffer are only used inside synchronous calls, so they are idle here).
+static int regrow(void **buf, size_t *have, size_t sz, hipStream_t s, hipEvent_t last_user) {
+    if (*buf) {
+        if (last_user) QK_HIP_TRY(hipStreamWaitEvent(s, last_user, 0));
+        QK_HIP_TRY(hipFreeAsync(*buf, s));
+        *buf = nullptr;
+        *have = 0;
+    }
+    if (hipMallocAsync(buf, sz, s) != hipSuccess) {
+        (void)hipGetLastError();
+        *buf = nullptr;
+        return QK_E_NOMEM;
+    }
+    *have = sz;
+    return QK_OK;
+}
+
+int ensure_scratch(qk_ctx *ctx, size_t bytes, hipStream_t s) {
     if (bytes <= ctx->scratch_bytes) return QK_OK;
-    // scratch may still be in use by queued work on any stream of this ctx
-    if (ctx->d_scratch) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(ctx->d_scratch);
-        ctx->d_scratch = nullptr;
-        ctx->scratch_bytes = 0;
-    }
-    size_t sz = std::max(bytes, (size_t)1 << 20);
-    if (hipMalloc(&ctx->d_scratch, sz) != hipSuccess) return QK_E_NOMEM;
-    ctx->scratch_bytes = sz;
-    return QK_OK;
+    return regrow(&ctx->d_scratch, &ctx->scratch_bytes, std::max(bytes, (size_t)1 << 20), s,
+                  ctx->scratch_ev_valid ? ctx->scratch_ev : nullptr);
 }
 
-int ensure_flow(qk_ctx *ctx, int which, size_t bytes) {
+int ensure_flow(qk_ctx *ctx, int which, size_t bytes, hipStream_t s) {
     if (bytes <= ctx->flow_bytes[which]) return QK_OK;
-    if (ctx->d_flow[which]) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(ctx->d_flow[which]);
-        ctx->d_flow[which] = nullptr;
-        ctx->flow_bytes[which] = 0;
-    }
-    const size_t sz = std::max(bytes + bytes / 8, (size_t)1 << 20); // headroom for growing batches
-    if (hipMalloc(&ctx->d_flow[which], sz) != hipSuccess) return QK_E_NOMEM;
-    ctx->flow_bytes[which] = sz;
-    return QK_OK;
+    // headroom for growing batches
+    return regrow(&ctx->d_flow[which], &ctx->flow_bytes[which], std::max(bytes + bytes / 8, (size_t)1 << 20), s,
+                  nullptr);
 }
 
-int ensure_hits(qk_ctx *ctx, size_t cap) {
+int ensure_hits(qk_ctx *ctx, size_t cap, hipStream_t s) {
     if (cap <= ctx->hits_cap) return QK_OK;
-    if (ctx->d_hits) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(ctx->d_hits);
-        ctx->d_hits = nullptr;
-        ctx->hits_cap = 0;
-    }
-    size_t c = std::max(cap, (size_t)1 << 16);
-    if (hipMalloc(&ctx->d_hits, c * sizeof(uint64_t)) != hipSuccess) return QK_E_NOMEM;
-    ctx->hits_cap = c;
-    return QK_OK;
+    size_t bytes = 0;
+    const size_t c = std::max(cap, (size_t)1 << 16);
+    int rc = regrow((void **)&ctx->d_hits, &bytes, c * sizeof(uint64_t), s, nullptr);
+    ctx->hits_cap = rc ? 0 : c;
+    return rc;
 }
 
 int ensure_stage(qk_ctx *ctx, size_t bytes) {
@@ -169,7 +171,23 @@ static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t,
     if (rc) return rc;
     const bool pinned = is_pinned_host_ptr(h_ids);
     hipStream_t cs = ctx->copy_stream, ks = ctx->stream;
-    hipEvent_t copied[2], consumed[2];
+    // destroyed on every exit; the streams are drained first so that no
+    // queued wait or record still refers to them
+    struct Events {
+        hipEvent_t copied[2] = {nullptr, nullptr}, consumed[2] = {nullptr, nullptr};
+        hipStream_t cs, ks;
+        ~Events() {
+            (void)hipStreamSynchronize(ks);
+            (void)hipStreamSynchronize(cs);
+            for (int i = 0; i < 2; ++i) {
+                if (copied[i]) (void)hipEventDestroy(copied[i]);
+                if (consumed[i]) (void)hipEventDestroy(consumed[i]);
+            }
+        }
+    } ev;
+    ev.cs = cs;
+    ev.ks = ks;
+    hipEvent_t *copied = ev.copied, *consumed = ev.consumed;
     for (int i = 0; i < 2; ++i) {
         if (hipEventCreateWithFlags(&copied[i], hipEventDisableTiming) != hipSuccess) return QK_E_HIP;
         if (hipEventCreateWithFlags(&consumed[i], hipEventDisableTiming) != hipSuccess) return QK_E_HIP;
@@ -202,13 +220,72 @@ static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t,
     QK_HIP_TRY(hipMemcpyAsync(partial_out, ctx->d_small, words * 8, hipMemcpyDeviceToHost, ks));
     QK_HIP_TRY(hipStreamSynchronize(ks));
     QK_HIP_TRY(hipStreamSynchronize(cs));
-    for (int i = 0; i < 2; ++i) { hipEventDestroy(copied[i]); hipEventDestroy(consumed[i]); }
     return QK_OK;
 }
 
-template <typename T, typename Launch>
+// Root test in two phases, so that several devices (a multi-GPU
+// communicator, comm.hip) can have theirs in flight at once.
+// root_test_begin enqueues on s: coefficients H2D, counter reset, the kernel,
+// counters D2H.  root_test_finish waits for s, reruns once with a larger hit
+// buffer if the kernel ran out of room, and returns the hit positions sorted
+// ascending (every hit of the log, not cut at the stop) and the first stop
+// position (n if none or !use_stop).
+template <typename T>
+int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
+                    hipStream_t s) {
+    int (*launch)(qk_ctx *, const T *, uint32_t, const T *, size_t, int, T, uint64_t *, uint64_t, uint64_t *,
+                  hipStream_t);
+    if constexpr (sizeof(T) == 4) launch = launch_root_test_u32;
+    else launch = launch_root_test_u64;
+    // layout of d_small: [0, SMALL_NHITS) coefficients, [SMALL_NHITS] hit count, [SMALL_STOP] stop index
+    uint64_t *d_counters = ctx->d_small + SMALL_NHITS;
+    T *d_c = (T *)ctx->d_small;
+    memcpy(ctx->h_small, coeffs, (size_t)d * sizeof(T));
+    if (d) QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, (size_t)d * sizeof(T), hipMemcpyHostToDevice, s));
+    if (int rc = ensure_hits(ctx, 4096, s)) return rc;
+    hipLaunchKernelGGL(k_init_counters, dim3(1), dim3(1), 0, s, d_counters);
+    if (n) {
+        int rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap, d_counters, s);
+        if (rc) return rc;
+    }
+    QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_NHITS, d_counters, 16, hipMemcpyDeviceToHost, s));
+    return QK_OK;
+}
+
+template <typename T>
+int root_test_finish(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
+                     hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index) {
+    QK_HIP_TRY(hipStreamSynchronize(s));
+    uint64_t cnt = ctx->h_small[SMALL_NHITS];
+    if (cnt > ctx->hits_cap) {   // grow and rerun once (the kernel counts every hit)
+        if (int rc = ensure_hits(ctx, (size_t)cnt, s)) return rc;
+        if (int rc = root_test_begin<T>(ctx, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
+        QK_HIP_TRY(hipStreamSynchronize(s));
+        cnt = ctx->h_small[SMALL_NHITS];
+        if (cnt > ctx->hits_cap) return QK_E_HIP;
+    }
+    const uint64_t stop = ctx->h_small[SMALL_STOP];
+    hits.resize(cnt);
+    if (cnt) {
+        QK_HIP_TRY(hipMemcpyAsync(hits.data(), ctx->d_hits, cnt * 8, hipMemcpyDeviceToHost, s));
+        QK_HIP_TRY(hipStreamSynchronize(s));
+    }
+    std::sort(hits.begin(), hits.end());
+    stop_index = use_stop ? std::min<uint64_t>(stop, (uint64_t)n) : (uint64_t)n;
+    return QK_OK;
+}
+template int root_test_begin<uint32_t>(qk_ctx *, const uint32_t *, uint32_t, const uint32_t *, size_t, int, uint32_t,
+                                       hipStream_t);
+template int root_test_begin<uint64_t>(qk_ctx *, const uint64_t *, uint32_t, const uint64_t *, size_t, int, uint64_t,
+                                       hipStream_t);
+template int root_test_finish<uint32_t>(qk_ctx *, const uint32_t *, uint32_t, const uint32_t *, size_t, int, uint32_t,
+                                        hipStream_t, std::vector<uint64_t> &, uint64_t &);
+template int root_test_finish<uint64_t>(qk_ctx *, const uint64_t *, uint32_t, const uint64_t *, size_t, int, uint64_t,
+                                        hipStream_t, std::vector<uint64_t> &, uint64_t &);
+
+template <typename T>
 static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop,
-                          T stop_value, uint64_t *hits, size_t cap, size_t *n_hits, void *stream, Launch launch,
+                          T stop_value, uint64_t *hits, size_t cap, size_t *n_hits, void *stream,
                           uint64_t *stop_index = nullptr) {
     if (!ctx || !n_hits || (d && !coeffs) || (n && !d_log)) return QK_E_INVAL;
     *n_hits = 0;
@@ -217,46 +294,23 @@ static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_l
     if (d == 0) {
         if (!stop_index || !use_stop) return QK_OK; // P == 1 has no roots
         // no roots, but a shard caller still needs the stop position: the
-        // degree-0 launch tests nothing and only records the stop (below)
+        // degree-0 launch tests nothing and only records the stop
     }
     if (d > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
     if (!is_device_ptr(d_log)) return QK_E_INVAL;
     std::lock_guard<std::mutex> g(ctx->mu);
     QK_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = pick_stream(ctx, stream);
-    // layout of d_small: [0, SMALL_NHITS) coefficients, [SMALL_NHITS] hit count, [SMALL_STOP] stop index
-    uint64_t *d_counters = ctx->d_small + SMALL_NHITS;
-    T *d_c = (T *)ctx->d_small;
-    memcpy(ctx->h_small, coeffs, (size_t)d * sizeof(T));
-    QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, (size_t)d * sizeof(T), hipMemcpyHostToDevice, s));
-    size_t dev_cap = std::max(cap, (size_t)4096);
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        int rc = ensure_hits(ctx, dev_cap);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_init_counters, dim3(1), dim3(1), 0, s, d_counters);
-        rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap, d_counters, s);
-        if (rc) return rc;
-        uint64_t cnt[2];
-        QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_NHITS, d_counters, 16, hipMemcpyDeviceToHost, s));
-        QK_HIP_TRY(hipStreamSynchronize(s));
-        cnt[0] = ctx->h_small[SMALL_NHITS];
-        cnt[1] = ctx->h_small[SMALL_STOP];
-        if (cnt[0] > ctx->hits_cap) { dev_cap = (size_t)cnt[0]; continue; } // grow and rerun once
-        std::vector<uint64_t> h(cnt[0]);
-        if (cnt[0]) {
-            QK_HIP_TRY(hipMemcpyAsync(h.data(), ctx->d_hits, cnt[0] * 8, hipMemcpyDeviceToHost, s));
-            QK_HIP_TRY(hipStreamSynchronize(s));
-        }
-        std::sort(h.begin(), h.end());
-        size_t m = h.size();
-        if (use_stop) m = (size_t)(std::lower_bound(h.begin(), h.end(), cnt[1]) - h.begin());
-        if (stop_index) *stop_index = use_stop ? std::min<uint64_t>(cnt[1], (uint64_t)n) : (uint64_t)n;
-        *n_hits = m;
-        if (m > cap || (m && !hits)) return QK_E_CAPACITY;
-        std::copy(h.begin(), h.begin() + m, hits);
-        return QK_OK;
-    }
-    return QK_E_HIP;
+    if (int rc = root_test_begin<T>(ctx, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
+    std::vector<uint64_t> h;
+    uint64_t stop = n;
+    if (int rc = root_test_finish<T>(ctx, coeffs, d, d_log, n, use_stop, stop_value, s, h, stop)) return rc;
+    const size_t m = (size_t)(std::lower_bound(h.begin(), h.end(), stop) - h.begin());
+    if (stop_index) *stop_index = stop;
+    *n_hits = m;
+    if (m > cap || (m && !hits)) return QK_E_CAPACITY;
+    std::copy(h.begin(), h.begin() + m, hits);
+    return QK_OK;
 }
 
 } // namespace qk
@@ -315,10 +369,12 @@ void qk_ctx_destroy(qk_ctx *ctx) {
         if (ctx->stage_ev[i]) hipEventDestroy(ctx->stage_ev[i]);
     }
     if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
-    if (ctx->d_scratch) hipFree(ctx->d_scratch);
-    if (ctx->d_hits) hipFree(ctx->d_hits);
+    // stream-ordered buffers (regrow) go back the same way
+    if (ctx->d_scratch) hipFreeAsync(ctx->d_scratch, ctx->stream);
+    if (ctx->d_hits) hipFreeAsync(ctx->d_hits, ctx->stream);
     for (void *f : ctx->d_flow)
-        if (f) hipFree(f);
+        if (f) hipFreeAsync(f, ctx->stream);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
     if (ctx->d_small) hipFree(ctx->d_small);
     if (ctx->h_small) hipHostFree(ctx->h_small);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -459,15 +515,13 @@ int qk_u64_encode_host(qk_ctx *ctx, const uint64_t *h_ids, size_t n, qk_u64 *q) 
 int qk_u32_root_test_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t d, const uint32_t *d_log, size_t n,
                             int stop_at_value, uint32_t stop_value, uint64_t *hits, size_t cap, size_t *n_hits,
                             void *stream) {
-    return root_test_impl<uint32_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
-                                    launch_root_test_u32);
+    return root_test_impl<uint32_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream);
 }
 
 int qk_u64_root_test_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log, size_t n,
                             int stop_at_value, uint64_t stop_value, uint64_t *hits, size_t cap, size_t *n_hits,
                             void *stream) {
-    return root_test_impl<uint64_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
-                                    launch_root_test_u64);
+    return root_test_impl<uint64_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream);
 }
 
 int qk_u32_root_test_shard_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t d, const uint32_t *d_log, size_t n,
@@ -475,7 +529,7 @@ int qk_u32_root_test_shard_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t 
                                   size_t *n_hits, uint64_t *stop_index, void *stream) {
     if (!stop_index) return QK_E_INVAL;
     return root_test_impl<uint32_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
-                                    launch_root_test_u32, stop_index);
+                                    stop_index);
 }
 
 int qk_u64_root_test_shard_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log, size_t n,
@@ -483,7 +537,7 @@ int qk_u64_root_test_shard_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t 
                                   size_t *n_hits, uint64_t *stop_index, void *stream) {
     if (!stop_index) return QK_E_INVAL;
     return root_test_impl<uint64_t>(ctx, coeffs, d, d_log, n, stop_at_value, stop_value, hits, cap, n_hits, stream,
-                                    launch_root_test_u64, stop_index);
+                                    stop_index);
 }
 
 int qk_u32_decode_device(qk_ctx *ctx, const qk_u32 *diff, const uint32_t *d_log, size_t n, int stop_at_last,

@@ -10,7 +10,8 @@
 struct qk_ctx {
     int device = 0;
     int num_cus = 256;
-    hipStream_t stream = nullptr;      // own stream (NULL stream arg selects it)
+    hipStream_t stream = nullptr;      // own stream (host-input pipeline, comm collectives); a NULL
+                                       // stream argument is the HIP null stream, not this one
     hipStream_t copy_stream = nullptr; // second stream for the host-input pipeline
     uint32_t grid_override = 0;
 
@@ -68,9 +69,11 @@ hipStream_t pick_stream(qk_ctx *ctx, void *stream);
 int scratch_acquire(qk_ctx *ctx, hipStream_t s);
 // mark the end of s's use of the scratch buffers
 int scratch_release(qk_ctx *ctx, hipStream_t s);
-int ensure_scratch(qk_ctx *ctx, size_t bytes);
-int ensure_hits(qk_ctx *ctx, size_t cap);
-int ensure_flow(qk_ctx *ctx, int which, size_t bytes);
+// grow-only buffers; growth never synchronises the device (stream-ordered
+// free/alloc on s after the buffer's last user)
+int ensure_scratch(qk_ctx *ctx, size_t bytes, hipStream_t s);
+int ensure_hits(qk_ctx *ctx, size_t cap, hipStream_t s);
+int ensure_flow(qk_ctx *ctx, int which, size_t bytes, hipStream_t s);
 int ensure_stage(qk_ctx *ctx, size_t bytes);
 bool is_device_ptr(const void *p);
 hipEvent_t prof_begin(qk_ctx *ctx, hipStream_t s);
@@ -95,5 +98,14 @@ int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uin
 int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uint64_t *log, size_t n,
                          int use_stop, uint64_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);
+
+// root test in two phases (api.hip): enqueue on s, then wait + collect the
+// sorted hit positions (all of them) and the first stop position
+template <typename T>
+int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
+                    hipStream_t s);
+template <typename T>
+int root_test_finish(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
+                     hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index);
 
 } // namespace qk

@@ -479,7 +479,7 @@ static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t
                       uint32_t per_block, uint64_t *d_partial, int accumulate, hipStream_t s) {
     const uint32_t nb = grid_for(ctx, kern, units, per_block);
     const size_t need = (size_t)nb * words_per_power * GK * sizeof(uint64_t);
-    int rc = ensure_scratch(ctx, need);
+    int rc = ensure_scratch(ctx, need, s);
     if (rc) return rc;
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
     rc = scratch_acquire(ctx, s);

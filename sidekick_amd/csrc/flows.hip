@@ -621,7 +621,7 @@ extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids,
     probe.take<SegItem>(items.size());
     probe.take<uint32_t>(nseg);
     probe.take<uint64_t>(nseg + 1);
-    if (int e = ensure_flow(ctx, 1, probe.off)) return e;
+    if (int e = ensure_flow(ctx, 1, probe.off, s)) return e;
     Carve cv{(char *)ctx->d_flow[1]};
     unsigned long long *d_acc = cv.take<unsigned long long>(nseg * T);
     SegItem *d_items = cv.take<SegItem>(items.size());
@@ -711,7 +711,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     {
         Carve probe{nullptr};
         layout0(probe);
-        if (int e = ensure_flow(ctx, 0, probe.off)) return e;
+        if (int e = ensure_flow(ctx, 0, probe.off, s)) return e;
         Carve cv{(char *)ctx->d_flow[0]};
         layout0(cv);
     }
@@ -739,7 +739,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 Carve probe{nullptr};
                 probe.take<FlowSlot>(C);
                 probe.take<uint32_t>(C);
-                if (int e = ensure_flow(ctx, 2, probe.off)) return e;
+                if (int e = ensure_flow(ctx, 2, probe.off, s)) return e;
                 Carve cv{(char *)ctx->d_flow[2]};
                 tab = cv.take<FlowSlot>(C);
                 rank_of_slot = cv.take<uint32_t>(C);
@@ -804,7 +804,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         {
             Carve probe{nullptr};
             layout1(probe);
-            rc = ensure_flow(ctx, 1, probe.off);
+            rc = ensure_flow(ctx, 1, probe.off, s);
         }
         if (!rc) {
             Carve cv{(char *)ctx->d_flow[1]};

@@ -162,7 +162,7 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     // device scratch in the context's per-packet arena (grow-only, shared with
     // the flow batches under ctx->mu): compact ids (n u32) + chunk stats
     const size_t ids_bytes = ((size_t)n * sizeof(uint32_t) + 255) & ~(size_t)255;
-    if (int e = ensure_flow(ctx, 0, ids_bytes + (size_t)nchunks * sizeof(ChunkStat))) return e;
+    if (int e = ensure_flow(ctx, 0, ids_bytes + (size_t)nchunks * sizeof(ChunkStat), s)) return e;
     uint32_t *d_ids = (uint32_t *)ctx->d_flow[0];
     ChunkStat *d_stats = (ChunkStat *)((char *)ctx->d_flow[0] + ids_bytes);
     const size_t lds = (size_t)PK_BLOCK * stride + 32;

@@ -1,4 +1,17 @@
-"""Multi-GPU sharding of the encode and decode paths (one process per GPU).
+"""Multi-GPU sharding of the encode and decode paths.
+
+The product path is the native communicator of libquack_hip.so (`Comm`,
+over qk_comm_* in include/quack_hip.h: RCCL over xGMI, one ncclReduce per
+sharded encode; comm.hip).  It runs with one process driving several GPUs
+(`Comm.create(devices)`, the shape of the reference's single-process callers)
+or one process per GPU (`Comm.from_process_group()` ships the RCCL unique id
+over an existing torch.distributed group — gloo is enough — and every rank
+joins).
+
+The torch.distributed helpers further down (`reduce_partial_`,
+`root_test_sharded`, ...) restate the same shard / reduce / fold / merge
+protocol over any torch.distributed backend.  They are the CPU rehearsal of
+that protocol (gloo, world 2-3, tests/test_dist.py), since RCCL needs GPUs.
 
 The sketch is additive: S_k(A ⊎ B) = S_k(A) + S_k(B) mod p
 and counts add, so the id stream is cut into contiguous shards, one per rank,
@@ -23,9 +36,127 @@ identical to the single-GPU root test of the whole log.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
-from ._lib import P32, P64
+from ._lib import P32, P64, QK_E_CAPACITY, check, lib
+
+
+# --------------------------------------------------------------------------
+# Native communicator (qk_comm_*): the product multi-GPU path
+# --------------------------------------------------------------------------
+COMM_ID_BYTES = 128
+
+
+class Comm:
+    """A qk_comm: local ranks (GPUs driven by this process) of a communicator.
+
+    Array arguments take one entry per local rank, in local rank order."""
+
+    def __init__(self, handle):
+        self.handle = handle
+        w, nl, fr = C.c_int(), C.c_int(), C.c_int()
+        check(lib().qk_comm_info(handle, C.byref(w), C.byref(nl), C.byref(fr)), "qk_comm_info")
+        self.world, self.nlocal, self.first_rank = w.value, nl.value, fr.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * COMM_ID_BYTES)()
+        check(lib().qk_comm_unique_id(buf), "qk_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def create(cls, devices) -> "Comm":
+        """One process, several GPUs (ncclCommInitAll): local rank i = devices[i]."""
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        check(lib().qk_comm_create(len(devices), devs, C.byref(h)), "qk_comm_create")
+        return cls(h)
+
+    @classmethod
+    def init_rank(cls, uid: bytes, rank: int, world: int, device: int) -> "Comm":
+        """One process per GPU: every rank calls this with rank 0's unique id."""
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib().qk_comm_init_rank(buf, rank, world, device, C.byref(h)), "qk_comm_init_rank")
+        return cls(h)
+
+    @classmethod
+    def from_process_group(cls, device: int, group=None) -> "Comm":
+        """Join a communicator spanning the ranks of a torch.distributed group
+        (any backend: it only carries the 128-byte unique id)."""
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls.init_rank(obj[0], rank, world, device)
+
+    def close(self):
+        if self.handle:
+            lib().qk_comm_destroy(self.handle)
+            self.handle = None
+
+    def barrier(self):
+        check(lib().qk_comm_barrier(self.handle), "qk_comm_barrier")
+
+    def context(self, local: int = 0):
+        """The (communicator-owned) qk_ctx of a local rank."""
+        from .quack import Context
+        h = C.c_void_p()
+        check(lib().qk_comm_context(self.handle, local, C.byref(h)), "qk_comm_context")
+        return Context(device=-1, handle=h)
+
+    @staticmethod
+    def _arrays(tensors, bits):
+        from .quack import _device_array
+        n = len(tensors)
+        ptrs, lens, streams = (C.c_void_p * n)(), (C.c_size_t * n)(), (C.c_void_p * n)()
+        for i, t in enumerate(tensors):
+            ptr, cnt, _, st = _device_array(t, bits)
+            ptrs[i], lens[i], streams[i] = ptr, cnt, st
+        return ptrs, lens, streams
+
+    def encode_sharded_async(self, shards, threshold: int, bits: int = 32, root: int = 0) -> None:
+        """Enqueue: encode local shard i on its GPU, then one RCCL reduce to root."""
+        assert len(shards) == self.nlocal
+        ptrs, lens, streams = self._arrays(shards, bits)
+        check(getattr(lib(), f"qk_u{bits}_encode_sharded_async")(self.handle, ptrs, lens, threshold, root, streams),
+              "encode_sharded_async")
+
+    def encode_sharded_wait(self, q) -> None:
+        """Drain; on the root merge the whole stream into q (others: q untouched)."""
+        check(getattr(lib(), f"qk_u{q.BITS}_encode_sharded_wait")(self.handle, q._buf if q is not None else None),
+              "encode_sharded_wait")
+
+    def encode_sharded(self, shards, q, root: int = 0) -> None:
+        assert len(shards) == self.nlocal
+        ptrs, lens, streams = self._arrays(shards, q.BITS)
+        check(getattr(lib(), f"qk_u{q.BITS}_encode_sharded")(self.handle, ptrs, lens, q._buf, root, streams),
+              "encode_sharded")
+
+    def decode_sharded(self, diff, logs, bits: int = 32, stop_at_last: bool = True, root: int = 0,
+                       cap: int = 1 << 16) -> list:
+        """Global ascending hit positions of the root test over the whole log
+        (log shard i on local rank i); diff is read on the root only."""
+        assert len(logs) == self.nlocal
+        ptrs, lens, streams = self._arrays(logs, bits)
+        f = getattr(lib(), f"qk_u{bits}_decode_sharded")
+        while True:
+            hits = (C.c_uint64 * max(cap, 1))()
+            nh = C.c_size_t()
+            rc = f(self.handle, diff._buf if diff is not None else None, root, ptrs, lens, int(stop_at_last), hits,
+                   cap, C.byref(nh), streams)
+            if rc == QK_E_CAPACITY:
+                cap = nh.value
+                continue
+            check(rc, "decode_sharded")
+            return [int(h) for h in hits[: nh.value]]
+
+
+# --------------------------------------------------------------------------
+# The same protocol over torch.distributed (CPU rehearsal with gloo)
+# --------------------------------------------------------------------------
 
 
 def shard(n_total: int, rank: int, world: int) -> tuple[int, int]:
@@ -74,6 +205,36 @@ def reduce_partial_(partial_tensor, threshold: int, bits: int, dst: int = 0, gro
     import torch.distributed as dist
     k = reduce_words(threshold, bits)
     dist.reduce(partial_tensor[:k], dst=dst, op=dist.ReduceOp.SUM, group=group)
+
+
+def pack_payload(partial, threshold: int, bits: int, rank: int, world: int) -> np.ndarray:
+    """The sharded-encode payload of one rank, as comm.hip's k_comm_pack builds
+    it: the summed words [S.., n] then one (has_last, last) slot per rank,
+    only this rank's filled.  Summing the payloads of all ranks (the one
+    reduce) leaves every slot with exactly one contributor."""
+    R = reduce_words(threshold, bits)
+    part = np.asarray(partial).astype(np.uint64)
+    out = np.zeros(R + 2 * world, dtype=np.uint64)
+    out[:R] = part[:R]
+    if part[R - 1]:
+        out[R + 2 * rank] = 1
+        out[R + 2 * rank + 1] = part[R]
+    return out
+
+
+def fold_payload(words, threshold: int, bits: int, world: int):
+    """(canonical power sums, wrapping count, last_value or None) of a summed
+    payload — the root's fold in comm.hip encode_sharded_wait: last_value is
+    the last id of the highest non-empty rank."""
+    w = np.asarray(words).astype(np.uint64)
+    R = reduce_words(threshold, bits)
+    S, count = fold_partial_sum(w[:R], threshold, bits)
+    last = None
+    for r in range(world - 1, -1, -1):
+        if int(w[R + 2 * r]):
+            last = int(w[R + 2 * r + 1])
+            break
+    return S, count, last
 
 
 def _coll_device(group=None):

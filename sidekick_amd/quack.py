@@ -44,14 +44,16 @@ __all__ = [
 class Context:
     """Owns a qk_ctx* (device scratch, streams, profiling events)."""
 
-    def __init__(self, device: int = 0):
-        h = C.c_void_p()
-        check(lib().qk_ctx_create(int(device), C.byref(h)), f"qk_ctx_create({device})")
-        self.handle = h
+    def __init__(self, device: int = 0, handle=None):
+        self.owned = handle is None
+        if handle is None:
+            handle = C.c_void_p()
+            check(lib().qk_ctx_create(int(device), C.byref(handle)), f"qk_ctx_create({device})")
+        self.handle = handle
         self.device = int(device)
 
     def close(self):
-        if self.handle:
+        if self.handle and self.owned:
             lib().qk_ctx_destroy(self.handle)
             self.handle = None
 

@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, bits, t, n_total, seed, q):
+def _worker(rank, world, port, bits, t, n_total, seed, q, empty_last):
     import torch
     import sidekick_amd as sk
     from sidekick_amd import dist as skd
@@ -32,37 +32,45 @@ def _worker(rank, world, port, bits, t, n_total, seed, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        start, cnt = skd.shard(n_total, rank, world)
+        # the native protocol (comm.hip): contiguous shards, the payload with
+        # per-rank last-id slots, ONE sum-reduce, the root's fold
+        start, cnt = skd.shard(n_total, rank, world - 1 if empty_last else world)
+        if empty_last and rank == world - 1:
+            start, cnt = n_total, 0          # an empty trailing shard: last_value from the rank before
         ids = qo.ids_u32(seed, cnt, start) if bits == 32 else qo.ids_u64(seed, cnt, start)
         local = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
         for x in ids.tolist():
             local.insert(int(x))
-        part = torch.from_numpy(skd.state_to_partial(local).view(np.int64).copy())
-        skd.reduce_partial_(part, t, bits, dst=0)
+        pay = skd.pack_payload(skd.state_to_partial(local), t, bits, rank, world)
+        part = torch.from_numpy(pay.view(np.int64).copy())
+        dist.reduce(part, dst=0, op=dist.ReduceOp.SUM)
         if rank == 0:
-            S, count = skd.fold_partial_sum(part.numpy().view(np.uint64), t, bits)
-            q.put((S, count))
+            q.put(skd.fold_payload(part.numpy().view(np.uint64), t, bits, world))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,bits,t", [(2, 32, 32), (3, 32, 16), (2, 64, 20)])
-def test_sharded_encode_reduce_matches_oracle(world, bits, t):
+@pytest.mark.parametrize("world,bits,t,empty_last", [(2, 32, 32, False), (3, 32, 16, False), (2, 64, 20, False),
+                                                     (3, 32, 8, True), (2, 64, 5, True)])
+def test_sharded_encode_reduce_matches_oracle(world, bits, t, empty_last):
     n_total, seed = 3001, 0xD15
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bits, t, n_total, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bits, t, n_total, seed, q, empty_last))
+             for r in range(world)]
     for p in procs:
         p.start()
-    S, count = q.get(timeout=120)
+    S, count, last = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     if bits == 32:
         assert S == coracle.encode_u32_seed(seed, n_total, t)
+        assert last == int(qo.ids_u32(seed, 1, n_total - 1)[0])
     else:
         assert S == coracle.encode_u64_seed(seed, n_total, t)
+        assert last == int(qo.ids_u64(seed, 1, n_total - 1)[0])
     assert count == n_total
 
 

@@ -43,3 +43,15 @@ def test_bench_contract_and_sharded_parity():
     assert two["n_gpus"] == 2 and two["cpu_baseline"] is None
     assert two["result"]["digest"] == one["result"]["digest"]
     assert two["result"]["count"] == n_total
+
+
+def test_bench_native_comm_world1_matches():
+    """bench.py's native multi-GPU step (encode + one ncclReduce through
+    qk_comm, comm.hip) at world 1: same folded result as the plain step."""
+    n_total = 20_000_000
+    a = run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--ids-per-gpu", str(n_total),
+             "--cpu-sample", "0"])
+    b = run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--ids-per-gpu", str(n_total),
+             "--cpu-sample", "0", "--comm"])
+    assert a["result"]["digest"] == b["result"]["digest"] and b["result"]["count"] == n_total
+    assert b["roofline"]["kernel_avg_ms"] > 0
