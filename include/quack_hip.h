@@ -138,6 +138,11 @@ int qk_ctx_synchronize(qk_ctx *ctx, void *stream);
  * and returns the summed duration and launch count, then resets. */
 int qk_ctx_set_profiling(qk_ctx *ctx, int on);
 int qk_ctx_kernel_stats(qk_ctx *ctx, double *total_ms, uint64_t *launches);
+/* Growing a context's scratch never synchronises the device: grown-out
+ * buffers are retired, not freed (hipFree synchronises every stream).
+ * qk_ctx_trim frees them — a device-wide synchronisation, so call it when
+ * that is acceptable (qk_ctx_destroy does it too). */
+int qk_ctx_trim(qk_ctx *ctx);
 /* Tuning knobs (0 = automatic): workgroups per launch. */
 int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
 /* Pinned host memory for the host-input path: ids written here by the

@@ -69,6 +69,7 @@ SIGNATURES = {
     "qk_ctx_set_profiling": (C.c_int, [vp, C.c_int]),
     "qk_ctx_kernel_stats": (C.c_int, [vp, C.POINTER(C.c_double), u64p]),
     "qk_ctx_set_grid": (C.c_int, [vp, C.c_uint32]),
+    "qk_ctx_trim": (C.c_int, [vp]),
     "qk_host_alloc": (C.c_int, [sz, C.POINTER(vp)]),
     "qk_host_free": (C.c_int, [vp]),
     "qk_u32_partial_words": (sz, [C.c_uint32]),

@@ -36,21 +36,23 @@ int scratch_release(qk_ctx *ctx, hipStream_t s) {
     return QK_OK;
 }
 
-// Grow-only device buffers use stream-ordered allocation: hipFree performs an
-// implicit hipDeviceSynchronize, which would stall every stream of the device
-// (the caller's unrelated work included) whenever a buffer grows.  The old
-// buffer is released with hipFreeAsync on the stream that needs the new one,
-// after that buffer's last user (ctx->scratch_ev for the encode scratch,
-// which async launches on any stream hand over; the flow arenas and the hit
-// buffer are only used inside synchronous calls, so they are idle here).
-static int regrow(void **buf, size_t *have, size_t sz, hipStream_t s, hipEvent_t last_user) {
+// Grow-only device buffers.  hipFree performs an implicit
+// hipDeviceSynchronize, which would stall every stream of the device (the
+// caller's unrelated work included) whenever a buffer grows, so a grown-out
+// buffer is retired instead: it stays allocated until qk_ctx_trim or
+// qk_ctx_destroy.  Growth is geometric (at least 2x), so the retired
+// buffers together stay smaller than the live one.  A retired buffer may
+// still be read by queued work (the encode scratch is handed between
+// streams by ctx->scratch_ev; the flow arenas and the hit buffer are used
+// only inside synchronous calls): nothing waits for that here.
+static int regrow(qk_ctx *ctx, void **buf, size_t *have, size_t sz) {
     if (*buf) {
-        if (last_user) QK_HIP_TRY(hipStreamWaitEvent(s, last_user, 0));
-        QK_HIP_TRY(hipFreeAsync(*buf, s));
+        ctx->retired.push_back(*buf);
+        sz = std::max(sz, 2 * *have);
         *buf = nullptr;
         *have = 0;
     }
-    if (hipMallocAsync(buf, sz, s) != hipSuccess) {
+    if (hipMalloc(buf, sz) != hipSuccess) {
         (void)hipGetLastError();
         *buf = nullptr;
         return QK_E_NOMEM;
@@ -60,24 +62,24 @@ static int regrow(void **buf, size_t *have, size_t sz, hipStream_t s, hipEvent_t
 }
 
 int ensure_scratch(qk_ctx *ctx, size_t bytes, hipStream_t s) {
+    (void)s;
     if (bytes <= ctx->scratch_bytes) return QK_OK;
-    return regrow(&ctx->d_scratch, &ctx->scratch_bytes, std::max(bytes, (size_t)1 << 20), s,
-                  ctx->scratch_ev_valid ? ctx->scratch_ev : nullptr);
+    return regrow(ctx, &ctx->d_scratch, &ctx->scratch_bytes, std::max(bytes, (size_t)1 << 20));
 }
 
 int ensure_flow(qk_ctx *ctx, int which, size_t bytes, hipStream_t s) {
+    (void)s;
     if (bytes <= ctx->flow_bytes[which]) return QK_OK;
     // headroom for growing batches
-    return regrow(&ctx->d_flow[which], &ctx->flow_bytes[which], std::max(bytes + bytes / 8, (size_t)1 << 20), s,
-                  nullptr);
+    return regrow(ctx, &ctx->d_flow[which], &ctx->flow_bytes[which], std::max(bytes + bytes / 8, (size_t)1 << 20));
 }
 
 int ensure_hits(qk_ctx *ctx, size_t cap, hipStream_t s) {
+    (void)s;
     if (cap <= ctx->hits_cap) return QK_OK;
-    size_t bytes = 0;
-    const size_t c = std::max(cap, (size_t)1 << 16);
-    int rc = regrow((void **)&ctx->d_hits, &bytes, c * sizeof(uint64_t), s, nullptr);
-    ctx->hits_cap = rc ? 0 : c;
+    size_t bytes = ctx->hits_cap * sizeof(uint64_t);
+    const int rc = regrow(ctx, (void **)&ctx->d_hits, &bytes, std::max(cap, (size_t)1 << 16) * sizeof(uint64_t));
+    ctx->hits_cap = rc ? 0 : bytes / sizeof(uint64_t);
     return rc;
 }
 
@@ -369,12 +371,11 @@ void qk_ctx_destroy(qk_ctx *ctx) {
         if (ctx->stage_ev[i]) hipEventDestroy(ctx->stage_ev[i]);
     }
     if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
-    // stream-ordered buffers (regrow) go back the same way
-    if (ctx->d_scratch) hipFreeAsync(ctx->d_scratch, ctx->stream);
-    if (ctx->d_hits) hipFreeAsync(ctx->d_hits, ctx->stream);
+    if (ctx->d_scratch) hipFree(ctx->d_scratch);
+    if (ctx->d_hits) hipFree(ctx->d_hits);
     for (void *f : ctx->d_flow)
-        if (f) hipFreeAsync(f, ctx->stream);
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+        if (f) hipFree(f);
+    for (void *r : ctx->retired) hipFree(r);
     if (ctx->d_small) hipFree(ctx->d_small);
     if (ctx->h_small) hipHostFree(ctx->h_small);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -411,6 +412,18 @@ int qk_ctx_kernel_stats(qk_ctx *ctx, double *total_ms, uint64_t *launches) {
     ctx->prof_pending.clear();
     *total_ms = tot;
     *launches = cnt;
+    return rc;
+}
+
+int qk_ctx_trim(qk_ctx *ctx) {
+    if (!ctx) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (ctx->retired.empty()) return QK_OK;
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    int rc = QK_OK;
+    for (void *r : ctx->retired)
+        if (hipFree(r) != hipSuccess) rc = QK_E_HIP;   // synchronises the device
+    ctx->retired.clear();
     return rc;
 }
 

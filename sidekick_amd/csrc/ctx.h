@@ -48,6 +48,10 @@ struct qk_ctx {
     hipEvent_t scratch_ev = nullptr;
     bool scratch_ev_valid = false;
 
+    // grown-out device buffers, freed by qk_ctx_trim / qk_ctx_destroy (hipFree
+    // synchronises the whole device; growth must not)
+    std::vector<void *> retired;
+
     std::mutex mu;
 };
 
@@ -69,8 +73,8 @@ hipStream_t pick_stream(qk_ctx *ctx, void *stream);
 int scratch_acquire(qk_ctx *ctx, hipStream_t s);
 // mark the end of s's use of the scratch buffers
 int scratch_release(qk_ctx *ctx, hipStream_t s);
-// grow-only buffers; growth never synchronises the device (stream-ordered
-// free/alloc on s after the buffer's last user)
+// grow-only buffers; growth never synchronises the device (the old buffer is
+// retired, api.hip regrow)
 int ensure_scratch(qk_ctx *ctx, size_t bytes, hipStream_t s);
 int ensure_hits(qk_ctx *ctx, size_t cap, hipStream_t s);
 int ensure_flow(qk_ctx *ctx, int which, size_t bytes, hipStream_t s);

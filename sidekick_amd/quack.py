@@ -73,6 +73,10 @@ class Context:
     def set_grid(self, blocks: int):
         check(lib().qk_ctx_set_grid(self.handle, int(blocks)))
 
+    def trim(self):
+        """Free grown-out scratch buffers (synchronises the device)."""
+        check(lib().qk_ctx_trim(self.handle), "trim")
+
 
 _ctx_lock = threading.Lock()
 _contexts: dict = {}
