@@ -1,0 +1,373 @@
+// bsgs64.h — baby-step / giant-step u64 encode over p64 = 2^64 - 59 for
+// 41 <= t <= 80 (configs[2] is t = 80).
+//
+// Power 8a + b (a = 0..NA-1, b = 1..8) is S = sum_i A_a(x_i) * B_b(x_i) with
+// babies B_b = x^b and giants A_a = x^(8a) (A_0 = 1): 7 + (NA - 2) modmuls
+// per id instead of t - 1, and (NA - 1) * 8 multiply-accumulates.  A 64x64
+// MAC is four 32x32 v_mad_u64_u32 into two 64-bit column accumulators: with
+// A = a0 + a1 2^32 and the per-baby precomputed Bsh = B * 2^32 mod p,
+//     A * B == B * a0 + Bsh * a1 (mod p)
+//     C0 += B.lo a0 + Bsh.lo a1      (weight 1)
+//     C1 += B.hi a0 + Bsh.hi a1      (weight 2^32)
+// and each mad's carry-out (a wrap of 2^64, i.e. 2^64 == 59 for C0 and 2^96
+// == 59 * 2^32 for C1) is counted: per wave on the scalar unit (only the sum
+// over lanes of a power matters) for the first SG MACs of a wave's tile,
+// per lane with v_addc for the rest.
+//
+// One MAC per power needs all lanes of a wave on the same power, and a wave
+// can hold about 20 powers' accumulators (5 VGPRs + 2 SGPR counters each),
+// so the powers are split over the 4 waves of a workgroup and the babies and
+// giants of an id are computed ONCE and shared through LDS:
+//   step 1  each thread takes one id of the 256-id tile: 7 baby and NA - 2
+//           giant modmuls (exact, hand-scheduled p64 step), Bsh per baby,
+//           and writes (B, Bsh) per baby and A per giant to LDS
+//   step 3  wave w takes babies 2w+1, 2w+2: their a = 0 row (S_b += B_b)
+//           and their MACs with every giant, over all 256 ids of the tile
+//           (4 per lane), reading the operands from LDS
+// LDS: 256 ids x (8 x 16 B + 9 x 8 B) = 50 KB per workgroup, 3 workgroups
+// per CU.  Integer-VALU (+SALU) bound; the ids are read once (8 B each).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bsgs.h"
+#include "field.h"
+
+namespace qk {
+namespace bsgs64 {
+
+constexpr int BLOCK = 256;
+constexpr int WAVES = BLOCK / 64;
+constexpr int NB = 8;
+
+// V <- V * x mod p, V and the result < 2^64 (not necessarily canonical),
+// exact.  V pinned in v[2:3] (the asm addresses its halves):
+//   A = V.lo x0;  B = V.hi x0 + A.hi;  C = V.lo x1 + B (carry cc);
+//   PH = V.hi x1 + C.hi + cc 2^32;  P_L = A.lo + C.lo 2^32          (P = V x)
+//   E = P_L + 59 PH.lo (carry ce);  F = E.hi + ce 2^32 + 59 PH.hi   (t-form)
+//   V' = (F.lo:E.lo) + 59 F.hi; a wrap past 2^64 leaves V' < 59*60, so +59
+// Every VALU-written carry is read >= 2 wait states after its write.
+#define QK_U64_MULV_ASM                                                                            \
+    "v_mov_b32_e32 v11, 0\n\t"                                                                     \
+    "v_mad_u64_u32 v[6:7], %[cx], v2, %[x0], 0\n\t"                                                  \
+    "v_mov_b32_e32 v10, v7\n\t"                                                                    \
+    "v_mad_u64_u32 v[8:9], %[cx], v3, %[x0], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[8:9], %[cc], v2, %[x1], v[8:9]\n\t"                                             \
+    "v_mov_b32_e32 v7, v8\n\t"                                                                     \
+    "v_mov_b32_e32 v10, v9\n\t"                                                                    \
+    "v_cndmask_b32_e64 v11, 0, 1, %[cc]\n\t"                                                         \
+    "v_mad_u64_u32 v[4:5], %[cx], v3, %[x1], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[2:3], %[ce], v4, 59, v[6:7]\n\t"                                                \
+    "v_mov_b32_e32 v8, v3\n\t"                                                                     \
+    "s_nop 0\n\t"                                                                                  \
+    "v_cndmask_b32_e64 v9, 0, 1, %[ce]\n\t"                                                          \
+    "v_mad_u64_u32 v[8:9], %[cx], v5, 59, v[8:9]\n\t"                                                \
+    "v_mov_b32_e32 v3, v8\n\t"                                                                     \
+    "v_mad_u64_u32 v[2:3], %[cw], v9, 59, v[2:3]\n\t"                                                \
+    "s_nop 1\n\t"                                                                                  \
+    "v_cndmask_b32_e64 %[tmp], 0, 59, %[cw]\n\t"                                                     \
+    "v_add_u32_e32 v2, v2, %[tmp]\n\t"
+
+__device__ __forceinline__ void mulv(uint64_t &V, uint32_t x0, uint32_t x1) {
+    uint64_t cw, cx, cc, ce;
+    uint32_t tmp;
+    asm volatile(QK_U64_MULV_ASM
+                 : "+{v[2:3]}"(V), [cw] "=&s"(cw), [cx] "=&s"(cx), [cc] "=&s"(cc), [ce] "=&s"(ce),
+                   [tmp] "=&v"(tmp)
+                 : [x0] "v"(x0), [x1] "v"(x1)
+                 : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11");
+}
+
+// B * 2^32 mod p for B < 2^64: B.lo 2^32 + 59 B.hi (+59 after a wrap, which
+// leaves < 59 2^32: the second mad cannot wrap)
+__device__ __forceinline__ uint64_t shift32(uint64_t B) {
+    uint64_t r, cw, cx;
+    uint32_t f;
+    asm volatile("v_mad_u64_u32 %[r], %[cw], %[bh], 59, %[sh]\n\t"
+                 "s_nop 1\n\t"
+                 "v_cndmask_b32_e64 %[f], 0, 1, %[cw]\n\t"
+                 "v_mad_u64_u32 %[r], %[cx], %[f], 59, %[r]"
+                 : [r] "=&v"(r), [cw] "=&s"(cw), [cx] "=&s"(cx), [f] "=&v"(f)
+                 : [bh] "v"((uint32_t)(B >> 32)), [sh] "v"(B << 32));
+    return r;
+}
+
+// ---- MAC of one power, carries counted ------------------------------------
+// operands: %0 C0, %1 C1 (64-bit), %2 k0, %3 k1 (counters), %4 a0, %5 a1,
+// %6 B.lo, %7 B.hi, %8 Bsh.lo, %9 Bsh.hi
+#define QK_MAC64S(P0, P1, P2, P3, T)                                                                    \
+    "v_mad_u64_u32 %0, " P0 ", %6, %4, %0\n\t"                                                        \
+    "v_mad_u64_u32 %1, " P1 ", %7, %4, %1\n\t"                                                        \
+    "v_mad_u64_u32 %0, " P2 ", %8, %5, %0\n\t"                                                        \
+    "v_mad_u64_u32 %1, " P3 ", %9, %5, %1\n\t"                                                        \
+    "s_bcnt1_i32_b64 " T ", " P0 "\n\ts_add_u32 %2, %2, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P1 "\n\ts_add_u32 %3, %3, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %2, %2, " T "\n\t"                                          \
+    "s_bcnt1_i32_b64 " T ", " P3 "\n\ts_add_u32 %3, %3, " T
+#define QK_MAC64V(P0, P1, P2, P3)                                                                       \
+    "v_mad_u64_u32 %0, " P0 ", %6, %4, %0\n\t"                                                        \
+    "v_mad_u64_u32 %1, " P1 ", %7, %4, %1\n\t"                                                        \
+    "v_mad_u64_u32 %0, " P2 ", %8, %5, %0\n\t"                                                        \
+    "v_mad_u64_u32 %1, " P3 ", %9, %5, %1\n\t"                                                        \
+    "v_addc_co_u32_e64 %2, " P0 ", %2, 0, " P0 "\n\t"                                                 \
+    "v_addc_co_u32_e64 %3, " P1 ", %3, 0, " P1 "\n\t"                                                 \
+    "v_addc_co_u32_e64 %2, " P2 ", %2, 0, " P2 "\n\t"                                                 \
+    "v_addc_co_u32_e64 %3, " P3 ", %3, 0, " P3
+
+// mixed: P0..P2 on the scalar unit, P3 (a C1 carry) per lane into kv —
+// the scalar unit issues one instruction per SIMD every 4 cycles, so a MAC
+// with all four carries scalar (8 SALU) outlasts its 4 mads.  The per-lane
+// v_addc reads P3 after six scalar instructions (>= 2 wait states).
+#define QK_MAC64M(P0, P1, P2, P3, T)                                                                    \
+    "v_mad_u64_u32 %[C0], " P0 ", %[bl], %[a0], %[C0]\n\t"                                             \
+    "v_mad_u64_u32 %[C1], " P1 ", %[bh], %[a0], %[C1]\n\t"                                             \
+    "v_mad_u64_u32 %[C0], " P2 ", %[sl], %[a1], %[C0]\n\t"                                             \
+    "v_mad_u64_u32 %[C1], " P3 ", %[sh], %[a1], %[C1]\n\t"                                             \
+    "s_bcnt1_i32_b64 " T ", " P0 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
+    "s_bcnt1_i32_b64 " T ", " P1 "\n\ts_add_u32 %[k1], %[k1], " T "\n\t"                                \
+    "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
+    "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
+
+template <int SET>
+__device__ __forceinline__ void mac_m(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &k1, uint32_t &kv,
+                                      uint32_t a0, uint32_t a1, uint4 b) {
+    if constexpr (SET == 0)
+        asm volatile(QK_EXPAND(QK_MAC64M, QK_SET0T)
+                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [k1] "+s"(k1), [kv] "+v"(kv)
+                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
+                     : "scc", "s56", QK_CLOB0);
+    else
+        asm volatile(QK_EXPAND(QK_MAC64M, QK_SET1T)
+                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [k1] "+s"(k1), [kv] "+v"(kv)
+                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
+                     : "scc", "s57", QK_CLOB1);
+}
+
+template <int SET>
+__device__ __forceinline__ void mac_s(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &k1, uint32_t a0,
+                                      uint32_t a1, uint4 b) {
+    if constexpr (SET == 0)
+        asm volatile(QK_EXPAND(QK_MAC64S, QK_SET0T)
+                     : "+v"(C0), "+v"(C1), "+s"(k0), "+s"(k1)
+                     : "v"(a0), "v"(a1), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)
+                     : "scc", "s56", QK_CLOB0);
+    else
+        asm volatile(QK_EXPAND(QK_MAC64S, QK_SET1T)
+                     : "+v"(C0), "+v"(C1), "+s"(k0), "+s"(k1)
+                     : "v"(a0), "v"(a1), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)
+                     : "scc", "s57", QK_CLOB1);
+}
+template <int SET>
+__device__ __forceinline__ void mac_v(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &k1, uint32_t a0,
+                                      uint32_t a1, uint4 b) {
+    if constexpr (SET == 0)
+        asm volatile(QK_EXPAND(QK_MAC64V, QK_SET0)
+                     : "+v"(C0), "+v"(C1), "+v"(k0), "+v"(k1)
+                     : "v"(a0), "v"(a1), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)
+                     : QK_CLOB0);
+    else
+        asm volatile(QK_EXPAND(QK_MAC64V, QK_SET1)
+                     : "+v"(C0), "+v"(C1), "+v"(k0), "+v"(k1)
+                     : "v"(a0), "v"(a1), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)
+                     : QK_CLOB1);
+}
+
+// ---- the a = 0 row: S_b += B_b as two 64-bit sums of 32-bit halves --------
+// lo_j += B_j.lo and hi_j += B_j.hi (weight 2^32) with v_mad_u64_u32 (x 1):
+// < 2^32 adds of 32-bit values cannot wrap a 64-bit sum, so no carry is
+// counted; the mads' carry-outs go to a dead SGPR set.
+#define QK_ROW64M(P0, P1, P2, P3)                                                                       \
+    "v_mad_u64_u32 %0, " P0 ", %4, 1, %0\n\t"                                                          \
+    "v_mad_u64_u32 %1, " P1 ", %5, 1, %1\n\t"                                                          \
+    "v_mad_u64_u32 %2, " P2 ", %6, 1, %2\n\t"                                                          \
+    "v_mad_u64_u32 %3, " P3 ", %7, 1, %3"
+template <int SET>
+__device__ __forceinline__ void row2(uint64_t (&lo)[2], uint64_t (&hi)[2], const uint4 (&b)[2]) {
+    if constexpr (SET == 0)
+        asm volatile(QK_EXPAND(QK_ROW64M, QK_SET0)
+                     : "+v"(lo[0]), "+v"(lo[1]), "+v"(hi[0]), "+v"(hi[1])
+                     : "v"(b[0].x), "v"(b[1].x), "v"(b[0].y), "v"(b[1].y)
+                     : QK_CLOB0);
+    else
+        asm volatile(QK_EXPAND(QK_ROW64M, QK_SET1)
+                     : "+v"(lo[0]), "+v"(lo[1]), "+v"(hi[0]), "+v"(hi[1])
+                     : "v"(b[0].x), "v"(b[1].x), "v"(b[0].y), "v"(b[1].y)
+                     : QK_CLOB1);
+}
+
+// (u128 value) mod p, canonical
+__device__ __forceinline__ uint64_t mod_p128(unsigned __int128 v) {
+    // v = H 2^64 + L == 59 H + L; twice brings it below 2^64 + 59^2
+    unsigned __int128 t = (unsigned __int128)(uint64_t)(v >> 64) * C64 + (uint64_t)v;
+    t = (unsigned __int128)(uint64_t)(t >> 64) * C64 + (uint64_t)t;
+    uint64_t r = (uint64_t)t + C64 * (uint64_t)(t >> 64);
+    r = canon64(r);
+    return r >= P64 ? r - P64 : r;
+}
+
+// The workgroup's operands of one tile in LDS, [value][id] so that lanes read
+// consecutive ids: babies (B.lo, B.hi, Bsh.lo, Bsh.hi) and giants (a0, a1).
+template <int NA>
+struct Smem {
+    uint4 bb[NB][BLOCK];
+    uint2 ga[NA - 1][BLOCK];
+};
+
+// The kernel body.  Tiles of 256 consecutive ids, grid-stride over tiles;
+// ids past n feed 0 (every power 0).  T <= 8 * NA.  Wave w owns babies 2w
+// and 2w+1: the a = 0 row of both and their MACs with every giant row, so
+// the four waves do equal work (a wave of a workgroup shares its SIMD with
+// the same wave of the other workgroups: an unbalanced split idles SIMDs at
+// the barriers).
+//   MODE 0  the first SG MACs of a wave's tile count all four carries on the
+//           scalar unit, the rest per lane (v_addc)
+//   MODE 1  every MAC: three carries on the scalar unit, one per lane
+// Writes, per block, partials[(2 m + limb) * gridDim.x + blockIdx.x] for
+// powers m < T (32-bit limbs of canonical lane values summed: < 2^40).
+// ABL (ablations for tools/tune_u64.hip only; the product uses 0): 1 skips
+// the MACs, 2 skips the modmuls (the id itself stands for every power).
+template <int NA, int MODE, int SG, int ABL = 0, int PF = 0>
+__device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
+                                     uint64_t *__restrict__ partials) {
+    static_assert(NA >= 2 && NA <= 10, "giant rows");
+    constexpr int NR = NA - 1;                   // MAC rows (giants x^8 .. x^(8 NR))
+    __shared__ Smem<NA> sm;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cb = 2 * wave;                     // this wave's babies (b = cb+1, cb+2)
+
+    // a = 0 row: 64-bit sums of the halves; MAC tile: C0/C1 + carry counters
+    uint64_t r0lo[2] = {0, 0}, r0hi[2] = {0, 0};
+    uint64_t C0[NR][2], C1[NR][2];
+    uint32_t K0[NR][2], K1[NR][2], KV[NR][2];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) { C0[r][c] = 0; C1[r][c] = 0; K0[r][c] = 0; K1[r][c] = 0; KV[r][c] = 0; }
+
+    const uint64_t ntiles = (n + BLOCK - 1) / BLOCK;
+    uint64_t tile = blockIdx.x;
+    uint64_t nxt = 0;
+    if (tile < ntiles && tile * BLOCK + tid < n) nxt = ids[tile * BLOCK + tid];
+    for (; tile < ntiles; tile += gridDim.x) {
+        // ---- step 1: this thread's id -> babies (+ B * 2^32), giants -> LDS
+        {
+            const uint64_t x = nxt;
+            const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
+            uint64_t V = x;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                if (b && ABL != 2) mulv(V, x0, x1);
+                const uint64_t sh = shift32(V);
+                sm.bb[b][tid] = make_uint4((uint32_t)V, (uint32_t)(V >> 32), (uint32_t)sh, (uint32_t)(sh >> 32));
+            }
+            const uint32_t g0 = (uint32_t)V, g1 = (uint32_t)(V >> 32);   // x^8
+            sm.ga[0][tid] = make_uint2(g0, g1);
+#pragma unroll
+            for (int a = 1; a < NR; ++a) {
+                if (ABL != 2) mulv(V, g0, g1);
+                sm.ga[a][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
+            }
+        }
+        __syncthreads();
+        // next tile's id in flight during step 3
+        const uint64_t tn = tile + gridDim.x;
+        nxt = 0;
+        if (tn < ntiles && tn * BLOCK + tid < n) nxt = ids[tn * BLOCK + tid];
+        // ---- step 3: this wave's 2 x NR MACs over the 256 ids (4 per lane)
+        // PF: the next chunk's operands are read from LDS while this chunk's
+        // MACs run (double-buffered registers, the chunk loop unrolled)
+        uint4 nbv[2];
+        uint2 ng[NR];
+        if constexpr (PF) {
+            nbv[0] = sm.bb[cb][lane];
+            nbv[1] = sm.bb[cb + 1][lane];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) ng[r] = sm.ga[r][lane];
+        }
+#pragma unroll (PF ? BLOCK / 64 : 1)
+        for (int q = 0; q < BLOCK / 64; ++q) {
+            const int j = q * 64 + lane;
+            uint4 bv[2];
+            uint2 g[NR];
+            if constexpr (PF) {
+                bv[0] = nbv[0];
+                bv[1] = nbv[1];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) g[r] = ng[r];
+                if (q + 1 < BLOCK / 64) {
+                    nbv[0] = sm.bb[cb][j + 64];
+                    nbv[1] = sm.bb[cb + 1][j + 64];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) ng[r] = sm.ga[r][j + 64];
+                }
+            } else {
+                bv[0] = sm.bb[cb][j];
+                bv[1] = sm.bb[cb + 1][j];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) g[r] = sm.ga[r][j];
+            }
+            row2<1>(r0lo, r0hi, bv);
+            if (ABL != 1) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int m = r * 2 + c;   // MAC index in the tile: parity picks the SGPR set
+                        if constexpr (MODE == 1) {
+                            if (m % 2 == 0) mac_m<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
+                            else mac_m<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
+                        } else if (m < SG) {
+                            if (m % 2 == 0) mac_s<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], g[r].x, g[r].y, bv[c]);
+                            else mac_s<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], g[r].x, g[r].y, bv[c]);
+                        } else {
+                            if (m % 2 == 0) mac_v<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], g[r].x, g[r].y, bv[c]);
+                            else mac_v<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], g[r].x, g[r].y, bv[c]);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- reduction: canonical lane values, limb sums over lanes, LDS over waves
+    __shared__ unsigned long long red[2 * NB * NA];
+    for (int i = tid; i < 2 * NB * NA; i += BLOCK) red[i] = 0;
+    __syncthreads();
+    auto put = [&](int m, uint64_t v) {   // v canonical; m = power - 1
+        uint64_t lo = (uint32_t)v, hi = v >> 32;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            lo += bsgs::shfl_xor_u64(lo, off);
+            hi += bsgs::shfl_xor_u64(hi, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&red[2 * m], lo);
+            atomicAdd(&red[2 * m + 1], hi);
+        }
+    };
+    const uint64_t W1 = 59ull << 32;   // 2^96 mod p
+#pragma unroll
+    for (int c = 0; c < 2; ++c) put(cb + c, mod_p128((unsigned __int128)r0lo[c] + ((unsigned __int128)r0hi[c] << 32)));
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int m = r * 2 + c;
+            unsigned __int128 v = (unsigned __int128)C0[r][c] + ((unsigned __int128)C1[r][c] << 32);
+            // scalar counts are the wave's totals: added once, by lane 0
+            const bool s0 = MODE == 1 || m < SG, s1 = MODE == 0 && m < SG;
+            const uint32_t k0 = s0 ? (lane == 0 ? K0[r][c] : 0u) : K0[r][c];
+            uint64_t k1 = s1 ? (lane == 0 ? K1[r][c] : 0u) : K1[r][c];
+            if (MODE == 1) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];
+            v += (unsigned __int128)k0 * C64 + (unsigned __int128)k1 * W1;
+            put((r + 1) * NB + cb + c, mod_p128(v));
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < 2 * T; i += BLOCK) partials[(size_t)i * gridDim.x + blockIdx.x] = red[i];
+}
+
+} // namespace bsgs64
+} // namespace qk

@@ -22,6 +22,7 @@
 #include "ctx.h"
 #include "field.h"
 #include "bsgs.h"
+#include "bsgs64.h"
 
 // scalar-counted wrap groups of the t = 25..32 BSGS kernel (tools/tune_bsgs.hip)
 #ifndef QK_BSGS_SG_T32
@@ -460,6 +461,17 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restri
     }
 }
 
+// u64 baby-step / giant-step (bsgs64.h): 256-id tiles, babies and giants
+// shared through LDS, the MAC powers split over the 4 waves.  50 KB of LDS
+// per workgroup: 3 per CU.
+template <int NA, int MODE, int SG>
+__global__ __launch_bounds__(bsgs64::BLOCK, 3) void k_encode_u64_bsgs(const uint64_t *__restrict__ ids, uint64_t n,
+                                                                      uint32_t head, uint32_t T,
+                                                                      uint64_t *__restrict__ partials) {
+    (void)head;
+    bsgs64::body<NA, MODE, SG>(ids, n, T, partials);
+}
+
 // ------------------------------------------------------------- dispatch
 template <typename KernelT>
 static uint32_t grid_for(qk_ctx *ctx, KernelT kern, uint64_t units, uint32_t per_block) {
@@ -654,6 +666,39 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     const uintptr_t a = (uintptr_t)ids;
     if (a & 7) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
+    // baby-step / giant-step for 21 <= T <= 80 (configs[2] is T = 80; below
+    // ~20 powers the 15-odd modmuls of the babies and giants cost more than
+    // the chain they save, tools/bench_configs.py sweep64): NA = ceil(T / 8)
+    // giant rows; its per-wave 32-bit carry totals need < 2^31 ids per
+    // workgroup.  QK_TUNE_BSGS64_SG (T > 72 only) picks a carry mode
+    // for measurements (tools/tune_u64.hip); QK_TUNE_BSGS64_OFF=1 forces the
+    // power chain.
+    static const int sg64 = [] { const char *e = getenv("QK_TUNE_BSGS64_SG"); return e ? atoi(e) : -1; }();
+    static const int no64 = [] { const char *e = getenv("QK_TUNE_BSGS64_OFF"); return e ? atoi(e) : 0; }();
+    const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
+    if (T >= 21 && T <= 80 && !no64 && n / min_grid64 < (1ull << 30)) {
+#define QK_BSGS64(NA_, MODE_, SG_)                                                                    \
+    run_encode<uint64_t>(ctx, k_encode_u64_bsgs<NA_, MODE_, SG_>, k_finalize_u64, 8 * NA_, 2, ids, n, head, T, \
+                         (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
+        switch ((T + 7) / 8) {
+        case 3: return QK_BSGS64(3, 1, 0);
+        case 4: return QK_BSGS64(4, 1, 0);
+        case 5: return QK_BSGS64(5, 1, 0);
+        case 6: return QK_BSGS64(6, 1, 0);
+        case 7: return QK_BSGS64(7, 1, 0);
+        case 8: return QK_BSGS64(8, 1, 0);
+        case 9: return QK_BSGS64(9, 1, 0);
+        default:
+            switch (sg64) {
+            case 0: return QK_BSGS64(10, 0, 0);
+            case 8: return QK_BSGS64(10, 0, 8);
+            case 12: return QK_BSGS64(10, 0, 12);
+            case 18: return QK_BSGS64(10, 0, 18);
+            default: return QK_BSGS64(10, 1, 0);   // 3 scalar + 1 lane carry per MAC (sg64 = -1, the default)
+            }
+        }
+#undef QK_BSGS64
+    }
     int G, K;
     // K <= 40 accumulators per lane (120 VGPRs, 3 waves/SIMD) beat K <= 20 at
     // 5 waves by needing fewer lanes per id (t = 80: 2 x (39 + 1) steps vs

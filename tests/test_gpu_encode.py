@@ -58,7 +58,7 @@ def test_golden_streams(golden):
 
 
 U32_TS = list(range(1, 34)) + [36, 40, 41, 47, 48, 49, 55, 56, 57, 63, 64, 65, 80, 100, 128, 129, 256, 300, 513, 1024]
-U64_TS = [1, 2, 3, 5, 8, 12, 16, 19, 20, 21, 32, 40, 64, 80, 81, 160, 300, 1024]
+U64_TS = [1, 2, 3, 5, 8, 12, 16, 19, 20, 21, 32, 40, 64, 65, 72, 73, 74, 79, 80, 81, 160, 300, 1024]
 
 
 @pytest.mark.parametrize("t", U32_TS)
@@ -70,6 +70,18 @@ def test_u32_threshold_sweep(t):
 @pytest.mark.parametrize("t", U64_TS)
 def test_u64_threshold_sweep(t):
     ids = coracle.splitmix_u64(0xDEF0 + t, 3001)
+    assert gpu_state(ids, t, 64).power_sums() == coracle.encode_u64(ids, t)
+
+
+@pytest.mark.parametrize("t", [80, 73])
+def test_u64_max_ids_carry_storm(t):
+    """ids at the top of the u64 range (2^64-1, p, p+1, ...): the largest
+    products, so the MAC accumulators of the u64 BSGS kernel wrap on almost
+    every multiply-accumulate."""
+    P64 = 18446744073709551557
+    edge = np.array([2**64 - 1, 2**64 - 2, P64 - 1, P64, P64 + 1, 2**63, 2**64 - 60], dtype=np.uint64)
+    ids = np.resize(edge, 100_003)
+    ids[::7] = coracle.splitmix_u64(3, len(ids[::7]))
     assert gpu_state(ids, t, 64).power_sums() == coracle.encode_u64(ids, t)
 
 

@@ -78,3 +78,21 @@ def test_u64_lane_split(kmax):
              ("t64", 50_001, 64, 0), ("t200", 20_001, 200, 1)]
     res = _run({"QK_TUNE_U64_KMAX": str(kmax)}, 64, cases)
     assert all(res.values()), res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sg", [-1, 0, 8, 12, 18])
+def test_u64_bsgs_scalar_carry_macs(sg):
+    """The u64 baby-step/giant-step kernel (bsgs64.h) with the first sg MACs
+    of each wave's tile counting carries on the scalar unit, the rest per
+    lane; t = 73..80 (the last giant row partly or fully used)."""
+    cases = [("t80", 300_001, 80, 1), ("t73", 100_003, 73, 0), ("t77", 4099, 77, 1), ("t79_tiny", 37, 79, 0)]
+    res = _run({"QK_TUNE_BSGS64_SG": str(sg)}, 64, cases)
+    assert all(res.values()), res
+
+
+@pytest.mark.gpu
+def test_u64_bsgs_off_matches_chain():
+    """The power-chain path the u64 BSGS kernel replaced gives the same sums."""
+    res = _run({"QK_TUNE_BSGS64_OFF": "1"}, 64, [("t80", 200_001, 80, 1), ("t75", 3001, 75, 0)])
+    assert all(res.values()), res

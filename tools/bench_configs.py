@@ -283,9 +283,20 @@ def run_sweep(args, ctx):
         emit({"config": f"encode u32 t={t}", "n": n, "ids_per_s": n / kern, "ns_per_id_per_power": kern / n / t * 1e9 * 1})
 
 
+def run_sweep64(args, ctx):
+    n = int(args.nsweep)
+    ids = torch.empty(n, dtype=torch.int64, device=DEV)
+    fill_splitmix(ctx, ids, 0x5EED0003, bits=64)
+    path = "chain" if os.environ.get("QK_TUNE_BSGS64_OFF") == "1" else "default"
+    for t in (8, 9, 16, 17, 24, 32, 40, 48, 56, 64, 72, 80, 81, 128):
+        wall, kern = time_encode(ctx, ids, t, 64, max(3, args.steps // 2))
+        emit({"config": f"encode u64 t={t} ({path})", "n": n, "ids_per_s": n / kern,
+              "ns_per_id_per_power": kern / n / t * 1e9})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "packets", "flows", "micro"])
+    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "sweep64", "packets", "flows", "micro"])
     ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--n64", type=float, default=1e9)
@@ -298,7 +309,7 @@ def main():
     args = ap.parse_args()
     ctx = sk.get_context(0)
     for w in args.what:
-        {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep,
+        {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep, "sweep64": run_sweep64,
          "packets": run_packets, "flows": run_flows, "micro": run_micro}[w](args, ctx)
         torch.cuda.empty_cache()
 
