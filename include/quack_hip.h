@@ -110,6 +110,15 @@ int qk_u64_to_coeffs(const qk_u64 *q, uint64_t *coeffs, uint32_t cap, uint32_t *
 uint32_t qk_u32_eval(const uint32_t *coeffs, uint32_t d, uint32_t x);
 uint64_t qk_u64_eval(const uint64_t *coeffs, uint32_t d, uint64_t x);
 
+/* decode_with_log over a HOST-resident log (the receiver's short logs,
+ * media_client.rs:304-313): to_coeffs, then the root test on the CPU; same
+ * contract as qk_u32_decode_device (hits = log positions ascending, cut at
+ * the first entry equal to diff->last_value when stop_at_last). */
+int qk_u32_decode_host(const qk_u32 *diff, const uint32_t *log, size_t n, int stop_at_last, uint64_t *hits,
+                       size_t cap, size_t *n_hits);
+int qk_u64_decode_host(const qk_u64 *diff, const uint64_t *log, size_t n, int stop_at_last, uint64_t *hits,
+                       size_t cap, size_t *n_hits);
+
 /* bincode 1.3 image of the serde-derived struct
  * {power_sums: Vec<ModularInteger>, last_value: Option<T>, count: u32}
  * (sidekick.rs:187, media_client.rs:227; layout [RECALL]). */

@@ -45,6 +45,7 @@ def lib():
             "qo_root_test_u32": (C.c_uint64, [u32p, C.c_uint32, u32p, C.c_uint64, i64p, C.c_uint64]),
             "qo_root_test_u64": (C.c_uint64, [u64p, C.c_uint32, u64p, C.c_uint64, i64p, C.c_uint64]),
             "qo_bench_construct": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, u64p]),
+            "qo_bench_decode": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -99,6 +100,15 @@ def bench_construct(bits, seed, n, t, trials):
     sink = C.c_uint64()
     ns = lib().qo_bench_construct(bits, seed, n, t, trials, C.byref(sink))
     return ns / max(1, n * trials)
+
+
+def bench_decode(bits, n, d, trials):
+    """Reference-shape CPU decode microbenchmark (benchmark_decode -n N -d D
+    -t D): mean microseconds per subtract + to_coeffs + root test over n,
+    and the hits found."""
+    found = C.c_uint64()
+    ns = lib().qo_bench_decode(bits, n, d, trials, C.byref(found))
+    return ns / max(1, trials) / 1e3, found.value
 
 
 def encode_u64(ids, t):

@@ -243,3 +243,46 @@ uint64_t qo_bench_construct(uint32_t bits, uint64_t seed, uint64_t n, uint32_t t
     free(S);
     return total;
 }
+
+/* CPU port of quack's benchmark_decode (figures/fig2_microbenchmarks.py:
+ * 134-141,175-183; timed region [RECALL]): sender sketch of n ids, receiver
+ * missing d of them (evenly spread), threshold t = d; each trial times
+ * diff = sender - receiver, to_coeffs, and the root test over the n-id log.
+ * Returns the summed timed nanoseconds; *found = hits of the last trial. */
+uint64_t qo_bench_decode(uint32_t bits, uint64_t n, uint32_t d, uint32_t trials, uint64_t *found) {
+    const size_t esz = bits == 32 ? 4 : 8;
+    void *log = malloc(n ? n * esz : 1), *SA = calloc(d, esz), *SB = calloc(d, esz), *S = calloc(d, esz),
+         *c = calloc(d, esz);
+    int64_t *hits = malloc((n + 1) * sizeof(int64_t));
+    if (!log || !SA || !SB || !S || !c || !hits || d == 0) return 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t v = qo_mix(0xDEC0DEull + (i + 1) * QO_GAMMA);
+        const int dropped = (i * d) % n < d;
+        if (bits == 32) {
+            ((uint32_t *)log)[i] = (uint32_t)(v >> 32);
+            insert32((uint32_t *)SA, d, (uint32_t)(v >> 32));
+            if (!dropped) insert32((uint32_t *)SB, d, (uint32_t)(v >> 32));
+        } else {
+            ((uint64_t *)log)[i] = v;
+            insert64((uint64_t *)SA, d, v);
+            if (!dropped) insert64((uint64_t *)SB, d, v);
+        }
+    }
+    uint64_t total = 0, nh = 0;
+    for (uint32_t r = 0; r < trials; ++r) {
+        const uint64_t t0 = qo_now_ns();
+        if (bits == 32) {
+            for (uint32_t k = 0; k < d; ++k) ((uint32_t *)S)[k] = sub32(((uint32_t *)SA)[k], ((uint32_t *)SB)[k]);
+            qo_to_coeffs_u32((const uint32_t *)S, d, (uint32_t *)c);
+            nh = qo_root_test_u32((const uint32_t *)c, d, (const uint32_t *)log, n, hits, n + 1);
+        } else {
+            for (uint32_t k = 0; k < d; ++k) ((uint64_t *)S)[k] = sub64(((uint64_t *)SA)[k], ((uint64_t *)SB)[k]);
+            qo_to_coeffs_u64((const uint64_t *)S, d, (uint64_t *)c);
+            nh = qo_root_test_u64((const uint64_t *)c, d, (const uint64_t *)log, n, hits, n + 1);
+        }
+        total += qo_now_ns() - t0;
+    }
+    if (found) *found = nh;
+    free(log); free(SA); free(SB); free(S); free(c); free(hits);
+    return total;
+}

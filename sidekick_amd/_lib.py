@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libquack_hip.so")
+# QK_LIB_PATH selects another build of the same library: the host-sanitized
+# libquack_hip_asan.so in tests/test_sanitizers.py
+LIB_PATH = os.environ.get("QK_LIB_PATH") or os.path.join(HERE, "libquack_hip.so")
 
 QK_OK = 0
 QK_E_INVAL = -1
@@ -56,6 +58,8 @@ SIGNATURES = {
     "qk_u64_to_coeffs": (C.c_int, [vp, u64p, C.c_uint32, u32p]),
     "qk_u32_eval": (C.c_uint32, [u32p, C.c_uint32, C.c_uint32]),
     "qk_u64_eval": (C.c_uint64, [u64p, C.c_uint32, C.c_uint64]),
+    "qk_u32_decode_host": (C.c_int, [vp, u32p, sz, C.c_int, u64p, sz, szp]),
+    "qk_u64_decode_host": (C.c_int, [vp, u64p, sz, C.c_int, u64p, sz, szp]),
     "qk_u32_serialized_size": (sz, [vp]),
     "qk_u32_serialize": (C.c_int, [vp, u8p, sz, szp]),
     "qk_u32_deserialize": (C.c_int, [u8p, sz, vp, u32p]),

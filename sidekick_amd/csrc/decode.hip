@@ -13,6 +13,7 @@
 // atomic ticket; the host sorts them into log order.  The `break` at the
 // first log entry equal to diff.last_value() becomes an atomicMin of that
 // position; the host drops hits at or after it.
+#include "bsgs64.h"
 #include "ctx.h"
 #include "field.h"
 
@@ -110,9 +111,30 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_test_u32(const uint32_t *__re
 }
 
 // ------------------------------------------------------------------ u64
+// Horner r <- r*x + c_i with the hand-scheduled p64 step (bsgs64.h: 7
+// mads, exact, result < 2^64) followed by a 64-bit add of c_i: a wrap past
+// 2^64 leaves < c_i < p - 59, so the +59 cannot wrap again.  r pinned in
+// v[2:3] like the step; c_i in VGPRs (gfx950 VALU reads at most one SGPR).
+__device__ __forceinline__ void horner64_step(uint64_t &V, uint32_t x0, uint32_t x1, uint64_t c) {
+    uint64_t cw, cx, cc, ce, cy;
+    uint32_t tmp;
+    asm volatile(QK_U64_MULV_ASM
+                 "v_add_co_u32_e64 v2, %[cy], v2, %[c0]\n\t"
+                 "s_nop 1\n\t"
+                 "v_addc_co_u32_e64 v3, %[cy], v3, %[c1], %[cy]\n\t"
+                 "s_nop 1\n\t"
+                 "v_cndmask_b32_e64 v11, 0, 1, %[cy]\n\t"
+                 "v_mad_u64_u32 v[2:3], %[cx], v11, 59, v[2:3]"
+                 : "+{v[2:3]}"(V), [cw] "=&s"(cw), [cx] "=&s"(cx), [cc] "=&s"(cc), [ce] "=&s"(ce), [cy] "=&s"(cy),
+                   [tmp] "=&v"(tmp)
+                 : [x0] "v"(x0), [x1] "v"(x1), [c0] "v"((uint32_t)c), [c1] "v"((uint32_t)(c >> 32))
+                 : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11");
+}
+
 __device__ __forceinline__ bool is_root64(uint64_t x, const uint64_t *__restrict__ c, uint32_t d) {
-    uint64_t r = mad64_lazy(1ull, x, c[0]);
-    for (uint32_t i = 1; i < d; ++i) r = mad64_lazy(r, x, c[i]);
+    const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
+    uint64_t r = 1;
+    for (uint32_t i = 0; i < d; ++i) horner64_step(r, x0, x1, c[i]);
     return canon64(r) == 0;
 }
 
@@ -128,14 +150,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_test_u64(const uint64_t *__re
     const ulonglong2 *__restrict__ v = reinterpret_cast<const ulonglong2 *>(log + h);
     for (uint64_t i = gtid; i < body; i += nthr) {
         const ulonglong2 w = v[i];
-        uint64_t r0 = mad64_lazy(1ull, w.x, c[0]), r1 = mad64_lazy(1ull, w.y, c[0]);
-#pragma unroll 2
-        for (uint32_t k = 1; k < d; ++k) {
-            const uint64_t ck = c[k];
-            r0 = mad64_lazy(r0, w.x, ck);
-            r1 = mad64_lazy(r1, w.y, ck);
-        }
-        const bool h0 = canon64(r0) == 0, h1 = canon64(r1) == 0;
+        const bool h0 = is_root64(w.x, c, d), h1 = is_root64(w.y, c, d);
         const bool s0 = use_stop && w.x == stop_value, s1 = use_stop && w.y == stop_value;
         if (h0 | h1 | s0 | s1) {
             rt_record(h + 2 * i, h0, s0, hits, cap, counters);

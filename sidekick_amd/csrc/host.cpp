@@ -259,6 +259,59 @@ uint64_t qk_u64_eval(const uint64_t *c, uint32_t d, uint64_t id) {
     return add64(r, c[d - 1]);
 }
 
+// ------------------------------------------------------------- host decode
+// decode_with_log over a host-resident log (media_client.rs:304-313 for the
+// short logs a receiver holds between quACKs: a kernel launch costs more
+// than the whole test).  Same arithmetic forms as the device root test:
+// t-form Horner r <- r*x + c_i for u32 (field.h tstep32), lazy 64-bit mads
+// for u64; a root iff the canonical value is 0.
+} // extern "C"
+namespace {
+template <typename Q, typename T, typename ToCoeffs, typename IsRoot>
+int decode_host_impl(const Q *diff, const T *log, size_t n, int stop_at_last, uint64_t *hits, size_t cap,
+                     size_t *n_hits, ToCoeffs to_coeffs, IsRoot is_root) {
+    if (!diff || !n_hits || (n && !log)) return QK_E_INVAL;
+    *n_hits = 0;
+    if (diff->count == 0) return QK_OK;
+    std::vector<T> c(diff->threshold ? diff->threshold : 1);
+    uint32_t d = 0;
+    if (int rc = to_coeffs(diff, c.data(), (uint32_t)c.size(), &d)) return rc;
+    const bool stop = stop_at_last && diff->has_last;
+    size_t m = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (stop && log[i] == (T)diff->last_value) break;   // media_client.rs:307-309
+        if (is_root(c.data(), d, log[i])) {
+            if (m < cap && hits) hits[m] = i;
+            ++m;
+        }
+    }
+    *n_hits = m;
+    return m > cap || (m && !hits) ? QK_E_CAPACITY : QK_OK;
+}
+
+bool root32(const uint32_t *c, uint32_t d, uint32_t id) {
+    const uint32_t x = canon32(id), x5 = times5_32(x);
+    uint32_t lo = 1, hi = 0;
+    for (uint32_t i = 0; i < d; ++i) tstep32(lo, hi, x, x5, c[i]);
+    return canon32(fold64_32(((uint64_t)hi << 32) | lo)) == 0;
+}
+bool root64(const uint64_t *c, uint32_t d, uint64_t id) {
+    uint64_t r = 1;
+    for (uint32_t i = 0; i < d; ++i) r = mad64_lazy(r, id, c[i]);
+    return canon64(r) == 0;
+}
+} // namespace
+extern "C" {
+
+int qk_u32_decode_host(const qk_u32 *diff, const uint32_t *log, size_t n, int stop_at_last, uint64_t *hits,
+                       size_t cap, size_t *n_hits) {
+    return decode_host_impl(diff, log, n, stop_at_last, hits, cap, n_hits, qk_u32_to_coeffs, root32);
+}
+int qk_u64_decode_host(const qk_u64 *diff, const uint64_t *log, size_t n, int stop_at_last, uint64_t *hits,
+                       size_t cap, size_t *n_hits) {
+    return decode_host_impl(diff, log, n, stop_at_last, hits, cap, n_hits, qk_u64_to_coeffs, root64);
+}
+
 // ------------------------------------------------------------- bincode
 // bincode 1.3 default options: little-endian fixed-width ints, u64 length
 // prefix for Vec, u8 tag for Option.  Field order as declared in the

@@ -342,6 +342,24 @@ class _PowerSumQuack:
             check(rc, "root_test_device")
             return [int(h) for h in hits[: nh.value]], int(stop_idx.value)
 
+    def decode_host(self, log, stop_at_last: bool = False) -> list:
+        """Positions of the missing entries of a HOST log (numpy / sequence),
+        tested on the CPU (qk_*_decode_host): to_coeffs, then the root test,
+        cut at the first entry equal to last_value() when stop_at_last
+        (media_client.rs:304-313).  For the short logs a receiver holds."""
+        arr = _host_array(log, self.BITS)
+        ptr = arr.ctypes.data_as(C.POINTER(self._ELEM))
+        cap = max(self._t, 1)
+        while True:
+            hits = (C.c_uint64 * cap)()
+            nh = C.c_size_t()
+            rc = self._f("decode_host")(self._buf, ptr, arr.size, int(stop_at_last), hits, cap, C.byref(nh))
+            if rc == QK_E_CAPACITY:
+                cap = nh.value
+                continue
+            check(rc, "decode_host")
+            return [int(h) for h in hits[: nh.value]]
+
     def decode_with_log(self, log, ctx: Context | None = None) -> list:
         """quack's decode_with_log: the ids of `log` that are missing (every
         log entry congruent to a root, in log order)."""

@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .quack import PowerSumQuackU32, arithmetic
+from .quack import PowerSumQuackU32
 
 BATCH_MIN = 4096  # log entries from which the batch (GPU) paths are used
 
@@ -62,13 +62,10 @@ class QuackReceiver:
             log = np.fromiter((i for _, i in self.seqno_ids), dtype=np.uint32, count=len(self.seqno_ids))
             pos = diff.root_test(coeffs, log, stop_value=stop)
             return [self.seqno_ids[p] for p in pos]
-        out = []
-        for seqno, ident in self.seqno_ids:
-            if stop is not None and ident == stop:
-                break
-            if arithmetic.eval(coeffs, ident).value() == 0:
-                out.append((seqno, ident))
-        return out
+        # short log: the same loop (stop at last_value, eval == 0) on the CPU
+        # in one native call (qk_u32_decode_host)
+        log = np.fromiter((i for _, i in self.seqno_ids), dtype=np.uint32, count=len(self.seqno_ids))
+        return [self.seqno_ids[p] for p in diff.decode_host(log, stop_at_last=True)]
 
     def on_quack(self, quack: PowerSumQuackU32, now: float) -> QuackAction:
         act = QuackAction()

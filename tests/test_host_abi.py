@@ -188,3 +188,31 @@ def test_merge_partial_roundtrip():
         m = Q(bits, 9)
         merge_partial(m, s, True, ids[-1])
         assert m == whole
+
+
+@pytest.mark.parametrize("bits,d,stop", [(32, 5, False), (32, 32, True), (64, 20, True), (64, 1, False)])
+def test_decode_host_matches_oracle(bits, d, stop):
+    """qk_*_decode_host (the receiver's short-log path) vs the oracle's root
+    test: every entry congruent to a dropped id, in log order, cut at the
+    first entry equal to last_value when stopping."""
+    import numpy as np
+    from oracle import quack_oracle as qo
+    rng = np.random.default_rng(d + bits)
+    n = 3000
+    log = (qo.ids_u32 if bits == 32 else qo.ids_u64)(0xD0 + d, n, 0)
+    log[rng.choice(n, 4, replace=False)] = log[rng.choice(n, 4, replace=False)]   # duplicates
+    drops = sorted(rng.choice(n, d, replace=False).tolist())
+    Q = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+    diff = Q(32)
+    for i in drops:
+        diff.insert(int(log[i]))
+    got = diff.decode_host(log, stop_at_last=stop)
+    want = qo.root_test_indices(diff.to_coeffs(), log.tolist(), qo.MOD[bits],
+                                stop_value=diff.last_value() if stop else None)
+    assert got == want and len(got) >= (1 if stop else d)
+    assert Q(8).decode_host(log) == []                     # empty difference: nothing missing
+    big = Q(2)
+    for v in log[:3]:
+        big.insert(int(v))
+    with pytest.raises(sk.UndecodableError):
+        big.decode_host(log)
