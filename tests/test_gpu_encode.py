@@ -229,17 +229,26 @@ def test_full_size_1e9_properties():
 
 
 def test_full_size_u64_properties():
-    """configs[2] size class: u64 ids at t = 80 (2.5e8 ids, 2 GB) — additivity
-    and oracle agreement on a prefix."""
-    n, t, seed = 250_000_000, 80, 0x5EED0003
+    """configs[2] at full size: 1e9 u64 ids at t = 80 (8 GB).  Additivity over
+    uneven pieces, grid-shape independence, exact count / last_value, and
+    oracle agreement on a prefix of the same stream."""
+    n, t, seed = 1_000_000_000, 80, 0x5EED0003
     ctx = sk.get_context(0)
     d = torch.empty(n, dtype=torch.int64, device=DEV)
     fill_splitmix(ctx, d, seed, bits=64)
     whole = gpu_state(d, t, 64)
+    assert whole.count() == n
+    assert whole.last_value() == int(coracle.splitmix_u64(seed, 1, start=n - 1)[0])
     pieces = sk.PowerSumQuackU64(t)
-    for a, b in ((0, 77_777_777), (77_777_777, n)):
+    for a, b in ((0, 77_777_777), (77_777_777, 77_777_778), (77_777_778, 999_999_999), (999_999_999, n)):
         pieces.insert_batch(d[a:b])
     assert pieces == whole
+    c2 = sk.Context(0)
+    try:
+        c2.set_grid(1000)
+        assert gpu_state(d, t, 64, ctx=c2) == whole
+    finally:
+        c2.close()
     assert gpu_state(d[:200_000], t, 64).power_sums() == coracle.encode_u64_seed(seed, 200_000, t)
     del d
     torch.cuda.empty_cache()

@@ -75,10 +75,11 @@ def run_u64(args, ctx):
               "parity_with_gpu": q.power_sums() == S})
 
 
-def run_decode(args, ctx):
-    n, t, seed = int(args.ndec), 32, 0x5EED0005
-    log = torch.empty(n, dtype=torch.int32, device=DEV)
-    fill_splitmix(ctx, log, seed)
+def run_decode(args, ctx, bits=32):
+    n, t, seed = int(args.ndec), 32, 0x5EED0005 + (bits == 64)
+    log = torch.empty(n, dtype=torch.int32 if bits == 32 else torch.int64, device=DEV)
+    fill_splitmix(ctx, log, seed, bits=bits)
+    cls = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
     rng = np.random.default_rng(seed)
     drops = np.sort(rng.choice(n, size=32, replace=False))
     keep = torch.ones(n, dtype=torch.bool, device=DEV)
@@ -89,7 +90,7 @@ def run_decode(args, ctx):
     reps = []
     for r in range(args.steps + 1):
         t0 = time.perf_counter()
-        sent, recv = sk.PowerSumQuackU32(t), sk.PowerSumQuackU32(t)
+        sent, recv = cls(t), cls(t)
         sent.insert_batch(log)
         recv.insert_batch(kept)
         diff = sent.clone()
@@ -106,18 +107,29 @@ def run_decode(args, ctx):
             reps.append((t1 - t0, t2 - t1, t3 - t2, ms / 1e3))
     a = np.median(np.array(reps), axis=0)
     ok = set(drops.tolist()) <= set(hits)
-    emit({"config": "decode-missing u32 n=1e8 d=32 (configs[4])", "n": n, "hits": len(hits), "drops_recovered": ok,
+    b = bits // 8
+    emit({"config": f"decode-missing u{bits} n=1e8 d=32" + (" (configs[4])" if bits == 32 else ""), "n": n,
+          "hits": len(hits), "drops_recovered": ok,
           "encode_both_s": a[0], "to_coeffs_s": a[1], "root_test_wall_s": a[2], "root_test_kernel_s": a[3],
-          "root_test_candidates_per_s": n / a[3], "total_s": a[0] + a[1] + a[2]})
+          "root_test_candidates_per_s": n / a[3], "root_test_GBps": b * n / a[3] / 1e9,
+          "frac_hbm_8TBs": b * n / a[3] / 8e12, "total_s": a[0] + a[1] + a[2]})
     if args.cpu:
         from oracle import coracle
         m = int(args.cpu_sample_dec)
-        h = log[:m].cpu().numpy().view(np.uint32)
+        h = log[:m].cpu().numpy().view(np.uint32 if bits == 32 else np.uint64)
         tc = time.perf_counter()
-        w, nh = coracle.root_test_u32(list(c), h)
+        if bits == 32:
+            w, nh = coracle.root_test_u32(list(c), h)
+        else:
+            w, nh = coracle.root_test_u64(list(c), h)
         cs = time.perf_counter() - tc
-        emit({"config": "cpu baseline root test d=32 (oracle C, 1 core)", "n": m, "candidates_per_s": m / cs,
-              "extrapolated_1e8_s": cs * n / m, "hits_match_gpu_prefix": w.tolist() == [x for x in hits if x < m]})
+        emit({"config": f"cpu baseline root test u{bits} d=32 (oracle C, 1 core)", "n": m,
+              "candidates_per_s": m / cs, "extrapolated_1e8_s": cs * n / m,
+              "hits_match_gpu_prefix": w.tolist() == [x for x in hits if x < m]})
+
+
+def run_decode64(args, ctx):
+    run_decode(args, ctx, bits=64)
 
 
 def run_host(args, ctx):
@@ -296,7 +308,7 @@ def run_sweep64(args, ctx):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["u64", "decode", "host", "sweep", "sweep64", "packets", "flows", "micro"])
+    ap.add_argument("what", nargs="+", choices=["u64", "decode", "decode64", "host", "sweep", "sweep64", "packets", "flows", "micro"])
     ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--n64", type=float, default=1e9)
@@ -309,7 +321,7 @@ def main():
     args = ap.parse_args()
     ctx = sk.get_context(0)
     for w in args.what:
-        {"u64": run_u64, "decode": run_decode, "host": run_host, "sweep": run_sweep, "sweep64": run_sweep64,
+        {"u64": run_u64, "decode": run_decode, "decode64": run_decode64, "host": run_host, "sweep": run_sweep, "sweep64": run_sweep64,
          "packets": run_packets, "flows": run_flows, "micro": run_micro}[w](args, ctx)
         torch.cuda.empty_cache()
 

@@ -24,7 +24,7 @@ for s in $STEPS; do
     ubdep) step ubdep 300 ./tools/ubench_dep || exit 3 ;;
     ubissue) step ubissue 300 ./tools/ubench_issue || exit 3 ;;
     smoke) step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
-    pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
+    pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
     sgsweep)
       for g in ${SG_LIST:-0 2 4 6 8}; do
@@ -51,6 +51,14 @@ for s in $STEPS; do
         QK_TUNE_BSGS_SG=$g step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
         QK_TUNE_BSGS_SG=$g step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
       done ;;
+    profcfg)  # kernel stats for the secondary configs' kernels (u64 encode, u32/u64 root test)
+      export TMPDIR=/tmp
+      step profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profcfg" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFCFG_ARGS:-u64 decode decode64} --steps 10 || exit 3 ;;
+    pmccfg)  # FETCH_SIZE and SQ passes over the same configs, one counter group per run
+      export TMPDIR=/tmp
+      step pmccfg_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmccfg_fetch" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFCFG_ARGS:-u64 decode decode64} --steps 2 || exit 3
+      step pmccfg_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmccfg_sq" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFCFG_ARGS:-u64 decode decode64} --steps 2 || exit 3 ;;
+    decshape) step decshape 600 python3 -u tools/bench_decode.py ${DECSHAPE_ARGS:-} || exit 3 ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
