@@ -242,7 +242,10 @@ typedef struct qk_flow_key {
  * only the inserts after the batch's last reset, stats.discarded counts the
  * inserts before it, stats.last_reset_index is its position, and a caller
  * with stats.resets > 0 must clear its own table before merging the output.
- * cap < flows -> QK_E_CAPACITY with *n_flows set. */
+ * cap < flows -> QK_E_CAPACITY with *n_flows set.  keys and sketches may
+ * both be host memory (two D2H copies at the end) or both device memory of
+ * ctx's GPU (written in place by the finalize kernel: nothing crosses PCIe;
+ * the caller synchronises `stream` before reading them); mixed -> QK_E_INVAL. */
 int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
                                const qk_pkt_meta *d_meta, const uint8_t my_addr[6], uint32_t threshold,
                                qk_flow_key *keys, uint8_t *sketches, size_t cap, size_t *n_flows,

@@ -779,6 +779,10 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         *n_flows = nf;
         if (nf > cap || (nf && (!keys || !sketches))) rc = QK_E_CAPACITY;
     }
+    // output in device memory (both arrays): k_flow_finalize writes it in
+    // place and nothing crosses PCIe; host memory gets two copies
+    const bool dev_out = keys && sketches && is_device_ptr(keys);
+    if (!rc && keys && sketches && dev_out != is_device_ptr(sketches)) rc = QK_E_INVAL;
     if (!rc && nf) {
         // per-flow arena 1: info, acc, work items (at most one per flow plus
         // one per SEG_CHUNK ids), output records and keys, offsets, and the
@@ -793,8 +797,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             info = c.take<uint64_t>((size_t)nf * 4);
             acc = c.take<unsigned long long>((size_t)nf * T);
             d_items = c.take<SegItem>(items_max);
-            d_rec = (uint32_t *)c.take<uint8_t>((size_t)nf * rec);
-            d_keys = c.take<uint8_t>((size_t)nf * 12);
+            d_rec = dev_out ? (uint32_t *)sketches : (uint32_t *)c.take<uint8_t>((size_t)nf * rec);
+            d_keys = dev_out ? (uint8_t *)keys : c.take<uint8_t>((size_t)nf * 12);
             d_offs = c.take<uint64_t>((size_t)nf + 1);
             kd = c.take<uint64_t>(nf); kd2 = c.take<uint64_t>(nf); ks = c.take<uint64_t>(nf); ks2 = c.take<uint64_t>(nf);
             used = c.take<uint32_t>(nf); sl2 = c.take<uint32_t>(nf); sl3 = c.take<uint32_t>(nf);
@@ -872,9 +876,10 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                                                              (uint64_t)ctx->num_cus * 16);
             hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info,
                                by_slot ? (const uint32_t *)perm : nullptr, (uint64_t)nf, T, d_rec, d_keys);
-            if (hipGetLastError() != hipSuccess ||
-                hipMemcpyAsync(sketches, d_rec, (size_t)nf * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipMemcpyAsync(keys, d_keys, (size_t)nf * 12, hipMemcpyDeviceToHost, s) != hipSuccess)
+            if (hipGetLastError() != hipSuccess)
+                rc = QK_E_HIP;
+            else if (!dev_out && (hipMemcpyAsync(sketches, d_rec, (size_t)nf * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                                  hipMemcpyAsync(keys, d_keys, (size_t)nf * 12, hipMemcpyDeviceToHost, s) != hipSuccess))
                 rc = QK_E_HIP;
         }
     }

@@ -455,6 +455,60 @@ def encode_segments(ids, offsets, threshold: int, ctx: Context | None = None) ->
     return res
 
 
+def encode_flows(bufs, threshold: int, stride: int = 67, meta=None, my_addr=None, ctx: Context | None = None,
+                 device_out: bool = False):
+    """One SidekickMulti batch (sidekick_multi.rs:65-90,101-143) without the
+    table merge: returns (keys, sketches, stats) for the batch's flows in
+    ascending AddrKey order.  device_out=False: keys is a list of 12-byte
+    AddrKeys and sketches a list of PowerSumQuackU32.  device_out=True: both
+    stay in HBM as CUDA tensors (uint8 [nf, 12] and int32 [nf, 4 + t], the
+    qk_u32 records), written in place by the finalize kernel."""
+    import torch
+    if not (isinstance(bufs, torch.Tensor) and bufs.is_cuda and bufs.dtype == torch.uint8 and bufs.is_contiguous()):
+        raise TypeError("bufs must be a contiguous CUDA uint8 tensor")
+    n = bufs.numel() // stride
+    dev = bufs.device.index if bufs.device.index is not None else torch.cuda.current_device()
+    ctx = ctx or get_context(dev)
+    mptr = None
+    if meta is not None:
+        if not (meta.is_cuda and meta.is_contiguous() and meta.numel() * meta.element_size() == 8 * n):
+            raise ValueError("meta must be a contiguous CUDA tensor of n 8-byte records")
+        mptr = meta.data_ptr()
+    addr = (C.c_uint8 * 6)(*my_addr) if my_addr is not None else None
+    rec = lib().qk_u32_size(threshold)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    cap = 1024
+    while True:
+        nf, st = C.c_size_t(), PktStats()
+        if device_out:
+            keys = torch.empty((cap, 12), dtype=torch.uint8, device=bufs.device)
+            sk = torch.empty((cap, rec // 4), dtype=torch.int32, device=bufs.device)
+            kp, sp = keys.data_ptr(), sk.data_ptr()
+        else:
+            keys = (FlowKey * cap)()
+            sk = C.create_string_buffer(cap * rec)
+            kp, sp = keys, sk
+        rc = lib().qk_u32_encode_flows_device(ctx.handle, bufs.data_ptr(), n, stride, mptr, addr, threshold, kp, sp,
+                                              cap, C.byref(nf), C.byref(st), stream)
+        if rc == QK_E_CAPACITY:
+            cap = nf.value
+            continue
+        check(rc, "encode_flows")
+        break
+    stats = {k: getattr(st, k) for k, _ in PktStats._fields_}
+    m = nf.value
+    if device_out:
+        return keys[:m], sk[:m], stats
+    out_k, out_q = [], []
+    for i in range(m):
+        out_k.append(bytes(keys[i].addr))
+        q = PowerSumQuackU32.__new__(PowerSumQuackU32)
+        q._t = threshold
+        q._buf = C.create_string_buffer(sk.raw[i * rec:(i + 1) * rec], rec)
+        out_q.append(q)
+    return out_k, out_q, stats
+
+
 class FlowQuacks:
     """SidekickMulti's flow table, HashMap<AddrKey, PowerSumQuackU32>
     (sidekick_multi.rs:22-37,57-90), with a GPU batch entry point.
@@ -489,48 +543,18 @@ class FlowQuacks:
     def insert_packets(self, bufs, stride: int = 67, meta=None, my_addr=None, ctx: Context | None = None) -> dict:
         """Batch of captured records (CUDA uint8 tensor) through the GPU:
         extract, group by AddrKey, encode per flow, merge into the table."""
-        import torch
-        if not (isinstance(bufs, torch.Tensor) and bufs.is_cuda and bufs.dtype == torch.uint8 and bufs.is_contiguous()):
-            raise TypeError("bufs must be a contiguous CUDA uint8 tensor")
-        n = bufs.numel() // stride
-        dev = bufs.device.index if bufs.device.index is not None else torch.cuda.current_device()
-        ctx = ctx or get_context(dev)
-        mptr = None
-        if meta is not None:
-            if not (meta.is_cuda and meta.is_contiguous() and meta.numel() * meta.element_size() == 8 * n):
-                raise ValueError("meta must be a contiguous CUDA tensor of n 8-byte records")
-            mptr = meta.data_ptr()
-        addr = (C.c_uint8 * 6)(*my_addr) if my_addr is not None else None
-        rec = lib().qk_u32_size(self.threshold)
-        cap = 1024
-        while True:
-            keys = (FlowKey * cap)()
-            sk = C.create_string_buffer(cap * rec)
-            nf = C.c_size_t()
-            st = PktStats()
-            rc = lib().qk_u32_encode_flows_device(ctx.handle, bufs.data_ptr(), n, stride, mptr, addr, self.threshold,
-                                                  keys, sk, cap, C.byref(nf), C.byref(st),
-                                                  torch.cuda.current_stream(dev).cuda_stream)
-            if rc == QK_E_CAPACITY:
-                cap = nf.value
-                continue
-            check(rc, "encode_flows")
-            break
-        if st.resets:
+        keys, quacks, stats = encode_flows(bufs, self.threshold, stride, meta, my_addr, ctx)
+        if stats["resets"]:
             # a Reset wipes every flow (`senders = HashMap::new()`,
             # sidekick_multi.rs:205,265); the batch output is what follows it
             self._senders = {}
-        for i in range(nf.value):
-            key = bytes(keys[i].addr)
-            q = PowerSumQuackU32.__new__(PowerSumQuackU32)
-            q._t = self.threshold
-            q._buf = C.create_string_buffer(sk.raw[i * rec:(i + 1) * rec], rec)
+        for key, q in zip(keys, quacks):
             old = self._senders.get(key)
             if old is None:
                 self._senders[key] = q
             else:
                 old.merge(q)
-        return {k: getattr(st, k) for k, _ in PktStats._fields_}
+        return stats
 
 
 def partial_words(threshold: int, bits: int = 32) -> int:

@@ -262,3 +262,36 @@ def test_gpu_flows_reset_wipes_table(where):
         assert g.power_sums() == q.power_sums and g.count() == q.count and g.last_value() == q.last_value
     if where == "last":
         assert table.senders() == {}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nflows", [16, 10_000])
+def test_gpu_flows_device_resident_output(nflows):
+    """keys/sketches in HBM (written in place by the finalize kernel) are the
+    same records as the host-output path, against the literal loop; mixed
+    host/device output pointers are rejected."""
+    import ctypes as C
+    import torch
+    from sidekick_amd._lib import lib
+    from sidekick_amd.quack import encode_flows, get_context
+    bufs, meta = make_flows(150_000, nflows, seed=nflows, p_reset=0.01)
+    want, nres, _ = vector_flows(bufs, meta)
+    d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
+    d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
+    hk, hq, hst = encode_flows(d_bufs, 32, meta=d_meta, my_addr=MY_ADDR)
+    dk, dq, dst = encode_flows(d_bufs, 32, meta=d_meta, my_addr=MY_ADDR, device_out=True)
+    torch.cuda.synchronize()
+    assert hst == dst and dst["resets"] == nres
+    assert hk == sorted(want) and [bytes(r) for r in dk.cpu().numpy()] == hk
+    recs = dq.cpu().numpy().view(np.uint32)
+    for i, (k, q) in enumerate(zip(hk, hq)):
+        assert bytes(q._buf.raw) == recs[i].tobytes(), k.hex()
+        assert q.power_sums() == coracle.encode_u32(np.array(want[k], dtype=np.uint32), 32)
+    # mixed output memory kinds -> QK_E_INVAL
+    keys = torch.empty((len(hk), 12), dtype=torch.uint8, device="cuda")
+    host_sk = C.create_string_buffer(len(hk) * lib().qk_u32_size(32))
+    nf = C.c_size_t()
+    rc = lib().qk_u32_encode_flows_device(get_context(0).handle, d_bufs.data_ptr(), bufs.shape[0], 67,
+                                          d_meta.data_ptr(), (C.c_uint8 * 6)(*MY_ADDR), 32, keys.data_ptr(), host_sk,
+                                          len(hk), C.byref(nf), None, None)
+    assert rc == -1

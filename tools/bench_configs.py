@@ -210,24 +210,28 @@ def run_flows(args, ctx):
         rec[:, 30:38] = torch.tensor([192, 168, 0, 9, 0x11, 0x5C, 0x1F, 0x90], dtype=torch.uint8, device=DEV)
         cap = nflows
         rsz = lib().qk_u32_size(t)
-        keys = (FlowKey * cap)()
-        sk_buf = C.create_string_buffer(cap * rsz)
-        times = []
-        for it in range(max(3, args.steps // 2) + 1):
-            nf, st = C.c_size_t(), PktStats()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            rc = lib().qk_u32_encode_flows_device(ctx.handle, raw.data_ptr(), n, stride, None, None, t, keys, sk_buf,
-                                                  cap, C.byref(nf), C.byref(st), 0)
-            torch.cuda.synchronize()
-            if rc != 0:
-                raise RuntimeError(f"encode_flows rc={rc}")
-            if it:
-                times.append(time.perf_counter() - t0)
-        tm = float(np.median(times))
-        emit({"config": f"per-flow batch: {n} records of {nflows} flows -> one quACK per AddrKey, t={t}",
-              "n_packets": n, "flows": int(nf.value), "packets_per_s": n / tm, "record_GBps": n * stride / tm / 1e9,
-              "seconds": tm, "inserted": int(st.inserted)})
+        outs = {"host output (pageable)": ((FlowKey * cap)(), C.create_string_buffer(cap * rsz)),
+                "device-resident output": (torch.empty((cap, 12), dtype=torch.uint8, device=DEV),
+                                           torch.empty((cap, rsz // 4), dtype=torch.int32, device=DEV))}
+        for where, (keys, sk_buf) in outs.items():
+            kp = keys.data_ptr() if isinstance(keys, torch.Tensor) else keys
+            sp = sk_buf.data_ptr() if isinstance(sk_buf, torch.Tensor) else sk_buf
+            times = []
+            for it in range(max(3, args.steps // 2) + 1):
+                nf, st = C.c_size_t(), PktStats()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                rc = lib().qk_u32_encode_flows_device(ctx.handle, raw.data_ptr(), n, stride, None, None, t, kp, sp,
+                                                      cap, C.byref(nf), C.byref(st), 0)
+                torch.cuda.synchronize()
+                if rc != 0:
+                    raise RuntimeError(f"encode_flows rc={rc}")
+                if it:
+                    times.append(time.perf_counter() - t0)
+            tm = float(np.median(times))
+            emit({"config": f"per-flow batch: {n} records of {nflows} flows -> one quACK per AddrKey, t={t}, {where}",
+                  "n_packets": n, "flows": int(nf.value), "packets_per_s": n / tm,
+                  "record_GBps": n * stride / tm / 1e9, "seconds": tm, "inserted": int(st.inserted)})
         del f
 
 

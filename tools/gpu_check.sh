@@ -59,6 +59,8 @@ for s in $STEPS; do
       step pmccfg_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmccfg_fetch" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFCFG_ARGS:-u64 decode decode64} --steps 2 || exit 3
       step pmccfg_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmccfg_sq" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFCFG_ARGS:-u64 decode decode64} --steps 2 || exit 3 ;;
     decshape) step decshape 600 python3 -u tools/bench_decode.py ${DECSHAPE_ARGS:-} || exit 3 ;;
+    tuneu64) step tuneu64 600 ./tools/tune_u64 || exit 3 ;;
+    flowsbench) step flowsbench 600 python3 -u tools/bench_configs.py flows --steps 6 || exit 3 ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
