@@ -445,6 +445,20 @@ __global__ void k_flow_counts(const uint64_t *__restrict__ offs, const uint32_t 
     info[4 * (uint64_t)r + 3] = ids[offs[g + 1] - 1];
 }
 
+// the flows the lane-per-flow kernel does not take (all of them when !small,
+// else those of more than SMALL_SEG ids), as (segment, [lo, hi)) work-item
+// seeds in any order: the host cuts them into SEG_CHUNK items.  With many
+// small flows the list is empty and the host never sees the offsets.
+__global__ void k_list_big(const uint64_t *__restrict__ offs, uint32_t nseg, int small,
+                           unsigned int *__restrict__ nbig, SegItem *__restrict__ big) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg) return;
+    const uint64_t lo = offs[g], hi = offs[g + 1];
+    if (hi == lo || (small && hi - lo <= SMALL_SEG)) return;
+    const unsigned int k = atomicAdd(nbig, 1u);
+    big[k] = SegItem{g, 0u, lo, hi};
+}
+
 // qk_u32 records (header + T canonical sums) and AddrKey bytes of every flow,
 // written on the device so the host receives exactly its output in two copies
 __global__ void k_flow_finalize(const unsigned long long *__restrict__ acc, const uint64_t *__restrict__ info,
@@ -524,6 +538,13 @@ __global__ void k_seg_last(const uint32_t *__restrict__ ids, const uint64_t *__r
 // work items of the flows k_seg_small does not take: every flow when T > 32,
 // else the flows of more than SMALL_SEG ids
 static bool small_ok(uint32_t T) { return T <= 32; }
+static std::vector<SegItem> seg_items_from_big(const std::vector<SegItem> &big) {
+    std::vector<SegItem> items;
+    for (const SegItem &b : big)
+        for (uint64_t lo = b.lo; lo < b.hi; lo += SEG_CHUNK)
+            items.push_back({b.seg, 0u, lo, std::min<uint64_t>(lo + SEG_CHUNK, b.hi)});
+    return items;
+}
 static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs, uint32_t T) {
     std::vector<SegItem> items;
     for (size_t g = 0; g + 1 < offs.size(); ++g) {
@@ -730,8 +751,10 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const qk_pkt_meta *pm = d_meta ? d_meta + p_from : nullptr;
         // >= 4 tiles per workgroup, enough workgroups to cover the chip
         const uint64_t ntiles = (pn + REC_TILE - 1) / REC_TILE;
+        // QK_TUNE_FLOW_WGPC: workgroups per CU (measurements; default 12: 4, 6, 8, 12 measured, 12 best at 1e4 and 1e6 flows)
+        static const uint64_t wgpc = [] { const char *e = getenv("QK_TUNE_FLOW_WGPC"); return e ? (uint64_t)atoi(e) : 12ull; }();
         const uint64_t tiles_per_chunk =
-            std::max<uint64_t>(4, (ntiles + (uint64_t)ctx->num_cus * 4 - 1) / ((uint64_t)ctx->num_cus * 4));
+            std::max<uint64_t>(4, (ntiles + (uint64_t)ctx->num_cus * wgpc - 1) / ((uint64_t)ctx->num_cus * wgpc));
         const uint64_t chunk = tiles_per_chunk * REC_TILE;
         const uint32_t nchunks = (uint32_t)std::max<uint64_t>(1, (pn + chunk - 1) / chunk);
         for (;;) {
@@ -792,6 +815,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         uint64_t *info = nullptr, *d_offs = nullptr, *kd = nullptr, *kd2 = nullptr, *ks = nullptr, *ks2 = nullptr;
         SegItem *d_items = nullptr;
         uint32_t *d_rec = nullptr, *used = nullptr, *sl2 = nullptr, *sl3 = nullptr, *nsel = nullptr, *perm = nullptr;
+        SegItem *big = nullptr;
         uint8_t *d_keys = nullptr;
         auto layout1 = [&](Carve &c) {
             info = c.take<uint64_t>((size_t)nf * 4);
@@ -803,7 +827,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             kd = c.take<uint64_t>(nf); kd2 = c.take<uint64_t>(nf); ks = c.take<uint64_t>(nf); ks2 = c.take<uint64_t>(nf);
             used = c.take<uint32_t>(nf); sl2 = c.take<uint32_t>(nf); sl3 = c.take<uint32_t>(nf);
             perm = c.take<uint32_t>(nf);
-            nsel = c.take<uint32_t>(1);
+            nsel = c.take<uint32_t>(2);   // [0] selected slots, [1] flows needing work items
+            big = c.take<SegItem>(nf);
         };
         {
             Carve probe{nullptr};
@@ -863,14 +888,27 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
         }
-        std::vector<uint64_t> offs((size_t)nf + 1);
-        uint32_t hsel = 0;
-        if (!rc && (hipMemcpyAsync(offs.data(), d_offs, ((size_t)nf + 1) * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                    hipMemcpyAsync(&hsel, nsel, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                    hipStreamSynchronize(s) != hipSuccess))
-            rc = QK_E_HIP;
-        if (!rc && hsel != nf) rc = QK_E_HIP;   // every occupied slot holds exactly one flow
-        if (!rc) rc = seg_encode(ctx, id_s, d_offs, seg_items(offs, T), nf, T, acc, d_items, s);
+        // only the flows that need work items come back to the host (none
+        // in the many-small-flows case): 8 bytes of counts, then their seeds
+        uint32_t hsel[2] = {0, 0};
+        std::vector<SegItem> bigs;
+        if (!rc) {
+            if (hipMemsetAsync(nsel + 1, 0, 4, s) != hipSuccess) rc = QK_E_HIP;
+            if (!rc) hipLaunchKernelGGL(k_list_big, dim3(fblocks), dim3(256), 0, s, d_offs, nf, (int)small_ok(T),
+                                        nsel + 1, big);
+            if (!rc && (hipGetLastError() != hipSuccess ||
+                        hipMemcpyAsync(hsel, nsel, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                        hipStreamSynchronize(s) != hipSuccess))
+                rc = QK_E_HIP;
+        }
+        if (!rc && hsel[0] != nf) rc = QK_E_HIP;   // every occupied slot holds exactly one flow
+        if (!rc && hsel[1]) {
+            bigs.resize(hsel[1]);
+            if (hipMemcpyAsync(bigs.data(), big, bigs.size() * sizeof(SegItem), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                rc = QK_E_HIP;
+        }
+        if (!rc) rc = seg_encode(ctx, id_s, d_offs, seg_items_from_big(bigs), nf, T, acc, d_items, s);
         if (!rc) {
             const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nf * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);

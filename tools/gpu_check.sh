@@ -61,6 +61,10 @@ for s in $STEPS; do
     decshape) step decshape 600 python3 -u tools/bench_decode.py ${DECSHAPE_ARGS:-} || exit 3 ;;
     tuneu64) step tuneu64 600 ./tools/tune_u64 || exit 3 ;;
     flowsbench) step flowsbench 600 python3 -u tools/bench_configs.py flows --steps 6 || exit 3 ;;
+    flowswg)
+      for w in ${WG_LIST:-4 6 8}; do
+        QK_TUNE_FLOW_WGPC=$w step flowswg$w 300 python3 -u tools/bench_configs.py flows --steps 6 || exit 3
+      done ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
