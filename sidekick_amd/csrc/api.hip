@@ -242,8 +242,14 @@ int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, si
     // layout of d_small: [0, SMALL_NHITS) coefficients, [SMALL_NHITS] hit count, [SMALL_STOP] stop index
     uint64_t *d_counters = ctx->d_small + SMALL_NHITS;
     T *d_c = (T *)ctx->d_small;
-    memcpy(ctx->h_small, coeffs, (size_t)d * sizeof(T));
-    if (d) QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, (size_t)d * sizeof(T), hipMemcpyHostToDevice, s));
+    size_t cbytes = (size_t)d * sizeof(T);
+    if constexpr (sizeof(T) == 8) {
+        if (rt64_use_bsgs(d)) cbytes = rt64_bsgs_table(coeffs, d, ctx->h_small) * 8;   // limb-shifted table
+        else memcpy(ctx->h_small, coeffs, cbytes);
+    } else {
+        memcpy(ctx->h_small, coeffs, cbytes);
+    }
+    if (cbytes) QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, cbytes, hipMemcpyHostToDevice, s));
     if (int rc = ensure_hits(ctx, 4096, s)) return rc;
     hipLaunchKernelGGL(k_init_counters, dim3(1), dim3(1), 0, s, d_counters);
     if (n) {

@@ -99,6 +99,10 @@ int launch_encode_u64_acc(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t
 int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uint32_t *log, size_t n,
                          int use_stop, uint32_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);
+// u64 root test by baby-step/giant-step for these degrees (decode.hip); the
+// coefficient buffer then holds rt64_bsgs_table's limb-shifted table
+bool rt64_use_bsgs(uint32_t d);
+size_t rt64_bsgs_table(const uint64_t *coeffs, uint32_t d, uint64_t *out);
 int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uint64_t *log, size_t n,
                          int use_stop, uint64_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);

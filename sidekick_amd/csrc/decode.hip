@@ -13,6 +13,8 @@
 // atomic ticket; the host sorts them into log order.  The `break` at the
 // first log entry equal to diff.last_value() becomes an atomicMin of that
 // position; the host drops hits at or after it.
+#include <cstdlib>
+
 #include "bsgs64.h"
 #include "ctx.h"
 #include "field.h"
@@ -169,6 +171,194 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_test_u64(const uint64_t *__re
     }
 }
 
+// u64, baby-step / giant-step evaluation for 16 <= d <= RT64_BSGS_MAXD:
+//   P(x) = x^d + sum_{k<d} p_k x^k = sum_a x^(8a) Q_a(x),  Q_a = sum_{b<8} p_(8a+b) x^b
+// (the top block holds x^r, r = d mod 8, as a coefficient 1; d = 8A: R starts
+// at 1), then Horner in x^8 over the blocks.  The inner sums are carry-free:
+// the babies x^1..x^7 are split into 22-bit limbs l_j (B = l0 + l1 2^22 +
+// l2 2^44), and the host pre-shifts every coefficient by 2^(22j) mod p, so
+//   p * B == sum_j l_j * (p 2^(22j) mod p)
+// is six 22x32-bit mads into two 64-bit sums (weights 1 and 2^32) per term:
+// 21 products < 2^54 per sum stay below 2^59, no carry is ever counted.
+// Per candidate at d = 32: 7 + 4 p64 multiplies and 168 mads, against 32
+// Horner steps of 7 multiplies each.  Table: tab[(8a + b) * 3 + j] =
+// p_(8a+b) * 2^(22j) mod p (u64), blocks a = 0 .. nblk - 1 (the last one the
+// top block when d % 8 != 0).
+constexpr uint32_t RT64_BSGS_MIND = 16;
+constexpr uint32_t RT64_BSGS_MAXD = 1000;   // (ceil((d+1)/8) * 24 words <= SMALL_NHITS)
+
+__device__ __forceinline__ uint64_t rt_limb_sum(uint64_t lo, uint64_t hi, uint64_t c) {
+    // lo + hi * 2^32 + c  (lo, hi < 2^59) reduced below 2^64 (not canonical)
+    const uint64_t h1 = hi >> 32, h0 = hi & 0xFFFFFFFFull;
+    unsigned __int128 v = (unsigned __int128)lo + (h0 << 32) + (unsigned __int128)h1 * C64 + c;
+    uint64_t r = (uint64_t)v;
+    const uint64_t top = (uint64_t)(v >> 64);           // <= 2
+    const uint64_t add = top * C64;
+    uint64_t q = r + add;
+    if (q < r) q += C64;                                 // wrapped past 2^64 once: < 2*59 + 59, no second wrap
+    return q;
+}
+
+// Q_a of W candidates at once: the block's coefficients are loaded once (scalar
+// loads) and feed the MACs of every candidate
+template <int W>
+__device__ __forceinline__ void rt_block(const uint64_t *__restrict__ tab, uint32_t a,
+                                         const uint32_t (&l)[W][7][3], uint64_t (&q)[W]) {
+    uint64_t slo[W], shi[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) { slo[w] = 0; shi[w] = 0; }
+#pragma unroll
+    for (int b = 1; b < 8; ++b)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t c = tab[((size_t)a * 8 + b) * 3 + j];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                slo[w] += (uint64_t)l[w][b - 1][j] * (uint32_t)c;
+                shi[w] += (uint64_t)l[w][b - 1][j] * (uint32_t)(c >> 32);
+            }
+        }
+    const uint64_t c0 = tab[(size_t)a * 8 * 3];
+#pragma unroll
+    for (int w = 0; w < W; ++w) q[w] = rt_limb_sum(slo[w], shi[w], c0);
+}
+
+// V + c (c < 2^64), reduced below 2^64
+__device__ __forceinline__ uint64_t rt_add64(uint64_t V, uint64_t c) {
+    uint64_t r = V + c;
+    if (r < V) r += C64;   // 2^64 == 59; r < c here, so no second wrap
+    return r;
+}
+
+// W candidates; NF > 0: the number of full blocks at compile time (unrolled)
+template <int W, int NF>
+__device__ __forceinline__ void is_root64_bsgs(const uint64_t (&x)[W], const uint64_t *__restrict__ tab,
+                                               uint32_t nfull, bool top, bool (&hit)[W]) {
+    uint32_t l[W][7][3], g0[W], g1[W];
+    uint64_t R[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const uint32_t x0 = (uint32_t)x[w], x1 = (uint32_t)(x[w] >> 32);
+        uint64_t V = x[w];
+#pragma unroll
+        for (int b = 1; b <= 7; ++b) {
+            if (b > 1) bsgs64::mulv(V, x0, x1);
+            l[w][b - 1][0] = (uint32_t)V & 0x3FFFFFu;
+            l[w][b - 1][1] = (uint32_t)(V >> 22) & 0x3FFFFFu;
+            l[w][b - 1][2] = (uint32_t)(V >> 44);
+        }
+        bsgs64::mulv(V, x0, x1);                        // x^8
+        g0[w] = (uint32_t)V;
+        g1[w] = (uint32_t)(V >> 32);
+    }
+    const uint32_t nf = NF > 0 ? (uint32_t)NF : nfull;
+    if (top) {
+        rt_block<W>(tab, nf, l, R);                     // x^r + lower terms of the top block
+    } else {
+#pragma unroll
+        for (int w = 0; w < W; ++w) R[w] = 1;
+    }
+    uint64_t q[W];
+    if constexpr (NF > 0) {
+#pragma unroll
+        for (int a = NF - 1; a >= 0; --a) {
+            rt_block<W>(tab, (uint32_t)a, l, q);
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                bsgs64::mulv(R[w], g0[w], g1[w]);
+                R[w] = rt_add64(R[w], q[w]);
+            }
+        }
+    } else {
+        for (uint32_t a = nf; a-- > 0;) {
+            rt_block<W>(tab, a, l, q);
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                bsgs64::mulv(R[w], g0[w], g1[w]);
+                R[w] = rt_add64(R[w], q[w]);
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) hit[w] = canon64(R[w]) == 0;
+}
+
+// candidates interleaved per evaluation (2 would share the coefficient loads,
+// but the pinned-register p64 step then forces hundreds of register copies)
+constexpr int RT64_W = 1;
+
+template <int NF>
+__global__ __launch_bounds__(RT_BLOCK) void k_root_test_u64_bsgs(const uint64_t *__restrict__ log, uint64_t n,
+                                                                 uint32_t head, const uint64_t *__restrict__ tab,
+                                                                 uint32_t nfull, int top, int use_stop,
+                                                                 uint64_t stop_value, uint64_t *__restrict__ hits,
+                                                                 uint64_t cap, uint64_t *__restrict__ counters) {
+    const uint64_t gtid = (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * RT_BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t body = (n - h) >> 1;
+    const ulonglong2 *__restrict__ v = reinterpret_cast<const ulonglong2 *>(log + h);
+    for (uint64_t i = gtid; i < body; i += nthr) {
+        const ulonglong2 wv = v[i];
+        bool hit[2];
+        if constexpr (RT64_W == 2) {
+            const uint64_t x[2] = {wv.x, wv.y};
+            is_root64_bsgs<2, NF>(x, tab, nfull, top, hit);
+        } else {
+            const uint64_t x0[1] = {wv.x}, x1[1] = {wv.y};
+            bool h0[1], h1[1];
+            is_root64_bsgs<1, NF>(x0, tab, nfull, top, h0);
+            is_root64_bsgs<1, NF>(x1, tab, nfull, top, h1);
+            hit[0] = h0[0];
+            hit[1] = h1[0];
+        }
+        const bool s0 = use_stop && wv.x == stop_value, s1 = use_stop && wv.y == stop_value;
+        if (hit[0] | hit[1] | s0 | s1) {
+            rt_record(h + 2 * i, hit[0], s0, hits, cap, counters);
+            rt_record(h + 2 * i + 1, hit[1], s1, hits, cap, counters);
+        }
+    }
+    const uint64_t tail0 = h + (body << 1);
+    if (gtid < h) {
+        const uint64_t x[1] = {log[gtid]};
+        bool hit[1];
+        is_root64_bsgs<1, NF>(x, tab, nfull, top, hit);
+        rt_record(gtid, hit[0], use_stop && x[0] == stop_value, hits, cap, counters);
+    }
+    if (gtid < n - tail0) {
+        const uint64_t pos = tail0 + gtid;
+        const uint64_t x[1] = {log[pos]};
+        bool hit[1];
+        is_root64_bsgs<1, NF>(x, tab, nfull, top, hit);
+        rt_record(pos, hit[0], use_stop && x[0] == stop_value, hits, cap, counters);
+    }
+}
+
+bool rt64_use_bsgs(uint32_t d) {
+    static const int no_bsgs = [] { const char *e = getenv("QK_TUNE_RT64_HORNER"); return e ? atoi(e) : 0; }();
+    return !no_bsgs && d >= RT64_BSGS_MIND && d <= RT64_BSGS_MAXD;
+}
+
+// host: the limb-shifted coefficient table of the BSGS kernel into out[]
+// (canonical c_1..c_d of the monic polynomial); returns the words written
+size_t rt64_bsgs_table(const uint64_t *coeffs, uint32_t d, uint64_t *out) {
+    const uint32_t nfull = d / 8, r = d % 8, nblk = nfull + (r ? 1 : 0);
+    const size_t words = (size_t)nblk * 24;
+    for (size_t i = 0; i < words; ++i) out[i] = 0;
+    for (uint32_t k = 0; k < 8 * nblk; ++k) {
+        uint64_t pk;   // coefficient of x^k: p_d = 1, p_(d-i) = c_i
+        if (k > d) pk = 0;
+        else if (k == d) pk = 1;
+        else pk = coeffs[d - k - 1];
+        unsigned __int128 v = pk;
+        for (int j = 0; j < 3; ++j) {
+            out[(size_t)k * 3 + j] = (uint64_t)(v % P64);
+            v = (v % P64) << 22;
+        }
+    }
+    return words;
+}
+
 // ---------------------------------------------------------- launchers
 template <typename KernelT>
 static uint32_t rt_grid(qk_ctx *ctx, KernelT kern, uint64_t units) {
@@ -214,8 +404,19 @@ int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uin
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
     const uint64_t units = (n + 1) / 2;
     hipEvent_t e0 = prof_begin(ctx, s);
-    hipLaunchKernelGGL(k_root_test_u64, dim3(rt_grid(ctx, k_root_test_u64, units)), dim3(RT_BLOCK), 0, s, log,
-                       (uint64_t)n, head, d_c, d, use_stop, stop_value, hits, cap, counters);
+    if (rt64_use_bsgs(d)) {
+        // d_c holds the limb-shifted table (root_test_begin, rt64_bsgs_table)
+        // one runtime loop over the blocks: an unrolled loop (d / 8 fixed) or
+        // two interleaved candidates made the compiler shuttle every value
+        // around the pinned registers of the p64 step (1300 copies per
+        // evaluation); measured slower
+        hipLaunchKernelGGL(k_root_test_u64_bsgs<0>, dim3(rt_grid(ctx, k_root_test_u64_bsgs<0>, units)),
+                           dim3(RT_BLOCK), 0, s, log, (uint64_t)n, head, d_c, d / 8, (int)(d % 8 != 0), use_stop,
+                           stop_value, hits, cap, counters);
+    } else {
+        hipLaunchKernelGGL(k_root_test_u64, dim3(rt_grid(ctx, k_root_test_u64, units)), dim3(RT_BLOCK), 0, s, log,
+                           (uint64_t)n, head, d_c, d, use_stop, stop_value, hits, cap, counters);
+    }
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());
     return QK_OK;

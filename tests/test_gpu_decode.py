@@ -47,7 +47,8 @@ def test_golden_decodes(golden):
 
 
 @pytest.mark.parametrize("bits", [32, 64])
-@pytest.mark.parametrize("d", [1, 2, 3, 7, 8, 15, 16, 20, 31, 32, 33, 64, 100])
+@pytest.mark.parametrize("d", [1, 2, 3, 7, 8, 15, 16, 17, 20, 23, 24, 25, 31, 32, 33, 40, 64, 100, 255, 256,
+                               999, 1000, 1001])
 def test_root_test_vs_oracle(bits, d):
     rng = np.random.default_rng(d * 7 + bits)
     n = 50_001
@@ -66,10 +67,10 @@ def test_root_test_vs_oracle(bits, d):
     assert set(roots_at.tolist()) <= set(got)
 
 
-@pytest.mark.parametrize("bits", [32, 64])
-def test_root_test_misaligned_small(bits):
+@pytest.mark.parametrize("bits,t", [(32, 8), (64, 8), (64, 20)])
+def test_root_test_misaligned_small(bits, t):
     log = coracle.splitmix_u32(3, 300) if bits == 32 else coracle.splitmix_u64(3, 300)
-    q = QT(bits)(8)
+    q = QT(bits)(t)
     for i in (0, 5, 6, 150, 299):
         q.insert(int(log[i]))
     c = q.to_coeffs()
@@ -79,6 +80,28 @@ def test_root_test_misaligned_small(bits):
             sub = log[off:off + n]
             want, _ = (coracle.root_test_u32 if bits == 32 else coracle.root_test_u64)(c, sub)
             assert q.root_test(c, d[off:off + n]) == want.tolist(), (off, n)
+
+
+@pytest.mark.parametrize("d", [16, 21, 32, 48])
+def test_root_test_u64_edge_ids(d):
+    """u64 candidates at the edges of the representation (0, p - 1, p, p + 1,
+    2^64 - 1 and neighbours, ids whose 22-bit limbs are all ones) as roots
+    and as non-roots: the baby-step/giant-step kernel (d >= 16) works on the
+    raw 64-bit id, its limb sums and folds must stay exact."""
+    P = (1 << 64) - 59
+    edge = [0, 1, 2, P - 2, P - 1, P, P + 1, P + 58, (1 << 64) - 1, (1 << 64) - 2, (1 << 44) - 1, (1 << 22) - 1,
+            ((1 << 64) - 1) ^ (1 << 22), (1 << 63), (1 << 63) - 1]
+    log = coracle.splitmix_u64(77 + d, 20_000)
+    log[::1000] = np.array(edge * 2, dtype=np.uint64)[: len(log[::1000])]
+    roots = [P - 1, (1 << 64) - 1, (1 << 44) - 1, 1] + [int(v) for v in log[3:3 + d - 4]]
+    q = QT(64)(d)
+    for r in roots:
+        q.insert(r)
+    c = q.to_coeffs()
+    want, _ = coracle.root_test_u64(c, log)
+    got = q.root_test(c, dev(log, 64))
+    assert got == want.tolist()
+    assert {i for i, v in enumerate(log.tolist()) if v % P in {r % P for r in roots}} == set(got)
 
 
 def test_stop_at_last_value():

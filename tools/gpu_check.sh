@@ -65,6 +65,9 @@ for s in $STEPS; do
       for w in ${WG_LIST:-4 6 8}; do
         QK_TUNE_FLOW_WGPC=$w step flowswg$w 300 python3 -u tools/bench_configs.py flows --steps 6 || exit 3
       done ;;
+    dec64)  # u64 root test: BSGS (default) vs Horner
+      step dec64_bsgs 300 python3 -u tools/bench_configs.py decode64 --steps 10 --cpu || exit 3
+      QK_TUNE_RT64_HORNER=1 step dec64_horner 300 python3 -u tools/bench_configs.py decode64 --steps 10 || exit 3 ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
