@@ -79,6 +79,29 @@ def test_stream_u64_1000(golden):
 
 
 @pytest.mark.parametrize("bits", [32, 64])
+def test_insert_remove_every_threshold_vs_oracle(bits):
+    """The host insert walks the powers as four interleaved chains for t >= 8:
+    every threshold 1..41 (each tail length) and ids at the field edges
+    (0, 1, p - 1, p, p + 1, 2^w - 1) match the oracle; remove() undoes insert."""
+    rnd = random.Random(5 * bits)
+    P = qo.MOD[bits]
+    edge = [0, 1, 2, P - 1, P, P + 1, (1 << bits) - 1, (1 << bits) - 2, 1 << (bits - 1)]
+    for t in range(1, 42):
+        ids = edge + [rnd.getrandbits(bits) for _ in range(30)]
+        q = Q(bits, t)
+        oq = qo.OracleQuack(t, bits)
+        for i in ids:
+            q.insert(i)
+        oq.insert_all(ids)
+        assert q.power_sums() == oq.power_sums, t
+        for i in ids[::2]:
+            q.remove(i)
+        rest = ids[1::2]
+        assert q.power_sums() == Q_from(rest, bits, t).power_sums(), t
+        assert q.count() == len(rest)
+
+
+@pytest.mark.parametrize("bits", [32, 64])
 def test_media_client_flow(bits):
     """media_client.rs:247-323 end to end on the host path: the receiver's
     cumulative quACK minus the proxy's, to_coeffs, eval == 0 over the log,
