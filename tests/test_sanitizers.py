@@ -81,3 +81,24 @@ def test_abi_c_device():
     r = subprocess.run([exe, "device"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "abi_c device ok" in r.stdout
+
+
+def test_abi_failure_paths_host_no_leaks(native):
+    """tests/native/abi_fail: every host error path of the ABI 3000 times,
+    plain and under ASan with the leak checker on."""
+    r = subprocess.run([os.path.join(native, "abi_fail"), "host"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "abi_fail host ok" in r.stdout, r.stdout + r.stderr
+    r = subprocess.run([os.path.join(native, "abi_fail_asan"), "host", "1000"], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
+    assert r.returncode == 0 and "abi_fail host ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_abi_failure_paths_device_no_growth():
+    """The device entry points' failures (early argument checks and late
+    capacity / undecodable returns after kernels ran) 300 times on one
+    context: every status as documented, device memory flat."""
+    exe = os.path.join(NATIVE, "abi_fail")
+    assert os.path.exists(exe), "build tests/native first (__graft_entry__.build())"
+    r = subprocess.run([exe, "device", "300"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "abi_fail device ok" in r.stdout, r.stdout + r.stderr
