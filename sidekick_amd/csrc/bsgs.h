@@ -225,34 +225,70 @@ __device__ __forceinline__ void row2m(uint64_t &a0, uint64_t &a1, uint32_t b0, u
 //          scalar unit); 1: plain add, wraps caught by a per-lane minimum of
 //          the fold results (a wrapped fold leaves a value < 25, field.h)
 //  PAIR    interleave the power chains of two ids
-template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false>
+//  OFF     offset pass (thresholds > 80, several passes over the ids): the
+//          giants are x^(base + a*NB) for a = 0..NA-1 with a runtime base
+//          (a multiple of NB), so every row is a MAC row (no a = 0 sum row)
+//          and the pass yields powers base+1 .. base+NB*NA
+template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false, bool OFF_ = false>
 struct Cfg {
     static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_;
-    static constexpr bool PAIR = PAIR_;
+    static constexpr bool PAIR = PAIR_, OFF = OFF_;
+    static constexpr int ROWS = OFF_ ? NA_ : NA_ - 1;   // MAC rows
+    static constexpr int ROW1 = OFF_ ? 0 : 1;           // group-row number of the first MAC row
     static_assert(NB % 2 == 0 && NA >= 2, "NB even, NA >= 2");
+    static_assert(!OFF_ || FOLD_ == 1, "offset passes use min-tracked folds");
 };
 
-template <int NB, int NA>
+template <int NB, int NA, int ROWS = NA - 1>
 struct Acc {
     uint32_t lo0[NB];         // a = 0 row (ROW0 == 0): sum of B_b mod 2^32
     uint32_t c0[NB];          // ... its wraps (lane count, or wave total if scalar)
     uint64_t r0[NB];          // a = 0 row (ROW0 == 1): sum of B_b, 64-bit
-    uint64_t m[NA - 1][NB];   // a >= 1: sum of A_a * B_b mod 2^64
-    uint32_t c[NA - 1][NB];   // ... its wraps (lane count, or wave total if scalar)
+    uint64_t m[ROWS][NB];     // MAC rows: sum of A_a * B_b mod 2^64
+    uint32_t c[ROWS][NB];     // ... its wraps (lane count, or wave total if scalar)
 };
 
+// group rows: 0 = the a = 0 sum row, ROW1.. = the MAC rows (an offset pass
+// has no sum row: its MAC rows start at 0)
 template <class C>
 __host__ __device__ constexpr bool scalar_group(int row, int b) {
-    return b / 4 * 4 + 4 <= C::NB && (row > 0 || C::ROW0 == 0) && row * (C::NB / 4) + b / 4 < C::SG;
+    return b / 4 * 4 + 4 <= C::NB && (row > 0 || C::ROW0 == 0 || C::OFF) && row * (C::NB / 4) + b / 4 < C::SG;
+}
+
+// x^(NB*q) from xn = x^NB by square-and-multiply over the (wave-uniform) q >= 1
+template <class MUL>
+__device__ __forceinline__ uint32_t pow_uniform(uint32_t xn, uint32_t q, MUL mul) {
+    uint32_t r = 0, sq = xn;
+    bool have = false;
+    for (;;) {
+        if (q & 1) {
+            r = have ? mul(r, sq) : sq;
+            have = true;
+        }
+        q >>= 1;
+        if (!q) break;
+        sq = mul(sq, sq);
+    }
+    return r;
 }
 
 // powers of one id; returns nonzero if a lazy fold may have wrapped (the
-// caller then recomputes exactly)
+// caller then recomputes exactly).  OFF: A[a] = x^(base + a*NB).
 template <class C>
-__device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], uint32_t (&A)[C::NA - 1]) {
+__device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], uint32_t (&A)[C::ROWS],
+                                           uint32_t base = 0) {
     constexpr int NB = C::NB, NA = C::NA;
     B[0] = id;
-    if constexpr (C::FOLD == 0) {
+    if constexpr (C::OFF) {
+        uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+        for (int b = 1; b < NB; ++b) B[b] = mulfold32_min(B[b - 1], B[0], mn);
+        const uint32_t xn = B[NB - 1];                                   // x^NB (B[b] = x^(b+1))
+        A[0] = pow_uniform(xn, base / NB, [&](uint32_t u, uint32_t v) { return mulfold32_min(u, v, mn); });
+#pragma unroll
+        for (int a = 1; a < NA; ++a) A[a] = mulfold32_min(A[a - 1], xn, mn);
+        return mn < 25u;
+    } else if constexpr (C::FOLD == 0) {
         uint32_t wrapped = 0;
 #pragma unroll
         for (int b = 1; b < NB; ++b) B[b] = mulfold32_fast(B[b - 1], B[0], wrapped);
@@ -271,9 +307,16 @@ __device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], ui
     }
 }
 template <class C>
-__device__ __forceinline__ void powers_exact(uint32_t (&B)[C::NB], uint32_t (&A)[C::NA - 1]) {
+__device__ __forceinline__ void powers_exact(uint32_t (&B)[C::NB], uint32_t (&A)[C::ROWS], uint32_t base = 0) {
 #pragma unroll
     for (int b = 1; b < C::NB; ++b) B[b] = mulfold32_exact(B[b - 1], B[0]);
+    if constexpr (C::OFF) {
+        const uint32_t xn = B[C::NB - 1];
+        A[0] = pow_uniform(xn, base / C::NB, [](uint32_t u, uint32_t v) { return mulfold32_exact(u, v); });
+#pragma unroll
+        for (int a = 1; a < C::NA; ++a) A[a] = mulfold32_exact(A[a - 1], xn);
+        return;
+    }
     A[0] = B[C::NB - 1];
 #pragma unroll
     for (int a = 1; a < C::NA - 1; ++a) A[a] = mulfold32_exact(A[a - 1], A[0]);
@@ -282,11 +325,12 @@ __device__ __forceinline__ void powers_exact(uint32_t (&B)[C::NB], uint32_t (&A)
 // Groups are issued in the order row 0, row 1, ... and alternate carry-SGPR
 // sets (group index parity), so no two adjacent blocks share SGPRs.
 template <class C>
-__device__ __forceinline__ void accumulate(Acc<C::NB, C::NA> &S, const uint32_t (&B)[C::NB],
-                                           const uint32_t (&A)[C::NA - 1]) {
-    constexpr int NB = C::NB, NA = C::NA;
+__device__ __forceinline__ void accumulate(Acc<C::NB, C::NA, C::ROWS> &S, const uint32_t (&B)[C::NB],
+                                           const uint32_t (&A)[C::ROWS]) {
+    constexpr int NB = C::NB;
 #pragma unroll
     for (int b = 0; b + 4 <= NB; b += 4) {
+        if constexpr (C::OFF) break;   // no sum row in an offset pass
         const bool s0 = (b / 4) % 2 == 0;
         if constexpr (C::ROW0 == 1) {
             if (s0) row4m<0>(S.r0[b], S.r0[b + 1], S.r0[b + 2], S.r0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
@@ -307,16 +351,16 @@ __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA> &S, const uint32_t 
                          S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
         }
     }
-    if constexpr (NB % 4 == 2) {
+    if constexpr (NB % 4 == 2 && !C::OFF) {
         if constexpr (C::ROW0 == 1) row2m(S.r0[NB - 2], S.r0[NB - 1], B[NB - 2], B[NB - 1]);
         else add2v(S.lo0[NB - 2], S.lo0[NB - 1], S.c0[NB - 2], S.c0[NB - 1], B[NB - 2], B[NB - 1]);
     }
 #pragma unroll
-    for (int a = 0; a < NA - 1; ++a) {
+    for (int a = 0; a < C::ROWS; ++a) {
 #pragma unroll
         for (int b = 0; b + 4 <= NB; b += 4) {
-            const int g = (a + 1) * (NB / 4) + b / 4;   // group index: parity picks the SGPR set
-            if (scalar_group<C>(a + 1, b)) {
+            const int g = (a + C::ROW1) * (NB / 4) + b / 4;   // group index: parity picks the SGPR set
+            if (scalar_group<C>(a + C::ROW1, b)) {
                 if (g % 2 == 0)
                     mac4s<0>(S.m[a][b], S.m[a][b + 1], S.m[a][b + 2], S.m[a][b + 3], S.c[a][b], S.c[a][b + 1],
                              S.c[a][b + 2], S.c[a][b + 3], A[a], B[b], B[b + 1], B[b + 2], B[b + 3]);
@@ -338,11 +382,11 @@ __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA> &S, const uint32_t 
 }
 
 template <class C>
-__device__ __forceinline__ void one(Acc<C::NB, C::NA> &S, uint32_t id) {
-    uint32_t B[C::NB], A[C::NA - 1];
-    const uint32_t w = powers<C>(id, B, A);
+__device__ __forceinline__ void one(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id, uint32_t base = 0) {
+    uint32_t B[C::NB], A[C::ROWS];
+    const uint32_t w = powers<C>(id, B, A, base);
     if (__builtin_expect(__any(w), 0)) {
-        if (w) powers_exact<C>(B, A);
+        if (w) powers_exact<C>(B, A, base);
     }
     accumulate<C>(S, B, A);
 }
@@ -350,8 +394,9 @@ __device__ __forceinline__ void one(Acc<C::NB, C::NA> &S, uint32_t id) {
 // two ids at once: their power chains are independent straight-line code, so
 // the compiler interleaves them (ILP for the dependent modmul chains)
 template <class C>
-__device__ __forceinline__ void two(Acc<C::NB, C::NA> &S, uint32_t id0, uint32_t id1) {
-    uint32_t B0[C::NB], A0[C::NA - 1], B1[C::NB], A1[C::NA - 1];
+__device__ __forceinline__ void two(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id0, uint32_t id1) {
+    static_assert(!C::OFF, "pairs: plain passes only");
+    uint32_t B0[C::NB], A0[C::ROWS], B1[C::NB], A1[C::ROWS];
     const uint32_t w0 = powers<C>(id0, B0, A0);
     const uint32_t w1 = powers<C>(id1, B1, A1);
     if (__builtin_expect(__any(w0 | w1), 0)) {
@@ -363,15 +408,15 @@ __device__ __forceinline__ void two(Acc<C::NB, C::NA> &S, uint32_t id0, uint32_t
 }
 
 template <class C>
-__device__ __forceinline__ void four(Acc<C::NB, C::NA> &S, uint4 w) {
+__device__ __forceinline__ void four(Acc<C::NB, C::NA, C::ROWS> &S, uint4 w, uint32_t base) {
     if constexpr (C::PAIR) {
         two<C>(S, w.x, w.y);
         two<C>(S, w.z, w.w);
     } else {
-        one<C>(S, w.x);
-        one<C>(S, w.y);
-        one<C>(S, w.z);
-        one<C>(S, w.w);
+        one<C>(S, w.x, base);
+        one<C>(S, w.y, base);
+        one<C>(S, w.z, base);
+        one<C>(S, w.w, base);
     }
 }
 
@@ -388,20 +433,20 @@ __device__ __forceinline__ void four(Acc<C::NB, C::NA> &S, uint4 w) {
 // body_gen: the ids are walked by `nthr` threads of which this is `gtid`
 // (the whole grid for the headline kernel, one workgroup for a flow's work
 // item); out(m, s) receives the workgroup's sum for power m + 1 (< 2^40) in
-// thread m.
+// thread m (an offset pass: power base + m + 1).
 template <class C, class Out>
 __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
-                                         uint64_t gtid, uint64_t nthr, Out out) {
+                                         uint64_t gtid, uint64_t nthr, Out out, uint32_t base = 0) {
     constexpr int NB = C::NB, NA = C::NA;
     __shared__ uint64_t sm[WAVES * NB * NA];
-    Acc<NB, NA> S;
+    Acc<NB, NA, C::ROWS> S;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         S.lo0[b] = 0;
         S.c0[b] = 0;
         S.r0[b] = 0;
 #pragma unroll
-        for (int a = 0; a < NA - 1; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; }
+        for (int a = 0; a < C::ROWS; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; }
     }
     const uint64_t h = head < n ? head : n;
     const uint64_t nbody = (n - h) >> 2;
@@ -417,18 +462,18 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
         const uint4 w = nxt;
         p += nthr;
         nxt = *p;
-        four<C>(S, w);
+        four<C>(S, w, base);
     }
     for (; it < tmax; ++it) {
         const uint4 w = nxt;
         p += nthr;
         nxt = make_uint4(0, 0, 0, 0);
         if (it + 1 < iters) nxt = *p;
-        four<C>(S, w);
+        four<C>(S, w, base);
     }
     const uint64_t tail0 = h + (nbody << 2);
-    one<C>(S, gtid < h ? ids[gtid] : 0u);
-    one<C>(S, gtid < n - tail0 ? ids[tail0 + gtid] : 0u);
+    one<C>(S, gtid < h ? ids[gtid] : 0u, base);
+    one<C>(S, gtid < n - tail0 ? ids[tail0 + gtid] : 0u, base);
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -438,14 +483,16 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
             // value = lo + c * W with W = 2^32 == 5 (a = 0) or 2^64 == 25 (a > 0);
             // a scalar-counted c is the wave's total, added once (by lane 0)
             const bool sc = scalar_group<C>(a, b);
-            const uint32_t c = a == 0 ? S.c0[b] : S.c[a - 1][b];
+            const uint32_t c = C::OFF ? S.c[a][b] : a == 0 ? S.c0[b] : S.c[a - C::ROW1][b];
             const uint32_t cl = sc ? (lane == 0 ? c : 0u) : c;
             uint64_t x;
-            if (a == 0) {
+            if (C::OFF) {
+                x = (uint64_t)fold64_32(S.m[a][b]) + fold64_32((uint64_t)cl * 25u);
+            } else if (a == 0) {
                 if constexpr (C::ROW0 == 1) x = S.r0[b];
                 else x = (uint64_t)S.lo0[b] + (uint64_t)cl * 5u;                      // < 6*2^32
             } else {
-                x = (uint64_t)fold64_32(S.m[a - 1][b]) + fold64_32((uint64_t)cl * 25u);
+                x = (uint64_t)fold64_32(S.m[a - C::ROW1][b]) + fold64_32((uint64_t)cl * 25u);
             }
             x = fold64_32(x);                                                         // < 2^32
 #pragma unroll
@@ -466,9 +513,10 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
 // stored [power][block]
 template <class C>
 __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
-                                     uint64_t *__restrict__ partials) {
-    body_gen<C>(ids, n, head, T, (uint64_t)blockIdx.x * BLOCK + threadIdx.x, (uint64_t)gridDim.x * BLOCK,
-                [=](uint32_t m, uint64_t s) { partials[(size_t)m * gridDim.x + blockIdx.x] = s; });
+                                     uint64_t *__restrict__ partials, uint32_t base = 0) {
+    body_gen<C>(
+        ids, n, head, T, (uint64_t)blockIdx.x * BLOCK + threadIdx.x, (uint64_t)gridDim.x * BLOCK,
+        [=](uint32_t m, uint64_t s) { partials[(size_t)m * gridDim.x + blockIdx.x] = s; }, base);
 }
 
 } // namespace bsgs

@@ -96,6 +96,15 @@ __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB *
     bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD>>(ids, n, head, T, partials);
 }
 
+// Offset pass for thresholds > 80 (several passes over the ids): powers
+// base+1 .. base+8*NA with giants x^(base + 8a), a = 0..NA-1 (bsgs.h OFF).
+template <int NA, int SG>
+__global__ __launch_bounds__(BLOCK, (NA > 6 ? 2 : NA > 5 ? 3 : 4)) void k_encode_u32_bsgs_off(
+    const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T, uint32_t base,
+    uint64_t *__restrict__ partials) {
+    bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true>>(ids, n, head, T, partials, base);
+}
+
 // lane j of a G-group: start = x^(j+1), step = x^G (square-and-multiply).
 template <int G>
 __device__ __forceinline__ void group_powers32(uint32_t x, int j, uint32_t &start, uint32_t &step) {
@@ -207,6 +216,36 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u32(const uint64_t *__restri
             out[T] = accumulate ? out[T] + n : n;
             if (n) out[T + 1] = ids[n - 1];
             else if (!accumulate) out[T + 1] = 0;
+        }
+    }
+}
+
+// One pass of a multi-pass encode: powers m < T of this pass go to
+// out[m] (out = the partial vector + the pass's base); the pass with
+// meta != nullptr also writes count and last id there (meta[0], meta[1]).
+__global__ __launch_bounds__(BLOCK) void k_finalize_u32_pass(const uint64_t *__restrict__ partials,
+                                                             uint32_t nblocks, uint32_t T,
+                                                             const uint32_t *__restrict__ ids, uint64_t n,
+                                                             uint64_t *__restrict__ out,
+                                                             uint64_t *__restrict__ meta, int accumulate) {
+    __shared__ uint64_t sm[WAVES];
+    const uint32_t m = blockIdx.x;
+    uint64_t s = 0;
+    for (uint32_t b = threadIdx.x; b < nblocks; b += BLOCK) s += partials[(size_t)m * nblocks + b];
+    s = fold64_32(s);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += shfl_xor_u64(s, off);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tot = 0;
+        for (int w = 0; w < WAVES; ++w) tot += sm[w];
+        const uint32_t c = canon32(fold64_32(tot));
+        out[m] = accumulate ? (uint64_t)add32((uint32_t)out[m], c) : (uint64_t)c;
+        if (m == 0 && meta) {
+            meta[0] = accumulate ? meta[0] + n : n;
+            if (n) meta[1] = ids[n - 1];
+            else if (!accumulate) meta[1] = 0;
         }
     }
 }
@@ -506,6 +545,57 @@ static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t
     return scratch_release(ctx, s);
 }
 
+// Thresholds 81..1024 by baby-step/giant-step passes: pass 0 is the (8,10)
+// kernel (powers 1..80), each further pass the offset kernel with giants
+// from x^base (the ids are read once per pass; HBM has the bandwidth, the
+// passes are integer-issue bound like the single-pass kernels).
+template <bool OFF, class KernelT>
+static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_ids, size_t n,
+                    uint32_t head, uint32_t Tp, uint32_t base, uint64_t *out, uint64_t *meta, int acc,
+                    hipStream_t s) {
+    const uint32_t nb = grid_for(ctx, kern, (n + 3) / 4, BLOCK);
+    if (int rc = ensure_scratch(ctx, (size_t)nb * GK * sizeof(uint64_t), s)) return rc;
+    uint64_t *partials = (uint64_t *)ctx->d_scratch;
+    if (int rc = scratch_acquire(ctx, s)) return rc;
+    hipEvent_t e0 = prof_begin(ctx, s);
+    if constexpr (OFF)
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, base, partials);
+    else
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, partials);
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_finalize_u32_pass, dim3(Tp), dim3(BLOCK), 0, s, partials, nb, Tp, d_ids, (uint64_t)n, out,
+                       meta, acc);
+    QK_HIP_TRY(hipGetLastError());
+    return scratch_release(ctx, s);
+}
+
+static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                        int acc, hipStream_t s) {
+    // pass 0: powers 1..80 with the single-pass (8,10) kernel; then passes of
+    // <= 48 powers with the offset (8,6) kernel (142 VGPRs, 3 waves/SIMD; the
+    // 64- and 80-power offset forms spill: every row of an offset pass is a
+    // MAC row)
+    // QK_TUNE_U32_PASS64=1: offset passes of 64 powers ((8,8), 2 waves/SIMD)
+    static const int p64 = [] { const char *e = getenv("QK_TUNE_U32_PASS64"); return e ? atoi(e) : 0; }();
+    for (uint32_t base = 0; base < T;) {
+        const uint32_t Tp = std::min<uint32_t>(base == 0 ? 80 : p64 ? 64 : 48, T - base);
+        uint64_t *meta = base == 0 ? out + T : nullptr;
+        int rc;
+        if (base == 0)
+            rc = run_pass<false>(ctx, k_encode_u32_bsgs<8, 10, 16>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
+        else if (Tp > 48)
+            rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<8, 16>, 64, ids, n, head, Tp, base, out + base, meta, acc, s);
+        else if (Tp <= 40)
+            rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10>, 40, ids, n, head, Tp, base, out + base, meta, acc, s);
+        else
+            rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12>, 48, ids, n, head, Tp, base, out + base, meta, acc, s);
+        if (rc) return rc;
+        base += Tp;
+    }
+    return QK_OK;
+}
+
 // Choose (G, K): the smallest G whose K = ceil(T/G) fits the register
 // budget, then the smallest instantiated K >= ceil(T/G).
 static const int K32_G1[] = {1, 2, 4, 8, 12, 16, 20, 24, 28, 32};
@@ -647,6 +737,9 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     if (T >= 49 && T <= 56 && sg(14)) return QK_BSGS(8, 7, 14);
     if (T >= 57 && T <= 64 && sg(16)) return QK_BSGS(8, 8, 16);
     if (T >= 65 && T <= 80 && sg(16)) return QK_BSGS(8, 10, 16);
+    // QK_TUNE_U32_PASSES=0 keeps t > 80 on the power chain (measurements)
+    static const int passes_env = [] { const char *e = getenv("QK_TUNE_U32_PASSES"); return e ? atoi(e) : 1; }();
+    if (T > 80 && sg(16) && passes_env) return enc32_passes(ctx, ids, n, head, T, out, acc, s);
 #undef QK_BSGS
     int G, K;
     choose_gk(T, 32, K32_G1, 10, K32_GN, 4, G, K);

@@ -57,7 +57,8 @@ def test_golden_streams(golden):
         assert q.count() == s["n"]
 
 
-U32_TS = list(range(1, 34)) + [36, 40, 41, 47, 48, 49, 55, 56, 57, 63, 64, 65, 80, 100, 128, 129, 256, 300, 513, 1024]
+U32_TS = list(range(1, 34)) + [36, 40, 41, 47, 48, 49, 55, 56, 57, 63, 64, 65, 80, 81, 88, 100, 120, 128, 129, 168,
+                               169, 256, 300, 513, 1023, 1024]
 U64_TS = [1, 2, 3, 5, 8, 12, 16, 19, 20, 21, 32, 40, 64, 65, 72, 73, 74, 79, 80, 81, 160, 300, 1024]
 
 
@@ -71,6 +72,24 @@ def test_u32_threshold_sweep(t):
 def test_u64_threshold_sweep(t):
     ids = coracle.splitmix_u64(0xDEF0 + t, 3001)
     assert gpu_state(ids, t, 64).power_sums() == coracle.encode_u64(ids, t)
+
+
+@pytest.mark.parametrize("t", [81, 128, 300, 1024])
+def test_u32_multipass_edges(golden, t):
+    """Thresholds above 80 run as baby-step/giant-step passes (80 powers, then
+    offset passes of <= 48 with giants from x^base): ids at the field edges,
+    the lazy-fold wrap ids of the shared baby chain, misaligned starts, and
+    equality with the power chain (QK_TUNE_U32_PASSES=0 is a process-wide
+    switch, so the chain side is the oracle here)."""
+    P32 = 4294967291
+    ids = coracle.splitmix_u32(0x77 + t, 30_011)
+    edge = np.array([0, 1, P32 - 1, P32, P32 + 1, 2**32 - 1, 2**31], dtype=np.uint32)
+    ids[::997] = np.resize(edge, len(ids[::997]))
+    wraps = np.array(golden["bsgs_wrap_ids"]["8x10"], dtype=np.uint32)
+    ids[5000:5000 + 64 * len(wraps):64] = wraps
+    d = dev_u32(ids)
+    for off in (0, 1, 3):
+        assert gpu_state(d[off:], t).power_sums() == coracle.encode_u32(ids[off:], t), (t, off)
 
 
 @pytest.mark.parametrize("t", [80, 73])
