@@ -573,19 +573,15 @@ static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_id
 static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
                         int acc, hipStream_t s) {
     // pass 0: powers 1..80 with the single-pass (8,10) kernel; then passes of
-    // <= 48 powers with the offset (8,6) kernel (142 VGPRs, 3 waves/SIMD; the
-    // 64- and 80-power offset forms spill: every row of an offset pass is a
-    // MAC row)
-    // QK_TUNE_U32_PASS64=1: offset passes of 64 powers ((8,8), 2 waves/SIMD)
-    static const int p64 = [] { const char *e = getenv("QK_TUNE_U32_PASS64"); return e ? atoi(e) : 0; }();
+    // <= 48 powers with the offset (8,6) kernel (142 VGPRs, 3 waves/SIMD;
+    // every row of an offset pass is a MAC row: the 80-power form spills, a
+    // 64-power (8,8) form at 2 waves/SIMD measured the same as 48)
     for (uint32_t base = 0; base < T;) {
-        const uint32_t Tp = std::min<uint32_t>(base == 0 ? 80 : p64 ? 64 : 48, T - base);
+        const uint32_t Tp = std::min<uint32_t>(base == 0 ? 80 : 48, T - base);
         uint64_t *meta = base == 0 ? out + T : nullptr;
         int rc;
         if (base == 0)
             rc = run_pass<false>(ctx, k_encode_u32_bsgs<8, 10, 16>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
-        else if (Tp > 48)
-            rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<8, 16>, 64, ids, n, head, Tp, base, out + base, meta, acc, s);
         else if (Tp <= 40)
             rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10>, 40, ids, n, head, Tp, base, out + base, meta, acc, s);
         else

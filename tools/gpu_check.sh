@@ -75,8 +75,7 @@ for s in $STEPS; do
       NCCL_DEBUG=WARN step dist2rccl 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29544 bench.py --gpus 2 --steps 3 --warmup 1 --ids-per-gpu 1e8 --cpu-sample 0 || exit 3 ;;
     passes)  # u32 t > 80: BSGS passes (default) vs the power chain
       step sweep_passes 300 python3 -u tools/bench_configs.py sweep --steps 6 || exit 3
-      QK_TUNE_U32_PASSES=0 step sweep_chain 300 python3 -u tools/bench_configs.py sweep --steps 6 || exit 3
-      QK_TUNE_U32_PASS64=1 step sweep_pass64 300 python3 -u tools/bench_configs.py sweep --steps 6 || exit 3 ;;
+      QK_TUNE_U32_PASSES=0 step sweep_chain 300 python3 -u tools/bench_configs.py sweep --steps 6 || exit 3 ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
