@@ -92,10 +92,25 @@ def main():
     dev_index = local % ndev  # == local on a real node (one process per GPU)
     torch.cuda.set_device(dev_index)
     comm = None
+    data_path_note = ""
     if world > 1:
         dist.init_process_group("gloo")          # control plane only
         if args.dist_backend == "rccl":
-            comm = skd.Comm.from_process_group(dev_index)
+            try:
+                comm = skd.Comm.from_process_group(dev_index)
+                ok = 1
+            except Exception as e:                # e.g. RCCL refuses the topology
+                log(f"rank {rank}: native RCCL communicator unavailable ({e})")
+                ok = 0
+            flag = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if not int(flag.item()):
+                # every rank falls back together: the same shard/reduce protocol
+                # over gloo (host copies of the t+1 partial words per step)
+                if comm is not None:
+                    comm.close()
+                    comm = None
+                data_path_note = " (native RCCL communicator unavailable: gloo reduce)"
     elif args.comm:
         comm = skd.Comm.create([dev_index])
 
@@ -196,7 +211,7 @@ def main():
             "workload": f"encode {n:.0e} u{bits} ids per GPU at t={t}, device-resident"
                         + ("" if world == 1 else
                            f", {world} contiguous shards + one RCCL reduce (native qk_comm)" if comm is not None else
-                           f", {world} contiguous shards + one gloo reduce (rehearsal)"),
+                           f", {world} contiguous shards + one gloo reduce (rehearsal)" + data_path_note),
             "ids_per_gpu": cnt, "global_ids": n_total, "threshold": t, "bits": bits,
             "seed": hex(args.seed), "parallelism": f"shard{world}",
         },
