@@ -357,7 +357,9 @@ int qk_ctx_create(int device, qk_ctx **out) {
         hipHostMalloc(&ctx->h_small, SMALL_WORDS * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->stage_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->stage_ev[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->flow_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->flow_ev[1], hipEventDisableTiming) != hipSuccess) {
         qk_ctx_destroy(ctx);
         return QK_E_HIP;
     }
@@ -377,6 +379,8 @@ void qk_ctx_destroy(qk_ctx *ctx) {
         if (ctx->stage_ev[i]) hipEventDestroy(ctx->stage_ev[i]);
     }
     if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
+    for (hipEvent_t e : ctx->flow_ev)
+        if (e) hipEventDestroy(e);
     if (ctx->d_scratch) hipFree(ctx->d_scratch);
     if (ctx->d_hits) hipFree(ctx->d_hits);
     for (void *f : ctx->d_flow)

@@ -420,61 +420,12 @@ __device__ __forceinline__ void four(Acc<C::NB, C::NA, C::ROWS> &S, uint4 w, uin
     }
 }
 
-// The kernel body: grid-stride over 16-byte groups of ids (+ unaligned head
-// and tail), then lane partials -> wave butterfly -> LDS -> one partial per
-// (power, block) stored [power][block].
-//
-// Every lane of a wave runs the wave's trip count (lane 0 has the largest):
-// lanes past their range feed id 0, whose powers are all 0, so EXEC is full
-// at every scalar-counted op.  The loop is split: while every lane of the
-// wave still has a next group, the prefetch is unconditional; the last <= 2
-// trips take the masked form.  Per-lane 32-bit trip counts (the host
-// guarantees body / nthr < 2^32).
-// body_gen: the ids are walked by `nthr` threads of which this is `gtid`
-// (the whole grid for the headline kernel, one workgroup for a flow's work
-// item); out(m, s) receives the workgroup's sum for power m + 1 (< 2^40) in
-// thread m (an offset pass: power base + m + 1).
+// Lane partials -> wave butterfly -> LDS -> one sum per power for the
+// workgroup: out(m, s) receives power m + 1's sum (< 2^40) in thread m.
 template <class C, class Out>
-__device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
-                                         uint64_t gtid, uint64_t nthr, Out out, uint32_t base = 0) {
+__device__ __forceinline__ void finish(const Acc<C::NB, C::NA, C::ROWS> &S, uint32_t T, Out out) {
     constexpr int NB = C::NB, NA = C::NA;
     __shared__ uint64_t sm[WAVES * NB * NA];
-    Acc<NB, NA, C::ROWS> S;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        S.lo0[b] = 0;
-        S.c0[b] = 0;
-        S.r0[b] = 0;
-#pragma unroll
-        for (int a = 0; a < C::ROWS; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; }
-    }
-    const uint64_t h = head < n ? head : n;
-    const uint64_t nbody = (n - h) >> 2;
-    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
-    const uint32_t iters = gtid < nbody ? (uint32_t)((nbody - gtid + nthr - 1) / nthr) : 0u;
-    const uint32_t tmax = (uint32_t)__builtin_amdgcn_readfirstlane(iters);           // lane 0: most trips
-    const uint32_t tmin = (uint32_t)__builtin_amdgcn_readlane((int)iters, 63);       // lane 63: fewest
-    const uint4 *__restrict__ p = v + gtid;
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (iters) nxt = *p;
-    uint32_t it = 0;
-    for (; it + 1 < tmin; ++it) {
-        const uint4 w = nxt;
-        p += nthr;
-        nxt = *p;
-        four<C>(S, w, base);
-    }
-    for (; it < tmax; ++it) {
-        const uint4 w = nxt;
-        p += nthr;
-        nxt = make_uint4(0, 0, 0, 0);
-        if (it + 1 < iters) nxt = *p;
-        four<C>(S, w, base);
-    }
-    const uint64_t tail0 = h + (nbody << 2);
-    one<C>(S, gtid < h ? ids[gtid] : 0u, base);
-    one<C>(S, gtid < n - tail0 ? ids[tail0 + gtid] : 0u, base);
-
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -507,6 +458,67 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
         for (int w = 0; w < WAVES; ++w) s += sm[w * (NB * NA) + m];
         out(m, s);
     }
+}
+
+// The kernel body: grid-stride over 16-byte groups of ids (+ unaligned head
+// and tail), then lane partials -> wave butterfly -> LDS -> one partial per
+// (power, block) stored [power][block].
+//
+// Every lane of a wave runs the wave's trip count (lane 0 has the largest):
+// lanes past their range feed id 0, whose powers are all 0, so EXEC is full
+// at every scalar-counted op.  The loop is split: while every lane of the
+// wave still has a next group, the prefetch is unconditional; the last <= 2
+// trips take the masked form.  Per-lane 32-bit trip counts (the host
+// guarantees body / nthr < 2^32).
+// body_gen: the ids are walked by `nthr` threads of which this is `gtid`
+// (the whole grid for the headline kernel, one workgroup for a flow's work
+// item); out(m, s) receives the workgroup's sum for power m + 1 (< 2^40) in
+// thread m (an offset pass: power base + m + 1).
+template <class C>
+__device__ __forceinline__ void clear(Acc<C::NB, C::NA, C::ROWS> &S) {
+#pragma unroll
+    for (int b = 0; b < C::NB; ++b) {
+        S.lo0[b] = 0;
+        S.c0[b] = 0;
+        S.r0[b] = 0;
+#pragma unroll
+        for (int a = 0; a < C::ROWS; ++a) { S.m[a][b] = 0; S.c[a][b] = 0; }
+    }
+}
+
+template <class C, class Out>
+__device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
+                                         uint64_t gtid, uint64_t nthr, Out out, uint32_t base = 0) {
+    Acc<C::NB, C::NA, C::ROWS> S;
+    clear<C>(S);
+    const uint64_t h = head < n ? head : n;
+    const uint64_t nbody = (n - h) >> 2;
+    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(ids + h);
+    const uint32_t iters = gtid < nbody ? (uint32_t)((nbody - gtid + nthr - 1) / nthr) : 0u;
+    const uint32_t tmax = (uint32_t)__builtin_amdgcn_readfirstlane(iters);           // lane 0: most trips
+    const uint32_t tmin = (uint32_t)__builtin_amdgcn_readlane((int)iters, 63);       // lane 63: fewest
+    const uint4 *__restrict__ p = v + gtid;
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (iters) nxt = *p;
+    uint32_t it = 0;
+    for (; it + 1 < tmin; ++it) {
+        const uint4 w = nxt;
+        p += nthr;
+        nxt = *p;
+        four<C>(S, w, base);
+    }
+    for (; it < tmax; ++it) {
+        const uint4 w = nxt;
+        p += nthr;
+        nxt = make_uint4(0, 0, 0, 0);
+        if (it + 1 < iters) nxt = *p;
+        four<C>(S, w, base);
+    }
+    const uint64_t tail0 = h + (nbody << 2);
+    one<C>(S, gtid < h ? ids[gtid] : 0u, base);
+    one<C>(S, gtid < n - tail0 ? ids[tail0 + gtid] : 0u, base);
+
+    finish<C>(S, T, out);
 }
 
 // the headline kernel's form: grid-stride, one partial per (power, block)

@@ -285,7 +285,8 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 #pragma unroll
             for (int r = 0; r < NR; ++r) ng[r] = sm.ga[r][lane];
         }
-#pragma unroll (PF ? BLOCK / 64 : 1)
+        constexpr int UNR = PF ? BLOCK / 64 : 1;
+#pragma unroll UNR
         for (int q = 0; q < BLOCK / 64; ++q) {
             const int j = q * 64 + lane;
             uint4 bv[2];

@@ -47,6 +47,8 @@ struct qk_ctx {
     // d_small / d_hits waits for the previous user's event, then records its own
     hipEvent_t scratch_ev = nullptr;
     bool scratch_ev_valid = false;
+    // per-flow batches: fork/join of the flow-key branch on the second stream
+    hipEvent_t flow_ev[2] = {nullptr, nullptr};
 
     // grown-out device buffers, freed by qk_ctx_trim / qk_ctx_destroy (hipFree
     // synchronises the whole device; growth must not)
@@ -99,6 +101,9 @@ int launch_encode_u64_acc(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t
 int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uint32_t *log, size_t n,
                          int use_stop, uint32_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);
+// canonical power sums out[0..T) from per-block partials [power][block] (encode.hip)
+int launch_finalize_powers_u32(const uint64_t *partials, uint32_t nblocks, uint32_t T, uint64_t *out,
+                               hipStream_t s);
 // u64 root test by baby-step/giant-step for these degrees (decode.hip); the
 // coefficient buffer then holds rt64_bsgs_table's limb-shifted table
 bool rt64_use_bsgs(uint32_t d);

@@ -23,6 +23,7 @@
 #include "field.h"
 #include "bsgs.h"
 #include "bsgs64.h"
+#include "mfma8.h"
 
 // scalar-counted wrap groups of the t = 25..32 BSGS kernel (tools/tune_bsgs.hip)
 #ifndef QK_BSGS_SG_T32
@@ -94,6 +95,44 @@ __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB *
                                                                                   uint32_t T,
                                                                                   uint64_t *__restrict__ partials) {
     bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD>>(ids, n, head, T, partials);
+}
+
+// ---- baby-step / giant-step products on the matrix cores (mfma8.h,
+// DESIGN.md §3.2b): NM blocks of 4 giants x NN blocks of 4 babies
+template <int NM, int NN>
+__global__ __launch_bounds__(mf8::BLOCK) void k_encode_u32_mfma(const uint32_t *__restrict__ ids, uint64_t n,
+                                                               uint64_t *__restrict__ partials) {
+    mf8::body<NM, NN>(ids, n, partials);
+}
+
+// The signed-byte corrections of mfma8.h: cw[P-1] = Cw of power P
+// (canonical), nmod = N mod p (id slots), inv = (1 - 128 R)^-1 mod p.
+// Row a = 0 first, then each giant row from the powers already resolved.
+__global__ __launch_bounds__(64) void k_mfma32_fix(const uint64_t *__restrict__ cw, uint32_t NB, uint32_t NA,
+                                                   uint32_t T, uint32_t nmod, uint32_t inv,
+                                                   const uint32_t *__restrict__ ids, uint64_t n,
+                                                   uint64_t *__restrict__ out, int accumulate) {
+    __shared__ uint32_t S[QK_MAX_THRESHOLD];
+    const uint32_t r128 = 0x80808080u;                   // 128 R, R = 0x01010101 (< p)
+    const uint32_t c1 = mul32(r128, nmod);               // 128 R N
+    const uint32_t c2 = mul32(mul32(r128, r128), nmod);  // 16384 R^2 N
+    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) S[b] = add32(mul32((uint32_t)cw[b], inv), c1);
+    __syncthreads();
+    for (uint32_t a = 1; a < NA; ++a) {
+        const uint32_t ga = S[a * NB - 1];               // sum of giant a = S_(NB a)
+        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) {
+            const uint32_t m = a * NB + b;
+            S[m] = sub32(add32((uint32_t)cw[m], mul32(r128, add32(ga, S[b]))), c2);
+        }
+        __syncthreads();
+    }
+    for (uint32_t m = threadIdx.x; m < T; m += blockDim.x)
+        out[m] = accumulate ? (uint64_t)add32((uint32_t)out[m], S[m]) : (uint64_t)S[m];
+    if (threadIdx.x == 0) {
+        out[T] = accumulate ? out[T] + n : n;
+        if (n) out[T + 1] = ids[n - 1];
+        else if (!accumulate) out[T + 1] = 0;
+    }
 }
 
 // Offset pass for thresholds > 80 (several passes over the ids): powers
@@ -545,6 +584,14 @@ static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t
     return scratch_release(ctx, s);
 }
 
+// sums of per-block partials [power][block] -> canonical S_1..S_T in out[0..T)
+int launch_finalize_powers_u32(const uint64_t *partials, uint32_t nblocks, uint32_t T, uint64_t *out,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize_u32_pass, dim3(T), dim3(BLOCK), 0, s, partials, nblocks, T,
+                       (const uint32_t *)nullptr, (uint64_t)0, out, (uint64_t *)nullptr, 0);
+    return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
+}
+
 // Thresholds 81..1024 by baby-step/giant-step passes: pass 0 is the (8,10)
 // kernel (powers 1..80), each further pass the offset kernel with giants
 // from x^base (the ids are read once per pass; HBM has the bandwidth, the
@@ -566,6 +613,30 @@ static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_id
     QK_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_finalize_u32_pass, dim3(Tp), dim3(BLOCK), 0, s, partials, nb, Tp, d_ids, (uint64_t)n, out,
                        meta, acc);
+    QK_HIP_TRY(hipGetLastError());
+    return scratch_release(ctx, s);
+}
+
+template <int NM, int NN>
+static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc,
+                      hipStream_t s) {
+    constexpr int NA = 4 * NM, NB = 4 * NN, NP = NA * NB;
+    static const uint32_t inv = pow32((uint32_t)(((uint64_t)P32 + 1 - 0x80808080u) % P32), P32 - 2);
+    auto kern = k_encode_u32_mfma<NM, NN>;
+    const uint64_t nsb = (n + 255) / 256;
+    const uint32_t nb = grid_for(ctx, kern, nsb, mf8::WAVES);
+    if (int rc = ensure_scratch(ctx, ((size_t)nb + 1) * NP * sizeof(uint64_t), s)) return rc;
+    uint64_t *partials = (uint64_t *)ctx->d_scratch, *cw = partials + (size_t)nb * NP;
+    if (int rc = scratch_acquire(ctx, s)) return rc;
+    hipEvent_t e0 = prof_begin(ctx, s);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n, partials);
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_finalize_u32_pass, dim3(NP), dim3(BLOCK), 0, s, partials, nb, (uint32_t)NP,
+                       (const uint32_t *)nullptr, (uint64_t)0, cw, (uint64_t *)nullptr, 0);
+    const uint32_t nmod = mul32((uint32_t)(nsb % P32), 256u);
+    hipLaunchKernelGGL(k_mfma32_fix, dim3(1), dim3(64), 0, s, cw, (uint32_t)NB, (uint32_t)NA, T, nmod, inv, ids,
+                       (uint64_t)n, out, acc);
     QK_HIP_TRY(hipGetLastError());
     return scratch_release(ctx, s);
 }
@@ -706,6 +777,16 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
     auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
+    // matrix-core form (mfma8.h) for 9 <= T <= 256; QK_TUNE_U32_MFMA=0 keeps
+    // the VALU kernels (measurements)
+    static const int mfma_env = [] { const char *e = getenv("QK_TUNE_U32_MFMA"); return e ? atoi(e) : 1; }();
+    if (mfma_env && T >= 9 && T <= 256) {
+        if (T <= 16) return enc32_mfma<1, 1>(ctx, ids, n, T, out, acc, s);
+        if (T <= 32) return enc32_mfma<1, 2>(ctx, ids, n, T, out, acc, s);
+        if (T <= 64) return enc32_mfma<2, 2>(ctx, ids, n, T, out, acc, s);
+        if (T <= 128) return enc32_mfma<2, 4>(ctx, ids, n, T, out, acc, s);
+        return enc32_mfma<4, 4>(ctx, ids, n, T, out, acc, s);
+    }
 #define QK_BSGS(NB_, NA_, G_)                                                                        \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)

@@ -817,6 +817,19 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         uint32_t *d_rec = nullptr, *used = nullptr, *sl2 = nullptr, *sl3 = nullptr, *nsel = nullptr, *perm = nullptr;
         SegItem *big = nullptr;
         uint8_t *d_keys = nullptr;
+        void *temp2 = nullptr;   // hipCUB temp of the flow-key branch (runs beside the packet sort)
+        size_t tb2 = 0;
+        {
+            size_t b = 0;
+            uint64_t *k = nullptr;
+            uint32_t *u = nullptr;
+            if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, k, u, u, nf, 0, 48, s) != hipSuccess) rc = QK_E_HIP;
+            tb2 = std::max(tb2, b);
+            if (hipcub::DeviceSelect::If(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), u, u, (int64_t)C,
+                                         SlotUsed{nullptr}, s) != hipSuccess)
+                rc = QK_E_HIP;
+            tb2 = std::max(tb2, b);
+        }
         auto layout1 = [&](Carve &c) {
             info = c.take<uint64_t>((size_t)nf * 4);
             acc = c.take<unsigned long long>((size_t)nf * T);
@@ -829,6 +842,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             perm = c.take<uint32_t>(nf);
             nsel = c.take<uint32_t>(2);   // [0] selected slots, [1] flows needing work items
             big = c.take<SegItem>(nf);
+            temp2 = c.take<char>(tb2);
         };
         {
             Carve probe{nullptr};
@@ -841,31 +855,47 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         }
         const uint32_t fblocks = (nf + 255) / 256;
         const uint32_t gb = (uint32_t)std::min<uint64_t>((n_eff + 255) / 256, (uint64_t)ctx->num_cus * 8);
-        // flows in ascending AddrKey order: stable LSD sort of the occupied
-        // slots by dst, then by src (48-bit halves)
-        if (!rc && hipcub::DeviceSelect::If(temp, tb, hipcub::CountingInputIterator<uint32_t>(0), used, nsel,
-                                            (int64_t)C, SlotUsed{tab}, s) != hipSuccess)
-            rc = QK_E_HIP;
-        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s, tab, used, nf, kd, (uint64_t *)nullptr);
-        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, kd, kd2, used, sl2, nf, 0, 48, s) != hipSuccess)
-            rc = QK_E_HIP;
-        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s, tab, sl2, nf, (uint64_t *)nullptr, ks);
-        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, ks, ks2, sl2, sl3, nf, 0, 48, s) != hipSuccess)
-            rc = QK_E_HIP;
-        // packets: one stable radix sort groups the ids by flow with packet
-        // order kept (last_value = the flow's last packet).  By rank (slot ->
-        // rank remap per packet, bit_width(flows) bits) or, when the table's
-        // log2(C) bits need no more 8-bit passes, directly by slot (no remap;
-        // segments come out in slot order and perm maps rank -> segment).
+        // Two branches (sidekick_multi.rs:265's map iteration order, and the
+        // per-packet grouping) that meet at the offsets:
+        //   side stream s2: flows in ascending AddrKey order — stable LSD sort
+        //     of the occupied slots by dst, then by src (48-bit halves) —
+        //     then slot -> segment / rank maps (nf-sized, launch-bound passes);
+        //   stream s: one stable radix sort of the packets (key, id), which
+        //     groups the ids by flow with packet order kept (last_value = the
+        //     flow's last packet).  By slot (no remap: segments come out in
+        //     slot order and perm maps rank -> segment) when the table's
+        //     log2(C) bits need no more 8-bit passes than the flow count's;
+        //     then the sort overlaps the whole s2 branch.  Otherwise by rank
+        //     (slot -> rank remap per packet, bit_width(flows) bits), which
+        //     waits for s2 first.
         const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
         const bool by_slot = (cbits + 7) / 8 <= (fbits + 7) / 8;
         const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
+        hipStream_t s2 = s == ctx->copy_stream ? ctx->stream : ctx->copy_stream;
+        if (!rc && (hipEventRecord(ctx->flow_ev[0], s) != hipSuccess || hipStreamWaitEvent(s2, ctx->flow_ev[0], 0) != hipSuccess))
+            rc = QK_E_HIP;
+        if (!rc && hipcub::DeviceSelect::If(temp2, tb2, hipcub::CountingInputIterator<uint32_t>(0), used, nsel,
+                                            (int64_t)C, SlotUsed{tab}, s2) != hipSuccess)
+            rc = QK_E_HIP;
+        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s2, tab, used, nf, kd, (uint64_t *)nullptr);
+        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp2, tb2, kd, kd2, used, sl2, nf, 0, 48, s2) != hipSuccess)
+            rc = QK_E_HIP;
+        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s2, tab, sl2, nf, (uint64_t *)nullptr, ks);
+        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp2, tb2, ks, ks2, sl2, sl3, nf, 0, 48, s2) != hipSuccess)
+            rc = QK_E_HIP;
+        if (!rc) {
+            if (by_slot) {
+                hipLaunchKernelGGL(k_slot_pos, dim3(fblocks), dim3(256), 0, s2, used, nf, rank_of_slot);
+                hipLaunchKernelGGL(k_rank_perm, dim3(fblocks), dim3(256), 0, s2, tab, sl3, nf, rank_of_slot, perm, info);
+            } else {
+                hipLaunchKernelGGL(k_slot_rank, dim3(fblocks), dim3(256), 0, s2, tab, sl3, nf, rank_of_slot, info);
+            }
+            if (hipGetLastError() != hipSuccess || hipEventRecord(ctx->flow_ev[1], s2) != hipSuccess) rc = QK_E_HIP;
+        }
         if (!rc && by_slot) {
-            hipLaunchKernelGGL(k_slot_pos, dim3(fblocks), dim3(256), 0, s, used, nf, rank_of_slot);
-            hipLaunchKernelGGL(k_rank_perm, dim3(fblocks), dim3(256), 0, s, tab, sl3, nf, rank_of_slot, perm, info);
-            if (hipGetLastError() != hipSuccess ||
-                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, cbits, s) !=
-                    hipSuccess)
+            if (hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, cbits, s) !=
+                    hipSuccess ||
+                hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess)
                 rc = QK_E_HIP;
             if (!rc) {
                 hipLaunchKernelGGL(k_slot_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted,
@@ -874,11 +904,11 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
         } else if (!rc) {
-            hipLaunchKernelGGL(k_slot_rank, dim3(fblocks), dim3(256), 0, s, tab, sl3, nf, rank_of_slot, info);
-            hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, n_eff, nf);
-            if (hipGetLastError() != hipSuccess ||
-                hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, fbits, s) !=
-                    hipSuccess)
+            if (hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess) rc = QK_E_HIP;
+            if (!rc) hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, n_eff, nf);
+            if (!rc && (hipGetLastError() != hipSuccess ||
+                        hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, fbits,
+                                                           s) != hipSuccess))
                 rc = QK_E_HIP;
             if (!rc) {
                 hipLaunchKernelGGL(k_rank_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted, nf,
@@ -922,6 +952,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         }
     }
     (void)hipStreamSynchronize(s); // the arenas are reused by the next call
+    (void)hipStreamSynchronize(s == ctx->copy_stream ? ctx->stream : ctx->copy_stream);   // the flow-key branch
     if (stats) *stats = st;
     return rc;
 }

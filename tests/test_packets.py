@@ -119,3 +119,33 @@ def test_gpu_packets_no_meta_no_ip():
     ids, last = vector_sniff(bufs, m, my_ip=None)
     assert last == -1 and st["resets"] == 0       # no own address: packets to 10.0.2.1 are ordinary
     assert q.power_sums() == coracle.encode_u32(ids, 16) and st["inserted"] == n - 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t", [4, 5, 8, 9, 12, 13, 16, 32, 33])
+def test_gpu_packets_fused_thresholds(golden, t):
+    """5 <= t <= 12 without a reset in the batch takes the fused kernel
+    (records -> baby-step/giant-step sums, no id array); the lazy-fold wrap ids
+    of the matching configuration sit in records so the exact-recompute branch
+    runs inside it; t = 4 / 13+ and a batch with a reset take the two-pass
+    path.  All against the sniff-loop restatement."""
+    import torch
+    import sidekick_amd as sk
+    from sidekick_amd.quack import encode_packets
+    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "8x4" if t <= 32 else "8x5"
+    wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
+    for resets in ((), (31_000,)):
+        n = 50_001
+        bufs, meta = make_batch(n, seed=t * 7 + len(resets), reset_at=resets, p_filter=0.05)
+        for j, w in enumerate(wraps):               # identifiers that force the exact branch
+            k = 1000 + 97 * j
+            bufs[k, 63:67] = np.frombuffer(int(w).to_bytes(4, "big"), dtype=np.uint8)
+        q = sk.PowerSumQuackU32(t)
+        st = encode_packets(q, torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
+                            meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_ipv4=MY_IP)
+        ids, last = vector_sniff(bufs, meta)
+        assert q.power_sums() == coracle.encode_u32(ids, t), (t, resets)
+        assert q.count() == len(ids) and st["inserted"] == len(ids) and st["last_reset_index"] == last
+        assert st["filtered"] == n - len(ids) - st["discarded"] - st["resets"]
+        if len(ids):
+            assert q.last_value() == int(ids[-1])

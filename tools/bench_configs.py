@@ -175,20 +175,21 @@ def run_packets(args, ctx):
     rec = raw.view(n, stride)
     rec[:, 23] = 17
     rec[:, 30] = 192
-    q = sk.PowerSumQuackU32(32)
-    encode_packets(q, raw, stride=stride, my_ipv4=(10, 0, 2, 1))   # warm
-    torch.cuda.synchronize()
-    times = []
-    for _ in range(args.steps):
-        q = sk.PowerSumQuackU32(32)
-        t0 = time.perf_counter()
-        st = encode_packets(q, raw, stride=stride, my_ipv4=(10, 0, 2, 1))
+    for t in [int(x) for x in args.pkt_t.split(",")]:
+        q = sk.PowerSumQuackU32(t)
+        encode_packets(q, raw, stride=stride, my_ipv4=(10, 0, 2, 1))   # warm
         torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    tm = float(np.median(times))
-    emit({"config": "sniff-loop batch: 67-byte records in HBM -> extract + encode u32 t=32", "n_packets": n,
-          "packets_per_s": n / tm, "record_GBps": n * stride / tm / 1e9, "frac_hbm_8TBs": n * stride / tm / 8e12,
-          "inserted": st["inserted"], "seconds": tm})
+        times = []
+        for _ in range(args.steps):
+            q = sk.PowerSumQuackU32(t)
+            t0 = time.perf_counter()
+            st = encode_packets(q, raw, stride=stride, my_ipv4=(10, 0, 2, 1))
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        tm = float(np.median(times))
+        emit({"config": f"sniff-loop batch: 67-byte records in HBM -> extract + encode u32 t={t}", "n_packets": n,
+              "packets_per_s": n / tm, "record_GBps": n * stride / tm / 1e9, "frac_hbm_8TBs": n * stride / tm / 8e12,
+              "inserted": st["inserted"], "seconds": tm})
 
 
 def run_flows(args, ctx):
@@ -314,6 +315,7 @@ def run_sweep64(args, ctx):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--pkt-t", default="32", help="packets: thresholds (comma list)")
     ap.add_argument("what", nargs="+", choices=["u64", "decode", "decode64", "host", "sweep", "sweep64", "packets", "flows", "micro"])
     ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=10)

@@ -31,6 +31,9 @@ for s in $STEPS; do
         QK_TUNE_BSGS_SG=$g step sg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 || exit 3
       done ;;
     configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
+    pktab)  # packet batch: fused extract+encode vs the two-pass path
+      step pkt_fused 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 || exit 3
+      QK_TUNE_PKT_FUSED=0 step pkt_twopass 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 || exit 3 ;;
     configs20) QK_TUNE_U64_KMAX=20 step configs20 900 python3 -u tools/bench_configs.py u64 || exit 3 ;;
     prof)
       export TMPDIR=/tmp
