@@ -104,31 +104,46 @@ __global__ __launch_bounds__(mf8::BLOCK) void k_encode_u32_mfma(const uint32_t *
                                                                uint64_t *__restrict__ partials) {
     mf8::body<NM, NN>(ids, n, partials);
 }
+// offset pass (T > 256): giants x^(base + NB a)
+template <int NM, int NN>
+__global__ __launch_bounds__(mf8::BLOCK) void k_encode_u32_mfma_off(const uint32_t *__restrict__ ids, uint64_t n,
+                                                                   uint64_t *__restrict__ partials, uint32_t base) {
+    mf8::body<NM, NN, 0, 1, true>(ids, n, partials, base);
+}
 
-// The signed-byte corrections of mfma8.h: cw[P-1] = Cw of power P
-// (canonical), nmod = N mod p (id slots), inv = (1 - 128 R)^-1 mod p.
-// Row a = 0 first, then each giant row from the powers already resolved.
+// The signed-byte corrections of mfma8.h for the pass's powers base + 1 ..
+// base + NB*NA: cw[m] = Cw of power base + m + 1 (canonical), nmod = N mod p
+// (id slots), inv = (1 - 128 R)^-1 mod p.  S holds this batch's canonical
+// power sums (S[P - 1]): the babies' sums S_1..S_NB and, for an offset pass,
+// S_base come from earlier passes; each row uses the previous row's last
+// power as its giants' sum.  The first Tp of the pass go to out[base ..].
 __global__ __launch_bounds__(64) void k_mfma32_fix(const uint64_t *__restrict__ cw, uint32_t NB, uint32_t NA,
-                                                   uint32_t T, uint32_t nmod, uint32_t inv,
-                                                   const uint32_t *__restrict__ ids, uint64_t n,
-                                                   uint64_t *__restrict__ out, int accumulate) {
-    __shared__ uint32_t S[QK_MAX_THRESHOLD];
+                                                   uint32_t T, uint32_t base, uint32_t Tp, uint32_t nmod,
+                                                   uint32_t inv, const uint32_t *__restrict__ ids, uint64_t n,
+                                                   uint64_t *__restrict__ out, int accumulate,
+                                                   uint64_t *__restrict__ S) {
     const uint32_t r128 = 0x80808080u;                   // 128 R, R = 0x01010101 (< p)
     const uint32_t c1 = mul32(r128, nmod);               // 128 R N
     const uint32_t c2 = mul32(mul32(r128, r128), nmod);  // 16384 R^2 N
-    for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) S[b] = add32(mul32((uint32_t)cw[b], inv), c1);
-    __syncthreads();
-    for (uint32_t a = 1; a < NA; ++a) {
-        const uint32_t ga = S[a * NB - 1];               // sum of giant a = S_(NB a)
+    uint32_t a0 = 0;
+    if (base == 0) {                                     // row 0 solves for its own babies' sums
+        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) S[b] = add32(mul32((uint32_t)cw[b], inv), c1);
+        __syncthreads();
+        a0 = 1;
+    }
+    for (uint32_t a = a0; a < NA; ++a) {
+        const uint32_t ga = (uint32_t)S[base + a * NB - 1];   // sum of giant a = S_(base + NB a)
         for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) {
             const uint32_t m = a * NB + b;
-            S[m] = sub32(add32((uint32_t)cw[m], mul32(r128, add32(ga, S[b]))), c2);
+            S[base + m] = sub32(add32((uint32_t)cw[m], mul32(r128, add32(ga, (uint32_t)S[b]))), c2);
         }
         __syncthreads();
     }
-    for (uint32_t m = threadIdx.x; m < T; m += blockDim.x)
-        out[m] = accumulate ? (uint64_t)add32((uint32_t)out[m], S[m]) : (uint64_t)S[m];
-    if (threadIdx.x == 0) {
+    for (uint32_t m = threadIdx.x; m < Tp; m += blockDim.x) {
+        const uint32_t v = (uint32_t)S[base + m];
+        out[base + m] = accumulate ? (uint64_t)add32((uint32_t)out[base + m], v) : (uint64_t)v;
+    }
+    if (threadIdx.x == 0 && base == 0) {
         out[T] = accumulate ? out[T] + n : n;
         if (n) out[T + 1] = ids[n - 1];
         else if (!accumulate) out[T + 1] = 0;
@@ -617,28 +632,65 @@ static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_id
     return scratch_release(ctx, s);
 }
 
-template <int NM, int NN>
-static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc,
-                      hipStream_t s) {
+// One matrix-core pass: powers base + 1 .. base + Tp of T (S = the batch's
+// canonical sums, T + 256 words of scratch).
+template <int NM, int NN, bool OFF>
+static int enc32_mfma_pass(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint32_t base, uint32_t Tp,
+                           uint64_t *out, int acc, uint64_t *partials, uint64_t *cw, uint64_t *S, uint32_t nb,
+                           hipStream_t s) {
     constexpr int NA = 4 * NM, NB = 4 * NN, NP = NA * NB;
     static const uint32_t inv = pow32((uint32_t)(((uint64_t)P32 + 1 - 0x80808080u) % P32), P32 - 2);
-    auto kern = k_encode_u32_mfma<NM, NN>;
-    const uint64_t nsb = (n + 255) / 256;
-    const uint32_t nb = grid_for(ctx, kern, nsb, mf8::WAVES);
-    if (int rc = ensure_scratch(ctx, ((size_t)nb + 1) * NP * sizeof(uint64_t), s)) return rc;
-    uint64_t *partials = (uint64_t *)ctx->d_scratch, *cw = partials + (size_t)nb * NP;
-    if (int rc = scratch_acquire(ctx, s)) return rc;
     hipEvent_t e0 = prof_begin(ctx, s);
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n, partials);
+    if constexpr (OFF)
+        hipLaunchKernelGGL((k_encode_u32_mfma_off<NM, NN>), dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n,
+                           partials, base);
+    else
+        hipLaunchKernelGGL((k_encode_u32_mfma<NM, NN>), dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n, partials);
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_finalize_u32_pass, dim3(NP), dim3(BLOCK), 0, s, partials, nb, (uint32_t)NP,
                        (const uint32_t *)nullptr, (uint64_t)0, cw, (uint64_t *)nullptr, 0);
-    const uint32_t nmod = mul32((uint32_t)(nsb % P32), 256u);
-    hipLaunchKernelGGL(k_mfma32_fix, dim3(1), dim3(64), 0, s, cw, (uint32_t)NB, (uint32_t)NA, T, nmod, inv, ids,
-                       (uint64_t)n, out, acc);
+    const uint32_t nmod = mul32((uint32_t)(((n + 255) / 256) % P32), 256u);
+    hipLaunchKernelGGL(k_mfma32_fix, dim3(1), dim3(64), 0, s, cw, (uint32_t)NB, (uint32_t)NA, T, base, Tp, nmod, inv,
+                       ids, (uint64_t)n, out, acc, S);
     QK_HIP_TRY(hipGetLastError());
-    return scratch_release(ctx, s);
+    return QK_OK;
+}
+
+template <int NM, int NN>
+static uint32_t mfma_grid(qk_ctx *ctx, size_t n) {
+    return grid_for(ctx, k_encode_u32_mfma<NM, NN>, (n + 255) / 256, mf8::WAVES);
+}
+
+// 9 <= T <= 256 in one pass; T > 256 in passes of <= 256 powers (pass 0 the
+// (4,4) shape, then offset passes with the same 16 babies, NM = the giant
+// tiles the pass needs)
+static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc,
+                      hipStream_t s) {
+    const uint32_t nb = std::max(mfma_grid<1, 1>(ctx, n), mfma_grid<4, 4>(ctx, n));
+    if (int rc = ensure_scratch(ctx, ((size_t)nb * 256 + 256 + T + 256) * sizeof(uint64_t), s)) return rc;
+    uint64_t *partials = (uint64_t *)ctx->d_scratch, *cw = partials + (size_t)nb * 256, *S = cw + 256;
+    if (int rc = scratch_acquire(ctx, s)) return rc;
+    int rc = QK_OK;
+    const uint32_t T0 = std::min<uint32_t>(T, 256);
+#define QK_MF(NM_, NN_, OFF_, B_, TP_)                                                                      enc32_mfma_pass<NM_, NN_, OFF_>(ctx, ids, n, T, B_, TP_, out, acc, partials, cw, S,                                                    std::min(nb, mfma_grid<NM_, NN_>(ctx, n)), s)
+    if (T <= 16) rc = QK_MF(1, 1, false, 0, T0);
+    else if (T <= 32) rc = QK_MF(1, 2, false, 0, T0);
+    else if (T <= 64) rc = QK_MF(2, 2, false, 0, T0);
+    else if (T <= 128) rc = QK_MF(2, 4, false, 0, T0);
+    else rc = QK_MF(4, 4, false, 0, T0);
+    for (uint32_t base = 256; base < T && !rc; base += 256) {
+        const uint32_t Tp = std::min<uint32_t>(256, T - base);
+        switch ((Tp + 63) / 64) {
+        case 1: rc = QK_MF(1, 4, true, base, Tp); break;
+        case 2: rc = QK_MF(2, 4, true, base, Tp); break;
+        case 3: rc = QK_MF(3, 4, true, base, Tp); break;
+        default: rc = QK_MF(4, 4, true, base, Tp); break;
+        }
+    }
+#undef QK_MF
+    if (int e = scratch_release(ctx, s); e && !rc) rc = e;
+    return rc;
 }
 
 static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
@@ -777,16 +829,10 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
     auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
-    // matrix-core form (mfma8.h) for 9 <= T <= 256; QK_TUNE_U32_MFMA=0 keeps
+    // matrix-core form (mfma8.h) for T >= 9; QK_TUNE_U32_MFMA=0 keeps
     // the VALU kernels (measurements)
     static const int mfma_env = [] { const char *e = getenv("QK_TUNE_U32_MFMA"); return e ? atoi(e) : 1; }();
-    if (mfma_env && T >= 9 && T <= 256) {
-        if (T <= 16) return enc32_mfma<1, 1>(ctx, ids, n, T, out, acc, s);
-        if (T <= 32) return enc32_mfma<1, 2>(ctx, ids, n, T, out, acc, s);
-        if (T <= 64) return enc32_mfma<2, 2>(ctx, ids, n, T, out, acc, s);
-        if (T <= 128) return enc32_mfma<2, 4>(ctx, ids, n, T, out, acc, s);
-        return enc32_mfma<4, 4>(ctx, ids, n, T, out, acc, s);
-    }
+    if (mfma_env && T >= 9) return enc32_mfma(ctx, ids, n, T, out, acc, s);
 #define QK_BSGS(NB_, NA_, G_)                                                                        \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)
@@ -843,6 +889,10 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     // workgroup.  QK_TUNE_BSGS64_SG (T > 72 only) picks a carry mode
     // for measurements (tools/tune_u64.hip); QK_TUNE_BSGS64_OFF=1 forces the
     // power chain.
+    // matrix-core form (mfma64.h) for 9 <= T <= 80; QK_TUNE_U64_MFMA=0 keeps
+    // the VALU kernels (measurements)
+    static const int mfma64_env = [] { const char *e = getenv("QK_TUNE_U64_MFMA"); return e ? atoi(e) : 1; }();
+    if (mfma64_env && T >= 9 && T <= 80) return launch_encode_u64_mfma(ctx, ids, n, T, out, acc, s);
     static const int sg64 = [] { const char *e = getenv("QK_TUNE_BSGS64_SG"); return e ? atoi(e) : -1; }();
     static const int no64 = [] { const char *e = getenv("QK_TUNE_BSGS64_OFF"); return e ? atoi(e) : 0; }();
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;

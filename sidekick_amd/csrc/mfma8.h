@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bsgs.h"
 #include "field.h"
 
 namespace qk {
@@ -93,8 +94,12 @@ __device__ __forceinline__ void fold_tile(v4i &acc, uint64_t &V, int k) {
 // PIPE 1: each K-block's MFMAs take the fragments read one K-block earlier,
 // so the transposed reads' latency hides behind the next id's modmuls
 // instead of stalling the wave (in-order issue) at the MFMA.
-template <int NM, int NN, int ABL = 0, int PIPE = 1, int ILP = 1>
-__device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint64_t *__restrict__ partials) {
+// OFF: an offset pass of a multi-pass encode (T > NB * NA): the giants are
+// x^(base + NB a) for a = 0..NA-1 (base a multiple of NB, wave-uniform), so
+// the pass yields powers base + 1 .. base + NB * NA.
+template <int NM, int NN, int ABL = 0, int PIPE = 1, bool OFF = false>
+__device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint64_t *__restrict__ partials,
+                                     uint32_t base = 0) {
     using S = Shape<NM, NN>;
     constexpr int NA = S::NA, NB = S::NB, SEGS = S::SEGS, NP = S::NP;
     __shared__ __attribute__((aligned(16))) uint8_t img[WAVES][SEGS][1024];
@@ -157,15 +162,12 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
     };
     // one K-block: store the id's segments, read the fragments transposed,
     // multiply (PIPE: the previous K-block's fragments)
-    auto emit = [&](const uint32_t (&B)[NB], const uint32_t (&A)[NA - 1], uint32_t mn) {
+    auto emit = [&](const uint32_t (&B)[NB], const uint32_t (&G)[NA], uint32_t mn) {
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
             uint32_t g[4];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int a = 4 * m + c;
-                g[c] = a == 0 ? (1u ^ OFS) : (A[a - 1] ^ OFS);
-            }
+            for (int c = 0; c < 4; ++c) g[c] = G[4 * m + c] ^ OFS;
             if constexpr (ABL != 1 && ABL < 5)
                 *reinterpret_cast<uint4 *>(my + m * 1024 + lane * 16) = make_uint4(g[0], g[1], g[2], g[3]);
             else
@@ -212,51 +214,51 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
             mma(af, bf, mn);
         }
     };
-    // ILP ids per lane at once: their power chains are independent, so a
-    // wave has ILP multiply chains in flight; then each id's K-block
-    auto kblocks = [&](const uint32_t *xs) {
-        uint32_t B[ILP][NB], A[ILP][NA - 1];
-        uint32_t mn[ILP];
-#pragma unroll
-        for (int i = 0; i < ILP; ++i) { B[i][0] = xs[i]; mn[i] = 0xFFFFFFFFu; }
+    // one id per lane: babies x^1..x^NB, giants G_a (G_0 = 1, or x^base for
+    // an offset pass), lazy modmuls with an exact redo when a fold may have
+    // wrapped (field.h mulfold32_min), then the K-block
+    auto kblock = [&](uint32_t x) {
+        uint32_t B[NB], G[NA];
+        uint32_t mn = 0xFFFFFFFFu;
+        B[0] = x;
         if constexpr (ABL == 4 || ABL == 7) {
 #pragma unroll
-            for (int i = 0; i < ILP; ++i) {
+            for (int b = 1; b < NB; ++b) B[b] = x + b;
 #pragma unroll
-                for (int b = 1; b < NB; ++b) B[i][b] = xs[i] + b;
-#pragma unroll
-                for (int a = 0; a < NA - 1; ++a) A[i][a] = xs[i] ^ a;
-                mn[i] = 99;
-            }
+            for (int a = 0; a < NA; ++a) G[a] = x ^ a;
+            mn = 99;
         } else {
 #pragma unroll
-            for (int b = 1; b < NB; ++b)
+            for (int b = 1; b < NB; ++b) B[b] = mulfold32_min(B[b - 1], x, mn);
+            const uint32_t xn = B[NB - 1];
+            if constexpr (OFF) {
+                G[0] = bsgs::pow_uniform(xn, base / NB, [&](uint32_t u, uint32_t v) { return mulfold32_min(u, v, mn); });
 #pragma unroll
-                for (int i = 0; i < ILP; ++i) B[i][b] = mulfold32_min(B[i][b - 1], xs[i], mn[i]);
+                for (int a = 1; a < NA; ++a) G[a] = mulfold32_min(G[a - 1], xn, mn);
+            } else {
+                G[0] = 1;
+                G[1] = xn;
 #pragma unroll
-            for (int i = 0; i < ILP; ++i) A[i][0] = B[i][NB - 1];
-#pragma unroll
-            for (int a = 1; a < NA - 1; ++a)
-#pragma unroll
-                for (int i = 0; i < ILP; ++i) A[i][a] = mulfold32_min(A[i][a - 1], A[i][0], mn[i]);
+                for (int a = 2; a < NA; ++a) G[a] = mulfold32_min(G[a - 1], xn, mn);
+            }
         }
-        uint32_t mall = mn[0];
+        if (__builtin_expect(__any(mn < 25u), 0)) {
+            if (mn < 25u) {
 #pragma unroll
-        for (int i = 1; i < ILP; ++i) mall = mall < mn[i] ? mall : mn[i];
-        if (__builtin_expect(__any(mall < 25u), 0)) {
+                for (int b = 1; b < NB; ++b) B[b] = mulfold32_exact(B[b - 1], x);
+                const uint32_t xn = B[NB - 1];
+                if constexpr (OFF) {
+                    G[0] = bsgs::pow_uniform(xn, base / NB, [](uint32_t u, uint32_t v) { return mulfold32_exact(u, v); });
 #pragma unroll
-            for (int i = 0; i < ILP; ++i) {
-                if (mn[i] < 25u) {
+                    for (int a = 1; a < NA; ++a) G[a] = mulfold32_exact(G[a - 1], xn);
+                } else {
+                    G[1] = xn;
 #pragma unroll
-                    for (int b = 1; b < NB; ++b) B[i][b] = mulfold32_exact(B[i][b - 1], xs[i]);
-                    A[i][0] = B[i][NB - 1];
-#pragma unroll
-                    for (int a = 1; a < NA - 1; ++a) A[i][a] = mulfold32_exact(A[i][a - 1], A[i][0]);
+                    for (int a = 2; a < NA; ++a) G[a] = mulfold32_exact(G[a - 1], xn);
                 }
             }
         }
-#pragma unroll
-        for (int i = 0; i < ILP; ++i) emit(B[i], A[i], mn[i]);
+        emit(B, G, mn);
     };
     if (sb < nsb) load(sb);
     // flush periods of FLUSH / 4 super-blocks: no branch inside the inner loop
@@ -268,7 +270,7 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
             for (int q = 0; q < 4; ++q) x4[q] = nx[q];
             if (sb + W < nsb) load(sb + W);   // next super-block in flight during this one
 #pragma unroll
-            for (int q = 0; q < 4; q += ILP) kblocks(x4 + q);
+            for (int q = 0; q < 4; ++q) kblock(x4[q]);
         }
 #pragma unroll
         for (int m = 0; m < NM; ++m)

@@ -28,11 +28,11 @@ __global__ void k_fill(uint32_t *out, uint64_t n, uint64_t seed) {
         out[i] = (uint32_t)(splitmix_mix(seed + (i + 1) * GAMMA) >> 32);
 }
 
-template <int NM, int NN, int ABL, int PIPE = 1, int OCC = 1, int ILP = 1>
+template <int NM, int NN, int ABL, int PIPE = 1, int OCC = 1>
 __global__ __launch_bounds__(256, OCC) void k_var(const uint32_t *ids, uint64_t n, uint64_t *partials, uint64_t *clk) {
     uint64_t t0 = 0, r0 = 0;
     if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
-    mf8::body<NM, NN, ABL, PIPE, ILP>(ids, n, partials);
+    mf8::body<NM, NN, ABL, PIPE>(ids, n, partials);
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
         clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
@@ -65,10 +65,6 @@ int main(int argc, char **argv) {
         {"t32 ablate: VALU only (modmuls, xor)", k_var<1, 2, 6>},
         {"t32 ablate: loads + MFMA only", k_var<1, 2, 7>},
         {"t32 (1,2) occ4", k_var<1, 2, 0, 1, 4>},
-        {"t32 (1,2) ilp2", k_var<1, 2, 0, 1, 1, 2>},
-        {"t32 (1,2) ilp4", k_var<1, 2, 0, 1, 1, 4>},
-        {"t32 VALU only ilp2", k_var<1, 2, 6, 1, 1, 2>},
-        {"t64 (2,2) ilp2", k_var<2, 2, 0, 1, 1, 2>},
         {"t32 VALU only occ4", k_var<1, 2, 6, 1, 4>},
         {"t16 (1,1)", k_var<1, 1, 0>},
         {"t64 (2,2)", k_var<2, 2, 0>},
