@@ -99,10 +99,10 @@ __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB *
 
 // ---- baby-step / giant-step products on the matrix cores (mfma8.h,
 // DESIGN.md §3.2b): NM blocks of 4 giants x NN blocks of 4 babies
-template <int NM, int NN>
+template <int NM, int NN, int NBU = 4 * NN, int NAU = 4 * NM>
 __global__ __launch_bounds__(mf8::BLOCK) void k_encode_u32_mfma(const uint32_t *__restrict__ ids, uint64_t n,
                                                                uint64_t *__restrict__ partials) {
-    mf8::body<NM, NN>(ids, n, partials);
+    mf8::body<NM, NN, 0, 1, false, NBU, NAU>(ids, n, partials);
 }
 // offset pass (T > 256): giants x^(base + NB a)
 template <int NM, int NN>
@@ -634,18 +634,19 @@ static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_id
 
 // One matrix-core pass: powers base + 1 .. base + Tp of T (S = the batch's
 // canonical sums, T + 256 words of scratch).
-template <int NM, int NN, bool OFF>
+template <int NM, int NN, bool OFF, int NBU = 4 * NN, int NAU = 4 * NM>
 static int enc32_mfma_pass(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint32_t base, uint32_t Tp,
                            uint64_t *out, int acc, uint64_t *partials, uint64_t *cw, uint64_t *S, uint32_t nb,
                            hipStream_t s) {
-    constexpr int NA = 4 * NM, NB = 4 * NN, NP = NA * NB;
+    constexpr int NA = NAU, NB = NBU, NP = NA * NB;
     static const uint32_t inv = pow32((uint32_t)(((uint64_t)P32 + 1 - 0x80808080u) % P32), P32 - 2);
     hipEvent_t e0 = prof_begin(ctx, s);
     if constexpr (OFF)
         hipLaunchKernelGGL((k_encode_u32_mfma_off<NM, NN>), dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n,
                            partials, base);
     else
-        hipLaunchKernelGGL((k_encode_u32_mfma<NM, NN>), dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n, partials);
+        hipLaunchKernelGGL((k_encode_u32_mfma<NM, NN, NBU, NAU>), dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n,
+                           partials);
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_finalize_u32_pass, dim3(NP), dim3(BLOCK), 0, s, partials, nb, (uint32_t)NP,
@@ -657,14 +658,15 @@ static int enc32_mfma_pass(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t 
     return QK_OK;
 }
 
-template <int NM, int NN>
+template <int NM, int NN, int NBU = 4 * NN, int NAU = 4 * NM>
 static uint32_t mfma_grid(qk_ctx *ctx, size_t n) {
-    return grid_for(ctx, k_encode_u32_mfma<NM, NN>, (n + 255) / 256, mf8::WAVES);
+    return grid_for(ctx, k_encode_u32_mfma<NM, NN, NBU, NAU>, (n + 255) / 256, mf8::WAVES);
 }
 
 // 9 <= T <= 256 in one pass; T > 256 in passes of <= 256 powers (pass 0 the
-// (4,4) shape, then offset passes with the same 16 babies, NM = the giant
-// tiles the pass needs)
+// (16 babies, 16 giants) shape, then offset passes with the same 16 babies,
+// NM = the giant tiles the pass needs).  Single-pass shapes: the fewest
+// modmuls (NB - 1 + NA - 2) with NB * NA >= T, ties to fewer tiles.
 static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc,
                       hipStream_t s) {
     const uint32_t nb = std::max(mfma_grid<1, 1>(ctx, n), mfma_grid<4, 4>(ctx, n));
@@ -673,12 +675,23 @@ static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, ui
     if (int rc = scratch_acquire(ctx, s)) return rc;
     int rc = QK_OK;
     const uint32_t T0 = std::min<uint32_t>(T, 256);
-#define QK_MF(NM_, NN_, OFF_, B_, TP_)                                                                      enc32_mfma_pass<NM_, NN_, OFF_>(ctx, ids, n, T, B_, TP_, out, acc, partials, cw, S,                                                    std::min(nb, mfma_grid<NM_, NN_>(ctx, n)), s)
-    if (T <= 16) rc = QK_MF(1, 1, false, 0, T0);
-    else if (T <= 32) rc = QK_MF(1, 2, false, 0, T0);
-    else if (T <= 64) rc = QK_MF(2, 2, false, 0, T0);
-    else if (T <= 128) rc = QK_MF(2, 4, false, 0, T0);
-    else rc = QK_MF(4, 4, false, 0, T0);
+#define QK_MF(NM_, NN_, OFF_, B_, TP_, ...)                                                             \
+    enc32_mfma_pass<NM_, NN_, OFF_, ##__VA_ARGS__>(ctx, ids, n, T, B_, TP_, out, acc, partials, cw, S, \
+                                                   std::min(nb, mfma_grid<NM_, NN_, ##__VA_ARGS__>(ctx, n)), s)
+    if (T <= 16) rc = QK_MF(1, 1, false, 0, T0);                 // 4 x 4: 5 modmuls
+    else if (T <= 20) rc = QK_MF(1, 2, false, 0, T0, 5, 4);      // 6
+    else if (T <= 24) rc = QK_MF(1, 2, false, 0, T0, 6, 4);      // 7
+    else if (T <= 32) rc = QK_MF(1, 2, false, 0, T0);            // 8 x 4: 9
+    else if (T <= 36) rc = QK_MF(2, 2, false, 0, T0, 6, 6);      // 9
+    else if (T <= 40) rc = QK_MF(2, 2, false, 0, T0, 8, 5);      // 10
+    else if (T <= 48) rc = QK_MF(2, 2, false, 0, T0, 8, 6);      // 11
+    else if (T <= 56) rc = QK_MF(2, 2, false, 0, T0, 8, 7);      // 12
+    else if (T <= 64) rc = QK_MF(2, 2, false, 0, T0);            // 8 x 8: 13
+    else if (T <= 80) rc = QK_MF(2, 3, false, 0, T0, 10, 8);     // 15
+    else if (T <= 96) rc = QK_MF(2, 3, false, 0, T0, 12, 8);     // 17
+    else if (T <= 128) rc = QK_MF(2, 4, false, 0, T0);           // 16 x 8: 21
+    else if (T <= 192) rc = QK_MF(3, 4, false, 0, T0, 16, 12);   // 25
+    else rc = QK_MF(4, 4, false, 0, T0);                         // 16 x 16: 29
     for (uint32_t base = 256; base < T && !rc; base += 256) {
         const uint32_t Tp = std::min<uint32_t>(256, T - base);
         switch ((Tp + 63) / 64) {

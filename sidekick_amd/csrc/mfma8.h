@@ -63,10 +63,13 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// NM blocks of 4 giants (NA = 4 NM), NN blocks of 4 babies (NB = 4 NN)
-template <int NM, int NN>
+// NM tiles of 4 giant rows, NN tiles of 4 baby columns; NA <= 4 NM giants and
+// NB <= 4 NN babies are used (powers 1 .. NA*NB; the spare rows/columns of a
+// tile hold zero and their products are dropped)
+template <int NM, int NN, int NBU = 4 * NN, int NAU = 4 * NM>
 struct Shape {
-    static constexpr int NA = 4 * NM, NB = 4 * NN, SEGS = NM + NN, NP = 16 * NM * NN;
+    static_assert(NBU <= 4 * NN && NAU <= 4 * NM && NBU >= 2 && NAU >= 2, "used rows fit the tiles");
+    static constexpr int NA = NAU, NB = NBU, SEGS = NM + NN, NP = NAU * NBU;
 };
 
 // int32 tile -> V += sum_r 256^(r + k) (acc_r mod p), k = this lane's baby limb
@@ -97,10 +100,10 @@ __device__ __forceinline__ void fold_tile(v4i &acc, uint64_t &V, int k) {
 // OFF: an offset pass of a multi-pass encode (T > NB * NA): the giants are
 // x^(base + NB a) for a = 0..NA-1 (base a multiple of NB, wave-uniform), so
 // the pass yields powers base + 1 .. base + NB * NA.
-template <int NM, int NN, int ABL = 0, int PIPE = 1, bool OFF = false>
+template <int NM, int NN, int ABL = 0, int PIPE = 1, bool OFF = false, int NBU = 4 * NN, int NAU = 4 * NM>
 __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint64_t *__restrict__ partials,
                                      uint32_t base = 0) {
-    using S = Shape<NM, NN>;
+    using S = Shape<NM, NN, NBU, NAU>;
     constexpr int NA = S::NA, NB = S::NB, SEGS = S::SEGS, NP = S::NP;
     __shared__ __attribute__((aligned(16))) uint8_t img[WAVES][SEGS][1024];
     __shared__ uint64_t red[WAVES][NP];
@@ -162,12 +165,13 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
     };
     // one K-block: store the id's segments, read the fragments transposed,
     // multiply (PIPE: the previous K-block's fragments)
+    auto bw = [](const uint32_t (&B)[NB], int b) { return b < NB ? B[b] ^ OFS : 0u; };   // stored baby word
     auto emit = [&](const uint32_t (&B)[NB], const uint32_t (&G)[NA], uint32_t mn) {
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
             uint32_t g[4];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) g[c] = G[4 * m + c] ^ OFS;
+            for (int c = 0; c < 4; ++c) g[c] = 4 * m + c < NA ? G[4 * m + c] ^ OFS : 0u;
             if constexpr (ABL != 1 && ABL < 5)
                 *reinterpret_cast<uint4 *>(my + m * 1024 + lane * 16) = make_uint4(g[0], g[1], g[2], g[3]);
             else
@@ -177,9 +181,9 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
         for (int c = 0; c < NN; ++c) {
             if constexpr (ABL != 1 && ABL < 5)
                 *reinterpret_cast<uint4 *>(my + (NM + c) * 1024 + lane * 16) =
-                    make_uint4(B[4 * c] ^ OFS, B[4 * c + 1] ^ OFS, B[4 * c + 2] ^ OFS, B[4 * c + 3] ^ OFS);
+                    make_uint4(bw(B, 4 * c), bw(B, 4 * c + 1), bw(B, 4 * c + 2), bw(B, 4 * c + 3));
             else
-                mn ^= B[4 * c] ^ B[4 * c + 1] ^ B[4 * c + 2] ^ B[4 * c + 3];
+                mn ^= bw(B, 4 * c) ^ bw(B, 4 * c + 1) ^ bw(B, 4 * c + 2) ^ bw(B, 4 * c + 3);
         }
         // the wave's own stores, then transposed reads of them: a wave's LDS
         // instructions execute in order, so only code motion is fenced here
@@ -198,7 +202,7 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
 #pragma unroll
         for (int c = 0; c < NN; ++c) {
             if constexpr (ABL == 2 || ABL >= 5) {
-                bf[c] = v4i{(int)B[4 * c], (int)B[4 * c + 1], (int)B[4 * c + 2], (int)(B[4 * c + 3] ^ mn)};
+                bf[c] = v4i{(int)bw(B, 4 * c), (int)bw(B, 4 * c + 1), (int)bw(B, 4 * c + 2), (int)(bw(B, 4 * c + 3) ^ mn)};
             } else {
                 const v2i lo = tr8(my + (NM + c) * 1024 + rd), hi = tr8(my + (NM + c) * 1024 + rd + 512);
                 bf[c] = v4i{lo.x, lo.y, hi.x, hi.y};
@@ -293,7 +297,8 @@ __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t 
             uint64_t v = V[m][c];                       // < 2^32
             v += shfl_xor_u64(v, 1);
             v += shfl_xor_u64(v, 2);                    // the four baby limbs: < 2^34
-            if (k == 0) red[wave][(4 * m + (lane >> 4)) * NB + 4 * c + ((lane & 15) >> 2)] = v;
+            const int a = 4 * m + (lane >> 4), b = 4 * c + ((lane & 15) >> 2);
+            if (k == 0 && a < NA && b < NB) red[wave][a * NB + b] = v;
         }
     __syncthreads();
     for (int p = threadIdx.x; p < NP; p += BLOCK) {

@@ -273,12 +273,24 @@ def test_full_size_u64_properties():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("t", [5, 8, 9, 12, 13, 16, 17, 20, 24, 25, 31, 32, 33, 37, 40, 41, 44, 48, 49, 56, 57, 64, 65, 72, 80])
+# (babies x giants) chain of the kernel each threshold runs (encode.hip enc32:
+# the VALU (4,2) kernel to t = 8, then the matrix-core shape table)
+def wrap_cfg(t):
+    for hi, cfg in ((8, "4x2"), (16, "4x4"), (20, "5x4"), (24, "6x4"), (32, "8x4"), (36, "6x6"), (40, "8x5"),
+                    (48, "8x6"), (56, "8x7"), (64, "8x8"), (80, "10x8"), (96, "12x8"), (128, "16x8"),
+                    (192, "16x12")):
+        if t <= hi:
+            return cfg
+    return "16x16"
+
+
+@pytest.mark.parametrize("t", [5, 8, 9, 12, 13, 16, 17, 20, 24, 25, 31, 32, 33, 37, 40, 41, 44, 48, 49, 56, 57, 64,
+                               65, 72, 80, 96, 128, 160, 192, 256, 300])
 def test_bsgs_rare_wrap_branch(golden, t):
     """Ids whose lazy folds wrap (prob ~2.6e-8 per id) force the exact
     recompute branch of the baby-step/giant-step kernel: alone in a wave,
     several in one wave, and in the unaligned head/tail (scalar path)."""
-    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "6x4" if t <= 24 else "8x4" if t <= 32 else "8x5" if t <= 40 else "8x6" if t <= 48 else "8x7" if t <= 56 else "8x8" if t <= 64 else "8x10"
+    cfg = wrap_cfg(t)
     wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
     ids = coracle.splitmix_u32(0xF00D + t, 20_003)
     ids[100] = wraps[0]                      # one lane of one wave
