@@ -101,7 +101,7 @@ int launch_encode_u64_acc(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t
 int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uint32_t *log, size_t n,
                          int use_stop, uint32_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);
-// u64 encode on the matrix cores for 9 <= T <= 80 (mfma64.hip); same output
+// u64 encode on the matrix cores for T >= 9 (mfma64.hip); same output
 // as launch_encode_u64 (accumulate: add into out)
 int launch_encode_u64_mfma(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t T, uint64_t *out, int acc,
                            hipStream_t s);

@@ -824,6 +824,12 @@ static void choose_gk(uint32_t T, int kmax, const int *kg1, int nkg1, const int 
         if ((uint32_t)ks[i] >= kneed) { K = ks[i]; break; }
 }
 
+// QK_MATRIX_CORES=1: the int8-MFMA encode variants (opt-in)
+static bool matrix_cores_enabled() {
+    const char *e = getenv("QK_MATRIX_CORES");
+    return e && atoi(e) != 0;
+}
+
 static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc, hipStream_t s) {
     if (T == 0 || T > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
     const uintptr_t a = (uintptr_t)ids;
@@ -842,10 +848,10 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
     auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
-    // matrix-core form (mfma8.h) for T >= 9; QK_TUNE_U32_MFMA=0 keeps
-    // the VALU kernels (measurements)
-    static const int mfma_env = [] { const char *e = getenv("QK_TUNE_U32_MFMA"); return e ? atoi(e) : 1; }();
-    if (mfma_env && T >= 9) return enc32_mfma(ctx, ids, n, T, out, acc, s);
+    // matrix-core variant (mfma8.h) for T >= 9: opt-in with
+    // QK_MATRIX_CORES=1 (north_star keeps the product on the vector ALUs);
+    // read per call so a process can compare both forms
+    if (T >= 9 && matrix_cores_enabled()) return enc32_mfma(ctx, ids, n, T, out, acc, s);
 #define QK_BSGS(NB_, NA_, G_)                                                                        \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)
@@ -902,10 +908,8 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     // workgroup.  QK_TUNE_BSGS64_SG (T > 72 only) picks a carry mode
     // for measurements (tools/tune_u64.hip); QK_TUNE_BSGS64_OFF=1 forces the
     // power chain.
-    // matrix-core form (mfma64.h) for 9 <= T <= 80; QK_TUNE_U64_MFMA=0 keeps
-    // the VALU kernels (measurements)
-    static const int mfma64_env = [] { const char *e = getenv("QK_TUNE_U64_MFMA"); return e ? atoi(e) : 1; }();
-    if (mfma64_env && T >= 9 && T <= 80) return launch_encode_u64_mfma(ctx, ids, n, T, out, acc, s);
+    // matrix-core variant (mfma64.h), opt-in as for u32
+    if (T >= 9 && matrix_cores_enabled()) return launch_encode_u64_mfma(ctx, ids, n, T, out, acc, s);
     static const int sg64 = [] { const char *e = getenv("QK_TUNE_BSGS64_SG"); return e ? atoi(e) : -1; }();
     static const int no64 = [] { const char *e = getenv("QK_TUNE_BSGS64_OFF"); return e ? atoi(e) : 0; }();
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;

@@ -52,8 +52,11 @@ struct Shape {
 
 // Writes partials[(power - 1) * gridDim.x + blockIdx.x] = the block's Cw mod
 // p (canonical) for powers 1 .. NB*NA; super-blocks of 256 ids as mfma8.h.
-template <int NM, int NN, int ABL = 0>
-__device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint64_t *__restrict__ partials) {
+// OFF: an offset pass (T > NB * NA): giants x^(base + NB a), a = 0..NA-1
+// (base a multiple of NB, wave-uniform), powers base + 1 .. base + NB * NA.
+template <int NM, int NN, int ABL = 0, bool OFF = false>
+__device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint64_t *__restrict__ partials,
+                                     uint32_t base = 0) {
     using S = Shape<NM, NN>;
     constexpr int NA = S::NA, NB = S::NB, SEGS = S::SEGS, NP = S::NP;
     __shared__ __attribute__((aligned(16))) uint8_t img[WAVES][SEGS][1024];
@@ -139,10 +142,31 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 #pragma unroll
         for (int c = 0; c < NN; ++c) put(NM + c, B[2 * c], B[2 * c + 1]);
         const uint32_t g0 = (uint32_t)V, g1 = (uint32_t)(V >> 32);   // x^NB
-        uint64_t prev = 1;                                            // A_0
+        uint64_t prev;                                                // G_(a-1) of an odd a
+        if constexpr (OFF) {
+            // G_0 = (x^NB)^(base / NB): square-and-multiply over the wave-uniform exponent
+            uint32_t q = base / NB;
+            uint64_t r = 0, sq = V;
+            bool have = false;
+            for (;;) {
+                if (q & 1) {
+                    if (have) bsgs64::mulv(r, (uint32_t)sq, (uint32_t)(sq >> 32));
+                    else r = sq;
+                    have = true;
+                }
+                q >>= 1;
+                if (!q) break;
+                const uint32_t s0 = (uint32_t)sq, s1 = (uint32_t)(sq >> 32);
+                bsgs64::mulv(sq, s0, s1);
+            }
+            V = r;
+            prev = r;
+        } else {
+            prev = 1;                                                 // G_0
+        }
 #pragma unroll
         for (int a = 1; a < NA; ++a) {
-            if (a > 1) {
+            if (OFF || a > 1) {
                 if constexpr (ABL != 4) bsgs64::mulv(V, g0, g1);
                 else V ^= a;
             }

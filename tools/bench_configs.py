@@ -307,7 +307,7 @@ def run_sweep64(args, ctx):
     ids = torch.empty(n, dtype=torch.int64, device=DEV)
     fill_splitmix(ctx, ids, 0x5EED0003, bits=64)
     path = "chain" if os.environ.get("QK_TUNE_BSGS64_OFF") == "1" else "default"
-    for t in (8, 9, 16, 17, 24, 32, 40, 48, 56, 64, 72, 80, 81, 128):
+    for t in (8, 9, 16, 17, 24, 32, 40, 48, 56, 64, 72, 80, 81, 128, 160, 256, 512, 1024):
         wall, kern = time_encode(ctx, ids, t, 64, max(3, args.steps // 2))
         emit({"config": f"encode u64 t={t} ({path})", "n": n, "ids_per_s": n / kern,
               "ns_per_id_per_power": kern / n / t * 1e9})
