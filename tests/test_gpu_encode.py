@@ -59,7 +59,8 @@ def test_golden_streams(golden):
 
 U32_TS = list(range(1, 34)) + [36, 40, 41, 47, 48, 49, 55, 56, 57, 63, 64, 65, 80, 81, 88, 100, 120, 128, 129, 168,
                                169, 256, 300, 513, 1023, 1024]
-U64_TS = [1, 2, 3, 5, 8, 12, 16, 19, 20, 21, 32, 40, 64, 65, 72, 73, 74, 79, 80, 81, 160, 300, 1024]
+U64_TS = [1, 2, 3, 5, 8, 12, 16, 19, 20, 21, 32, 40, 64, 65, 72, 73, 74, 79, 80, 81, 88, 96, 97, 120, 160, 161, 176,
+          240, 300, 513, 1024]
 
 
 @pytest.mark.parametrize("t", U32_TS)
@@ -72,6 +73,26 @@ def test_u32_threshold_sweep(t):
 def test_u64_threshold_sweep(t):
     ids = coracle.splitmix_u64(0xDEF0 + t, 3001)
     assert gpu_state(ids, t, 64).power_sums() == coracle.encode_u64(ids, t)
+
+
+@pytest.mark.parametrize("t", [81, 90, 160, 300, 1024])
+def test_u64_multipass_edges(t):
+    """u64 thresholds above 80 run as baby-step/giant-step passes (powers
+    1..80, then offset passes of <= 80 with giants x^(base + 8a) and x^base by
+    square-and-multiply): field-edge ids, misaligned starts, ragged tails,
+    incremental batches."""
+    P64 = 18446744073709551557
+    ids = coracle.splitmix_u64(0x64 + t, 20_011)
+    edge = np.array([0, 1, P64 - 1, P64, P64 + 1, 2**64 - 1, 2**63], dtype=np.uint64)
+    ids[::991] = np.resize(edge, len(ids[::991]))
+    d = dev_u64(ids)
+    for off in (0, 1, 3):
+        assert gpu_state(d[off:], t, 64).power_sums() == coracle.encode_u64(ids[off:], t), (t, off)
+    q = sk.PowerSumQuackU64(t)
+    for a, b in ((0, 5), (5, 10_000), (10_000, len(ids))):
+        q.insert_batch(d[a:b])
+    assert q.power_sums() == coracle.encode_u64(ids, t)
+    assert q.count() == len(ids) and q.last_value() == int(ids[-1])
 
 
 @pytest.mark.parametrize("t", [81, 128, 300, 1024])
@@ -92,7 +113,7 @@ def test_u32_multipass_edges(golden, t):
         assert gpu_state(d[off:], t).power_sums() == coracle.encode_u32(ids[off:], t), (t, off)
 
 
-@pytest.mark.parametrize("t", [80, 73])
+@pytest.mark.parametrize("t", [80, 73, 96, 160, 250])
 def test_u64_max_ids_carry_storm(t):
     """ids at the top of the u64 range (2^64-1, p, p+1, ...): the largest
     products, so the MAC accumulators of the u64 BSGS kernel wrap on almost
@@ -302,3 +323,51 @@ def test_bsgs_rare_wrap_branch(golden, t):
         assert gpu_state(d[off:], t).power_sums() == coracle.encode_u32(sub, t), (t, off)
     only = dev_u32(np.tile(wraps, 11))
     assert gpu_state(only, t).power_sums() == coracle.encode_u32(np.tile(wraps, 11), t)
+
+
+P32, P64 = 4294967291, 18446744073709551557
+
+
+@pytest.mark.parametrize("bits,t,m", [(32, 32, 1_000_003), (64, 80, 500_009)])
+def test_beyond_2pow32_ids(bits, t, m):
+    """Maximum sizes: one encode over more than 2^32 ids (17 GB of u32, 34 GB
+    of u64).  The stream is one oracle-encoded block tiled R times, so the
+    expected sums are R * S_block mod p exactly; count wraps as the crate's
+    u32 does; last_value is the block's last id."""
+    p = P32 if bits == 32 else P64
+    blk = coracle.splitmix_u32(0xB16 + t, m) if bits == 32 else coracle.splitmix_u64(0xB16 + t, m)
+    want_blk = coracle.encode_u32(blk, t) if bits == 32 else coracle.encode_u64(blk, t)
+    R = (1 << 32) // m + 2
+    n = R * m
+    assert n > (1 << 32)
+    big = (dev_u32(blk) if bits == 32 else dev_u64(blk)).repeat(R)
+    q = gpu_state(big, t, bits)
+    assert q.count() == n & 0xFFFFFFFF
+    assert q.last_value() == int(blk[-1])
+    assert q.power_sums() == [(R * s) % p for s in want_blk]
+    del big
+    torch.cuda.empty_cache()
+
+
+def test_root_test_positions_beyond_2pow32():
+    """Hit positions past 2^32 in a 4.3e9-entry candidate log come back as
+    exact 64-bit positions in log order (u32 log, d = 3 roots planted at the
+    start, past 2^32 and at the end)."""
+    m = 1_000_003
+    blk = coracle.splitmix_u32(0x5106, m)
+    R = (1 << 32) // m + 2
+    n = R * m
+    roots = [v for v in (7, 11, 13, 17, 19) if not np.isin(v, blk)][:3]
+    assert len(roots) == 3
+    log = dev_u32(blk).repeat(R)
+    pos = [5, (1 << 32) + 7, n - 1]
+    for p_, r in zip(pos, roots):
+        log[p_] = int(np.uint32(r).view(np.int32))
+    want = sorted(pos)
+    q = sk.PowerSumQuackU32(8)
+    for r in roots:
+        q.insert(r)
+    hits = q.root_test(q.to_coeffs(), log)
+    assert hits == want
+    del log
+    torch.cuda.empty_cache()
