@@ -226,12 +226,16 @@ struct Smem {
 // powers m < T (32-bit limbs of canonical lane values summed: < 2^40).
 // ABL (ablations for tools/tune_u64.hip only; the product uses 0): 1 skips
 // the MACs, 2 skips the modmuls (the id itself stands for every power).
-template <int NA, int MODE, int SG, int ABL = 0, int PF = 0>
+//   OFF     offset pass of a multi-pass encode (t > 80): powers base+1 ..
+//           base+8NA with giants x^(base+8a), a = 0..NA-1 — every row a MAC
+//           row, no a = 0 row; x^base by square-and-multiply from x^8 over
+//           the uniform exponent base/8 (base a multiple of 8)
+template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
-                                     uint64_t *__restrict__ partials) {
+                                     uint64_t *__restrict__ partials, uint32_t base = 0) {
     static_assert(NA >= 2 && NA <= 10, "giant rows");
-    constexpr int NR = NA - 1;                   // MAC rows (giants x^8 .. x^(8 NR))
-    __shared__ Smem<NA> sm;
+    constexpr int NR = OFF ? NA : NA - 1;        // MAC rows (giants x^8 .. x^(8 NR), or x^base ..)
+    __shared__ Smem<NR + 1> sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cb = 2 * wave;                     // this wave's babies (b = cb+1, cb+2)
@@ -262,7 +266,25 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 sm.bb[b][tid] = make_uint4((uint32_t)V, (uint32_t)(V >> 32), (uint32_t)sh, (uint32_t)(sh >> 32));
             }
             const uint32_t g0 = (uint32_t)V, g1 = (uint32_t)(V >> 32);   // x^8
-            sm.ga[0][tid] = make_uint2(g0, g1);
+            if constexpr (OFF) {
+                // x^base = (x^8)^(base/8): square-and-multiply, uniform exponent
+                uint32_t q = base / NB;
+                uint64_t r = 0, sq = V;
+                bool have = false;
+                for (;;) {
+                    if (q & 1) {
+                        if (have) mulv(r, (uint32_t)sq, (uint32_t)(sq >> 32));
+                        else r = sq;
+                        have = true;
+                    }
+                    q >>= 1;
+                    if (!q) break;
+                    const uint32_t s0 = (uint32_t)sq, s1 = (uint32_t)(sq >> 32);
+                    mulv(sq, s0, s1);
+                }
+                V = r;
+            }
+            sm.ga[0][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
 #pragma unroll
             for (int a = 1; a < NR; ++a) {
                 if (ABL != 2) mulv(V, g0, g1);
@@ -308,7 +330,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 #pragma unroll
                 for (int r = 0; r < NR; ++r) g[r] = sm.ga[r][j];
             }
-            row2<1>(r0lo, r0hi, bv);
+            if constexpr (!OFF) row2<1>(r0lo, r0hi, bv);
             if (ABL != 1) {
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
@@ -333,7 +355,11 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     }
 
     // ---- reduction: canonical lane values, limb sums over lanes, LDS over waves
-    __shared__ unsigned long long red[2 * NB * NA];
+    // the tile operands are dead after the loop's last barrier: the reduction
+    // reuses their LDS (a separate array pushes the offset pass with NA = 10
+    // past 1/3 of the CU's LDS, i.e. to 2 workgroups per CU)
+    static_assert(sizeof(Smem<NR + 1>) >= 2 * NB * NA * sizeof(unsigned long long), "reduction space");
+    unsigned long long *red = reinterpret_cast<unsigned long long *>(&sm);
     for (int i = tid; i < 2 * NB * NA; i += BLOCK) red[i] = 0;
     __syncthreads();
     auto put = [&](int m, uint64_t v) {   // v canonical; m = power - 1
@@ -350,7 +376,8 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     };
     const uint64_t W1 = 59ull << 32;   // 2^96 mod p
 #pragma unroll
-    for (int c = 0; c < 2; ++c) put(cb + c, mod_p128((unsigned __int128)r0lo[c] + ((unsigned __int128)r0hi[c] << 32)));
+    for (int c = 0; c < 2; ++c)
+        if constexpr (!OFF) put(cb + c, mod_p128((unsigned __int128)r0lo[c] + ((unsigned __int128)r0hi[c] << 32)));
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
 #pragma unroll
@@ -363,7 +390,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             uint64_t k1 = s1 ? (lane == 0 ? K1[r][c] : 0u) : K1[r][c];
             if (MODE == 1) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];
             v += (unsigned __int128)k0 * C64 + (unsigned __int128)k1 * W1;
-            put((r + 1) * NB + cb + c, mod_p128(v));
+            put((r + (OFF ? 0 : 1)) * NB + cb + c, mod_p128(v));
         }
     }
     __syncthreads();

@@ -513,10 +513,13 @@ __global__ __launch_bounds__(BLOCK) void k_encode_u64_gn(const uint64_t *__restr
     block_store64<G, K>(a0, a1, a2, T, partials, sm);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restrict__ partials,
-                                                        uint32_t nblocks, uint32_t T,
-                                                        const uint64_t *__restrict__ ids, uint64_t n,
-                                                        uint64_t *__restrict__ out, int accumulate) {
+// Sum block limb partials of power m = blockIdx.x; write canonical S_m as
+// two 32-bit limbs out[2m], out[2m+1] (or add it in when accumulate); the
+// launch with meta != nullptr also writes count and last id (meta[0..1]).
+__device__ __forceinline__ void finalize_u64_body(const uint64_t *__restrict__ partials, uint32_t nblocks,
+                                                  uint32_t T, const uint64_t *__restrict__ ids, uint64_t n,
+                                                  uint64_t *__restrict__ out, uint64_t *__restrict__ meta,
+                                                  int accumulate) {
     __shared__ uint64_t sm[2][WAVES];
     const uint32_t m = blockIdx.x; // power index
     uint64_t a = 0, b = 0;         // limb sums, each < nblocks * 2^40
@@ -546,12 +549,28 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restri
         if (accumulate) v = add64(canon64(out[2 * m] | (out[2 * m + 1] << 32)), v);
         out[2 * m] = (uint32_t)v;
         out[2 * m + 1] = v >> 32;
-        if (m == 0) {
-            out[2 * T] = accumulate ? out[2 * T] + n : n;
-            if (n) out[2 * T + 1] = ids[n - 1];
-            else if (!accumulate) out[2 * T + 1] = 0;
+        if (m == 0 && meta) {
+            meta[0] = accumulate ? meta[0] + n : n;
+            if (n) meta[1] = ids[n - 1];
+            else if (!accumulate) meta[1] = 0;
         }
     }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_finalize_u64_pass(const uint64_t *__restrict__ partials,
+                                                             uint32_t nblocks, uint32_t T,
+                                                             const uint64_t *__restrict__ ids, uint64_t n,
+                                                             uint64_t *__restrict__ out,
+                                                             uint64_t *__restrict__ meta, int accumulate) {
+    finalize_u64_body(partials, nblocks, T, ids, n, out, meta, accumulate);
+}
+
+// single-pass form: count and last id right after the T limb pairs
+__global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restrict__ partials,
+                                                        uint32_t nblocks, uint32_t T,
+                                                        const uint64_t *__restrict__ ids, uint64_t n,
+                                                        uint64_t *__restrict__ out, int accumulate) {
+    finalize_u64_body(partials, nblocks, T, ids, n, out, out + 2 * T, accumulate);
 }
 
 // u64 baby-step / giant-step (bsgs64.h): 256-id tiles, babies and giants
@@ -563,6 +582,17 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 3) void k_encode_u64_bsgs(const uint
                                                                       uint64_t *__restrict__ partials) {
     (void)head;
     bsgs64::body<NA, MODE, SG>(ids, n, T, partials);
+}
+
+// Offset pass for u64 thresholds > 80: powers base+1 .. base+8NA with giants
+// x^(base + 8a) (bsgs64.h OFF); the ids are read once per pass.
+template <int NA>
+__global__ __launch_bounds__(bsgs64::BLOCK, 3) void k_encode_u64_bsgs_off(const uint64_t *__restrict__ ids,
+                                                                          uint64_t n, uint32_t head, uint32_t T,
+                                                                          uint32_t base,
+                                                                          uint64_t *__restrict__ partials) {
+    (void)head;
+    bsgs64::body<NA, 1, 0, 0, 0, true>(ids, n, T, partials, base);
 }
 
 // ------------------------------------------------------------- dispatch
@@ -722,6 +752,68 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
             rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10>, 40, ids, n, head, Tp, base, out + base, meta, acc, s);
         else
             rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12>, 48, ids, n, head, Tp, base, out + base, meta, acc, s);
+        if (rc) return rc;
+        base += Tp;
+    }
+    return QK_OK;
+}
+
+// u64 thresholds > 80: pass 0 is the single-pass (8 babies, 10 giants)
+// kernel for powers 1..80, then offset passes of <= 80 powers (giants
+// x^(base + 8a), every row a MAC row; NA = ceil(Tp / 8)).  Each pass reads the
+// 8-byte ids once more: at ~25 ms of integer issue per pass over 1e9 ids, the
+// extra 1 ms of HBM reads is noise.
+template <int NA>
+static int run_pass64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t Tp, uint32_t base,
+                      uint64_t *out, uint64_t *meta, int acc, hipStream_t s) {
+    auto kern = k_encode_u64_bsgs_off<NA>;
+    const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
+    if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 8 * NA * sizeof(uint64_t), s)) return rc;
+    uint64_t *partials = (uint64_t *)ctx->d_scratch;
+    if (int rc = scratch_acquire(ctx, s)) return rc;
+    hipEvent_t e0 = prof_begin(ctx, s);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, Tp, base, partials);
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_finalize_u64_pass, dim3(Tp), dim3(BLOCK), 0, s, partials, nb, Tp, ids, (uint64_t)n, out,
+                       meta, acc);
+    QK_HIP_TRY(hipGetLastError());
+    return scratch_release(ctx, s);
+}
+
+static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                        int acc, hipStream_t s) {
+    uint64_t *meta = out + 2 * T;
+    {   // pass 0: powers 1..80
+        auto kern = k_encode_u64_bsgs<10, 1, 0>;
+        const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
+        if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 80 * sizeof(uint64_t), s)) return rc;
+        uint64_t *partials = (uint64_t *)ctx->d_scratch;
+        if (int rc = scratch_acquire(ctx, s)) return rc;
+        hipEvent_t e0 = prof_begin(ctx, s);
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, 80u, partials);
+        prof_end(ctx, s, e0);
+        QK_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_finalize_u64_pass, dim3(80), dim3(BLOCK), 0, s, partials, nb, 80u, ids, (uint64_t)n,
+                           out, meta, acc);
+        QK_HIP_TRY(hipGetLastError());
+        if (int rc = scratch_release(ctx, s)) return rc;
+    }
+    for (uint32_t base = 80; base < T;) {
+        const uint32_t Tp = std::min<uint32_t>(80, T - base);
+        uint64_t *o = out + 2 * base;
+        int rc;
+        switch (std::max<uint32_t>(2, (Tp + 7) / 8)) {
+        case 2: rc = run_pass64<2>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        case 3: rc = run_pass64<3>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        case 4: rc = run_pass64<4>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        case 5: rc = run_pass64<5>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        case 6: rc = run_pass64<6>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        case 7: rc = run_pass64<7>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        case 8: rc = run_pass64<8>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        case 9: rc = run_pass64<9>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        default: rc = run_pass64<10>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+        }
         if (rc) return rc;
         base += Tp;
     }
@@ -936,6 +1028,9 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
         }
 #undef QK_BSGS64
     }
+    // QK_TUNE_U64_PASSES=0 keeps t > 80 on the power chain (measurements)
+    static const int passes64 = [] { const char *e = getenv("QK_TUNE_U64_PASSES"); return e ? atoi(e) : 1; }();
+    if (T > 80 && !no64 && passes64 && n / min_grid64 < (1ull << 30)) return enc64_passes(ctx, ids, n, head, T, out, acc, s);
     int G, K;
     // K <= 40 accumulators per lane (120 VGPRs, 3 waves/SIMD) beat K <= 20 at
     // 5 waves by needing fewer lanes per id (t = 80: 2 x (39 + 1) steps vs
