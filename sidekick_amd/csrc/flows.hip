@@ -169,7 +169,16 @@ __global__ __launch_bounds__(SG_BLOCK) void k_seg_small(const uint32_t *__restri
 #pragma unroll
         for (int a = 0; a < C::NA - 1; ++a) { S.m[a][j] = 0; S.c[a][j] = 0; }
     }
-    for (uint64_t i = b; i < e; ++i) bsgs::one<C>(S, ids[i]);
+    // the next two ids are in flight while this one is encoded: a lane walks
+    // its own flow, so without the prefetch every id waits out a full
+    // L2/HBM load latency (~300 cycles of work per id against ~1000+ of it)
+    uint32_t p0 = b < e ? ids[b] : 0u, p1 = b + 1 < e ? ids[b + 1] : 0u;
+    for (uint64_t i = b; i < e; ++i) {
+        const uint32_t cur = p0;
+        p0 = p1;
+        p1 = i + 2 < e ? ids[i + 2] : 0u;
+        bsgs::one<C>(S, cur);
+    }
     // power a*NB + j + 1: a = 0 row is a 64-bit sum; a >= 1 is m + c * 2^64,
     // 2^64 == 25 (mod p)
 #pragma unroll
