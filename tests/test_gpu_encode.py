@@ -139,7 +139,7 @@ def test_misaligned_and_ragged(bits):
             assert q.last_value() == (int(ids[off + n - 1]) if n else None)
 
 
-@pytest.mark.parametrize("bits,t", [(32, 32), (32, 16), (32, 80), (64, 80), (64, 16)])
+@pytest.mark.parametrize("bits,t", [(32, 32), (32, 16), (32, 80), (32, 200), (64, 80), (64, 16), (64, 200)])
 def test_grid_shape_independent(bits, t):
     n = 300_007
     ids = coracle.splitmix_u32(77, n) if bits == 32 else coracle.splitmix_u64(77, n)
