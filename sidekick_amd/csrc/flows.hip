@@ -153,7 +153,7 @@ __global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 
 constexpr uint64_t SMALL_SEG = 4096;
 
 template <class C>
-__global__ __launch_bounds__(SG_BLOCK) void k_seg_small(const uint32_t *__restrict__ ids,
+__global__ __launch_bounds__(SG_BLOCK, 4) void k_seg_small(const uint32_t *__restrict__ ids,
                                                         const uint64_t *__restrict__ offs, uint32_t nseg,
                                                         uint32_t T, unsigned long long *__restrict__ acc_out) {
     const uint32_t g = blockIdx.x * SG_BLOCK + threadIdx.x;
@@ -169,15 +169,21 @@ __global__ __launch_bounds__(SG_BLOCK) void k_seg_small(const uint32_t *__restri
 #pragma unroll
         for (int a = 0; a < C::NA - 1; ++a) { S.m[a][j] = 0; S.c[a][j] = 0; }
     }
-    // the next two ids are in flight while this one is encoded: a lane walks
-    // its own flow, so without the prefetch every id waits out a full
-    // L2/HBM load latency (~300 cycles of work per id against ~1000+ of it)
-    uint32_t p0 = b < e ? ids[b] : 0u, p1 = b + 1 < e ? ids[b + 1] : 0u;
-    for (uint64_t i = b; i < e; ++i) {
-        const uint32_t cur = p0;
-        p0 = p1;
-        p1 = i + 2 < e ? ids[i + 2] : 0u;
-        bsgs::one<C>(S, cur);
+    // The lane walks its flow in the 16-byte blocks that hold it (4 ids per
+    // load; components outside [b, e) of the first and last block read as id
+    // 0, which adds nothing): the 64 lanes of a wave read 64 different lines,
+    // so 4-byte loads moved a whole cache line from L2 per id.  A 16-byte
+    // block never straddles a page, so the partial end blocks are safe reads.
+    const uintptr_t lo = (uintptr_t)(ids + b), hi = (uintptr_t)(ids + e);
+    for (uintptr_t blk = lo & ~(uintptr_t)15; blk < hi; blk += 16) {
+        uint4 w = *reinterpret_cast<const uint4 *>(blk);
+        if (blk < lo || blk + 16 > hi) {
+            w.x = blk + 0 >= lo && blk + 0 < hi ? w.x : 0u;
+            w.y = blk + 4 >= lo && blk + 4 < hi ? w.y : 0u;
+            w.z = blk + 8 >= lo && blk + 8 < hi ? w.z : 0u;
+            w.w = blk + 12 >= lo && blk + 12 < hi ? w.w : 0u;
+        }
+        bsgs::four<C>(S, w, 0);
     }
     // power a*NB + j + 1: a = 0 row is a 64-bit sum; a >= 1 is m + c * 2^64,
     // 2^64 == 25 (mod p)
@@ -418,12 +424,31 @@ __global__ void k_rank_perm(const FlowSlot *__restrict__ tab, const uint32_t *__
 }
 
 // by-slot grouping: segment starts of the slot-sorted packets
+// Segment starts of the sorted keys: position i starts a segment when
+// key[i] != key[i-1].  Each thread compares 4 keys of one 16-byte load (key
+// is an arena buffer, 256-byte aligned) with the last key of the previous
+// block; segment `seg(k)` gets offs[seg(k)] = i.
+template <class Seg>
+__device__ __forceinline__ void segment_starts(const uint32_t *__restrict__ key, uint64_t ninserted, uint32_t nf,
+                                               uint64_t *__restrict__ offs, Seg seg) {
+    const uint64_t nv = ninserted >> 2;
+    const uint4 *__restrict__ kv = reinterpret_cast<const uint4 *>(key);
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 k = kv[v];
+        const uint64_t i = v << 2;
+        if (v == 0 || k.x != key[i - 1]) offs[seg(k.x)] = i;
+        if (k.y != k.x) offs[seg(k.y)] = i + 1;
+        if (k.z != k.y) offs[seg(k.z)] = i + 2;
+        if (k.w != k.z) offs[seg(k.w)] = i + 3;
+    }
+    const uint64_t t = (nv << 2) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // < 4 tail keys
+    if (t < ninserted && (t == 0 || key[t] != key[t - 1])) offs[seg(key[t])] = t;
+    if (blockIdx.x == 0 && threadIdx.x == 0) offs[nf] = ninserted;
+}
+
 __global__ void k_slot_offsets(const uint32_t *__restrict__ key, uint64_t ninserted,
                                const uint32_t *__restrict__ pos_of_slot, uint32_t nf, uint64_t *__restrict__ offs) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ninserted;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        if (i == 0 || key[i] != key[i - 1]) offs[pos_of_slot[key[i]]] = i;
-    if (blockIdx.x == 0 && threadIdx.x == 0) offs[nf] = ninserted;
+    segment_starts(key, ninserted, nf, offs, [=](uint32_t k) { return pos_of_slot[k]; });
 }
 
 // per packet, in place: slot -> flow rank (non-inserts -> nf, sorting last)
@@ -438,10 +463,7 @@ __global__ void k_slot_to_rank(uint32_t *__restrict__ key, const uint32_t *__res
 // segment starts of the rank-sorted packets (every rank 0..nf-1 occurs)
 __global__ void k_rank_offsets(const uint32_t *__restrict__ key, uint64_t ninserted, uint32_t nf,
                                uint64_t *__restrict__ offs) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ninserted;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        if (i == 0 || key[i] != key[i - 1]) offs[key[i]] = i;
-    if (blockIdx.x == 0 && threadIdx.x == 0) offs[nf] = ninserted;
+    segment_starts(key, ninserted, nf, offs, [](uint32_t k) { return k; });
 }
 
 // info[4r+2] = count, [4r+3] = last id of flow r (segment perm[r], or r)
@@ -468,29 +490,61 @@ __global__ void k_list_big(const uint64_t *__restrict__ offs, uint32_t nseg, int
     big[k] = SegItem{g, 0u, lo, hi};
 }
 
-// qk_u32 records (header + T canonical sums) and AddrKey bytes of every flow,
-// written on the device so the host receives exactly its output in two copies
-__global__ void k_flow_finalize(const unsigned long long *__restrict__ acc, const uint64_t *__restrict__ info,
-                                const uint32_t *__restrict__ perm, uint64_t nseg, uint32_t T,
-                                uint32_t *__restrict__ rec, uint8_t *__restrict__ keys) {
-    const uint64_t words = 4ull + T, stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nseg * words; j += stride) {
-        const uint64_t i = j / words;
+template <typename Idx>
+__device__ __forceinline__ void flow_finalize_body(const unsigned long long *__restrict__ acc,
+                                                   const uint64_t *__restrict__ info, const uint32_t *__restrict__ perm,
+                                                   Idx nseg, uint32_t T, uint32_t *__restrict__ rec,
+                                                   uint8_t *__restrict__ keys) {
+    const Idx words = (Idx)4 + T, stride = (Idx)gridDim.x * blockDim.x, tid = (Idx)blockIdx.x * blockDim.x + threadIdx.x;
+    for (Idx j = tid; j < nseg * words; j += stride) {
+        const Idx i = j / words;
         const uint32_t w = (uint32_t)(j - i * words);
         uint32_t v;
         if (w == 0) v = T;
-        else if (w == 1) v = (uint32_t)info[4 * i + 2];  // count
-        else if (w == 2) v = 1u;                          // has_last
-        else if (w == 3) v = (uint32_t)info[4 * i + 3];  // last_value
-        else v = canon32(fold64_32(acc[(perm ? (uint64_t)perm[i] : i) * T + (w - 4)]));
+        else if (w == 1) v = (uint32_t)info[4 * (uint64_t)i + 2];  // count
+        else if (w == 2) v = 1u;                                    // has_last
+        else if (w == 3) v = (uint32_t)info[4 * (uint64_t)i + 3];  // last_value
+        else v = canon32(fold64_32(acc[(perm ? (uint64_t)perm[i] : (uint64_t)i) * T + (w - 4)]));
         rec[j] = v;
     }
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nseg * 12; j += stride) {
-        const uint64_t i = j / 12;
-        const uint32_t b = (uint32_t)(j - i * 12);
-        const uint64_t k = b < 6 ? info[4 * i] : info[4 * i + 1];
-        keys[j] = (uint8_t)(k >> (40 - 8 * (b % 6)));
+    if (((uintptr_t)keys & 3) == 0) {
+        // 12 key bytes = 3 words per flow: the two 48-bit halves, big-endian
+        uint32_t *kw = reinterpret_cast<uint32_t *>(keys);
+        for (Idx j = tid; j < nseg * 3; j += stride) {
+            const Idx i = j / 3;
+            const uint32_t q = (uint32_t)(j - i * 3);
+            const uint64_t a = info[4 * (uint64_t)i], b = info[4 * (uint64_t)i + 1];
+            // byte 4q + r of the key is byte 4q + r of (a[47..0], b[47..0]) in big-endian order
+            uint32_t v = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t bi = 4 * q + r;
+                const uint64_t k = bi < 6 ? a : b;
+                v |= (uint32_t)(uint8_t)(k >> (40 - 8 * (bi % 6))) << (8 * r);
+            }
+            kw[j] = v;
+        }
+    } else {
+        for (Idx j = tid; j < nseg * 12; j += stride) {
+            const Idx i = j / 12;
+            const uint32_t bi = (uint32_t)(j - i * 12);
+            const uint64_t k = bi < 6 ? info[4 * (uint64_t)i] : info[4 * (uint64_t)i + 1];
+            keys[j] = (uint8_t)(k >> (40 - 8 * (bi % 6)));
+        }
     }
+}
+
+// qk_u32 records (header + T canonical sums) and AddrKey bytes of every flow,
+// written on the device so the host receives exactly its output in two copies
+// (32-bit index arithmetic whenever the record words fit: a 64-bit division
+// per word made this kernel 4x slower than its stores)
+__global__ void k_flow_finalize(const unsigned long long *__restrict__ acc, const uint64_t *__restrict__ info,
+                                const uint32_t *__restrict__ perm, uint64_t nseg, uint32_t T,
+                                uint32_t *__restrict__ rec, uint8_t *__restrict__ keys) {
+    if (nseg * (4ull + T) < (1ull << 31) && nseg * 12 < (1ull << 31))
+        flow_finalize_body<uint32_t>(acc, info, perm, (uint32_t)nseg, T, rec, keys);
+    else
+        flow_finalize_body<uint64_t>(acc, info, perm, nseg, T, rec, keys);
 }
 
 // (G, K) for a threshold: smallest G with ceil(T/G) <= 32, K = ceil(T/G) rounded to a supported size
