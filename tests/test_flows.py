@@ -174,6 +174,28 @@ def test_gpu_many_small_segments(golden, t):
         assert q.count() == len(seg) and q.last_value() == (int(seg[-1]) if len(seg) else None)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("t", [16, 32])
+def test_gpu_small_segments_misaligned_base(t):
+    """The lane-per-segment kernel reads each segment in the 16-byte blocks
+    that hold it (masked first/last block): a caller id array starting 4, 8
+    or 12 bytes past a 16-byte boundary, segments of 0..40 ids."""
+    import torch
+    from sidekick_amd.quack import encode_segments
+    rng = np.random.default_rng(100 + t)
+    lens = rng.integers(0, 41, size=2000)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ids = coracle.splitmix_u32(0xA11 + t, int(offs[-1]) + 3)
+    d = torch.from_numpy(ids.view(np.int32)).cuda()
+    for off in (1, 2, 3):
+        sub = ids[off:off + int(offs[-1])]
+        qs = encode_segments(d[off:off + int(offs[-1])], offs.tolist(), t)
+        for g, q in enumerate(qs):
+            seg = sub[offs[g]:offs[g + 1]]
+            assert q.power_sums() == coracle.encode_u32(seg, t), (off, g, len(seg))
+            assert q.count() == len(seg) and q.last_value() == (int(seg[-1]) if len(seg) else None)
+
+
 def check_flows_table(table, flows, t):
     assert set(table.senders()) == set(flows)
     for k, ids in flows.items():
