@@ -257,6 +257,10 @@ int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, si
         if (rc) return rc;
     }
     QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_NHITS, d_counters, 16, hipMemcpyDeviceToHost, s));
+    // and the first hits with them: a decode finds ~d hits, so one
+    // synchronisation (not a second, pageable, round trip) returns them
+    QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_HITPF, ctx->d_hits,
+                              std::min<size_t>(ctx->hits_cap, SMALL_HITPF_N) * 8, hipMemcpyDeviceToHost, s));
     return QK_OK;
 }
 
@@ -274,7 +278,9 @@ int root_test_finish(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, s
     }
     const uint64_t stop = ctx->h_small[SMALL_STOP];
     hits.resize(cnt);
-    if (cnt) {
+    if (cnt && cnt <= std::min<size_t>(ctx->hits_cap, SMALL_HITPF_N)) {
+        memcpy(hits.data(), ctx->h_small + SMALL_HITPF, cnt * 8);
+    } else if (cnt) {
         QK_HIP_TRY(hipMemcpyAsync(hits.data(), ctx->d_hits, cnt * 8, hipMemcpyDeviceToHost, s));
         QK_HIP_TRY(hipStreamSynchronize(s));
     }

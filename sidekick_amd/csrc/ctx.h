@@ -69,6 +69,8 @@ namespace qk {
 constexpr size_t SMALL_WORDS = 4096;   // >= max partial words (2*1024+2) plus counters
 constexpr size_t SMALL_NHITS = 3072;   // hit counter
 constexpr size_t SMALL_STOP = 3073;    // first stop index
+constexpr size_t SMALL_HITPF = 3076;   // h_small only: the first hits, copied with the counters
+constexpr size_t SMALL_HITPF_N = SMALL_WORDS - SMALL_HITPF;
 
 hipStream_t pick_stream(qk_ctx *ctx, void *stream);
 // order stream s after the previous user of the context's scratch buffers
