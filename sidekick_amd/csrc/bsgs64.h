@@ -128,35 +128,6 @@ __device__ __forceinline__ uint64_t shift32(uint64_t B) {
     "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
     "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
 
-// half: the two C0 carries on the scalar unit, the two C1 carries per lane
-// (kv) — one more VALU and two fewer SALU than QK_MAC64M, to balance the two
-// issue ports (MODE 2 uses it for the first SG MACs of a wave's tile).  P1 is
-// read 4 and P3 3 instructions after their writes.
-#define QK_MAC64H(P0, P1, P2, P3, T)                                                                    \
-    "v_mad_u64_u32 %[C0], " P0 ", %[bl], %[a0], %[C0]\n\t"                                             \
-    "v_mad_u64_u32 %[C1], " P1 ", %[bh], %[a0], %[C1]\n\t"                                             \
-    "v_mad_u64_u32 %[C0], " P2 ", %[sl], %[a1], %[C0]\n\t"                                             \
-    "v_mad_u64_u32 %[C1], " P3 ", %[sh], %[a1], %[C1]\n\t"                                             \
-    "s_bcnt1_i32_b64 " T ", " P0 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
-    "v_addc_co_u32_e64 %[kv], " P1 ", %[kv], 0, " P1 "\n\t"                                             \
-    "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
-    "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
-
-template <int SET>
-__device__ __forceinline__ void mac_h(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &kv, uint32_t a0,
-                                      uint32_t a1, uint4 b) {
-    if constexpr (SET == 0)
-        asm volatile(QK_EXPAND(QK_MAC64H, QK_SET0T)
-                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [kv] "+v"(kv)
-                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
-                     : "scc", "s56", QK_CLOB0);
-    else
-        asm volatile(QK_EXPAND(QK_MAC64H, QK_SET1T)
-                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [kv] "+v"(kv)
-                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
-                     : "scc", "s57", QK_CLOB1);
-}
-
 template <int SET>
 __device__ __forceinline__ void mac_m(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &k1, uint32_t &kv,
                                       uint32_t a0, uint32_t a1, uint4 b) {
@@ -366,15 +337,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
                         const int m = r * 2 + c;   // MAC index in the tile: parity picks the SGPR set
-                        if constexpr (MODE == 2) {
-                            if (m < SG) {
-                                if (m % 2 == 0) mac_h<0>(C0[r][c], C1[r][c], K0[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
-                                else mac_h<1>(C0[r][c], C1[r][c], K0[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
-                            } else {
-                                if (m % 2 == 0) mac_m<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
-                                else mac_m<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
-                            }
-                        } else if constexpr (MODE == 1) {
+                        if constexpr (MODE == 1) {
                             if (m % 2 == 0) mac_m<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                             else mac_m<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                         } else if (m < SG) {
@@ -422,13 +385,10 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             const int m = r * 2 + c;
             unsigned __int128 v = (unsigned __int128)C0[r][c] + ((unsigned __int128)C1[r][c] << 32);
             // scalar counts are the wave's totals: added once, by lane 0
-            // MODE 2: C0 carries scalar everywhere; C1 carries per lane (KV),
-            // plus the scalar K1 of the MODE-1 MACs (m >= SG)
-            const bool s0 = MODE >= 1 || m < SG, s1 = MODE == 0 && m < SG;
+            const bool s0 = MODE == 1 || m < SG, s1 = MODE == 0 && m < SG;
             const uint32_t k0 = s0 ? (lane == 0 ? K0[r][c] : 0u) : K0[r][c];
             uint64_t k1 = s1 ? (lane == 0 ? K1[r][c] : 0u) : K1[r][c];
-            if (MODE == 1 || (MODE == 2 && m >= SG)) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];
-            if (MODE == 2 && m < SG) k1 = KV[r][c];
+            if (MODE == 1) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];
             v += (unsigned __int128)k0 * C64 + (unsigned __int128)k1 * W1;
             put((r + (OFF ? 0 : 1)) * NB + cb + c, mod_p128(v));
         }

@@ -66,11 +66,6 @@ int main() {
         {"mode0 sg18 prefetch", k_var<10, 0, 18, 0, 3, 1>, 3},
         {"mode0 sg12 prefetch", k_var<10, 0, 12, 0, 3, 1>, 3},
         {"mode1 prefetch occ2", k_var<10, 1, 0, 0, 2, 1>, 2},
-        {"mode2 sg2 (2 half-scalar MACs)", k_var<10, 2, 2, 0, 3>, 3},
-        {"mode2 sg4", k_var<10, 2, 4, 0, 3>, 3},
-        {"mode2 sg6", k_var<10, 2, 6, 0, 3>, 3},
-        {"mode2 sg9", k_var<10, 2, 9, 0, 3>, 3},
-        {"mode2 sg18 (all half)", k_var<10, 2, 18, 0, 3>, 3},
         {"ablate: no MACs", k_var<10, 1, 0, 1, 3>, 3},
         {"ablate: no modmuls", k_var<10, 1, 0, 2, 3>, 3},
     };
