@@ -328,7 +328,8 @@ def test_bsgs_rare_wrap_branch(golden, t):
 P32, P64 = 4294967291, 18446744073709551557
 
 
-@pytest.mark.parametrize("bits,t,m", [(32, 32, 1_000_003), (64, 80, 500_009)])
+@pytest.mark.parametrize("bits,t,m", [(32, 32, 1_000_003), (64, 80, 500_009), (32, 100, 1_000_003),
+                                      (64, 100, 500_009)])
 def test_beyond_2pow32_ids(bits, t, m):
     """Maximum sizes: one encode over more than 2^32 ids (17 GB of u32, 34 GB
     of u64).  The stream is one oracle-encoded block tiled R times, so the
@@ -369,5 +370,33 @@ def test_root_test_positions_beyond_2pow32():
         q.insert(r)
     hits = q.root_test(q.to_coeffs(), log)
     assert hits == want
+    del log
+    torch.cuda.empty_cache()
+
+
+def test_root_test_u64_positions_beyond_2pow32():
+    """u64 log of 4.3e9 entries (34 GB): roots planted at the start, past
+    2^32 and at the end come back as exact 64-bit positions (d = 3 runs the
+    Horner kernel; the 17-root case the baby-step/giant-step one)."""
+    m = 500_009
+    blk = coracle.splitmix_u64(0x5107, m)
+    R = (1 << 32) // m + 2
+    n = R * m
+    cands = [v for v in range(2, 200) if not np.isin(np.uint64(v), blk)]
+    log = dev_u64(blk).repeat(R)
+    for d in (3, 17):
+        roots = cands[:d]
+        pos = sorted({5 + 3 * i for i in range(d // 2)} | {(1 << 32) + 7 + 11 * i for i in range(d - d // 2 - 1)}
+                     | {n - 1})
+        assert len(pos) == d
+        saved = [int(log[p_].item()) for p_ in pos]
+        for p_, r in zip(pos, roots):
+            log[p_] = int(np.uint64(r).view(np.int64))
+        q = sk.PowerSumQuackU64(d)
+        for r in roots:
+            q.insert(r)
+        assert q.root_test(q.to_coeffs(), log) == pos, d
+        for p_, v in zip(pos, saved):
+            log[p_] = v
     del log
     torch.cuda.empty_cache()
