@@ -80,13 +80,15 @@ def test_stream_u64_1000(golden):
 
 @pytest.mark.parametrize("bits", [32, 64])
 def test_insert_remove_every_threshold_vs_oracle(bits):
-    """The host insert walks the powers as four interleaved chains for t >= 8:
-    every threshold 1..41 (each tail length) and ids at the field edges
-    (0, 1, p - 1, p, p + 1, 2^w - 1) match the oracle; remove() undoes insert."""
+    """The host insert walks the powers as four interleaved chains for t >= 8
+    (u32 on an AVX-512 CPU: eight chains in the lanes of a zmm): every
+    threshold 1..41 (each tail length) plus long walks, and ids at the field
+    edges (0, 1, p - 1, p, p + 1, 2^w - 1) match the oracle; remove() undoes
+    insert."""
     rnd = random.Random(5 * bits)
     P = qo.MOD[bits]
     edge = [0, 1, 2, P - 1, P, P + 1, (1 << bits) - 1, (1 << bits) - 2, 1 << (bits - 1)]
-    for t in range(1, 42):
+    for t in list(range(1, 42)) + [63, 64, 65, 80, 257, 1024]:
         ids = edge + [rnd.getrandbits(bits) for _ in range(30)]
         q = Q(bits, t)
         oq = qo.OracleQuack(t, bits)
