@@ -362,6 +362,46 @@ uint64_t qk_u64_eval(const uint64_t *c, uint32_t d, uint64_t id) {
 // for u64; a root iff the canonical value is 0.
 } // extern "C"
 namespace {
+// u32 candidate scan on an AVX-512 CPU: 32 candidates per iteration as four
+// independent zmm Horner chains (lane value r < 2^32 lazy: r <- r x + c_i is
+// < 2^64, then the two 2^32 == 5 folds); a root iff r == 0 or r == p.  Hits
+// in log order.  Returns the number of hits (all counted, <= cap stored).
+QK_AVX512 static size_t root_scan32_avx512(const uint32_t *c, uint32_t d, const uint32_t *log, size_t n,
+                                           uint64_t *hits, size_t cap) {
+    const __m512i P = _mm512_set1_epi64(P32), TWO32 = _mm512_set1_epi64(1ll << 32), ONE = _mm512_set1_epi64(1);
+    size_t m = 0;
+    for (size_t i = 0; i < n; i += 32) {
+        __m512i x[4], r[4];
+        __mmask8 valid[4];
+        for (int u = 0; u < 4; ++u) {
+            const size_t b = i + 8 * (size_t)u;
+            const size_t rem = b < n ? n - b : 0;
+            valid[u] = rem >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << rem) - 1u);
+            const __m512i v = _mm512_cvtepu32_epi64(_mm256_maskz_loadu_epi32(valid[u], log + (b < n ? b : 0)));
+            x[u] = _mm512_mask_sub_epi64(v, _mm512_cmpge_epu64_mask(v, P), v, P);   // canonical id
+            r[u] = ONE;
+        }
+        for (uint32_t k = 0; k < d; ++k) {
+            const __m512i ck = _mm512_set1_epi64(c[k]);
+            for (int u = 0; u < 4; ++u) {
+                const __m512i v = fold512(fold512(_mm512_add_epi64(_mm512_mul_epu32(r[u], x[u]), ck)));
+                r[u] = _mm512_mask_sub_epi64(v, _mm512_cmpge_epu64_mask(v, TWO32), v, P);   // < 2^32
+            }
+        }
+        for (int u = 0; u < 4; ++u) {
+            __mmask8 h = (_mm512_cmpeq_epu64_mask(r[u], _mm512_setzero_si512()) |
+                          _mm512_cmpeq_epu64_mask(r[u], P)) & valid[u];
+            while (h) {
+                const int j = __builtin_ctz(h);
+                if (m < cap && hits) hits[m] = i + 8 * (size_t)u + j;
+                ++m;
+                h &= (__mmask8)(h - 1);
+            }
+        }
+    }
+    return m;
+}
+
 template <typename Q, typename T, typename ToCoeffs, typename IsRoot>
 int decode_host_impl(const Q *diff, const T *log, size_t n, int stop_at_last, uint64_t *hits, size_t cap,
                      size_t *n_hits, ToCoeffs to_coeffs, IsRoot is_root) {
@@ -373,6 +413,17 @@ int decode_host_impl(const Q *diff, const T *log, size_t n, int stop_at_last, ui
     if (int rc = to_coeffs(diff, c.data(), (uint32_t)c.size(), &d)) return rc;
     const bool stop = stop_at_last && diff->has_last;
     size_t m = 0;
+    if constexpr (sizeof(T) == 4) {
+        if (cpu_has_avx512() && d > 0) {
+            size_t ne = n;   // the scan ends at the first entry equal to last_value (media_client.rs:307-309)
+            if (stop)
+                for (size_t i = 0; i < n; ++i)
+                    if (log[i] == (T)diff->last_value) { ne = i; break; }
+            m = root_scan32_avx512(c.data(), d, log, ne, hits, cap);
+            *n_hits = m;
+            return m > cap || (m && !hits) ? QK_E_CAPACITY : QK_OK;
+        }
+    }
     for (size_t i = 0; i < n; ++i) {
         if (stop && log[i] == (T)diff->last_value) break;   // media_client.rs:307-309
         if (is_root(c.data(), d, log[i])) {

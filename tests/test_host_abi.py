@@ -215,6 +215,29 @@ def test_merge_partial_roundtrip():
         assert m == whole
 
 
+@pytest.mark.parametrize("n", [1, 7, 31, 32, 33, 1001])
+def test_decode_host_u32_edges_and_ragged(n):
+    """u32 candidate scan (AVX-512 lanes on such CPUs, 32 candidates per
+    iteration): logs of every ragged length, ids >= p aliasing ids < 5, id 0
+    as a root, and the stop at last_value inside the scan."""
+    import numpy as np
+    from oracle import quack_oracle as qo
+    P = qo.MOD[32]
+    rng = np.random.default_rng(n)
+    log = qo.ids_u32(0xE0 + n, n, 0)
+    edge = np.array([0, 1, 3, P, P + 1, P + 3, 2**32 - 1, P - 1], dtype=np.uint32)
+    log[rng.choice(n, min(n, len(edge)), replace=False)] = edge[:min(n, len(edge))]
+    for drops in ([0, 1, 3], [P - 1, 7, 11], [int(log[-1])]):
+        diff = sk.PowerSumQuackU32(16)
+        for v in drops:
+            diff.insert(v)
+        for stop in (False, True):
+            got = diff.decode_host(log, stop_at_last=stop)
+            want = qo.root_test_indices(diff.to_coeffs(), log.tolist(), P,
+                                        stop_value=diff.last_value() if stop else None)
+            assert got == want, (n, drops, stop)
+
+
 @pytest.mark.parametrize("bits,d,stop", [(32, 5, False), (32, 32, True), (64, 20, True), (64, 1, False)])
 def test_decode_host_matches_oracle(bits, d, stop):
     """qk_*_decode_host (the receiver's short-log path) vs the oracle's root
