@@ -306,6 +306,29 @@ int qk_u64_merge_partial(qk_u64 *q, const uint64_t *part, int has_last, uint64_t
 // ----------------------------------------------------------- to_coeffs
 // Newton's identities, 0-indexed: c[i] = -(S[i] + sum_{j<i} S[j] c[i-j-1]) / (i+1).
 // Inverses of 1..d by the linear recurrence inv[i] = -(p/i) * inv[p mod i].
+} // extern "C"
+namespace {
+// sum_{j<i} S[j] c[i-j-1] on AVX-512: eight products per step (c read
+// backwards by a lane reversal), each folded once to < 6 2^32 and summed in
+// 64-bit lanes (< 2^29 terms cannot overflow), the lanes added at the end.
+QK_AVX512 static uint64_t newton_dot_avx512(const uint32_t *S, const uint32_t *c, uint32_t i) {
+    const __m512i rev = _mm512_set_epi64(0, 1, 2, 3, 4, 5, 6, 7);
+    __m512i acc = _mm512_setzero_si512();
+    uint32_t j = 0;
+    for (; j + 8 <= i; j += 8) {
+        const __m512i s = _mm512_cvtepu32_epi64(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(S + j)));
+        // c[i-j-1] .. c[i-j-8]: load c[i-j-8 .. i-j-1] and reverse the lanes
+        const __m512i cv = _mm512_permutexvar_epi64(
+            rev, _mm512_cvtepu32_epi64(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(c + (i - j - 8)))));
+        acc = _mm512_add_epi64(acc, fold512(_mm512_mul_epu32(s, cv)));
+    }
+    uint64_t r = _mm512_reduce_add_epi64(acc);   // < 2^29 * 6 * 2^32
+    for (; j < i; ++j) r += mul32(S[j], c[i - j - 1]);
+    return r;
+}
+} // namespace
+extern "C" {
+
 int qk_u32_to_coeffs(const qk_u32 *q, uint32_t *c, uint32_t cap, uint32_t *d_out) {
     if (!q || !d_out) return QK_E_INVAL;
     const uint32_t d = q->count;
@@ -314,9 +337,14 @@ int qk_u32_to_coeffs(const qk_u32 *q, uint32_t *c, uint32_t cap, uint32_t *d_out
     if (cap < d || (d && !c)) return QK_E_CAPACITY;
     std::vector<uint32_t> inv(d + 2, 1);
     for (uint32_t i = 2; i <= d; ++i) inv[i] = mul32(P32 - P32 / i, inv[P32 % i]);
+    const bool vec = d > 16 && cpu_has_avx512();
     for (uint32_t i = 0; i < d; ++i) {
-        uint64_t acc = q->power_sums[i];            // lazy: < 2^32 + i * 2^32
-        for (uint32_t j = 0; j < i; ++j) acc += mul32(q->power_sums[j], c[i - j - 1]);
+        uint64_t acc = q->power_sums[i];            // lazy: < 2^32 + i * 6 * 2^32
+        if (vec) {
+            acc += newton_dot_avx512(q->power_sums, c, i);
+        } else {
+            for (uint32_t j = 0; j < i; ++j) acc += mul32(q->power_sums[j], c[i - j - 1]);
+        }
         c[i] = mul32(neg32(canon32(fold64_32(acc))), inv[i + 1]);
     }
     return QK_OK;

@@ -142,8 +142,8 @@ def Q_from(ids, bits, t):
 @pytest.mark.parametrize("bits", [32, 64])
 def test_to_coeffs_and_eval_match_oracle(bits):
     rnd = random.Random(11 * bits)
-    for d in (1, 2, 7, 31, 32):
-        q = Q(bits, 32)
+    for d in (1, 2, 7, 17, 24, 31, 32, 33, 100, 301):   # d > 16: the AVX-512 Newton dot product (u32)
+        q = Q(bits, max(32, d))
         for _ in range(d):
             q.insert(rnd.getrandbits(bits))
         c = q.to_coeffs()
