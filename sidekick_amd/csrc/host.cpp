@@ -58,10 +58,11 @@ int deser(const uint8_t *buf, size_t len, Q *q, uint32_t *t_out, T modulus) {
 // reference walks x, x^2, .., x^t as one dependent chain of modmuls; here
 // the powers run as four independent chains (x^(j+1) * (x^4)^i, j < 4) so the
 // multiplier latency overlaps: ~3x fewer cycles per insert at t >= 16 on one
-// core; u32 inserts on an AVX-512 CPU run eight chains in one zmm instead
-// (another 2-2.5x: t = 32 39 -> 16 ns on the GPU box's EPYC 9575F).  Chain
-// values stay lazy (< 2^32 / < 2^64, any representative); every stored sum
-// is canonical.
+// core; on an AVX-512 CPU the powers run as sixteen chains in two zmm (u32
+// t >= 8, u64 t >= 16) instead: on the GPU box's EPYC 9575F u32 t = 32 / 300
+// 39 -> 16 / 320 -> 114 ns, u64 t = 80 / 300 118 -> 58 / 421 -> 215 ns.
+// Chain values stay lazy (< 2^32 / < 2^64, any representative); every
+// stored sum is canonical.
 namespace {
 struct F32 {
     using T = uint32_t;
@@ -78,13 +79,14 @@ struct F64 {
     static T sub(T s, T y) { return sub64(s, canon64(y)); }
 };
 
-// u32, t >= 16, on a CPU with AVX-512 (the GPU box hosts are Zen 5 EPYCs):
-// eight chains in the eight 64-bit lanes of a zmm — lane j holds x^(j+1) *
-// (x^8)^i — each step one vpmuludq of the lanes by x^8 and the same two
-// pseudo-Mersenne folds as mul32_lazy (2^32 == 5), the sums updated eight at
-// a time (zero-extended loads, truncating stores, masked for the last < 8).
-// Lane values stay < 2^32 (lazy), the stored sums canonical: the results are
-// those of the scalar chains bit for bit (tests/test_host_abi.py, every t).
+// u32 on a CPU with AVX-512 (the GPU box hosts are Zen 5 EPYCs): sixteen
+// chains in the 64-bit lanes of two zmm — lane j of v0 / v1 holds x^(j+1) /
+// x^(j+9) times (x^16)^i — each step one vpmuludq per vector by x^16 and the
+// same two pseudo-Mersenne folds as mul32_lazy (2^32 == 5), the two vectors'
+// steps independent; the sums updated eight at a time (zero-extended loads,
+// truncating stores, masked for the last < 8).  Lane values stay < 2^32
+// (lazy), the stored sums canonical: the results are those of the scalar
+// chains bit for bit (tests/test_host_abi.py, every t).
 #define QK_AVX512 __attribute__((target("avx512f,avx512vl,avx512dq")))
 QK_AVX512 static inline __m512i fold512(__m512i m) {   // l + 5 h of each 64-bit lane
     const __m512i h = _mm512_srli_epi64(m, 32);
@@ -96,33 +98,111 @@ QK_AVX512 static inline __m512i mulmod512(__m512i a, __m512i b) {   // a, b < 2^
     return _mm512_mask_sub_epi64(r, _mm512_cmpge_epu64_mask(r, _mm512_set1_epi64(1ll << 32)), r,
                                  _mm512_set1_epi64(P32));
 }
-QK_AVX512 static void power_walk32_avx512(uint32_t *S, uint32_t t, uint32_t x, bool add) {
+// sums S[k..k+8) (masked past t) += or -= the canonical form of the lanes of v
+QK_AVX512 static inline void acc32_512(uint32_t *S, uint32_t k, uint32_t t, __m512i v, bool add) {
     const __m512i P = _mm512_set1_epi64(P32);
+    const uint32_t rem = t - k;
+    // full chunks unmasked: the next insert's load of the same 32 bytes is
+    // then forwarded from this store (masked stores do not forward)
+    const __mmask8 m = rem >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << rem) - 1u);
+    const __m256i sraw = rem >= 8 ? _mm256_loadu_si256(reinterpret_cast<const __m256i *>(S + k))
+                                  : _mm256_maskz_loadu_epi32(m, S + k);
+    const __m512i s = _mm512_cvtepu32_epi64(sraw);
+    const __m512i y = _mm512_mask_sub_epi64(v, _mm512_cmpge_epu64_mask(v, P), v, P);   // canonical
+    __m512i r;
+    if (add) {
+        r = _mm512_add_epi64(s, y);
+        r = _mm512_mask_sub_epi64(r, _mm512_cmpge_epu64_mask(r, P), r, P);
+    } else {
+        r = _mm512_sub_epi64(s, y);
+        r = _mm512_mask_add_epi64(r, _mm512_cmplt_epu64_mask(s, y), r, P);
+    }
+    if (rem >= 8) _mm256_storeu_si256(reinterpret_cast<__m256i *>(S + k), _mm512_cvtepi64_epi32(r));
+    else _mm512_mask_cvtepi64_storeu_epi32(S + k, m, r);
+}
+// two chains of eight lanes (x^1..x^8 and x^9..x^16, step x^16): the two
+// vector modmuls of a step are independent, so their latency overlaps
+QK_AVX512 static void power_walk32_avx512(uint32_t *S, uint32_t t, uint32_t x, bool add) {
     uint32_t pw[8];
     pw[0] = x;
     for (int j = 1; j < 8; ++j) pw[j] = mul32_lazy(pw[(j - 1) / 2], pw[j / 2]);   // x^(j+1)
-    __m512i v = _mm512_cvtepu32_epi64(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(pw)));
-    const __m512i step = _mm512_set1_epi64(pw[7]);
-    for (uint32_t k = 0; k < t; k += 8) {
-        const uint32_t rem = t - k;
-        // full chunks unmasked: the next insert's load of the same 32 bytes is
-        // then forwarded from this store (masked stores do not forward)
-        const __mmask8 m = rem >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << rem) - 1u);
-        const __m256i sraw = rem >= 8 ? _mm256_loadu_si256(reinterpret_cast<const __m256i *>(S + k))
-                                      : _mm256_maskz_loadu_epi32(m, S + k);
-        const __m512i s = _mm512_cvtepu32_epi64(sraw);
-        const __m512i y = _mm512_mask_sub_epi64(v, _mm512_cmpge_epu64_mask(v, P), v, P);   // canonical
-        __m512i r;
-        if (add) {
-            r = _mm512_add_epi64(s, y);
-            r = _mm512_mask_sub_epi64(r, _mm512_cmpge_epu64_mask(r, P), r, P);
-        } else {
-            r = _mm512_sub_epi64(s, y);
-            r = _mm512_mask_add_epi64(r, _mm512_cmplt_epu64_mask(s, y), r, P);
+    __m512i v0 = _mm512_cvtepu32_epi64(_mm256_loadu_si256(reinterpret_cast<const __m256i *>(pw)));
+    __m512i v1 = t > 8 ? mulmod512(v0, _mm512_set1_epi64(pw[7])) : v0;           // x^9 .. x^16
+    const __m512i step = _mm512_set1_epi64(t > 16 ? mul32_lazy(pw[7], pw[7]) : 0u);   // x^16
+    for (uint32_t k = 0; k < t; k += 16) {
+        acc32_512(S, k, t, v0, add);
+        if (k + 8 < t) acc32_512(S, k + 8, t, v1, add);
+        if (k + 16 < t) {
+            v0 = mulmod512(v0, step);
+            v1 = mulmod512(v1, step);
         }
-        if (rem >= 8) _mm256_storeu_si256(reinterpret_cast<__m256i *>(S + k), _mm512_cvtepi64_epi32(r));
-        else _mm512_mask_cvtepi64_storeu_epi32(S + k, m, r);
-        if (rem > 8) v = mulmod512(v, step);
+    }
+}
+
+// u64 twin (p = 2^64 - 59): the lane product a b of two 64-bit values from
+// four vpmuludq (32-bit halves) with the carries of the middle and low sums
+// restored by compares, then hi 2^64 == 59 hi twice as in mul64_lazy; the
+// result < 2^64 (lazy), == a b.  b's halves are the chain step (hoisted).
+QK_AVX512 static inline __m512i mulmod64_512(__m512i a, __m512i b0, __m512i b1) {
+    const __m512i a1 = _mm512_srli_epi64(a, 32);
+    const __m512i p00 = _mm512_mul_epu32(a, b0), p01 = _mm512_mul_epu32(a, b1);
+    const __m512i p10 = _mm512_mul_epu32(a1, b0), p11 = _mm512_mul_epu32(a1, b1);
+    const __m512i mid = _mm512_add_epi64(p01, p10);
+    const __mmask8 cm = _mm512_cmplt_epu64_mask(mid, p01);             // mid wrapped: + 2^96
+    const __m512i lo = _mm512_add_epi64(p00, _mm512_slli_epi64(mid, 32));
+    const __mmask8 cl = _mm512_cmplt_epu64_mask(lo, p00);              // lo wrapped: + 2^64
+    __m512i hi = _mm512_add_epi64(p11, _mm512_srli_epi64(mid, 32));
+    hi = _mm512_mask_add_epi64(hi, cm, hi, _mm512_set1_epi64(1ll << 32));
+    hi = _mm512_mask_add_epi64(hi, cl, hi, _mm512_set1_epi64(1));      // a b = hi 2^64 + lo exactly
+    // 59 hi + lo = c 2^64 + s2 with c <= 66, then s2 + 59 c (one more wrap at most)
+    const __m512i c59 = _mm512_set1_epi64(59);
+    const __m512i x = _mm512_mul_epu32(hi, c59), y = _mm512_mul_epu32(_mm512_srli_epi64(hi, 32), c59);
+    const __m512i s1 = _mm512_add_epi64(x, _mm512_slli_epi64(y, 32));
+    const __mmask8 c1 = _mm512_cmplt_epu64_mask(s1, x);
+    const __m512i s2 = _mm512_add_epi64(s1, lo);
+    const __mmask8 c2 = _mm512_cmplt_epu64_mask(s2, s1);
+    __m512i c = _mm512_srli_epi64(y, 32);
+    c = _mm512_mask_add_epi64(c, c1, c, _mm512_set1_epi64(1));
+    c = _mm512_mask_add_epi64(c, c2, c, _mm512_set1_epi64(1));
+    const __m512i r = _mm512_add_epi64(s2, _mm512_mul_epu32(c, c59));
+    return _mm512_mask_add_epi64(r, _mm512_cmplt_epu64_mask(r, s2), r, c59);
+}
+QK_AVX512 static inline void acc64_512(uint64_t *S, uint32_t k, uint32_t t, __m512i v, bool add) {
+    const __m512i P = _mm512_set1_epi64((long long)P64), c59 = _mm512_set1_epi64(59);
+    const uint32_t rem = t - k;
+    const __mmask8 m = rem >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << rem) - 1u);
+    const __m512i s = rem >= 8 ? _mm512_loadu_si512(S + k) : _mm512_maskz_loadu_epi64(m, S + k);
+    const __m512i y = _mm512_mask_sub_epi64(v, _mm512_cmpge_epu64_mask(v, P), v, P);   // canonical
+    __m512i r;
+    if (add) {   // s + y < 2p: a wrap past 2^64 means s + y - p = r + 59
+        r = _mm512_add_epi64(s, y);
+        const __mmask8 w = _mm512_cmplt_epu64_mask(r, s);
+        r = _mm512_mask_add_epi64(r, w, r, c59);
+        r = _mm512_mask_sub_epi64(r, _mm512_cmpge_epu64_mask(r, P) & (__mmask8)~w, r, P);
+    } else {     // s - y, + p when it borrowed
+        r = _mm512_sub_epi64(s, y);
+        r = _mm512_mask_add_epi64(r, _mm512_cmplt_epu64_mask(s, y), r, P);
+    }
+    if (rem >= 8) _mm512_storeu_si512(S + k, r);
+    else _mm512_mask_storeu_epi64(S + k, m, r);
+}
+QK_AVX512 static void power_walk64_avx512(uint64_t *S, uint32_t t, uint64_t x, bool add) {
+    uint64_t pw[8];
+    pw[0] = x;
+    for (int j = 1; j < 8; ++j) pw[j] = mul64_lazy(pw[(j - 1) / 2], pw[j / 2]);   // x^(j+1)
+    const uint64_t x16 = t > 16 ? mul64_lazy(pw[7], pw[7]) : 0;
+    __m512i v0 = _mm512_loadu_si512(pw);
+    __m512i v1 = t > 8 ? mulmod64_512(v0, _mm512_set1_epi64((long long)(pw[7] & 0xFFFFFFFFull)),
+                                      _mm512_set1_epi64((long long)(pw[7] >> 32)))
+                       : v0;                                                          // x^9 .. x^16
+    const __m512i b0 = _mm512_set1_epi64((long long)(x16 & 0xFFFFFFFFull)), b1 = _mm512_set1_epi64((long long)(x16 >> 32));
+    for (uint32_t k = 0; k < t; k += 16) {
+        acc64_512(S, k, t, v0, add);
+        if (k + 8 < t) acc64_512(S, k + 8, t, v1, add);
+        if (k + 16 < t) {
+            v0 = mulmod64_512(v0, b0, b1);
+            v1 = mulmod64_512(v1, b0, b1);
+        }
     }
 }
 
@@ -138,6 +218,11 @@ inline void power_walk(typename F::T *S, uint32_t t, typename F::T x) {
     if constexpr (sizeof(T) == 4) {
         if (t >= 8 && cpu_has_avx512()) {
             power_walk32_avx512(S, t, x, ADD);
+            return;
+        }
+    } else {
+        if (t >= 16 && cpu_has_avx512()) {   // below 16 the scalar chains win (measured)
+            power_walk64_avx512(S, t, x, ADD);
             return;
         }
     }
