@@ -435,6 +435,35 @@ int qk_u32_to_coeffs(const qk_u32 *q, uint32_t *c, uint32_t cap, uint32_t *d_out
     return QK_OK;
 }
 
+} // extern "C"
+namespace {
+// u64 twin of newton_dot_avx512: lane products by mulmod64_512 (< 2^64, lazy)
+// summed with the 2^64 == 59 wrap fix, the eight lanes folded canonically
+QK_AVX512 static uint64_t newton_dot64_avx512(const uint64_t *S, const uint64_t *c, uint32_t i) {
+    const __m512i rev = _mm512_set_epi64(0, 1, 2, 3, 4, 5, 6, 7), c59 = _mm512_set1_epi64(59);
+    __m512i acc = _mm512_setzero_si512();
+    uint32_t j = 0;
+    for (; j + 8 <= i; j += 8) {
+        const __m512i s = _mm512_loadu_si512(S + j);
+        const __m512i cv = _mm512_permutexvar_epi64(rev, _mm512_loadu_si512(c + (i - j - 8)));
+        const __m512i pr = mulmod64_512(s, cv, _mm512_srli_epi64(cv, 32));
+        // acc, pr < 2^64 (lazy): a wrap adds 59, and that +59 can wrap once more
+        // (sm > 2^64 - 60 only when both were near 2^64): then +59 again
+        const __m512i sm = _mm512_add_epi64(acc, pr);
+        const __mmask8 w1 = _mm512_cmplt_epu64_mask(sm, pr);
+        const __m512i s1 = _mm512_mask_add_epi64(sm, w1, sm, c59);
+        acc = _mm512_mask_add_epi64(s1, w1 & _mm512_cmplt_epu64_mask(s1, c59), s1, c59);
+    }
+    alignas(64) uint64_t lane[8];
+    _mm512_store_si512(lane, acc);
+    uint64_t r = 0;
+    for (int k = 0; k < 8; ++k) r = add64(r, canon64(lane[k]));
+    for (; j < i; ++j) r = add64(r, mul64(S[j], c[i - j - 1]));
+    return r;
+}
+} // namespace
+extern "C" {
+
 int qk_u64_to_coeffs(const qk_u64 *q, uint64_t *c, uint32_t cap, uint32_t *d_out) {
     if (!q || !d_out) return QK_E_INVAL;
     const uint32_t d = q->count;
@@ -443,9 +472,12 @@ int qk_u64_to_coeffs(const qk_u64 *q, uint64_t *c, uint32_t cap, uint32_t *d_out
     if (cap < d || (d && !c)) return QK_E_CAPACITY;
     std::vector<uint64_t> inv(d + 2, 1);
     for (uint32_t i = 2; i <= d; ++i) inv[i] = mul64(P64 - P64 / i, inv[P64 % i]);
+    const bool vec = d > 16 && cpu_has_avx512();
     for (uint32_t i = 0; i < d; ++i) {
         uint64_t acc = q->power_sums[i];
-        for (uint32_t j = 0; j < i; ++j) acc = add64(acc, mul64(q->power_sums[j], c[i - j - 1]));
+        if (vec) acc = add64(acc, newton_dot64_avx512(q->power_sums, c, i));
+        else
+            for (uint32_t j = 0; j < i; ++j) acc = add64(acc, mul64(q->power_sums[j], c[i - j - 1]));
         c[i] = mul64(neg64(acc), inv[i + 1]);
     }
     return QK_OK;
@@ -515,6 +547,47 @@ QK_AVX512 static size_t root_scan32_avx512(const uint32_t *c, uint32_t d, const 
     return m;
 }
 
+// u64 twin: r <- r x + c_i with the lane products of mulmod64_512 (x's
+// halves per lane) and a lazy add (a wrap past 2^64 adds 59); a root iff
+// r == 0 or r == p.  Same stop handling and hit order as the u32 scan.
+QK_AVX512 static size_t root_scan64_avx512(const uint64_t *c, uint32_t d, const uint64_t *log, size_t n,
+                                           uint64_t *hits, size_t cap) {
+    const __m512i P = _mm512_set1_epi64((long long)P64), c59 = _mm512_set1_epi64(59), ONE = _mm512_set1_epi64(1);
+    size_t m = 0;
+    for (size_t i = 0; i < n; i += 32) {
+        __m512i x0[4], x1[4], r[4];
+        __mmask8 valid[4];
+        for (int u = 0; u < 4; ++u) {
+            const size_t b = i + 8 * (size_t)u;
+            const size_t rem = b < n ? n - b : 0;
+            valid[u] = rem >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << rem) - 1u);
+            const __m512i v = _mm512_maskz_loadu_epi64(valid[u], log + (b < n ? b : 0));
+            x0[u] = v;                                  // vpmuludq reads the low halves
+            x1[u] = _mm512_srli_epi64(v, 32);
+            r[u] = ONE;
+        }
+        for (uint32_t k = 0; k < d; ++k) {
+            const __m512i ck = _mm512_set1_epi64((long long)c[k]);
+            for (int u = 0; u < 4; ++u) {
+                const __m512i pr = mulmod64_512(r[u], x0[u], x1[u]);
+                const __m512i sm = _mm512_add_epi64(pr, ck);
+                r[u] = _mm512_mask_add_epi64(sm, _mm512_cmplt_epu64_mask(sm, pr), sm, c59);
+            }
+        }
+        for (int u = 0; u < 4; ++u) {
+            __mmask8 h = (_mm512_cmpeq_epu64_mask(r[u], _mm512_setzero_si512()) |
+                          _mm512_cmpeq_epu64_mask(r[u], P)) & valid[u];
+            while (h) {
+                const int j = __builtin_ctz(h);
+                if (m < cap && hits) hits[m] = i + 8 * (size_t)u + j;
+                ++m;
+                h &= (__mmask8)(h - 1);
+            }
+        }
+    }
+    return m;
+}
+
 template <typename Q, typename T, typename ToCoeffs, typename IsRoot>
 int decode_host_impl(const Q *diff, const T *log, size_t n, int stop_at_last, uint64_t *hits, size_t cap,
                      size_t *n_hits, ToCoeffs to_coeffs, IsRoot is_root) {
@@ -526,16 +599,15 @@ int decode_host_impl(const Q *diff, const T *log, size_t n, int stop_at_last, ui
     if (int rc = to_coeffs(diff, c.data(), (uint32_t)c.size(), &d)) return rc;
     const bool stop = stop_at_last && diff->has_last;
     size_t m = 0;
-    if constexpr (sizeof(T) == 4) {
-        if (cpu_has_avx512() && d > 0) {
-            size_t ne = n;   // the scan ends at the first entry equal to last_value (media_client.rs:307-309)
-            if (stop)
-                for (size_t i = 0; i < n; ++i)
-                    if (log[i] == (T)diff->last_value) { ne = i; break; }
-            m = root_scan32_avx512(c.data(), d, log, ne, hits, cap);
-            *n_hits = m;
-            return m > cap || (m && !hits) ? QK_E_CAPACITY : QK_OK;
-        }
+    if (cpu_has_avx512() && d > 0) {
+        size_t ne = n;   // the scan ends at the first entry equal to last_value (media_client.rs:307-309)
+        if (stop)
+            for (size_t i = 0; i < n; ++i)
+                if (log[i] == (T)diff->last_value) { ne = i; break; }
+        if constexpr (sizeof(T) == 4) m = root_scan32_avx512(c.data(), d, log, ne, hits, cap);
+        else m = root_scan64_avx512(c.data(), d, log, ne, hits, cap);
+        *n_hits = m;
+        return m > cap || (m && !hits) ? QK_E_CAPACITY : QK_OK;
     }
     for (size_t i = 0; i < n; ++i) {
         if (stop && log[i] == (T)diff->last_value) break;   // media_client.rs:307-309

@@ -215,20 +215,22 @@ def test_merge_partial_roundtrip():
         assert m == whole
 
 
+@pytest.mark.parametrize("bits", [32, 64])
 @pytest.mark.parametrize("n", [1, 7, 31, 32, 33, 1001])
-def test_decode_host_u32_edges_and_ragged(n):
-    """u32 candidate scan (AVX-512 lanes on such CPUs, 32 candidates per
-    iteration): logs of every ragged length, ids >= p aliasing ids < 5, id 0
+def test_decode_host_edges_and_ragged(bits, n):
+    """Host candidate scan (AVX-512 lanes on such CPUs, 32 candidates per
+    iteration): logs of every ragged length, ids >= p aliasing small ids, id 0
     as a root, and the stop at last_value inside the scan."""
     import numpy as np
     from oracle import quack_oracle as qo
-    P = qo.MOD[32]
-    rng = np.random.default_rng(n)
-    log = qo.ids_u32(0xE0 + n, n, 0)
-    edge = np.array([0, 1, 3, P, P + 1, P + 3, 2**32 - 1, P - 1], dtype=np.uint32)
+    P = qo.MOD[bits]
+    rng = np.random.default_rng(n + bits)
+    log = (qo.ids_u32 if bits == 32 else qo.ids_u64)(0xE0 + n, n, 0)
+    dt = np.uint32 if bits == 32 else np.uint64
+    edge = np.array([0, 1, 3, P, P + 1, P + 3, 2**bits - 1, P - 1], dtype=dt)
     log[rng.choice(n, min(n, len(edge)), replace=False)] = edge[:min(n, len(edge))]
     for drops in ([0, 1, 3], [P - 1, 7, 11], [int(log[-1])]):
-        diff = sk.PowerSumQuackU32(16)
+        diff = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(16)
         for v in drops:
             diff.insert(v)
         for stop in (False, True):
