@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "ctx.h"
@@ -161,9 +162,37 @@ __global__ void k_init_counters(uint64_t *c) {
     c[1] = ~0ull;
 }
 
+// Pageable -> pinned staging copy, split over a few host threads: one core's
+// memcpy (~24 GB/s) is under half of the PCIe Gen5 rate the DMA can take.
+static void staging_copy(void *dst, const void *src, size_t bytes) {
+    static const unsigned nthr = [] {
+        const unsigned hc = std::thread::hardware_concurrency();
+        return hc >= 4 ? std::min(8u, hc / 2) : 1u;
+    }();
+    if (nthr <= 1 || bytes < ((size_t)8 << 20)) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t part = (bytes / nthr + 4095) & ~(size_t)4095;
+    std::vector<std::thread> pool;
+    pool.reserve(nthr - 1);
+    size_t done = part;   // pieces below `done` are handed out (piece 0 to this thread)
+    try {
+        for (unsigned i = 1; i < nthr && done < bytes; ++i) {
+            const size_t b = done, e = std::min(bytes, done + part);
+            pool.emplace_back([=] { memcpy((char *)dst + b, (const char *)src + b, e - b); });
+            done = e;
+        }
+    } catch (...) {   // no thread to spare: this thread copies the rest (no exception crosses the C ABI)
+    }
+    memcpy(dst, src, std::min(bytes, part));
+    if (done < bytes) memcpy((char *)dst + done, (const char *)src + done, bytes - done);
+    for (auto &th : pool) th.join();
+}
+
 // Host-resident ids: chunked H2D on copy_stream overlapped with the encode
 // kernel on ctx->stream; two device slots.  Pinned input is DMA'd directly,
-// pageable input is first copied into pinned staging.
+// pageable input is first copied into pinned staging (staging_copy).
 template <typename IdT, typename Launch>
 static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t, size_t words, Launch launch,
                             uint64_t *partial_out) {
@@ -208,7 +237,7 @@ static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t,
         }
         const void *src = h_ids + off;
         if (!pinned) {
-            memcpy(ctx->h_stage[slot], h_ids + off, m * sizeof(IdT));
+            staging_copy(ctx->h_stage[slot], h_ids + off, m * sizeof(IdT));
             src = ctx->h_stage[slot];
         }
         QK_HIP_TRY(hipMemcpyAsync(ctx->d_stage[slot], src, m * sizeof(IdT), hipMemcpyHostToDevice, cs));
