@@ -765,7 +765,9 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     // copies (16 B per packet), counters, hipCUB temp storage.  Arena 2: the
     // flow table (C slots) and slot -> rank.  Arena 1, per flow: see below.
     const uint64_t cmax = std::min<uint64_t>(next_pow2(2 * (uint64_t)n + 2), 1ull << 31);
-    uint64_t C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(4096, 4 * (uint64_t)ctx->flow_hint)));
+    // table slots per expected flow (QK_TUNE_FLOW_LOAD overrides for measurements)
+    static const uint64_t spf = [] { const char *e = getenv("QK_TUNE_FLOW_LOAD"); return e ? (uint64_t)atoi(e) : 4ull; }();
+    uint64_t C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(4096, spf * (uint64_t)ctx->flow_hint)));
     size_t tb = 0;
     {
         uint32_t *u = nullptr;
