@@ -10,7 +10,11 @@ rank 0 (weak scaling: every GPU owns a fixed 1e9-id shard of one global
 stream).  For N > 1 the data path is the library's native communicator
 (qk_u32_encode_sharded_async: encode + ONE ncclReduce over xGMI, comm.hip);
 torch.distributed (gloo) only carries the control plane — the RCCL unique
-id, the barriers around the timed region and the max-over-ranks time.
+id, the barriers around the timed region and the max-over-ranks time.  On a
+node with fewer GPUs than ranks (a one-GPU rehearsal: RCCL refuses two ranks
+on one device) the same native protocol runs with its collectives over gloo
+(qk_comm_init_host), and the line says so; with enough GPUs a communicator
+that cannot be built is an error, never a silent fallback.
 
     python bench.py [--gpus N --steps K --warmup W --n IDS_PER_GPU --t 32 --bits 32]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -19,7 +23,10 @@ Rank 0 prints ONE JSON line.  Alongside the metric it reports
   roofline      the encode kernel's achieved algorithmic HBM bytes/s (4 B per
                 u32 id) over its average launch duration, measured with HIP
                 events on the launch stream, against the 8 TB/s HBM3E peak;
-                plus the integer-VALU view (modmuls/s);
+                and `valu`, the integer-issue roofline that actually binds
+                (tools/issue_roofline.py: the kernel's measured VALU
+                instructions per id x their issue cost, against the SIMD
+                cycles the launch spent per id);
   cpu_baseline  the oracle's scalar C restatement of the reference insert
                 loop on ONE host core over a bounded prefix of the same
                 stream (rank 0, N = 1 only), with a GPU/CPU parity check on
@@ -56,6 +63,33 @@ def load_traffic(bits: int, t: int, n: int):
         return None, None
 
 
+def valu_roofline(bits: int, t: int, n: int, kern_avg_ms: float):
+    """The integer-issue roofline of the encode kernel (tools/issue_roofline.py,
+    profiles/r03/issue_roofline.json): peak = the measured VALU
+    wave-instructions per id x the mean issue cost of the kernel's hot-loop
+    mix; achieved = the SIMD-cycles per id of THIS run's kernel time at the
+    effective clock of the committed counter run (GRBM_GUI_ACTIVE / 8 / its
+    kernel time)."""
+    path = os.path.join(ROOT, "profiles", "r03", "issue_roofline.json")
+    key = {(32, 32): "encode_u32_t32", (64, 80): "encode_u64_t80"}.get((bits, t))
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"][key]
+    except Exception:
+        return None
+    clock = k["clock_ghz"] * 1e9
+    achieved = clock * kern_avg_ms * 1e-3 * 1024 / n
+    peak = k["issue_cycles_per_unit_peak"]
+    return {
+        "bound": "valu-issue", "unit": "SIMD-cycles/id",
+        "valu_insts_per_id": k["valu_insts_per_unit"], "salu_insts_per_id": k["salu_insts_per_unit"],
+        "mean_issue_cycles_per_valu": k["mean_issue_cycles_per_valu"],
+        "peak": peak, "achieved": achieved, "frac": peak / achieved,
+        "clock_ghz": k["clock_ghz"], "frac_counter_run": k["frac"], "salu_busy_counter_run": k["salu_busy"],
+        "source": os.path.relpath(path, ROOT),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,10 +103,10 @@ def main():
     ap.add_argument("--grid", type=int, default=0, help="override workgroups per launch")
     ap.add_argument("--comm", action="store_true",
                     help="at N = 1 too, run each step through the native communicator (a world-1 ncclReduce)")
-    ap.add_argument("--dist-backend", default="rccl", choices=("rccl", "gloo"),
-                    help="rccl: the native communicator (RCCL over xGMI, one GPU per rank) for real runs; gloo: "
-                         "the same shard/reduce protocol over torch.distributed CPU tensors, only to rehearse "
-                         "several ranks on one GPU")
+    ap.add_argument("--dist-backend", default="auto", choices=("auto", "rccl", "host"),
+                    help="rccl: the native communicator over RCCL/xGMI (one GPU per rank); host: the same native "
+                         "protocol with its collectives over gloo (qk_comm_init_host), to rehearse more ranks than "
+                         "GPUs; auto: rccl when the node has a GPU per rank, else host")
     args = ap.parse_args()
 
     import numpy as np
@@ -92,27 +126,24 @@ def main():
     dev_index = local % ndev  # == local on a real node (one process per GPU)
     torch.cuda.set_device(dev_index)
     comm = None
-    data_path_note = ""
+    data_path = "single"
     if world > 1:
         dist.init_process_group("gloo")          # control plane only
-        if args.dist_backend == "rccl":
-            try:
-                comm = skd.Comm.from_process_group(dev_index)
-                ok = 1
-            except Exception as e:                # e.g. RCCL refuses the topology
-                log(f"rank {rank}: native RCCL communicator unavailable ({e})")
-                ok = 0
-            flag = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if not int(flag.item()):
-                # every rank falls back together: the same shard/reduce protocol
-                # over gloo (host copies of the t+1 partial words per step)
-                if comm is not None:
-                    comm.close()
-                    comm = None
-                data_path_note = " (native RCCL communicator unavailable: gloo reduce)"
+        backend = args.dist_backend
+        if backend == "auto":
+            backend = "rccl" if ndev >= world else "host"
+        if backend == "rccl":
+            if ndev < world:
+                raise SystemExit(f"--dist-backend rccl needs a GPU per rank ({world} ranks, {ndev} GPUs)")
+            # a failure here is an error (torch.distributed.run then stops every rank)
+            comm = skd.Comm.from_process_group(dev_index)
+            data_path = "rccl"
+        else:
+            comm = skd.Comm.init_host(skd.ProcessGroupChannel(), rank, world, dev_index)
+            data_path = "host"
     elif args.comm:
         comm = skd.Comm.create([dev_index])
+        data_path = "rccl"
 
     n = int(args.ids_per_gpu)
     t, bits = args.t, args.bits
@@ -132,13 +163,9 @@ def main():
 
     def step():
         if comm is not None:
-            comm.encode_sharded_async([ids], t, bits=bits, root=0)   # encode + one ncclReduce (comm.hip)
+            comm.encode_sharded_async([ids], t, bits=bits, root=0)   # encode + one reduce (comm.hip)
             return
         encode_device_async(ctx, ids, t, partial, bits=bits)
-        if world > 1:                                                 # gloo rehearsal (CPU tensors)
-            host = partial.cpu()
-            skd.reduce_partial_(host, t, bits, dst=0)
-            partial.copy_(host)
 
     for _ in range(args.warmup):
         step()
@@ -192,7 +219,7 @@ def main():
     value = n_total * args.steps / elapsed
     achieved_gbs = bytes_per_id * cnt / (kern_avg_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(bits, t, cnt)
-    modmul_rate = cnt * (t - 1) / (kern_avg_ms * 1e-3)
+    valu = valu_roofline(bits, t, cnt, kern_avg_ms)
 
     out = {
         "metric": f"quACK encode identifiers/s (device-resident), u{bits} ids, threshold t={t}",
@@ -209,11 +236,13 @@ def main():
         "data": "synthetic: splitmix64 uniform ids generated in HBM (seeded), no host copies in the timed region",
         "config": {
             "workload": f"encode {n:.0e} u{bits} ids per GPU at t={t}, device-resident"
-                        + ("" if world == 1 else
-                           f", {world} contiguous shards + one RCCL reduce (native qk_comm)" if comm is not None else
-                           f", {world} contiguous shards + one gloo reduce (rehearsal)" + data_path_note),
+                        + {"single": "",
+                           "rccl": f", {world} contiguous shards + one RCCL reduce over xGMI (native qk_comm)",
+                           "host": f", {world} contiguous shards on {ndev} GPU(s) + one reduce of the native "
+                                   f"protocol over gloo (qk_comm_init_host): a rehearsal, not a scaling result"
+                           }[data_path],
             "ids_per_gpu": cnt, "global_ids": n_total, "threshold": t, "bits": bits,
-            "seed": hex(args.seed), "parallelism": f"shard{world}",
+            "seed": hex(args.seed), "parallelism": f"shard{world}", "collectives": data_path,
         },
         "roofline": {
             "bound": "hbm",
@@ -226,7 +255,7 @@ def main():
             "kernel": f"k_encode_u{bits} (avg of {launches} launches, HIP events on the launch stream)",
             "kernel_avg_ms": kern_avg_ms,
             "algorithmic_bytes_per_launch": bytes_per_id * cnt,
-            "int_valu_view": {"modmuls_per_s": modmul_rate, "ids_per_s_per_gpu": cnt / (kern_avg_ms * 1e-3)},
+            "valu": valu,
         },
         "cpu_baseline": None,
         "result": {"count": count, "power_sums_head": S[:4], "digest": digest,

@@ -52,7 +52,8 @@ enum {
     QK_E_NO_DEVICE = -7,    /* no usable gfx950 device */
     QK_E_NOMEM = -8,
     QK_E_FORMAT = -9,       /* malformed serialized bytes */
-    QK_E_COMM = -10         /* an RCCL call failed */
+    QK_E_COMM = -10,        /* a collective failed: the communicator is aborted and unusable */
+    QK_E_PEER = -11         /* another rank of the communicator failed (its own call reports why) */
 };
 
 const char *qk_strerror(int status);
@@ -302,36 +303,62 @@ int qk_u64_decode_device(qk_ctx *ctx, const qk_u64 *diff, const uint64_t *d_log,
  *     (ncclCommInitAll; local rank i = global rank i = devices[i]);
  *   - one process per GPU:        rank 0 calls qk_comm_unique_id and ships
  *     the QK_COMM_ID_BYTES bytes to the other ranks by any channel, then
- *     every rank calls qk_comm_init_rank(id, rank, world, device).
+ *     every rank calls qk_comm_init_rank(id, rank, world, device);
+ *   - collectives over a host channel: qk_comm_init_host (below).
  * Each local rank owns its own qk_ctx.  Array arguments (d_ids, n, d_log,
  * streams) have one entry per LOCAL rank (qk_comm_info's nlocal), in local
  * rank order.  streams may be NULL (every local rank uses its device's null
  * stream); the work runs on the context's stream, ordered after the given
  * stream, and the given stream is ordered after it.  Every rank of the
- * communicator must make the same sequence of collective calls.
+ * communicator must make the same sequence of collective calls with the same
+ * threshold and root.
+ * Failure semantics: a rank whose own arguments or local work fail still
+ * takes part in every collective of the call (its failure travels as data),
+ * so no peer is left blocked; see each call for what every rank returns.  A
+ * failed collective aborts the communicator (ncclCommAbort): that call and
+ * every later one return QK_E_COMM; destroy it.
  * ---------------------------------------------------------------------- */
 typedef struct qk_comm qk_comm;
 #define QK_COMM_ID_BYTES 128
 int qk_comm_unique_id(uint8_t id[QK_COMM_ID_BYTES]);
 int qk_comm_create(int ndev, const int *devices, qk_comm **out);
 int qk_comm_init_rank(const uint8_t id[QK_COMM_ID_BYTES], int rank, int world, int device, qk_comm **out);
+/* One rank on `device` whose collectives run through the caller's host
+ * channel instead of RCCL: the identical sharded protocol, every collective
+ * staged through pinned host memory (the async encode completes before it
+ * returns).  For more ranks than GPUs (RCCL takes one rank per device) and for
+ * ranks RCCL cannot connect.  Each callback acts as the collective of its name
+ * over all ranks (uint64 elements, wrapping sums; allgather: recv[r*n .. r*n+n)
+ * = rank r's send) and returns 0, nonzero on failure (-> QK_E_COMM). */
+typedef struct qk_comm_host_ops {
+    void *user;
+    int (*reduce_sum_u64)(void *user, uint64_t *buf, size_t n, int root);
+    int (*broadcast_u64)(void *user, uint64_t *buf, size_t n, int root);
+    int (*allgather_u64)(void *user, const uint64_t *send, uint64_t *recv, size_t n);
+} qk_comm_host_ops;
+int qk_comm_init_host(const qk_comm_host_ops *ops, int rank, int world, int device, qk_comm **out);
 void qk_comm_destroy(qk_comm *comm);
 /* world size, local ranks in this process, global rank of local rank 0 */
 int qk_comm_info(const qk_comm *comm, int *world, int *nlocal, int *first_rank);
-/* the qk_ctx of a local rank (owned by the communicator: profiling, grid
- * knobs, and the single-GPU calls on that device) */
+/* the qk_ctx of a local rank (owned by the communicator, valid until
+ * qk_comm_destroy: profiling, grid knobs, and the single-GPU calls on that
+ * device) */
 int qk_comm_context(qk_comm *comm, int local, qk_ctx **out);
-/* all ranks reach this point (one 8-byte all-reduce), then the local streams drain */
+/* all ranks reach this point (one 8-byte reduce), then the local streams drain */
 int qk_comm_barrier(qk_comm *comm);
 
 /* Sharded encode: local rank i encodes d_ids[i][0 .. n[i]) on its GPU, then
  * one ncclReduce(sum, uint64) of its partial to global rank `root`:
- * (t + 1) power-sum/count words (u64 ids: 2t + 1, 32-bit limbs) plus a
+ * (t + 1) power-sum/count words (u64 ids: 2t + 1, 32-bit limbs), a
  * (has_last, last) slot per rank, so the root learns the last id of the last
- * non-empty shard without a second collective.  The root merges the whole
- * stream into q (as if inserted after q's content); other ranks leave q
- * untouched.  _async only enqueues; _wait (every rank) drains the local
- * streams and merges on the root. */
+ * non-empty shard without a second collective, and a failed-rank count.  The
+ * root merges the whole stream into q (as if inserted after q's content);
+ * other ranks leave q untouched.  _async only enqueues; _wait (every rank)
+ * drains the local streams and merges on the root.
+ * Failures: a rank whose shard argument is bad (non-device, misaligned) or
+ * whose encode fails returns that error from _async and _wait and sends a
+ * failed payload; the root then returns QK_E_PEER (or its own error) and
+ * leaves q untouched. */
 int qk_u32_encode_sharded_async(qk_comm *comm, const uint32_t *const *d_ids, const size_t *n, uint32_t threshold,
                                 int root, void *const *streams);
 int qk_u64_encode_sharded_async(qk_comm *comm, const uint64_t *const *d_ids, const size_t *n, uint32_t threshold,
@@ -345,11 +372,13 @@ int qk_u64_encode_sharded(qk_comm *comm, const uint64_t *const *d_ids, const siz
 /* Sharded decode over a candidate log cut the same way (log shard i on local
  * rank i): the root turns diff into coefficients (diff is read on the root
  * only; other ranks may pass NULL) and broadcasts them, every rank
- * root-tests its shard, the shards' stop positions and hits are
- * all-gathered.  Every rank returns the single-GPU qk_*_decode_device result
- * for the whole log (global positions, ascending, cut at the first entry
- * equal to diff->last_value when stop_at_last).  An undecodable diff fails
- * on every rank with the same status. */
+ * root-tests its shard, the shards' stop positions, hit counts and statuses
+ * are all-gathered, then the hits.  Every rank returns the single-GPU
+ * qk_*_decode_device result for the whole log (global positions, ascending,
+ * cut at the first entry equal to diff->last_value when stop_at_last).  Any
+ * failure — an undecodable diff on the root, a bad log shard or a failed root
+ * test on any rank — makes every rank return the same status (the lowest
+ * failing rank's). */
 int qk_u32_decode_sharded(qk_comm *comm, const qk_u32 *diff, int root, const uint32_t *const *d_log, const size_t *n,
                           int stop_at_last, uint64_t *hits, size_t cap, size_t *n_hits, void *const *streams);
 int qk_u64_decode_sharded(qk_comm *comm, const qk_u64 *diff, int root, const uint64_t *const *d_log, const size_t *n,

@@ -28,6 +28,7 @@ pub const QK_E_NO_DEVICE: c_int = -7;
 pub const QK_E_NOMEM: c_int = -8;
 pub const QK_E_FORMAT: c_int = -9;
 pub const QK_E_COMM: c_int = -10;
+pub const QK_E_PEER: c_int = -11;
 
 /// `qk_u32`: header words then `threshold` canonical power sums.
 #[repr(C)]
@@ -92,6 +93,17 @@ pub struct qk_ctx {
 #[repr(C)]
 pub struct qk_comm {
     _private: [u8; 0],
+}
+
+/// Host-channel collectives of `qk_comm_init_host` (each returns 0 on success).
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct qk_comm_host_ops {
+    pub user: *mut c_void,
+    pub reduce_sum_u64: Option<unsafe extern "C" fn(user: *mut c_void, buf: *mut u64, n: usize, root: c_int) -> c_int>,
+    pub broadcast_u64: Option<unsafe extern "C" fn(user: *mut c_void, buf: *mut u64, n: usize, root: c_int) -> c_int>,
+    pub allgather_u64:
+        Option<unsafe extern "C" fn(user: *mut c_void, send: *const u64, recv: *mut u64, n: usize) -> c_int>,
 }
 
 #[link(name = "quack_hip")]
@@ -194,6 +206,8 @@ extern "C" {
     pub fn qk_comm_unique_id(id: *mut u8) -> c_int;
     pub fn qk_comm_create(ndev: c_int, devices: *const c_int, out: *mut *mut qk_comm) -> c_int;
     pub fn qk_comm_init_rank(id: *const u8, rank: c_int, world: c_int, device: c_int,
+                             out: *mut *mut qk_comm) -> c_int;
+    pub fn qk_comm_init_host(ops: *const qk_comm_host_ops, rank: c_int, world: c_int, device: c_int,
                              out: *mut *mut qk_comm) -> c_int;
     pub fn qk_comm_destroy(comm: *mut qk_comm);
     pub fn qk_comm_info(comm: *const qk_comm, world: *mut c_int, nlocal: *mut c_int, first_rank: *mut c_int) -> c_int;

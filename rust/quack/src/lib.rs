@@ -26,6 +26,7 @@ use arithmetic::{Field, ModularInteger};
 use serde::{Deserialize, Deserializer, Serialize, Serializer};
 use std::ffi::CStr;
 use std::fmt;
+use std::marker::PhantomData;
 use std::os::raw::{c_int, c_void};
 use std::ptr;
 
@@ -521,11 +522,23 @@ impl Comm {
         check(unsafe { ffi::qk_comm_info(self.raw, &mut w, &mut l, &mut f) })?;
         Ok((w, l, f))
     }
-    /// The context of a local rank, owned by the communicator.
-    pub fn context(&self, local: i32) -> Result<Context> {
+    /// One rank whose collectives run through a host channel (`ops`) instead
+    /// of RCCL: the same protocol, e.g. more ranks than GPUs.
+    ///
+    /// # Safety
+    /// The callbacks must implement the collectives over all ranks and stay
+    /// valid (with `ops.user`) until the communicator is dropped.
+    pub unsafe fn init_host(ops: &ffi::qk_comm_host_ops, rank: i32, world: i32, device: i32) -> Result<Comm> {
+        let mut raw = ptr::null_mut();
+        check(ffi::qk_comm_init_host(ops, rank, world, device, &mut raw))?;
+        Ok(Comm { raw, nlocal: 1 })
+    }
+    /// The context of a local rank, owned by the communicator: the borrow
+    /// keeps the communicator (and so the context) alive.
+    pub fn context(&self, local: i32) -> Result<ContextRef<'_>> {
         let mut raw = ptr::null_mut();
         check(unsafe { ffi::qk_comm_context(self.raw, local, &mut raw) })?;
-        Ok(Context { raw, owned: false })
+        Ok(ContextRef { ctx: Context { raw, owned: false }, _comm: PhantomData })
     }
     pub fn barrier(&self) -> Result<()> {
         check(unsafe { ffi::qk_comm_barrier(self.raw) })
@@ -535,6 +548,19 @@ impl Comm {
             return Err(QuackError { status: ffi::QK_E_INVAL });
         }
         Ok(())
+    }
+}
+
+/// A communicator-owned [`Context`], borrowed from its [`Comm`].
+pub struct ContextRef<'a> {
+    ctx: Context,
+    _comm: PhantomData<&'a Comm>,
+}
+
+impl std::ops::Deref for ContextRef<'_> {
+    type Target = Context;
+    fn deref(&self) -> &Context {
+        &self.ctx
     }
 }
 

@@ -25,6 +25,7 @@ QK_E_NO_DEVICE = -7
 QK_E_NOMEM = -8
 QK_E_FORMAT = -9
 QK_E_COMM = -10
+QK_E_PEER = -11
 
 P32 = 4294967291
 P64 = 18446744073709551557
@@ -100,6 +101,7 @@ SIGNATURES = {
     "qk_comm_unique_id": (C.c_int, [u8p]),
     "qk_comm_create": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
     "qk_comm_init_rank": (C.c_int, [u8p, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+    "qk_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
     "qk_comm_destroy": (None, [vp]),
     "qk_comm_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "qk_comm_context": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),

@@ -6,16 +6,19 @@
 // are summed.  Per sharded encode:
 //   each local rank   encode its shard into its payload buffer (the
 //                     ordinary encode kernel + finalize), then k_comm_pack
-//                     turns [S.., n, last] into [S.., n, slots]: slot r =
-//                     (has_last, last) of rank r, zero elsewhere
+//                     turns [S.., n, last] into [S.., n, slots, failed]:
+//                     slot r = (has_last, last) of rank r, zero elsewhere;
+//                     failed = 1 on a rank whose local work failed (its
+//                     payload is otherwise zero: it still joins the reduce)
 //   ONE ncclReduce    (sum, uint64) of the payload to the root rank:
 //                     the summed power-sum words cannot overflow (canonical
 //                     residues / 32-bit limbs, < 2^27 ranks), the count word
-//                     sums the shard sizes, and every slot has exactly one
-//                     contributor, so the root reads each rank's last id
-//   root              fold mod p, count mod 2^32, last_value = the last
-//                     id of the highest non-empty rank
-// Payload at t = 32 on 8 GPUs: 33 + 16 words = 392 B — latency-bound; the
+//                     sums the shard sizes, every slot has exactly one
+//                     contributor, and the last word counts failed ranks
+//   root              nonzero failed count -> QK_E_PEER, q untouched; else
+//                     fold mod p, count mod 2^32, last_value = the last id of
+//                     the highest non-empty rank
+// Payload at t = 32 on 8 GPUs: 33 + 16 + 1 words = 400 B — latency-bound; the
 // xGMI bandwidth is irrelevant.
 //
 // Sharded decode (the log cut the same way):
@@ -23,10 +26,29 @@
 //                     root, which ran to_coeffs (host, O(t^2))
 //   each local rank   the root test over its log shard (api.hip phases, all
 //                     local GPUs in flight at once)
-//   ncclAllGather     (n, first stop position, hits below it) per rank
-//   ncclAllGather     the hit positions (+ shard base), padded to the
-//                     largest count; every rank cuts at the global stop
+//   ncclAllGather     (n, first stop position, hits below it, status) per rank
+//   ncclAllGather     the hit positions (+ shard base), padded, in chunks of
+//                     a fixed size; every rank cuts at the global stop
 // so every rank returns the single-GPU answer for the whole log.
+//
+// Collective safety (one process per GPU: a rank that returned early would
+// leave its peers blocked in the next collective forever).  Every rank enters
+// every collective of an operation; the only early returns precede the first
+// collective and test arguments every rank passes alike by contract
+// (threshold, root).  A local failure travels as data — the failed word of
+// the encode payload, the status word of the decode gather — and the gathered
+// statuses decide, identically on every rank, whether a further collective
+// runs.  No buffer is allocated between collectives (the payload buffer is
+// sized for the largest operation at init; hits travel in fixed-size chunks).
+// A collective that fails leaves the communicator in an unknown state: its
+// RCCL communicators are aborted (ncclCommAbort, which also releases peers
+// blocked on them) and every later call returns QK_E_COMM.
+//
+// Collectives go through RCCL (device buffers, the context's stream) or,
+// for a communicator made by qk_comm_init_host, through the caller's host
+// callbacks on the pinned mirror of the payload buffer: the same protocol
+// with a host channel (several ranks rehearsed on one GPU — RCCL refuses two
+// ranks on one device — or ranks RCCL cannot connect).
 //
 // Streams: each local rank's work runs on its qk_ctx's own stream, ordered
 // after the caller's stream (event) and, for the async encode, with the
@@ -51,36 +73,49 @@ struct qk_comm {
         int rank = 0, device = 0;
         qk_ctx *ctx = nullptr;
         ncclComm_t nc = nullptr;
-        uint64_t *d_coll = nullptr;   // collective payload (device)
+        uint64_t *d_coll = nullptr;   // collective payload (device), coll_cap(world) words
         uint64_t *h_coll = nullptr;   // pinned host mirror
-        size_t coll_words = 0;
         hipEvent_t ev_in = nullptr, ev_out = nullptr;
         hipStream_t user = nullptr;   // caller stream of the operation in flight
     };
     int world = 1;
     std::vector<Local> local;
+    bool host = false;                // collectives through ops (qk_comm_init_host)
+    qk_comm_host_ops ops{};
+    bool broken = false;              // a collective failed: unusable
     // sharded encode in flight (qk_*_encode_sharded_async -> _wait)
     int pend_bits = 0;
     uint32_t pend_t = 0;
     int pend_root = -1;
+    int pend_rc = QK_OK;              // local / collective status of the async half
     std::mutex mu;
 };
-
-#define QK_NCCL_TRY(expr)                                                                          \
-    do {                                                                                           \
-        if ((expr) != ncclSuccess) return QK_E_COMM;                                               \
-    } while (0)
 
 namespace qk {
 
 using Local = qk_comm::Local;
 
-// [S.., n, last] -> [S.., n, slot_0 .. slot_{world-1}], slot = (has_last, last)
-// (R = the summed words, n at R - 1, last at R)
+// Words of every payload buffer: the largest encode payload, the decode
+// header, the decode status gather, and hit chunks of >= 64 positions per rank.
+static size_t coll_cap(int world) {
+    const size_t W = (size_t)world;
+    size_t c = 8192;
+    c = std::max(c, 2 * (size_t)QK_MAX_THRESHOLD + 1 + 2 * W + 1);
+    c = std::max(c, 4 + (size_t)QK_MAX_THRESHOLD);
+    c = std::max(c, 4 + 4 * W);
+    c = std::max(c, 64 * (W + 1));
+    return c;
+}
+
+// summed words of the partial vector
+static size_t reduce_words(int bits, uint32_t t) { return bits == 32 ? (size_t)t + 1 : 2 * (size_t)t + 1; }
+
+// [S.., n, last] -> [S.., n, slot_0 .. slot_{world-1}, failed = 0]
+// (R = the summed words, n at R - 1, last at R; slot = (has_last, last))
 __global__ void k_comm_pack(uint64_t *buf, uint32_t R, uint32_t world, uint32_t rank) {
     const uint64_t n = buf[R - 1], last = buf[R];
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < 2 * world; j += blockDim.x) buf[R + j] = 0;
+    for (uint32_t j = threadIdx.x; j < 2 * world + 1; j += blockDim.x) buf[R + j] = 0;
     __syncthreads();
     if (threadIdx.x == 0 && n) {
         buf[R + 2 * rank] = 1;
@@ -88,27 +123,14 @@ __global__ void k_comm_pack(uint64_t *buf, uint32_t R, uint32_t world, uint32_t 
     }
 }
 
-static int ensure_coll(Local &L, size_t words) {
-    if (words <= L.coll_words) return QK_OK;
-    // grown only between operations (every comm call drains its streams
-    // before returning, except the async encode, whose size is fixed per t)
-    QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
-    if (L.d_coll) hipFree(L.d_coll);
-    if (L.h_coll) hipHostFree(L.h_coll);
-    L.d_coll = nullptr;
-    L.h_coll = nullptr;
-    L.coll_words = 0;
-    const size_t w = std::max<size_t>(words, 4096);
-    if (hipMalloc(&L.d_coll, w * 8) != hipSuccess) return QK_E_NOMEM;
-    if (hipHostMalloc(&L.h_coll, w * 8, hipHostMallocDefault) != hipSuccess) return QK_E_NOMEM;
-    L.coll_words = w;
-    return QK_OK;
+// the payload of a rank whose local work failed: zeros, failed = 1
+__global__ void k_comm_fail(uint64_t *buf, uint32_t words) {
+    for (uint32_t j = threadIdx.x; j < words; j += blockDim.x) buf[j] = j + 1 == words ? 1 : 0;
 }
 
 // order the local rank's stream after the caller's stream
-static int enter(Local &L, void *user) {
+static int enter(Local &L) {
     QK_HIP_TRY(hipSetDevice(L.device));
-    L.user = (hipStream_t)user;
     QK_HIP_TRY(hipEventRecord(L.ev_in, L.user));
     QK_HIP_TRY(hipStreamWaitEvent(L.ctx->stream, L.ev_in, 0));
     return QK_OK;
@@ -121,38 +143,111 @@ static int leave(Local &L) {
     return QK_OK;
 }
 
-static int init_local(Local &L, int device) {
+static int sync_local(Local &L) {
+    QK_HIP_TRY(hipSetDevice(L.device));
+    QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
+    return QK_OK;
+}
+
+static int init_local(Local &L, int device, int world) {
     L.device = device;
     if (int rc = qk_ctx_create(device, &L.ctx)) return rc;
     QK_HIP_TRY(hipSetDevice(device));
     QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_in, hipEventDisableTiming));
     QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_out, hipEventDisableTiming));
-    return ensure_coll(L, 4096);
+    const size_t w = coll_cap(world);
+    if (hipMalloc(&L.d_coll, w * 8) != hipSuccess) return QK_E_NOMEM;
+    if (hipHostMalloc(&L.h_coll, w * 8, hipHostMallocDefault) != hipSuccess) return QK_E_NOMEM;
+    return QK_OK;
 }
 
-// summed words of the partial vector
-static size_t reduce_words(int bits, uint32_t t) { return bits == 32 ? (size_t)t + 1 : 2 * (size_t)t + 1; }
+static int abort_comm(qk_comm *c) {
+    c->broken = true;
+    for (auto &L : c->local)
+        if (L.nc) {
+            ncclCommAbort(L.nc);
+            L.nc = nullptr;
+        }
+    return QK_E_COMM;
+}
+
+// Collectives over every local rank, in place on d_coll:
+//   Reduce:  d_coll[0..w) summed over ranks into the root's
+//   Bcast:   the root's d_coll[0..w) to every rank
+//   Gather:  rank r's d_coll[0..w) to d_coll[w + r*w .. w + (r+1)*w) everywhere
+// Enqueued on the local streams (RCCL) or run now through the host callbacks
+// (staged through h_coll).  A failed collective aborts the communicator.
+enum class Op { Reduce, Bcast, Gather };
+
+static int collective(qk_comm *c, Op op, size_t w, int root) {
+    if (c->broken) return QK_E_COMM;
+    if (c->host) {
+        Local &L = c->local[0];
+        hipStream_t s = L.ctx->stream;
+        int e = QK_OK;
+        if (hipSetDevice(L.device) != hipSuccess ||
+            hipMemcpyAsync(L.h_coll, L.d_coll, w * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            memset(L.h_coll, 0, w * 8);   // still take part: the peers are in the collective
+            e = QK_E_HIP;
+        }
+        int cb = -1;
+        switch (op) {
+        case Op::Reduce: cb = c->ops.reduce_sum_u64(c->ops.user, L.h_coll, w, root); break;
+        case Op::Bcast: cb = c->ops.broadcast_u64(c->ops.user, L.h_coll, w, root); break;
+        case Op::Gather: cb = c->ops.allgather_u64(c->ops.user, L.h_coll, L.h_coll + w, w); break;
+        }
+        if (cb != 0) {
+            c->broken = true;
+            return QK_E_COMM;
+        }
+        const size_t off = op == Op::Gather ? w : 0, words = op == Op::Gather ? w * (size_t)c->world : w;
+        if (!e && (hipMemcpyAsync(L.d_coll + off, L.h_coll + off, words * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+                   hipStreamSynchronize(s) != hipSuccess))
+            e = QK_E_HIP;
+        return e;
+    }
+    bool ok = ncclGroupStart() == ncclSuccess;
+    for (auto &L : c->local) {
+        if (!ok) break;
+        ncclResult_t r = ncclSuccess;
+        switch (op) {
+        case Op::Reduce:
+            r = ncclReduce(L.d_coll, L.d_coll, w, ncclUint64, ncclSum, root, L.nc, L.ctx->stream);
+            break;
+        case Op::Bcast: r = ncclBroadcast(L.d_coll, L.d_coll, w, ncclUint64, root, L.nc, L.ctx->stream); break;
+        case Op::Gather: r = ncclAllGather(L.d_coll, L.d_coll + w, w, ncclUint64, L.nc, L.ctx->stream); break;
+        }
+        ok = r == ncclSuccess;
+    }
+    if (ncclGroupEnd() != ncclSuccess) ok = false;
+    return ok ? QK_OK : abort_comm(c);
+}
 
 template <int BITS>
 static int encode_sharded_async(qk_comm *c, const void *const *d_ids, const size_t *n, uint32_t t, int root,
                                 void *const *streams) {
-    if (!c || !d_ids || !n) return QK_E_INVAL;
+    if (c->broken) return QK_E_COMM;
+    // arguments every rank passes alike (the collective contract): failing
+    // them returns before any collective, on every rank
     if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
     if (root < 0 || root >= c->world) return QK_E_INVAL;
     const size_t esz = BITS == 32 ? 4 : 8;
-    for (size_t i = 0; i < c->local.size(); ++i) {
-        if (n[i] && (!d_ids[i] || !is_device_ptr(d_ids[i]) || ((uintptr_t)d_ids[i] & (esz - 1)))) return QK_E_INVAL;
-        if (n[i] >= (1ull << 40)) return QK_E_INVAL;
-    }
-    const size_t R = reduce_words(BITS, t), W = R + 2 * (size_t)c->world;
-    for (auto &L : c->local)
-        if (int rc = ensure_coll(L, W)) return rc;
-    // every check that can fail before the collective has run: from here on a
-    // local failure still joins the reduce (the other ranks would wait in it)
+    const size_t R = reduce_words(BITS, t), W = R + 2 * (size_t)c->world + 1;
+    // per-rank arguments and local work: a failure still joins the reduce,
+    // with the failed payload
     int rc = QK_OK;
     for (size_t i = 0; i < c->local.size(); ++i) {
         Local &L = c->local[i];
-        int e = enter(L, streams ? streams[i] : nullptr);
+        L.user = streams ? (hipStream_t)streams[i] : nullptr;
+        int e = QK_OK;
+        if (!d_ids || !n) {
+            e = QK_E_INVAL;
+        } else if (n[i] && (!d_ids[i] || ((uintptr_t)d_ids[i] & (esz - 1)) || n[i] >= (1ull << 40) ||
+                            !is_device_ptr(d_ids[i]))) {
+            e = QK_E_INVAL;
+        }
+        if (!e) e = enter(L);
         if (!e) {
             std::lock_guard<std::mutex> g(L.ctx->mu);
             e = BITS == 32 ? launch_encode_u32(L.ctx, (const uint32_t *)d_ids[i], n[i], t, L.d_coll, L.ctx->stream)
@@ -163,15 +258,16 @@ static int encode_sharded_async(qk_comm *c, const void *const *d_ids, const size
                                (uint32_t)c->world, (uint32_t)L.rank);
             if (hipGetLastError() != hipSuccess) e = QK_E_HIP;
         }
-        if (e && !rc) rc = e;
+        if (e) {
+            (void)hipSetDevice(L.device);
+            hipLaunchKernelGGL(k_comm_fail, dim3(1), dim3(256), 0, L.ctx->stream, L.d_coll, (uint32_t)W);
+            (void)hipGetLastError();
+            if (!rc) rc = e;
+        }
     }
-    if (ncclGroupStart() != ncclSuccess) return QK_E_COMM;
-    int nrc = QK_OK;
-    for (auto &L : c->local)
-        if (ncclReduce(L.d_coll, L.d_coll, W, ncclUint64, ncclSum, root, L.nc, L.ctx->stream) != ncclSuccess)
-            nrc = QK_E_COMM;
-    if (ncclGroupEnd() != ncclSuccess) nrc = QK_E_COMM;
+    const int crc = collective(c, Op::Reduce, W, root);
     for (auto &L : c->local) {
+        (void)hipSetDevice(L.device);
         if (L.rank == root && hipMemcpyAsync(L.h_coll, L.d_coll, W * 8, hipMemcpyDeviceToHost, L.ctx->stream) !=
                                   hipSuccess && !rc)
             rc = QK_E_HIP;
@@ -180,21 +276,20 @@ static int encode_sharded_async(qk_comm *c, const void *const *d_ids, const size
     c->pend_bits = BITS;
     c->pend_t = t;
     c->pend_root = root;
-    return rc ? rc : nrc;
+    c->pend_rc = rc ? rc : crc;
+    return c->pend_rc;
 }
 
 template <int BITS, typename Q>
 static int encode_sharded_wait(qk_comm *c, Q *q) {
-    if (!c) return QK_E_INVAL;
     if (c->pend_bits != BITS) return QK_E_INVAL;   // nothing in flight for this id width
     const uint32_t t = c->pend_t;
-    const int root = c->pend_root;
+    const int root = c->pend_root, prc = c->pend_rc;
     c->pend_bits = 0;
     int rc = QK_OK;
-    for (auto &L : c->local) {
-        (void)hipSetDevice(L.device);
-        if (hipStreamSynchronize(L.ctx->stream) != hipSuccess) rc = QK_E_HIP;
-    }
+    for (auto &L : c->local)
+        if (int e = sync_local(L); e && !rc) rc = e;
+    if (prc) return prc;                           // q untouched
     if (rc) return rc;
     for (auto &L : c->local) {
         if (L.rank != root) continue;
@@ -202,6 +297,7 @@ static int encode_sharded_wait(qk_comm *c, Q *q) {
         if (q->threshold != t) return QK_E_MISMATCH;
         const size_t R = reduce_words(BITS, t);
         const uint64_t *h = L.h_coll;
+        if (h[R + 2 * (size_t)c->world]) return QK_E_PEER;   // another rank failed: q untouched
         int has = 0;
         uint64_t last = 0;
         for (int r = c->world - 1; r >= 0; --r)
@@ -219,29 +315,31 @@ static int encode_sharded_wait(qk_comm *c, Q *q) {
 template <typename T, typename Q>
 static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d_log, const size_t *n,
                           int stop_at_last, uint64_t *hits, size_t cap, size_t *n_hits, void *const *streams) {
-    if (!c || !d_log || !n || !n_hits) return QK_E_INVAL;
-    if (root < 0 || root >= c->world) return QK_E_INVAL;
-    *n_hits = 0;
-    const size_t nl = c->local.size(), W = (size_t)c->world;
-    for (size_t i = 0; i < nl; ++i)
-        if (n[i] && (!d_log[i] || !is_device_ptr(d_log[i]) || ((uintptr_t)d_log[i] & (sizeof(T) - 1))))
-            return QK_E_INVAL;
-    const size_t B = 4 + QK_MAX_THRESHOLD;   // broadcast header + coefficients
-    for (auto &L : c->local)
-        if (int rc = ensure_coll(L, std::max(B, 6 * W + 6))) return rc;
-
-    // 1. coefficients from the root (status travels with them, so an
-    //    undecodable difference fails on every rank alike)
+    if (c->broken) return QK_E_COMM;
+    if (root < 0 || root >= c->world) return QK_E_INVAL;   // alike on every rank
+    if (n_hits) *n_hits = 0;
+    const size_t nl = c->local.size(), W = (size_t)c->world, B = 4 + QK_MAX_THRESHOLD;
+    // local status per local rank: travels in the status gather of step 3
+    std::vector<int> ls(nl, QK_OK);
     for (size_t i = 0; i < nl; ++i) {
         Local &L = c->local[i];
-        if (int e = enter(L, streams ? streams[i] : nullptr)) return e;
+        L.user = streams ? (hipStream_t)streams[i] : nullptr;
+        if (!d_log || !n || !n_hits) ls[i] = QK_E_INVAL;
+        else if (n[i] && (!d_log[i] || ((uintptr_t)d_log[i] & (sizeof(T) - 1)) || !is_device_ptr(d_log[i])))
+            ls[i] = QK_E_INVAL;
+        if (int e = enter(L); e && !ls[i]) ls[i] = e;
+    }
+
+    // 1. coefficients from the root (its status travels with them)
+    for (size_t i = 0; i < nl; ++i) {
+        Local &L = c->local[i];
         if (L.rank != root) continue;
         uint64_t *h = L.h_coll;
         memset(h, 0, B * 8);
-        int64_t status = QK_OK;
+        int64_t status = ls[i];
         uint32_t d = 0;
-        if (!diff) status = QK_E_INVAL;
-        else if (diff->count != 0) {
+        if (!status && !diff) status = QK_E_INVAL;
+        if (!status && diff->count != 0) {
             std::vector<T> cf(std::max<uint32_t>(diff->threshold, 1));
             if constexpr (sizeof(T) == 4) status = qk_u32_to_coeffs(diff, cf.data(), (uint32_t)cf.size(), &d);
             else status = qk_u64_to_coeffs(diff, cf.data(), (uint32_t)cf.size(), &d);
@@ -251,109 +349,158 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
         }
         h[0] = (uint64_t)status;
         h[1] = status == QK_OK ? d : 0;
-        h[2] = diff && stop_at_last && diff->has_last ? 1 : 0;
-        h[3] = diff ? (uint64_t)diff->last_value : 0;
-        QK_HIP_TRY(hipMemcpyAsync(L.d_coll, h, B * 8, hipMemcpyHostToDevice, L.ctx->stream));
+        h[2] = !status && stop_at_last && diff->has_last ? 1 : 0;
+        h[3] = !status ? (uint64_t)diff->last_value : 0;
+        (void)hipSetDevice(L.device);
+        if (hipMemcpyAsync(L.d_coll, h, B * 8, hipMemcpyHostToDevice, L.ctx->stream) != hipSuccess && !ls[i])
+            ls[i] = QK_E_HIP;
     }
-    QK_NCCL_TRY(ncclGroupStart());
-    for (auto &L : c->local)
-        QK_NCCL_TRY(ncclBroadcast(L.d_coll, L.d_coll, B, ncclUint64, root, L.nc, L.ctx->stream));
-    QK_NCCL_TRY(ncclGroupEnd());
-    for (auto &L : c->local) {
-        QK_HIP_TRY(hipMemcpyAsync(L.h_coll, L.d_coll, B * 8, hipMemcpyDeviceToHost, L.ctx->stream));
-        QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
+    int crc = collective(c, Op::Bcast, B, root);
+    if (crc) return crc;
+    std::vector<std::vector<uint64_t>> hdr(nl);
+    for (size_t i = 0; i < nl; ++i) {
+        Local &L = c->local[i];
+        int e = sync_local(L);
+        if (!e && hipMemcpyAsync(L.h_coll, L.d_coll, B * 8, hipMemcpyDeviceToHost, L.ctx->stream) != hipSuccess)
+            e = QK_E_HIP;
+        if (!e) e = sync_local(L);
+        if (e) {
+            if (!ls[i]) ls[i] = e;
+            hdr[i].assign(B, 0);
+        } else {
+            hdr[i].assign(L.h_coll, L.h_coll + B);
+        }
+        if (!ls[i] && hdr[i][0]) ls[i] = (int)(int64_t)hdr[i][0];   // the root's status
     }
-    const uint64_t *hdr = c->local[0].h_coll;
-    const int status = (int)(int64_t)hdr[0];
-    const uint32_t d = (uint32_t)hdr[1];
-    const int use_stop = (int)hdr[2];
-    const T stop_value = (T)hdr[3];
-    std::vector<T> coeffs(std::max<uint32_t>(d, 1));
-    for (uint32_t k = 0; k < d; ++k) coeffs[k] = (T)hdr[4 + k];
-    if (status != QK_OK) return status;
 
     // 2. root test of every local shard, all GPUs in flight
-    const bool test = d > 0 || use_stop;
     std::vector<std::vector<uint64_t>> lh(nl);
-    std::vector<uint64_t> lstop(nl);
+    std::vector<uint64_t> lstop(nl, 0);
+    std::vector<T> coeffs;
+    std::vector<char> began(nl, 0);
     for (size_t i = 0; i < nl; ++i) {
         Local &L = c->local[i];
-        lstop[i] = n[i];
-        if (!test || !n[i]) continue;
+        lstop[i] = n ? n[i] : 0;
+        if (ls[i]) continue;
+        const uint64_t *hd = hdr[i].data();
+        const uint32_t d = (uint32_t)std::min<uint64_t>(hd[1], QK_MAX_THRESHOLD);
+        const int use_stop = (int)hd[2];
+        coeffs.assign(std::max<uint32_t>(d, 1), 0);
+        for (uint32_t k = 0; k < d; ++k) coeffs[k] = (T)hd[4 + k];
+        if (!(d > 0 || use_stop) || !n[i]) continue;
         std::lock_guard<std::mutex> g(L.ctx->mu);
-        QK_HIP_TRY(hipSetDevice(L.device));
-        if (int e = root_test_begin<T>(L.ctx, coeffs.data(), d, d_log[i], n[i], use_stop, stop_value, L.ctx->stream))
-            return e;
+        if (int e = hipSetDevice(L.device) == hipSuccess ? QK_OK : QK_E_HIP) {
+            ls[i] = e;
+            continue;
+        }
+        if (int e = root_test_begin<T>(L.ctx, coeffs.data(), d, d_log[i], n[i], use_stop, (T)hd[3], L.ctx->stream))
+            ls[i] = e;
+        else
+            began[i] = 1;
     }
     for (size_t i = 0; i < nl; ++i) {
+        if (!began[i]) continue;
         Local &L = c->local[i];
-        if (!test || !n[i]) continue;
+        const uint64_t *hd = hdr[i].data();
+        const uint32_t d = (uint32_t)std::min<uint64_t>(hd[1], QK_MAX_THRESHOLD);
+        coeffs.assign(std::max<uint32_t>(d, 1), 0);
+        for (uint32_t k = 0; k < d; ++k) coeffs[k] = (T)hd[4 + k];
         std::lock_guard<std::mutex> g(L.ctx->mu);
-        QK_HIP_TRY(hipSetDevice(L.device));
-        if (int e = root_test_finish<T>(L.ctx, coeffs.data(), d, d_log[i], n[i], use_stop, stop_value, L.ctx->stream,
-                                        lh[i], lstop[i]))
-            return e;
+        (void)hipSetDevice(L.device);
+        if (int e = root_test_finish<T>(L.ctx, coeffs.data(), d, d_log[i], n[i], (int)hd[2], (T)hd[3], L.ctx->stream,
+                                        lh[i], lstop[i])) {
+            ls[i] = e;
+            lh[i].clear();
+            continue;
+        }
         // hits at or past this shard's own stop are past the global one too
         lh[i].resize((size_t)(std::lower_bound(lh[i].begin(), lh[i].end(), lstop[i]) - lh[i].begin()));
     }
 
-    // 3. (n, stop, hits) of every rank
+    // 3. (n, stop, hits, status) of every rank
     for (size_t i = 0; i < nl; ++i) {
         Local &L = c->local[i];
         uint64_t *h = L.h_coll;
-        h[0] = n[i];
-        h[1] = lstop[i];
-        h[2] = lh[i].size();
-        QK_HIP_TRY(hipMemcpyAsync(L.d_coll, h, 24, hipMemcpyHostToDevice, L.ctx->stream));
+        h[0] = ls[i] ? 0 : n[i];
+        h[1] = ls[i] ? 0 : lstop[i];
+        h[2] = ls[i] ? 0 : lh[i].size();
+        h[3] = (uint64_t)(int64_t)ls[i];
+        (void)hipSetDevice(L.device);
+        if (hipMemcpyAsync(L.d_coll, h, 32, hipMemcpyHostToDevice, L.ctx->stream) != hipSuccess)
+            ls[i] = QK_E_HIP;   // (sent anyway: the peers are in the collective)
     }
-    QK_NCCL_TRY(ncclGroupStart());
-    for (auto &L : c->local)
-        QK_NCCL_TRY(ncclAllGather(L.d_coll, L.d_coll + 3, 3, ncclUint64, L.nc, L.ctx->stream));
-    QK_NCCL_TRY(ncclGroupEnd());
-    for (auto &L : c->local) {
-        QK_HIP_TRY(hipMemcpyAsync(L.h_coll, L.d_coll + 3, 3 * W * 8, hipMemcpyDeviceToHost, L.ctx->stream));
-        QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
+    if ((crc = collective(c, Op::Gather, 4, root))) return crc;
+    Local &L0 = c->local[0];
+    int rc = sync_local(L0);
+    if (!rc && hipMemcpyAsync(L0.h_coll, L0.d_coll + 4, 4 * W * 8, hipMemcpyDeviceToHost, L0.ctx->stream) != hipSuccess)
+        rc = QK_E_HIP;
+    if (!rc) rc = sync_local(L0);
+    for (size_t i = 1; i < nl; ++i)
+        if (int e = sync_local(c->local[i]); e && !rc) rc = e;
+    // every rank gathered the same words (RCCL) — unless its own copies
+    // failed, which only it sees: it reports that error alone
+    if (rc) {
+        for (auto &L : c->local) leave(L);
+        return rc;
     }
-    std::vector<uint64_t> base(W + 1, 0), cnt(W);
+    std::vector<uint64_t> base(W + 1, 0), cnt(W, 0);
     uint64_t gstop = UINT64_MAX, M = 0;
+    int gstatus = QK_OK;
     {
-        const uint64_t *m = c->local[0].h_coll;
+        const uint64_t *m = L0.h_coll;
         for (size_t r = 0; r < W; ++r) {
-            base[r + 1] = base[r] + m[3 * r];
-            if (m[3 * r + 1] < m[3 * r]) gstop = std::min(gstop, base[r] + m[3 * r + 1]);
-            cnt[r] = m[3 * r + 2];
+            const int st = (int)(int64_t)m[4 * r + 3];
+            if (st && !gstatus) gstatus = st;   // the lowest failing rank's status, on every rank
+            base[r + 1] = base[r] + m[4 * r];
+            if (m[4 * r + 1] < m[4 * r]) gstop = std::min(gstop, base[r] + m[4 * r + 1]);
+            cnt[r] = m[4 * r + 2];
+        }
+        for (size_t r = 0; r < W; ++r) {
+            if (base[r] >= gstop) cnt[r] = 0;   // wholly past the global stop
             M = std::max(M, cnt[r]);
         }
     }
+    if (gstatus) {
+        for (auto &L : c->local) leave(L);
+        return gstatus;
+    }
 
-    // 4. the hit positions, padded to the largest count
+    // 4. the hit positions, in rounds of C per rank (padded), C fixed by the
+    //    payload capacity: no allocation between collectives
     std::vector<uint64_t> all;
-    if (M) {
+    const size_t C = coll_cap(c->world) / (W + 1);
+    for (uint64_t off = 0; off < M; off += C) {
         for (size_t i = 0; i < nl; ++i) {
             Local &L = c->local[i];
-            if (int e = ensure_coll(L, M * (W + 1))) return e;
             uint64_t *h = L.h_coll;
             const uint64_t b = base[L.rank];
-            for (size_t k = 0; k < M; ++k) h[k] = k < lh[i].size() ? b + lh[i][k] : UINT64_MAX;
-            QK_HIP_TRY(hipMemcpyAsync(L.d_coll, h, M * 8, hipMemcpyHostToDevice, L.ctx->stream));
+            for (size_t k = 0; k < C; ++k) {
+                const size_t j = (size_t)off + k;
+                h[k] = j < lh[i].size() && j < cnt[L.rank] ? b + lh[i][j] : UINT64_MAX;
+            }
+            (void)hipSetDevice(L.device);
+            if (hipMemcpyAsync(L.d_coll, h, C * 8, hipMemcpyHostToDevice, L.ctx->stream) != hipSuccess && !rc)
+                rc = QK_E_HIP;
         }
-        QK_NCCL_TRY(ncclGroupStart());
-        for (auto &L : c->local)
-            QK_NCCL_TRY(ncclAllGather(L.d_coll, L.d_coll + M, M, ncclUint64, L.nc, L.ctx->stream));
-        QK_NCCL_TRY(ncclGroupEnd());
-        Local &L0 = c->local[0];
-        QK_HIP_TRY(hipMemcpyAsync(L0.h_coll, L0.d_coll + M, M * W * 8, hipMemcpyDeviceToHost, L0.ctx->stream));
-        for (auto &L : c->local) QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
+        if ((crc = collective(c, Op::Gather, C, root))) return crc;
+        int e = sync_local(L0);
+        if (!e && hipMemcpyAsync(L0.h_coll, L0.d_coll + C, C * W * 8, hipMemcpyDeviceToHost, L0.ctx->stream) !=
+                      hipSuccess)
+            e = QK_E_HIP;
+        if (!e) e = sync_local(L0);
+        for (size_t i = 1; i < nl; ++i)
+            if (int e2 = sync_local(c->local[i]); e2 && !e) e = e2;
+        if (e && !rc) rc = e;
+        if (rc) continue;   // keep joining the remaining rounds
         for (size_t r = 0; r < W; ++r)
-            for (uint64_t k = 0; k < cnt[r]; ++k) {
-                const uint64_t p = L0.h_coll[r * M + k];
+            for (size_t k = 0; k < C && off + k < cnt[r]; ++k) {
+                const uint64_t p = L0.h_coll[r * C + k];
                 if (p < gstop) all.push_back(p);
             }
-    } else {
-        for (auto &L : c->local) QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
     }
     for (auto &L : c->local)
-        if (int e = leave(L)) return e;
+        if (int e = leave(L); e && !rc) rc = e;
+    if (rc) return rc;
     *n_hits = all.size();
     if (all.size() > cap || (!all.empty() && !hits)) return QK_E_CAPACITY;
     std::copy(all.begin(), all.end(), hits);
@@ -382,7 +529,7 @@ int qk_comm_unique_id(uint8_t id[QK_COMM_ID_BYTES]) {
     int n = 0;
     if (qk_device_count(&n) != QK_OK) return QK_E_NO_DEVICE;
     ncclUniqueId u;
-    QK_NCCL_TRY(ncclGetUniqueId(&u));
+    if (ncclGetUniqueId(&u) != ncclSuccess) return QK_E_COMM;
     memcpy(id, &u, sizeof(u));
     return QK_OK;
 }
@@ -399,7 +546,7 @@ int qk_comm_create(int ndev, const int *devices, qk_comm **out) {
     c->local.resize(ndev);
     for (int i = 0; i < ndev; ++i) {
         c->local[i].rank = i;
-        if (int rc = init_local(c->local[i], devices[i])) {
+        if (int rc = init_local(c->local[i], devices[i], ndev)) {
             qk_comm_destroy(c);
             return rc;
         }
@@ -422,7 +569,7 @@ int qk_comm_init_rank(const uint8_t id[QK_COMM_ID_BYTES], int rank, int world, i
     c->world = world;
     c->local.resize(1);
     c->local[0].rank = rank;
-    if (int rc = init_local(c->local[0], device)) {
+    if (int rc = init_local(c->local[0], device, world)) {
         qk_comm_destroy(c);
         return rc;
     }
@@ -432,6 +579,26 @@ int qk_comm_init_rank(const uint8_t id[QK_COMM_ID_BYTES], int rank, int world, i
         c->local[0].nc = nullptr;
         qk_comm_destroy(c);
         return QK_E_COMM;
+    }
+    *out = c;
+    return QK_OK;
+}
+
+int qk_comm_init_host(const qk_comm_host_ops *ops, int rank, int world, int device, qk_comm **out) {
+    if (!out || !ops || !ops->reduce_sum_u64 || !ops->broadcast_u64 || !ops->allgather_u64 || world < 1 ||
+        rank < 0 || rank >= world)
+        return QK_E_INVAL;
+    *out = nullptr;
+    qk_comm *c = new (std::nothrow) qk_comm();
+    if (!c) return QK_E_NOMEM;
+    c->world = world;
+    c->host = true;
+    c->ops = *ops;
+    c->local.resize(1);
+    c->local[0].rank = rank;
+    if (int rc = init_local(c->local[0], device, world)) {
+        qk_comm_destroy(c);
+        return rc;
     }
     *out = c;
     return QK_OK;
@@ -466,16 +633,16 @@ int qk_comm_context(qk_comm *comm, int local, qk_ctx **out) {
 int qk_comm_barrier(qk_comm *comm) {
     if (!comm) return QK_E_INVAL;
     std::lock_guard<std::mutex> g(comm->mu);
+    if (comm->broken) return QK_E_COMM;
+    int rc = QK_OK;
     for (auto &L : comm->local) {
-        QK_HIP_TRY(hipSetDevice(L.device));
-        QK_HIP_TRY(hipMemsetAsync(L.d_coll, 0, 8, L.ctx->stream));
+        (void)hipSetDevice(L.device);
+        if (hipMemsetAsync(L.d_coll, 0, 8, L.ctx->stream) != hipSuccess && !rc) rc = QK_E_HIP;
     }
-    QK_NCCL_TRY(ncclGroupStart());
+    if (int e = collective(comm, Op::Reduce, 1, 0)) return e;
     for (auto &L : comm->local)
-        QK_NCCL_TRY(ncclAllReduce(L.d_coll, L.d_coll, 1, ncclUint64, ncclSum, L.nc, L.ctx->stream));
-    QK_NCCL_TRY(ncclGroupEnd());
-    for (auto &L : comm->local) QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
-    return QK_OK;
+        if (int e = sync_local(L); e && !rc) rc = e;
+    return rc;
 }
 
 int qk_u32_encode_sharded_async(qk_comm *comm, const uint32_t *const *d_ids, const size_t *n, uint32_t threshold,
@@ -500,11 +667,14 @@ int qk_u64_encode_sharded_wait(qk_comm *comm, qk_u64 *q) {
     std::lock_guard<std::mutex> g(comm->mu);
     return encode_sharded_wait<64>(comm, q);
 }
+// q is read for its threshold on every rank (a NULL q on a non-root rank
+// would make that rank skip the collective: it is an argument error, alike
+// on every rank by contract)
 int qk_u32_encode_sharded(qk_comm *comm, const uint32_t *const *d_ids, const size_t *n, qk_u32 *q, int root,
                           void *const *streams) {
     if (!comm || !q) return QK_E_INVAL;
     std::lock_guard<std::mutex> g(comm->mu);
-    int rc = encode_sharded_async<32>(comm, (const void *const *)d_ids, n, q->threshold, root, streams);
+    const int rc = encode_sharded_async<32>(comm, (const void *const *)d_ids, n, q->threshold, root, streams);
     const int w = encode_sharded_wait<32>(comm, q);
     return rc ? rc : w;
 }
@@ -512,7 +682,7 @@ int qk_u64_encode_sharded(qk_comm *comm, const uint64_t *const *d_ids, const siz
                           void *const *streams) {
     if (!comm || !q) return QK_E_INVAL;
     std::lock_guard<std::mutex> g(comm->mu);
-    int rc = encode_sharded_async<64>(comm, (const void *const *)d_ids, n, q->threshold, root, streams);
+    const int rc = encode_sharded_async<64>(comm, (const void *const *)d_ids, n, q->threshold, root, streams);
     const int w = encode_sharded_wait<64>(comm, q);
     return rc ? rc : w;
 }

@@ -264,7 +264,8 @@ const char *qk_strerror(int s) {
     case QK_E_NO_DEVICE: return "no usable gfx950 device";
     case QK_E_NOMEM: return "out of memory";
     case QK_E_FORMAT: return "malformed serialized quACK";
-    case QK_E_COMM: return "RCCL error";
+    case QK_E_COMM: return "collective failed (communicator aborted)";
+    case QK_E_PEER: return "another rank of the communicator failed";
     default: return "unknown error";
     }
 }

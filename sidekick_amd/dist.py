@@ -6,39 +6,46 @@ sharded encode; comm.hip).  It runs with one process driving several GPUs
 (`Comm.create(devices)`, the shape of the reference's single-process callers)
 or one process per GPU (`Comm.from_process_group()` ships the RCCL unique id
 over an existing torch.distributed group — gloo is enough — and every rank
-joins).
-
-The torch.distributed helpers further down (`reduce_partial_`,
-`root_test_sharded`, ...) restate the same shard / reduce / fold / merge
-protocol over any torch.distributed backend.  They are the CPU rehearsal of
-that protocol (gloo, world 2-3, tests/test_dist.py), since RCCL needs GPUs.
+joins).  `Comm.init_host(channel, ...)` builds the same communicator with its
+collectives over a host channel instead of RCCL — the identical native
+protocol (payload packing, failed-rank word, root fold, status gathers):
+`ProcessGroupChannel` carries them over a torch.distributed group (several
+ranks rehearsed on one GPU, which RCCL refuses) and `LoopbackHub` over
+threads of one process (world 2-8 on one GPU in the test suite).
 
 The sketch is additive: S_k(A ⊎ B) = S_k(A) + S_k(B) mod p
 and counts add, so the id stream is cut into contiguous shards, one per rank,
 each rank encodes its shard into a partial vector on its own GPU, and ONE
-sum-reduce of the partial words (RCCL over xGMI with backend "nccl"; gloo in
-the CPU tests) merges them on rank 0.  Partial words are canonical residues
-(< 2^32, limbs for the u64 field) stored as uint64, so the integer sum of up
-to 2^27 ranks cannot overflow; rank 0 folds the sum mod p.  last_value comes
-from the last non-empty shard, which rank 0 learns without communication
-(shards are contiguous and their sizes are known to every rank).
+sum-reduce of the payload merges them on the root.  Payload words are
+canonical residues (< 2^32, limbs for the u64 field) stored as uint64, so the
+integer sum of up to 2^27 ranks cannot overflow; the root folds the sum mod p
+and reads last_value from the per-rank (has_last, last) slots.
 
-Decode shards the same way: rank 0 turns the merged
-difference into coefficients (O(t^2), host), ONE broadcast ships
-[d, stop flag, stop value, c_1..c_d] to every rank, each rank root-tests its
-contiguous log shard on its own GPU (`root_test_shard`, which also reports
-where the stop value first occurs in the shard), ONE all-reduce(MIN) finds
-the global stop position (the caller's `break` at media_client.rs:307-309
-applies to the whole log), and the hit positions — offset by the shard base
-and cut at the global stop — are all-gathered (two small collectives: counts,
-then the padded positions).  Every rank returns the same ascending list,
-identical to the single-GPU root test of the whole log.
+Decode (comm.hip decode_sharded): the root turns the merged difference into
+coefficients (O(t^2), host) and broadcasts [status, d, stop flag, stop value,
+c_1..c_d]; each rank root-tests its contiguous log shard on its own GPU and
+finds where the stop value first occurs in it; one all-gather of (n, stop,
+hit count, status) per rank gives every rank the global stop (the caller's
+`break` at media_client.rs:307-309 applies to the whole log) and the lowest
+failing rank's status; then the hit positions — offset by the shard base, cut
+at the global stop — are all-gathered in fixed-size rounds.  Every rank
+returns the same ascending list, identical to the single-GPU root test.
+
+The torch.distributed helpers at the end (`pack_payload`, `fold_payload`,
+`root_test_sharded`, ...) restate that protocol in numpy over any
+torch.distributed backend: the CPU-only rehearsal (gloo, world 2-3,
+tests/test_dist.py) for a container without a GPU.  (`root_test_sharded`
+exchanges the stop with an all-reduce(MIN) instead of the native status
+gather; the merge it computes is the same.)
 """
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
+
+import sys
+import threading
 
 from ._lib import P32, P64, QK_E_CAPACITY, check, lib
 
@@ -47,6 +54,124 @@ from ._lib import P32, P64, QK_E_CAPACITY, check, lib
 # Native communicator (qk_comm_*): the product multi-GPU path
 # --------------------------------------------------------------------------
 COMM_ID_BYTES = 128
+
+_REDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.c_int)
+_BCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.c_int)
+_GATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_size_t)
+
+
+class _HostOps(C.Structure):
+    """qk_comm_host_ops (include/quack_hip.h)."""
+    _fields_ = [("user", C.c_void_p), ("reduce_sum_u64", _REDUCE_FN), ("broadcast_u64", _BCAST_FN),
+                ("allgather_u64", _GATHER_FN)]
+
+
+def _u64(ptr, n) -> np.ndarray:
+    return np.ctypeslib.as_array(ptr, (n,)) if n else np.zeros(0, dtype=np.uint64)
+
+
+class HostChannel:
+    """Collectives over uint64 numpy arrays (in place) for Comm.init_host:
+    reduce_sum(buf, root), broadcast(buf, root), allgather(send, recv) with
+    recv[r*n:(r+1)*n] = rank r's send.  Raise on failure."""
+
+    def reduce_sum(self, buf: np.ndarray, root: int) -> None:
+        raise NotImplementedError
+
+    def broadcast(self, buf: np.ndarray, root: int) -> None:
+        raise NotImplementedError
+
+    def allgather(self, send: np.ndarray, recv: np.ndarray) -> None:
+        raise NotImplementedError
+
+    def _ops(self):
+        """ctypes qk_comm_host_ops calling this channel (keep the result alive)."""
+        def guard(fn):
+            def call(*a):
+                try:
+                    fn(*a)
+                    return 0
+                except BaseException as e:   # noqa: BLE001 — nothing may unwind through C
+                    print(f"host channel collective failed: {e!r}", file=sys.stderr, flush=True)
+                    return -1
+            return call
+        red = _REDUCE_FN(guard(lambda _u, b, n, root: self.reduce_sum(_u64(b, n), root)))
+        bc = _BCAST_FN(guard(lambda _u, b, n, root: self.broadcast(_u64(b, n), root)))
+        ga = _GATHER_FN(guard(lambda _u, s, r, n: self.allgather(_u64(s, n), _u64(r, n * self.world))))
+        return _HostOps(None, red, bc, ga)
+
+
+class ProcessGroupChannel(HostChannel):
+    """The host collectives over a torch.distributed group (CPU tensors: gloo)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    @staticmethod
+    def _t(a):
+        import torch
+        return torch.from_numpy(a.view(np.int64))
+
+    def reduce_sum(self, buf, root):
+        import torch.distributed as dist
+        dist.reduce(self._t(buf), dst=root, op=dist.ReduceOp.SUM, group=self.group)
+
+    def broadcast(self, buf, root):
+        import torch.distributed as dist
+        dist.broadcast(self._t(buf), src=root, group=self.group)
+
+    def allgather(self, send, recv):
+        import torch.distributed as dist
+        n = len(send)
+        outs = list(self._t(recv).split(n)) if n else [self._t(recv)[:0] for _ in range(self.world)]
+        dist.all_gather(outs, self._t(send.copy()), group=self.group)
+
+
+class LoopbackHub:
+    """Host collectives between `world` ranks living in threads of one process
+    (each thread drives its own Comm.init_host rank).  A rank that never
+    arrives breaks the barrier after `timeout` s: the others fail instead of
+    waiting forever."""
+
+    def __init__(self, world: int, timeout: float = 120.0):
+        self.world = world
+        self.barrier = threading.Barrier(world, timeout=timeout)
+        self.slots = [None] * world
+
+    def channel(self, rank: int) -> "HostChannel":
+        return _LoopbackChannel(self, rank)
+
+
+class _LoopbackChannel(HostChannel):
+    def __init__(self, hub: LoopbackHub, rank: int):
+        self.hub, self.rank, self.world = hub, rank, hub.world
+
+    def reduce_sum(self, buf, root):
+        h = self.hub
+        h.slots[self.rank] = buf.copy()
+        h.barrier.wait()
+        if self.rank == root:
+            buf[:] = np.sum(np.stack(h.slots), axis=0, dtype=np.uint64)
+        h.barrier.wait()
+
+    def broadcast(self, buf, root):
+        h = self.hub
+        if self.rank == root:
+            h.slots[root] = buf.copy()
+        h.barrier.wait()
+        if self.rank != root:
+            buf[:] = h.slots[root]
+        h.barrier.wait()
+
+    def allgather(self, send, recv):
+        h = self.hub
+        h.slots[self.rank] = send.copy()
+        h.barrier.wait()
+        recv[:] = np.concatenate(h.slots)
+        h.barrier.wait()
 
 
 class Comm:
@@ -83,6 +208,17 @@ class Comm:
         return cls(h)
 
     @classmethod
+    def init_host(cls, channel: HostChannel, rank: int, world: int, device: int) -> "Comm":
+        """One rank whose collectives run over `channel` (qk_comm_init_host):
+        the native protocol with a host channel instead of RCCL."""
+        ops = channel._ops()
+        h = C.c_void_p()
+        check(lib().qk_comm_init_host(C.byref(ops), rank, world, device, C.byref(h)), "qk_comm_init_host")
+        c = cls(h)
+        c._keep = (channel, ops)     # the callbacks must outlive the communicator
+        return c
+
+    @classmethod
     def from_process_group(cls, device: int, group=None) -> "Comm":
         """Join a communicator spanning the ranks of a torch.distributed group
         (any backend: it only carries the 128-byte unique id)."""
@@ -105,7 +241,9 @@ class Comm:
         from .quack import Context
         h = C.c_void_p()
         check(lib().qk_comm_context(self.handle, local, C.byref(h)), "qk_comm_context")
-        return Context(device=-1, handle=h)
+        ctx = Context(device=-1, handle=h)
+        ctx._owner = self            # valid until this communicator is closed
+        return ctx
 
     @staticmethod
     def _arrays(tensors, bits):

@@ -32,6 +32,8 @@ def test_bench_contract_and_sharded_parity():
     assert one["n_gpus"] == 1 and one["steps"] == 3 and one["value"] > 0
     rf = one["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    v = rf["valu"]                        # the integer-issue roofline (tools/issue_roofline.py)
+    assert v["bound"] == "valu-issue" and 0 < v["frac"] < 1.5 and abs(v["frac"] - v["peak"] / v["achieved"]) < 1e-9
     cb = one["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["parity_with_gpu"] is True
     want = coracle.encode_u32_seed(seed, n_total, t)
@@ -39,8 +41,9 @@ def test_bench_contract_and_sharded_parity():
 
     two = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", "29561", "bench.py", "--gpus", "2", "--steps", "3",
-               "--warmup", "1", "--ids-per-gpu", str(n_total // 2), "--dist-backend", "gloo"])
+               "--warmup", "1", "--ids-per-gpu", str(n_total // 2), "--dist-backend", "host"])
     assert two["n_gpus"] == 2 and two["cpu_baseline"] is None
+    assert two["config"]["collectives"] == "host" and "rehearsal" in two["config"]["workload"]
     assert two["result"]["digest"] == one["result"]["digest"]
     assert two["result"]["count"] == n_total
 

@@ -99,3 +99,278 @@ def test_sharded_decode_undecodable_and_empty(comm):
         comm.decode_sharded(q, [log])
     z = sk.PowerSumQuackU32(4)
     assert comm.decode_sharded(z, [log]) == []
+
+
+# ----------------------------------------------------------------------------
+# World 2-8 on one GPU: the native protocol (comm.hip) with its collectives over
+# a host channel between threads (qk_comm_init_host + LoopbackHub).  RCCL takes
+# one rank per GPU, so this is how the multi-rank payload packing, the
+# failed-rank word, the root fold, the status gather and the chunked hit
+# gather run before the driver's 8-GPU node.
+# ----------------------------------------------------------------------------
+import threading  # noqa: E402
+
+
+def _run_ranks(world, fn, timeout=120.0, comms=None):
+    """fn(rank, comm) on one thread per rank, each with its own host-channel
+    communicator on device 0; returns [(ok, value_or_exception)] per rank."""
+    from sidekick_amd.dist import Comm, LoopbackHub
+    own = comms is None
+    if own:
+        hub = LoopbackHub(world, timeout=timeout)
+        comms = [Comm.init_host(hub.channel(r), r, world, 0) for r in range(world)]
+    out = [None] * world
+
+    def run(r):
+        try:
+            out[r] = (True, fn(r, comms[r]))
+        except Exception as e:  # noqa: BLE001
+            out[r] = (False, e)
+    ths = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout + 60)
+    assert not any(th.is_alive() for th in ths), "a rank hung"
+    if own:
+        for c in comms:
+            c.close()
+    return out
+
+
+def _shards(n_total, world, empty=()):
+    """Contiguous shards of a global stream; ranks in `empty` get none."""
+    from sidekick_amd.dist import shard
+    live = [r for r in range(world) if r not in empty]
+    bounds, pos = [], 0
+    for r in range(world):
+        if r in empty:
+            bounds.append((pos, 0))
+        else:
+            s, c = shard(n_total, live.index(r), len(live))
+            bounds.append((s, c))
+            pos = s + c
+    return bounds
+
+
+@pytest.mark.parametrize("world,bits,t,empty", [(2, 32, 32, ()), (4, 32, 16, (0, 2)), (8, 32, 32, (3, 7)),
+                                                (8, 64, 80, (0, 5)), (3, 64, 20, (2,))])
+def test_host_channel_world_n_encode_bit_exact(world, bits, t, empty):
+    import torch
+    import sidekick_amd as sk
+    Q = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+    n_total = 400_003 if bits == 32 else 150_001
+    host, ids = _ids(bits, n_total, 0x5A + world + t)
+    bounds = _shards(n_total, world, empty)
+    views = [ids[s:s + c] if c else torch.empty(0, dtype=ids.dtype, device="cuda") for s, c in bounds]
+
+    def rank_fn(r, comm):
+        q = Q(t)
+        q.insert(777)                   # the root's existing content: the stream follows it
+        comm.encode_sharded([views[r]], q)
+        return q
+
+    res = _run_ranks(world, rank_fn)
+    assert all(ok for ok, _ in res), res
+    root = res[0][1]
+    full = np.concatenate([np.array([777], dtype=host.dtype), host])
+    assert root.power_sums() == (coracle.encode_u32(full, t) if bits == 32 else coracle.encode_u64(full, t))
+    assert root.count() == n_total + 1 and root.last_value() == int(host[-1])
+    for r in range(1, world):           # non-root: untouched
+        q = res[r][1]
+        assert q.count() == 1 and q.last_value() == 777
+
+
+def test_host_channel_async_steps_and_root_not_zero():
+    import sidekick_amd as sk
+    world, t = 4, 32
+    host, ids = _ids(32, 1_000_000, 0xA7)
+    bounds = _shards(len(host), world)
+
+    def rank_fn(r, comm):
+        for _ in range(3):              # back-to-back async steps reuse the payload buffer
+            comm.encode_sharded_async([ids[bounds[r][0]:sum(bounds[r])]], t, root=2)
+        q = sk.PowerSumQuackU32(t)
+        comm.encode_sharded_wait(q)
+        comm.barrier()
+        return q
+
+    res = _run_ranks(world, rank_fn)
+    assert all(ok for ok, _ in res), res
+    assert res[2][1].power_sums() == coracle.encode_u32(host, t) and res[2][1].count() == len(host)
+    assert all(res[r][1].count() == 0 for r in (0, 1, 3))
+
+
+def _decode_case_gpu(bits, n_total, seed, dup_rank_pos=None, n_dup=0):
+    """Log with `n_dup` copies of one dropped id placed at dup_rank_pos (so one
+    shard holds more hits than a gather round carries)."""
+    import torch
+    import sidekick_amd as sk
+    Q = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+    a = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(seed, n_total).copy()
+    rng = np.random.default_rng(seed & 0xFFFF)
+    drops = np.sort(rng.choice(n_total, 30, replace=False))
+    if n_dup:
+        a[dup_rank_pos:dup_rank_pos + n_dup] = a[drops[0]]
+    keep = np.ones(n_total, bool)
+    keep[drops] = False
+    dt = np.int32 if bits == 32 else np.int64
+    log = torch.from_numpy(a.view(dt)).cuda()
+    A, B = Q(32), Q(32)
+    A.insert_batch(log)
+    B.insert_batch(torch.from_numpy(a[keep].view(dt)).cuda())
+    A.sub_assign(B)
+    return a, log, A
+
+
+@pytest.mark.parametrize("world,bits,n_dup,stop", [(8, 32, 0, True), (8, 32, 2500, False), (4, 64, 1200, True),
+                                                   (2, 32, 0, False), (5, 64, 0, False)])
+def test_host_channel_world_n_decode_matches_single_gpu(world, bits, n_dup, stop):
+    n_total = 200_000
+    a, log, diff = _decode_case_gpu(bits, n_total, 0xDE0 + world + bits, dup_rank_pos=60_000, n_dup=n_dup)
+    want = diff.root_test(diff.to_coeffs(), log, stop_value=diff.last_value() if stop else None)
+    assert len(want) >= (n_dup or 25)
+    bounds = _shards(n_total, world)
+
+    def rank_fn(r, comm):
+        s, c = bounds[r]
+        return comm.decode_sharded(diff if r == 0 else None, [log[s:s + c]], bits=bits, stop_at_last=stop)
+
+    res = _run_ranks(world, rank_fn)
+    assert all(ok for ok, _ in res), res
+    for ok, got in res:
+        assert got == want
+
+
+def test_host_channel_decode_stop_in_middle_shard():
+    """The stop value first occurs in rank 2's shard: every later hit is cut."""
+    world, n_total = 4, 100_000
+    a, log, diff = _decode_case_gpu(32, n_total, 0x5707)
+    want_all = diff.root_test(diff.to_coeffs(), log)
+    stop_pos = 55_000
+    stop_val = int(a[stop_pos])
+    first = int(np.nonzero(a == stop_val)[0][0])
+    want = [h for h in want_all if h < first]
+    assert len(want) < len(want_all)
+    import ctypes as C
+    q = diff.clone()                        # the same difference, last_value = the stop id
+    C.memmove(C.addressof(q._buf) + 8, np.array([1, stop_val], dtype=np.uint32).ctypes.data, 8)
+    assert q.last_value() == stop_val and q.count() == diff.count()
+    assert diff.root_test(diff.to_coeffs(), log, stop_value=stop_val) == want
+    bounds = _shards(n_total, world)
+
+    def rank_fn(r, comm):
+        s, c = bounds[r]
+        return comm.decode_sharded(q if r == 0 else None, [log[s:s + c]], stop_at_last=True)
+
+    res = _run_ranks(world, rank_fn)
+    assert all(ok for ok, _ in res), res
+    assert all(got == want for _, got in res)
+
+
+def test_host_channel_failure_on_one_rank_errors_everywhere_no_hang():
+    """A bad shard on one rank (misaligned device pointer): the sharded encode
+    returns its error on that rank and QK_E_PEER on the root, q untouched; the
+    sharded decode returns the same error on every rank; the communicator
+    stays usable."""
+    import torch
+    import sidekick_amd as sk
+    from sidekick_amd._lib import QK_E_INVAL, QK_E_PEER
+    world, t = 3, 16
+    host, ids = _ids(32, 30_000, 0xFA11)
+    raw = torch.zeros(10_001, dtype=torch.int32, device="cuda")
+    bad = raw.view(torch.uint8)[1:1 + 4 * 10_000]          # misaligned by one byte
+    bounds = _shards(len(host), world)
+    from sidekick_amd.dist import Comm, LoopbackHub
+    hub = LoopbackHub(world, timeout=60)
+    comms = [Comm.init_host(hub.channel(r), r, world, 0) for r in range(world)]
+    try:
+        from sidekick_amd._lib import lib
+        import ctypes as C
+
+        def enc(r, comm, bad_rank):
+            q = sk.PowerSumQuackU32(t)
+            q.insert(5)
+            before = q.power_sums()
+            s, c = bounds[r]
+            if r == bad_rank:
+                ptr, cnt = bad.data_ptr(), 10_000
+            else:
+                ptr, cnt = ids[s:s + c].data_ptr(), c
+            rc = lib().qk_u32_encode_sharded(comm.handle, (C.c_void_p * 1)(ptr), (C.c_size_t * 1)(cnt), q._buf, 0,
+                                             None)
+            return rc, q.power_sums() == before and q.count() == 1
+
+        for bad_rank in (1, 0):
+            res = _run_ranks(world, lambda r, cm: enc(r, cm, bad_rank), comms=comms)
+            assert all(ok for ok, _ in res), res
+            rcs = [v[0] for _, v in res]
+            assert rcs[bad_rank] == QK_E_INVAL
+            if bad_rank != 0:
+                assert rcs[0] == QK_E_PEER
+            assert all(v[1] for _, v in res)               # q untouched everywhere
+
+        a, log, diff = _decode_case_gpu(32, 60_000, 0xBAD)
+
+        def dec(r, comm):
+            s, c = bounds[r]
+            ptr = bad.data_ptr() if r == 2 else log[s:s + c].data_ptr()
+            hits = (C.c_uint64 * 64)()
+            nh = C.c_size_t()
+            return lib().qk_u32_decode_sharded(comm.handle, diff._buf if r == 0 else None, 0,
+                                               (C.c_void_p * 1)(ptr), (C.c_size_t * 1)(c), 1, hits, 64,
+                                               C.byref(nh), None)
+
+        res = _run_ranks(world, dec, comms=comms)
+        assert [v for _, v in res] == [QK_E_INVAL] * world
+
+        # still usable: a clean round after the failures
+        def good(r, comm):
+            q = sk.PowerSumQuackU32(t)
+            s, c = bounds[r]
+            comm.encode_sharded([ids[s:s + c]], q)
+            return q
+        res = _run_ranks(world, good, comms=comms)
+        assert res[0][1].power_sums() == coracle.encode_u32(host, t)
+    finally:
+        for c in comms:
+            c.close()
+
+
+def test_host_channel_peer_never_arrives_fails_instead_of_hanging():
+    """A rank that never joins: the channel times out, the caller gets
+    QK_E_COMM and the communicator stays failed (no hang)."""
+    import sidekick_amd as sk
+    from sidekick_amd._lib import QK_E_COMM, QuackError
+    from sidekick_amd.dist import Comm, LoopbackHub
+    hub = LoopbackHub(2, timeout=3)
+    c0 = Comm.init_host(hub.channel(0), 0, 2, 0)
+    try:
+        host, ids = _ids(32, 1000, 0x1)
+        q = sk.PowerSumQuackU32(8)
+        with pytest.raises(QuackError) as ei:
+            c0.encode_sharded([ids], q)
+        assert ei.value.code == QK_E_COMM and q.count() == 0
+        with pytest.raises(QuackError) as ei:
+            c0.barrier()
+        assert ei.value.code == QK_E_COMM
+    finally:
+        c0.close()
+
+
+def test_rccl_world1_local_failure_leaves_q_untouched(comm):
+    """World-1 RCCL communicator: a bad shard fails the call, q is untouched,
+    and the communicator keeps working."""
+    import torch
+    import ctypes as C
+    import sidekick_amd as sk
+    from sidekick_amd._lib import QK_E_INVAL, lib
+    raw = torch.zeros(1001, dtype=torch.int32, device="cuda")
+    q = sk.PowerSumQuackU32(32)
+    q.insert(3)
+    rc = lib().qk_u32_encode_sharded(comm.handle, (C.c_void_p * 1)(raw.data_ptr() + 2), (C.c_size_t * 1)(1000),
+                                     q._buf, 0, None)
+    assert rc == QK_E_INVAL and q.count() == 1 and q.power_sums()[0] == 3
+    host, ids = _ids(32, 5000, 0x33)
+    comm.encode_sharded([ids], q)
+    assert q.count() == 5001

@@ -108,7 +108,8 @@ def header_struct_fields(name):
     for decl in body.split(";"):
         decl = decl.strip()
         if decl:
-            fields.append(re.findall(r"(\w+)\s*(?:\[[^\]]*\])?$", decl)[0])
+            fp = re.search(r"\(\s*\*\s*(\w+)\s*\)", decl)          # function-pointer field
+            fields.append(fp.group(1) if fp else re.findall(r"(\w+)\s*(?:\[[^\]]*\])?$", decl)[0])
     return fields
 
 
@@ -119,7 +120,7 @@ def rust_struct_fields(name):
 
 
 def test_repr_c_structs_match_header():
-    for s in ("qk_u32", "qk_u64", "qk_pkt_meta", "qk_pkt_stats", "qk_flow_key"):
+    for s in ("qk_u32", "qk_u64", "qk_pkt_meta", "qk_pkt_stats", "qk_flow_key", "qk_comm_host_ops"):
         assert rust_struct_fields(s) == header_struct_fields(s), s
 
 

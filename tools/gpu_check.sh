@@ -25,6 +25,7 @@ for s in $STEPS; do
     ubissue) step ubissue 300 ./tools/ubench_issue || exit 3 ;;
     smoke) step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 3 ;;
     pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
+    pytestf) step pytestf 1200 python3 -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q -x -p no:cacheprovider -rA --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
     sgsweep)
       for g in ${SG_LIST:-0 2 4 6 8}; do
@@ -38,7 +39,8 @@ for s in $STEPS; do
     prof)
       export TMPDIR=/tmp
       step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 1 --cpu-sample 0 || exit 3 ;;
-    dist2) step dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --ids-per-gpu 2e8 --dist-backend gloo || exit 3 ;;
+    dist2) step dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --ids-per-gpu 2e8 --cpu-sample 0 || exit 3 ;;
+    dist4) step dist4 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --steps 3 --warmup 1 --ids-per-gpu 1e8 --cpu-sample 0 || exit 3 ;;
     tune) step tune 600 ./tools/tune_encode ${TUNE_ARGS:-} || exit 3 ;;
     tunebsgs) step tunebsgs 600 ./tools/tune_bsgs ${TUNE_ARGS:-} || exit 3 ;;
     listctr) step listctr 120 rocprofv3 -L || true ;;
