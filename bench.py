@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     ap.add_argument("--cpu-sample", type=float, default=1e8, help="ids for the CPU baseline (0 disables)")
     ap.add_argument("--grid", type=int, default=0, help="override workgroups per launch")
+    ap.add_argument("--knob", action="append", default=[], help="NAME=VALUE measurement knob (qk_ctx_set_knob)")
     ap.add_argument("--comm", action="store_true",
                     help="at N = 1 too, run each step through the native communicator (a world-1 ncclReduce)")
     ap.add_argument("--dist-backend", default="auto", choices=("auto", "rccl", "host"),
@@ -154,6 +155,9 @@ def main():
     ctx = comm.context(0) if comm is not None else sk.get_context(dev_index)
     if args.grid:
         ctx.set_grid(args.grid)
+    for kv in args.knob:                       # measurements only (tools/gpu_check.sh sweeps)
+        k, v = kv.split("=")
+        ctx.set_knob(k, int(v))
 
     idt = torch.int32 if bits == 32 else torch.int64
     ids = torch.empty(cnt, dtype=idt, device=f"cuda:{dev_index}")

@@ -155,6 +155,13 @@ int qk_ctx_kernel_stats(qk_ctx *ctx, double *total_ms, uint64_t *launches);
 int qk_ctx_trim(qk_ctx *ctx);
 /* Tuning knobs (0 = automatic): workgroups per launch. */
 int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
+/* Measurement knobs of this context (the defaults are the
+ * product's measured choices — tools/ and the variant tests set them):
+ * "bsgs_sg", "u32_passes", "bsgs64_sg", "bsgs64_off", "u64_passes",
+ * "u64_kmax", "flow_load" (2..64), "flow_wgpc", "pkt_fused", "rt64_horner",
+ * "root_test" (0 automatic, 1 Horner, 2 root-set scan).  Unknown name or
+ * out-of-range value -> QK_E_INVAL. */
+int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value);
 /* Pinned host memory for the host-input path: ids written here by the
  * sniffer are DMA'd without a staging copy. */
 int qk_host_alloc(size_t bytes, void **out);
@@ -285,6 +292,16 @@ int qk_u32_root_test_shard_device(qk_ctx *ctx, const uint32_t *coeffs, uint32_t 
 int qk_u64_root_test_shard_device(qk_ctx *ctx, const uint64_t *coeffs, uint32_t d, const uint64_t *d_log,
                                   size_t n, int stop_at_value, uint64_t stop_value, uint64_t *hits,
                                   size_t cap, size_t *n_hits, uint64_t *stop_index, void *stream);
+/* The distinct roots in GF(p), ascending, of the monic polynomial
+ * z^d + c_1 z^(d-1) + ... + c_d (coeffs as qk_*_to_coeffs writes them; any
+ * value is taken mod p).  An entry x of a log is a root-test hit
+ * (media_client.rs:310, eval(&coeffs, x) == 0) exactly when x mod p is one of
+ * them: the device root test scans the log against this set (O(1) per entry)
+ * when that beats d Horner steps per entry.  gcd(P, z^(p-1) - 1) and
+ * Cantor-Zassenhaus splitting on the host, O(d^2 log p).  *k = number of
+ * roots (<= d); cap < *k -> QK_E_CAPACITY. */
+int qk_u32_roots(const uint32_t *coeffs, uint32_t d, uint32_t *roots, uint32_t cap, uint32_t *k);
+int qk_u64_roots(const uint64_t *coeffs, uint32_t d, uint64_t *roots, uint32_t cap, uint32_t *k);
 /* decode_with_log on the device: to_coeffs(diff) on the host (O(t^2)), then
  * the root test over the device-resident log.  diff->count == 0 -> no hits;
  * diff->count > threshold -> QK_E_UNDECODABLE. */

@@ -152,6 +152,7 @@ extern "C" {
     pub fn qk_ctx_kernel_stats(ctx: *mut qk_ctx, total_ms: *mut f64, launches: *mut u64) -> c_int;
     pub fn qk_ctx_trim(ctx: *mut qk_ctx) -> c_int;
     pub fn qk_ctx_set_grid(ctx: *mut qk_ctx, blocks: u32) -> c_int;
+    pub fn qk_ctx_set_knob(ctx: *mut qk_ctx, name: *const c_char, value: i64) -> c_int;
     pub fn qk_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
     pub fn qk_host_free(p: *mut c_void) -> c_int;
 
@@ -195,6 +196,8 @@ extern "C" {
     pub fn qk_u64_root_test_shard_device(ctx: *mut qk_ctx, coeffs: *const u64, d: u32, d_log: *const u64, n: usize,
                                          stop_at_value: c_int, stop_value: u64, hits: *mut u64, cap: usize,
                                          n_hits: *mut usize, stop_index: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn qk_u32_roots(coeffs: *const u32, d: u32, roots: *mut u32, cap: u32, k: *mut u32) -> c_int;
+    pub fn qk_u64_roots(coeffs: *const u64, d: u32, roots: *mut u64, cap: u32, k: *mut u32) -> c_int;
     pub fn qk_u32_decode_device(ctx: *mut qk_ctx, diff: *const qk_u32, d_log: *const u32, n: usize,
                                 stop_at_last: c_int, hits: *mut u64, cap: usize, n_hits: *mut usize,
                                 stream: *mut c_void) -> c_int;

@@ -127,6 +127,11 @@ impl Context {
     pub fn set_grid(&self, blocks: u32) -> Result<()> {
         check(unsafe { ffi::qk_ctx_set_grid(self.raw, blocks) })
     }
+    /// A measurement knob (`qk_ctx_set_knob`).
+    pub fn set_knob(&self, name: &str, value: i64) -> Result<()> {
+        let c = std::ffi::CString::new(name).map_err(|_| QuackError { status: ffi::QK_E_INVAL })?;
+        check(unsafe { ffi::qk_ctx_set_knob(self.raw, c.as_ptr(), value) })
+    }
     /// Frees retired scratch (a device-wide synchronisation).
     pub fn trim(&self) -> Result<()> {
         check(unsafe { ffi::qk_ctx_trim(self.raw) })

@@ -2,7 +2,7 @@
 behind the C ABI in include/quack_hip.h).  See DESIGN.md."""
 from .quack import (  # noqa: F401
     CoefficientVector, Context, FlowQuacks, ModularInteger, PowerSumQuackU32, PowerSumQuackU64,
-    arithmetic, device_count, get_context,
+    arithmetic, device_count, get_context, roots,
 )
 from ._lib import P32, P64, QuackError, UndecodableError  # noqa: F401
 

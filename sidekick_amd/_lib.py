@@ -74,6 +74,7 @@ SIGNATURES = {
     "qk_ctx_set_profiling": (C.c_int, [vp, C.c_int]),
     "qk_ctx_kernel_stats": (C.c_int, [vp, C.POINTER(C.c_double), u64p]),
     "qk_ctx_set_grid": (C.c_int, [vp, C.c_uint32]),
+    "qk_ctx_set_knob": (C.c_int, [vp, C.c_char_p, C.c_int64]),
     "qk_ctx_trim": (C.c_int, [vp]),
     "qk_host_alloc": (C.c_int, [sz, C.POINTER(vp)]),
     "qk_host_free": (C.c_int, [vp]),
@@ -93,6 +94,8 @@ SIGNATURES = {
                                                 u64p, vp]),
     "qk_u64_root_test_shard_device": (C.c_int, [vp, u64p, C.c_uint32, vp, sz, C.c_int, C.c_uint64, u64p, sz, szp,
                                                 u64p, vp]),
+    "qk_u32_roots": (C.c_int, [u32p, C.c_uint32, u32p, C.c_uint32, u32p]),
+    "qk_u64_roots": (C.c_int, [u64p, C.c_uint32, u64p, C.c_uint32, u32p]),
     "qk_u32_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
     "qk_u64_decode_device": (C.c_int, [vp, vp, vp, sz, C.c_int, u64p, sz, szp, vp]),
     "qk_u32_encode_packets_device": (C.c_int, [vp, vp, sz, sz, vp, vp, vp, vp, vp]),

@@ -261,28 +261,70 @@ static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t,
 // buffer if the kernel ran out of room, and returns the hit positions sorted
 // ascending (every hit of the log, not cut at the stop) and the first stop
 // position (n if none or !use_stop).
+// Root test by the root-set scan (decode.hip k_root_scan) or by Horner
+// (k_root_test_*): the same hit list (P(x) == 0 <=> x mod p is a root of P).
+// The scan costs the host root finding (roots.cpp, ~c d^2) plus an HBM-bound
+// pass; Horner costs d multiply steps per candidate.  Cost model in
+// microseconds from the measurements in DESIGN.md §3.4 (MI355X kernels,
+// EPYC host root finding): the scan is taken when it is cheaper.
+template <typename T> static bool rt_use_scan(qk_ctx *ctx, uint32_t d, size_t n) {
+    if (d < 2 || d > RT_SCAN_MAXD) return false;          // d = 1: the root is -c_1, Horner is one step
+    if (ctx->knobs.root_test == 1) return false;
+    if (ctx->knobs.root_test == 2) return true;
+    const double nn = (double)n, dd = (double)d;
+    const bool w32 = sizeof(T) == 4;
+    const double horner = nn * dd * (w32 ? 1.43e-7 : 3.8e-7);
+    const double scan = nn * (w32 ? 0.7e-6 : 1.4e-6) + dd * dd * (w32 ? 0.16 : 0.7);
+    return scan < horner;
+}
+
 template <typename T>
 int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
                     hipStream_t s) {
-    int (*launch)(qk_ctx *, const T *, uint32_t, const T *, size_t, int, T, uint64_t *, uint64_t, uint64_t *,
-                  hipStream_t);
-    if constexpr (sizeof(T) == 4) launch = launch_root_test_u32;
-    else launch = launch_root_test_u64;
-    // layout of d_small: [0, SMALL_NHITS) coefficients, [SMALL_NHITS] hit count, [SMALL_STOP] stop index
+    // layout of d_small: [0, SMALL_NHITS) coefficients (or the root set), [SMALL_NHITS] hit count,
+    // [SMALL_STOP] stop index
     uint64_t *d_counters = ctx->d_small + SMALL_NHITS;
     T *d_c = (T *)ctx->d_small;
+    bool scan = n && rt_use_scan<T>(ctx, d, n);
+    RtScanSet set;
     size_t cbytes = (size_t)d * sizeof(T);
-    if constexpr (sizeof(T) == 8) {
-        if (rt64_use_bsgs(d)) cbytes = rt64_bsgs_table(coeffs, d, ctx->h_small) * 8;   // limb-shifted table
-        else memcpy(ctx->h_small, coeffs, cbytes);
-    } else {
-        memcpy(ctx->h_small, coeffs, cbytes);
+    if (scan) {
+        std::vector<T> r(d), tab;
+        uint32_t k = 0;
+        int rc;
+        if constexpr (sizeof(T) == 4) rc = qk_u32_roots(coeffs, d, r.data(), d, &k);
+        else rc = qk_u64_roots(coeffs, d, r.data(), d, &k);
+        if (rc) return rc;
+        scan = rt_scan_table<T>(r.data(), k, set, tab) && set.words * sizeof(T) <= SMALL_NHITS * 8;
+        if (scan) {
+            cbytes = (size_t)set.words * sizeof(T);
+            memcpy(ctx->h_small, tab.data(), cbytes);
+        }
+    }
+    if (!scan) {
+        if constexpr (sizeof(T) == 8) {
+            if (rt64_use_bsgs(ctx, d)) cbytes = rt64_bsgs_table(coeffs, d, ctx->h_small) * 8;   // limb-shifted table
+            else memcpy(ctx->h_small, coeffs, cbytes);
+        } else {
+            memcpy(ctx->h_small, coeffs, cbytes);
+        }
     }
     if (cbytes) QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, cbytes, hipMemcpyHostToDevice, s));
     if (int rc = ensure_hits(ctx, 4096, s)) return rc;
     hipLaunchKernelGGL(k_init_counters, dim3(1), dim3(1), 0, s, d_counters);
     if (n) {
-        int rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap, d_counters, s);
+        int rc;
+        if (scan) {
+            rc = launch_root_scan<T>(ctx, d_c, set, d_log, n, use_stop, stop_value, ctx->d_hits,
+                                     (uint64_t)ctx->hits_cap, d_counters, s);
+        } else {
+            int (*launch)(qk_ctx *, const T *, uint32_t, const T *, size_t, int, T, uint64_t *, uint64_t, uint64_t *,
+                          hipStream_t);
+            if constexpr (sizeof(T) == 4) launch = launch_root_test_u32;
+            else launch = launch_root_test_u64;
+            rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap,
+                        d_counters, s);
+        }
         if (rc) return rc;
     }
     QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_NHITS, d_counters, 16, hipMemcpyDeviceToHost, s));
@@ -476,6 +518,34 @@ int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks) {
     if (!ctx) return QK_E_INVAL;
     ctx->grid_override = blocks;
     return QK_OK;
+}
+
+int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
+    if (!ctx || !name) return QK_E_INVAL;
+    struct K {
+        const char *name;
+        int qk_knobs::*field;
+        int64_t lo, hi;
+    };
+    static const K table[] = {
+        {"bsgs_sg", &qk_knobs::bsgs_sg, -1, 64},       {"u32_passes", &qk_knobs::u32_passes, 0, 1},
+        {"bsgs64_sg", &qk_knobs::bsgs64_sg, -1, 64},   {"bsgs64_off", &qk_knobs::bsgs64_off, 0, 1},
+        {"u64_passes", &qk_knobs::u64_passes, 0, 1},   {"u64_kmax", &qk_knobs::u64_kmax, 4, 40},
+        {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
+        {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
+        {"root_test", &qk_knobs::root_test, 0, 2},
+#ifdef QK_WITH_MATRIX_CORES
+        {"matrix_cores", &qk_knobs::matrix_cores, 0, 1},
+#endif
+    };
+    for (const K &k : table)
+        if (strcmp(k.name, name) == 0) {
+            if (value < k.lo || value > k.hi) return QK_E_INVAL;
+            std::lock_guard<std::mutex> g(ctx->mu);
+            ctx->knobs.*(k.field) = (int)value;
+            return QK_OK;
+        }
+    return QK_E_INVAL;
 }
 
 int qk_host_alloc(size_t bytes, void **out) {

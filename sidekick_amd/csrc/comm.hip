@@ -501,6 +501,7 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
     for (auto &L : c->local)
         if (int e = leave(L); e && !rc) rc = e;
     if (rc) return rc;
+    std::sort(all.begin(), all.end());   // rounds arrive rank-major: restore log order
     *n_hits = all.size();
     if (all.size() > cap || (!all.empty() && !hits)) return QK_E_CAPACITY;
     std::copy(all.begin(), all.end(), hits);

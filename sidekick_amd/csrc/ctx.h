@@ -7,6 +7,24 @@
 
 #include "quack_hip.h"
 
+// Measurement knobs (qk_ctx_set_knob; only tools/ and tests set them — the
+// defaults below are the product's choices, each backed by a measurement in
+// DESIGN.md).  Per context, so one process can compare variants.
+struct qk_knobs {
+    int bsgs_sg = -1;      // u32 BSGS: scalar-counted wrap groups (-1: the per-shape default)
+    int u32_passes = 1;    // 0: u32 t > 80 on the power chain instead of BSGS passes
+    int bsgs64_sg = -1;    // u64 BSGS MAC mode override (-1: default)
+    int bsgs64_off = 0;    // 1: u64 on the power chain instead of BSGS
+    int u64_passes = 1;    // 0: u64 t > 80 on the power chain instead of BSGS passes
+    int u64_kmax = 40;     // u64 power chain: accumulators per lane
+    int flow_load = 4;     // flow-table slots per expected flow
+    int flow_wgpc = 12;    // flow extract: workgroups per CU
+    int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
+    int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
+    int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)
+    int matrix_cores = 0;  // 1: the int8-MFMA encode variants (libquack_hip_mfma.so build only)
+};
+
 struct qk_ctx {
     int device = 0;
     int num_cus = 256;
@@ -14,6 +32,7 @@ struct qk_ctx {
                                        // stream argument is the HIP null stream, not this one
     hipStream_t copy_stream = nullptr; // second stream for the host-input pipeline
     uint32_t grid_override = 0;
+    qk_knobs knobs;
 
     // scratch: block partials of the encode kernels, hit buffers of the root test
     void *d_scratch = nullptr;
@@ -103,20 +122,33 @@ int launch_encode_u64_acc(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t
 int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uint32_t *log, size_t n,
                          int use_stop, uint32_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);
-// u64 encode on the matrix cores for T >= 9 (mfma64.hip); same output
-// as launch_encode_u64 (accumulate: add into out)
+#ifdef QK_WITH_MATRIX_CORES
+// u64 encode on the matrix cores for T >= 9 (mfma64.hip; the opt-in
+// libquack_hip_mfma.so build); same output as launch_encode_u64
 int launch_encode_u64_mfma(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t T, uint64_t *out, int acc,
                            hipStream_t s);
+#endif
 // canonical power sums out[0..T) from per-block partials [power][block] (encode.hip)
 int launch_finalize_powers_u32(const uint64_t *partials, uint32_t nblocks, uint32_t T, uint64_t *out,
                                hipStream_t s);
 // u64 root test by baby-step/giant-step for these degrees (decode.hip); the
 // coefficient buffer then holds rt64_bsgs_table's limb-shifted table
-bool rt64_use_bsgs(uint32_t d);
+bool rt64_use_bsgs(const qk_ctx *ctx, uint32_t d);
+// largest degree the root-set scan takes (its set must fit d_small)
+constexpr uint32_t RT_SCAN_MAXD = 256;
 size_t rt64_bsgs_table(const uint64_t *coeffs, uint32_t d, uint64_t *out);
 int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uint64_t *log, size_t n,
                          int use_stop, uint64_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);
+
+// root-set scan (decode.hip): the hash set of P's roots in LDS
+struct RtScanSet {
+    uint32_t S = 1, words = 0, m1 = 1, m2 = 1, shift = 28;
+};
+template <typename T> bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &out);
+template <typename T>
+int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
+                     T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, hipStream_t s);
 
 // root test in two phases (api.hip): enqueue on s, then wait + collect the
 // sorted hit positions (all of them) and the first stop position

@@ -14,6 +14,8 @@
 // first log entry equal to diff.last_value() becomes an atomicMin of that
 // position; the host drops hits at or after it.
 #include <cstdlib>
+#include <type_traits>
+#include <vector>
 
 #include "bsgs64.h"
 #include "ctx.h"
@@ -334,9 +336,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_test_u64_bsgs(const uint64_t 
     }
 }
 
-bool rt64_use_bsgs(uint32_t d) {
-    static const int no_bsgs = [] { const char *e = getenv("QK_TUNE_RT64_HORNER"); return e ? atoi(e) : 0; }();
-    return !no_bsgs && d >= RT64_BSGS_MIND && d <= RT64_BSGS_MAXD;
+bool rt64_use_bsgs(const qk_ctx *ctx, uint32_t d) {
+    return !ctx->knobs.rt64_horner && d >= RT64_BSGS_MIND && d <= RT64_BSGS_MAXD;
 }
 
 // host: the limb-shifted coefficient table of the BSGS kernel into out[]
@@ -357,6 +358,168 @@ size_t rt64_bsgs_table(const uint64_t *coeffs, uint32_t d, uint64_t *out) {
         }
     }
     return words;
+}
+
+template <typename KernelT>
+static uint32_t rs_grid(qk_ctx *ctx, KernelT kern, uint64_t units, size_t lds) {
+    if (ctx->grid_override) return ctx->grid_override;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, RT_BLOCK, lds) != hipSuccess || occ < 1) occ = 1;
+    const uint64_t full = (uint64_t)ctx->num_cus * occ;
+    uint64_t need = (units + RT_BLOCK - 1) / RT_BLOCK;
+    if (need < 1) need = 1;
+    return (uint32_t)(need < full ? need : full);
+}
+
+// ------------------------------------------------------- root-set scan
+// The same hit list from the roots of P (roots.cpp): P(x) == 0 exactly when
+// x mod p is a root, so each candidate is reduced mod p and looked up in a
+// hash set of the k <= d roots held in LDS — O(1) per candidate, the scan is
+// bound by the HBM read of the log instead of d Horner steps.
+// Set layout (built on the host, rt_scan_table): nb = 2^b buckets of S
+// slots; root r sits in bucket h(r) = (lo(r) m1 + hi(r) m2 mod 2^32) >> (32 - b)
+// (hi = 0 for u32), the multipliers chosen so that no bucket overflows; free
+// slots hold all-ones (>= p, never equal to a reduced candidate).
+template <typename T> __device__ __forceinline__ T rs_reduce(T x);
+template <> __device__ __forceinline__ uint32_t rs_reduce<uint32_t>(uint32_t x) {
+    const uint32_t y = x + C32;   // wraps exactly when x >= p (to x - p)
+    return y < x ? y : x;
+}
+template <> __device__ __forceinline__ uint64_t rs_reduce<uint64_t>(uint64_t x) {
+    const uint64_t y = x + C64;
+    return y < x ? y : x;
+}
+
+template <typename T, int S>
+__device__ __forceinline__ bool rs_member(T x, const T *__restrict__ set, uint32_t m1, uint32_t m2, uint32_t shift) {
+    const T xr = rs_reduce<T>(x);
+    uint32_t hh = (uint32_t)xr * m1;
+    if constexpr (sizeof(T) == 8) hh += (uint32_t)(xr >> 32) * m2;
+    const T *b = set + (size_t)(hh >> shift) * S;
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < S; ++j) hit |= b[j] == xr;
+    return hit;
+}
+
+template <typename T, int S>
+__global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ log, uint64_t n, uint32_t head,
+                                                        const T *__restrict__ tab, uint32_t words, uint32_t m1,
+                                                        uint32_t m2, uint32_t shift, int use_stop, T stop_value,
+                                                        uint64_t *__restrict__ hits, uint64_t cap,
+                                                        uint64_t *__restrict__ counters) {
+    extern __shared__ __align__(16) unsigned char rs_lds[];
+    T *set = reinterpret_cast<T *>(rs_lds);
+    for (uint32_t i = threadIdx.x; i < words; i += RT_BLOCK) set[i] = tab[i];
+    __syncthreads();
+    constexpr int V = 16 / sizeof(T);   // candidates per 16-byte load
+    using Vec = typename std::conditional<sizeof(T) == 4, uint4, ulonglong2>::type;
+    const uint64_t gtid = (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * RT_BLOCK;
+    const uint64_t h = head < n ? head : n;
+    const uint64_t body = (n - h) / V;
+    const Vec *__restrict__ v = reinterpret_cast<const Vec *>(log + h);
+    // two loads in flight per lane
+    uint64_t i = gtid;
+    for (; i + nthr < body; i += 2 * nthr) {
+        const Vec w0 = v[i], w1 = v[i + nthr];
+        const T *e0 = reinterpret_cast<const T *>(&w0), *e1 = reinterpret_cast<const T *>(&w1);
+        bool any = false, hit[2][V], st[2][V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            hit[0][j] = rs_member<T, S>(e0[j], set, m1, m2, shift);
+            hit[1][j] = rs_member<T, S>(e1[j], set, m1, m2, shift);
+            st[0][j] = use_stop && e0[j] == stop_value;
+            st[1][j] = use_stop && e1[j] == stop_value;
+            any |= hit[0][j] | hit[1][j] | st[0][j] | st[1][j];
+        }
+        if (any) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                rt_record(h + (uint64_t)V * i + j, hit[0][j], st[0][j], hits, cap, counters);
+                rt_record(h + (uint64_t)V * (i + nthr) + j, hit[1][j], st[1][j], hits, cap, counters);
+            }
+        }
+    }
+    if (i < body) {
+        const Vec w0 = v[i];
+        const T *e0 = reinterpret_cast<const T *>(&w0);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const bool hit = rs_member<T, S>(e0[j], set, m1, m2, shift);
+            const bool st = use_stop && e0[j] == stop_value;
+            if (hit | st) rt_record(h + (uint64_t)V * i + j, hit, st, hits, cap, counters);
+        }
+    }
+    const uint64_t tail0 = h + body * V;
+    if (gtid < h) {
+        const T x = log[gtid];
+        rt_record(gtid, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters);
+    }
+    if (gtid < n - tail0) {
+        const uint64_t pos = tail0 + gtid;
+        const T x = log[pos];
+        rt_record(pos, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters);
+    }
+}
+
+// host: the hash set of the roots (see k_root_scan).  S = 1 for up to 32
+// roots (2^b >= 2 k^2 buckets: a multiplier pair without collisions is found
+// in ~1.3 tries on average), else S = 4 with 2^b >= 2k buckets (mean load
+// 1/2).  Returns false when no multipliers fit within the attempt limit.
+template <typename T>
+bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &out) {
+    set.S = k <= 32 ? 1 : 4;
+    uint32_t b = 4;
+    const uint64_t want = set.S == 1 ? 2ull * k * k : 2ull * k;
+    while ((1ull << b) < want) ++b;
+    set.shift = 32 - b;
+    const uint32_t nb = 1u << b;
+    set.words = nb * set.S;
+    out.assign(set.words, (T)~(T)0);
+    std::vector<uint32_t> fill(nb);
+    uint64_t st = 0x9E3779B97F4A7C15ull ^ k;
+    for (int attempt = 0; attempt < 1000; ++attempt) {
+        st = splitmix_mix(st + GAMMA);
+        set.m1 = (uint32_t)st | 1u;
+        set.m2 = (uint32_t)(st >> 32) | 1u;
+        std::fill(fill.begin(), fill.end(), 0u);
+        std::fill(out.begin(), out.end(), (T)~(T)0);
+        bool ok = true;
+        for (uint32_t r = 0; r < k && ok; ++r) {
+            const T x = roots[r];
+            uint32_t hh = (uint32_t)x * set.m1;
+            if constexpr (sizeof(T) == 8) hh += (uint32_t)((uint64_t)x >> 32) * set.m2;
+            const uint32_t bi = hh >> set.shift;
+            if (fill[bi] == set.S) ok = false;
+            else out[(size_t)bi * set.S + fill[bi]++] = x;
+        }
+        if (ok) return true;
+    }
+    return false;
+}
+template bool rt_scan_table<uint32_t>(const uint32_t *, uint32_t, RtScanSet &, std::vector<uint32_t> &);
+template bool rt_scan_table<uint64_t>(const uint64_t *, uint32_t, RtScanSet &, std::vector<uint64_t> &);
+
+template <typename T>
+int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
+                     T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, hipStream_t s) {
+    const uintptr_t a = (uintptr_t)log;
+    if (a & (sizeof(T) - 1)) return QK_E_INVAL;
+    const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / sizeof(T));
+    const size_t lds = (size_t)set.words * sizeof(T);
+    const uint64_t units = (n + 2 * (16 / sizeof(T)) - 1) / (2 * (16 / sizeof(T)));
+    hipEvent_t e0 = prof_begin(ctx, s);
+#define QK_RS(SS)                                                                                             \
+    hipLaunchKernelGGL((k_root_scan<T, SS>), dim3(rs_grid(ctx, k_root_scan<T, SS>, units, lds)), dim3(RT_BLOCK), \
+                       lds, s, log, (uint64_t)n, head, d_tab, set.words, set.m1, set.m2, set.shift, use_stop,     \
+                       stop_value, hits, cap, counters)
+    if (set.S == 1) QK_RS(1);
+    else QK_RS(4);
+#undef QK_RS
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
 }
 
 // ---------------------------------------------------------- launchers
@@ -404,7 +567,7 @@ int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uin
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
     const uint64_t units = (n + 1) / 2;
     hipEvent_t e0 = prof_begin(ctx, s);
-    if (rt64_use_bsgs(d)) {
+    if (rt64_use_bsgs(ctx, d)) {
         // d_c holds the limb-shifted table (root_test_begin, rt64_bsgs_table)
         // one runtime loop over the blocks: an unrolled loop (d / 8 fixed) or
         // two interleaved candidates made the compiler shuttle every value
@@ -421,5 +584,10 @@ int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uin
     QK_HIP_TRY(hipGetLastError());
     return QK_OK;
 }
+
+template int launch_root_scan<uint32_t>(qk_ctx *, const uint32_t *, const RtScanSet &, const uint32_t *, size_t, int,
+                                        uint32_t, uint64_t *, uint64_t, uint64_t *, hipStream_t);
+template int launch_root_scan<uint64_t>(qk_ctx *, const uint64_t *, const RtScanSet &, const uint64_t *, size_t, int,
+                                        uint64_t, uint64_t *, uint64_t, uint64_t *, hipStream_t);
 
 } // namespace qk

@@ -23,7 +23,9 @@
 #include "field.h"
 #include "bsgs.h"
 #include "bsgs64.h"
+#ifdef QK_WITH_MATRIX_CORES
 #include "mfma8.h"
+#endif
 
 // scalar-counted wrap groups of the t = 25..32 BSGS kernel (tools/tune_bsgs.hip)
 #ifndef QK_BSGS_SG_T32
@@ -97,6 +99,7 @@ __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB *
     bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD>>(ids, n, head, T, partials);
 }
 
+#ifdef QK_WITH_MATRIX_CORES
 // ---- baby-step / giant-step products on the matrix cores (mfma8.h,
 // DESIGN.md §3.2b): NM blocks of 4 giants x NN blocks of 4 babies
 template <int NM, int NN, int NBU = 4 * NN, int NAU = 4 * NM>
@@ -149,6 +152,7 @@ __global__ __launch_bounds__(64) void k_mfma32_fix(const uint64_t *__restrict__ 
         else if (!accumulate) out[T + 1] = 0;
     }
 }
+#endif // QK_WITH_MATRIX_CORES
 
 // Offset pass for thresholds > 80 (several passes over the ids): powers
 // base+1 .. base+8*NA with giants x^(base + 8a), a = 0..NA-1 (bsgs.h OFF).
@@ -662,6 +666,7 @@ static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_id
     return scratch_release(ctx, s);
 }
 
+#ifdef QK_WITH_MATRIX_CORES
 // One matrix-core pass: powers base + 1 .. base + Tp of T (S = the batch's
 // canonical sums, T + 256 words of scratch).
 template <int NM, int NN, bool OFF, int NBU = 4 * NN, int NAU = 4 * NM>
@@ -735,6 +740,8 @@ static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, ui
     if (int e = scratch_release(ctx, s); e && !rc) rc = e;
     return rc;
 }
+
+#endif // QK_WITH_MATRIX_CORES
 
 static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
                         int acc, hipStream_t s) {
@@ -916,11 +923,6 @@ static void choose_gk(uint32_t T, int kmax, const int *kg1, int nkg1, const int 
         if ((uint32_t)ks[i] >= kneed) { K = ks[i]; break; }
 }
 
-// QK_MATRIX_CORES=1: the int8-MFMA encode variants (opt-in)
-static bool matrix_cores_enabled() {
-    const char *e = getenv("QK_MATRIX_CORES");
-    return e && atoi(e) != 0;
-}
 
 static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc, hipStream_t s) {
     if (T == 0 || T > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
@@ -934,16 +936,18 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     // wave sees at most 64 * (4 * trips + 2) wraps per accumulator, so trips
     // must stay < 2^24 - 1 — true for any n < 2^40 at >= 1 workgroup per CU;
     // a tiny override grid over a huge n takes the all-VALU form.
-    // QK_TUNE_BSGS_SG=g overrides the number of scalar-counted groups
+    // knob bsgs_sg overrides the number of scalar-counted groups
     // (measurements; tools/tune_bsgs.hip).
-    static const int sg_env = [] { const char *e = getenv("QK_TUNE_BSGS_SG"); return e ? atoi(e) : -1; }();
+    const int sg_env = ctx->knobs.bsgs_sg;
     const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
     auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
-    // matrix-core variant (mfma8.h) for T >= 9: opt-in with
-    // QK_MATRIX_CORES=1 (north_star keeps the product on the vector ALUs);
-    // read per call so a process can compare both forms
-    if (T >= 9 && matrix_cores_enabled()) return enc32_mfma(ctx, ids, n, T, out, acc, s);
+#ifdef QK_WITH_MATRIX_CORES
+    // matrix-core variant (mfma8.h) for T >= 9: only in the
+    // opt-in libquack_hip_mfma.so build, with knob matrix_cores = 1
+    // (north_star keeps the product on the vector ALUs)
+    if (T >= 9 && ctx->knobs.matrix_cores) return enc32_mfma(ctx, ids, n, T, out, acc, s);
+#endif
 #define QK_BSGS(NB_, NA_, G_)                                                                        \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)
@@ -971,8 +975,8 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     if (T >= 49 && T <= 56 && sg(14)) return QK_BSGS(8, 7, 14);
     if (T >= 57 && T <= 64 && sg(16)) return QK_BSGS(8, 8, 16);
     if (T >= 65 && T <= 80 && sg(16)) return QK_BSGS(8, 10, 16);
-    // QK_TUNE_U32_PASSES=0 keeps t > 80 on the power chain (measurements)
-    static const int passes_env = [] { const char *e = getenv("QK_TUNE_U32_PASSES"); return e ? atoi(e) : 1; }();
+    // knob u32_passes = 0 keeps t > 80 on the power chain (measurements)
+    const int passes_env = ctx->knobs.u32_passes;
     if (T > 80 && sg(16) && passes_env) return enc32_passes(ctx, ids, n, head, T, out, acc, s);
 #undef QK_BSGS
     int G, K;
@@ -997,13 +1001,15 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     // ~20 powers the 15-odd modmuls of the babies and giants cost more than
     // the chain they save, tools/bench_configs.py sweep64): NA = ceil(T / 8)
     // giant rows; its per-wave 32-bit carry totals need < 2^31 ids per
-    // workgroup.  QK_TUNE_BSGS64_SG (T > 72 only) picks a carry mode
-    // for measurements (tools/tune_u64.hip); QK_TUNE_BSGS64_OFF=1 forces the
+    // workgroup.  knob bsgs64_sg (T > 72 only) picks a carry mode
+    // for measurements (tools/tune_u64.hip); knob bsgs64_off = 1 forces the
     // power chain.
+#ifdef QK_WITH_MATRIX_CORES
     // matrix-core variant (mfma64.h), opt-in as for u32
-    if (T >= 9 && matrix_cores_enabled()) return launch_encode_u64_mfma(ctx, ids, n, T, out, acc, s);
-    static const int sg64 = [] { const char *e = getenv("QK_TUNE_BSGS64_SG"); return e ? atoi(e) : -1; }();
-    static const int no64 = [] { const char *e = getenv("QK_TUNE_BSGS64_OFF"); return e ? atoi(e) : 0; }();
+    if (T >= 9 && ctx->knobs.matrix_cores) return launch_encode_u64_mfma(ctx, ids, n, T, out, acc, s);
+#endif
+    const int sg64 = ctx->knobs.bsgs64_sg;
+    const int no64 = ctx->knobs.bsgs64_off;
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     if (T >= 21 && T <= 80 && !no64 && n / min_grid64 < (1ull << 30)) {
 #define QK_BSGS64(NA_, MODE_, SG_)                                                                    \
@@ -1028,14 +1034,14 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
         }
 #undef QK_BSGS64
     }
-    // QK_TUNE_U64_PASSES=0 keeps t > 80 on the power chain (measurements)
-    static const int passes64 = [] { const char *e = getenv("QK_TUNE_U64_PASSES"); return e ? atoi(e) : 1; }();
+    // knob u64_passes = 0 keeps t > 80 on the power chain (measurements)
+    const int passes64 = ctx->knobs.u64_passes;
     if (T > 80 && !no64 && passes64 && n / min_grid64 < (1ull << 30)) return enc64_passes(ctx, ids, n, head, T, out, acc, s);
     int G, K;
     // K <= 40 accumulators per lane (120 VGPRs, 3 waves/SIMD) beat K <= 20 at
     // 5 waves by needing fewer lanes per id (t = 80: 2 x (39 + 1) steps vs
-    // 4 x (19 + 3)); QK_TUNE_U64_KMAX overrides for measurements.
-    static const int kmax = [] { const char *e = getenv("QK_TUNE_U64_KMAX"); return e ? atoi(e) : 40; }();
+    // 4 x (19 + 3)); knob u64_kmax overrides for measurements.
+    const int kmax = ctx->knobs.u64_kmax;
     choose_gk(T, kmax, K64_G1, 10, K64_GN, 6, G, K);
     switch (G) {
     case 1: return enc64_g<1>(ctx, K, ids, n, head, T, out, acc, s);

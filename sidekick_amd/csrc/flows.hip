@@ -765,8 +765,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     // copies (16 B per packet), counters, hipCUB temp storage.  Arena 2: the
     // flow table (C slots) and slot -> rank.  Arena 1, per flow: see below.
     const uint64_t cmax = std::min<uint64_t>(next_pow2(2 * (uint64_t)n + 2), 1ull << 31);
-    // table slots per expected flow (QK_TUNE_FLOW_LOAD overrides for measurements)
-    static const uint64_t spf = [] { const char *e = getenv("QK_TUNE_FLOW_LOAD"); return e ? (uint64_t)atoi(e) : 4ull; }();
+    // table slots per expected flow (knob flow_load, [2, 64], for measurements)
+    const uint64_t spf = (uint64_t)ctx->knobs.flow_load;
     uint64_t C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(4096, spf * (uint64_t)ctx->flow_hint)));
     size_t tb = 0;
     {
@@ -816,8 +816,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const qk_pkt_meta *pm = d_meta ? d_meta + p_from : nullptr;
         // >= 4 tiles per workgroup, enough workgroups to cover the chip
         const uint64_t ntiles = (pn + REC_TILE - 1) / REC_TILE;
-        // QK_TUNE_FLOW_WGPC: workgroups per CU (measurements; default 12: 4, 6, 8, 12 measured, 12 best at 1e4 and 1e6 flows)
-        static const uint64_t wgpc = [] { const char *e = getenv("QK_TUNE_FLOW_WGPC"); return e ? (uint64_t)atoi(e) : 12ull; }();
+        // knob flow_wgpc: workgroups per CU (measurements; default 12: 4, 6, 8, 12 measured, 12 best at 1e4 and 1e6 flows)
+        const uint64_t wgpc = (uint64_t)ctx->knobs.flow_wgpc;
         const uint64_t tiles_per_chunk =
             std::max<uint64_t>(4, (ntiles + (uint64_t)ctx->num_cus * wgpc - 1) / ((uint64_t)ctx->num_cus * wgpc));
         const uint64_t chunk = tiles_per_chunk * REC_TILE;

@@ -208,7 +208,7 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     // occupancy (182 VGPRs at t = 32, 2 waves/SIMD) below what the record
     // stream needs — measured per 1e8 records, fused vs two-pass: t = 12
     // 1.40 vs 1.68 ms, 16 1.89 vs 1.69, 24 1.95 vs 1.75, 32 2.06 vs 1.81.
-    static const int fused_env = [] { const char *e = getenv("QK_TUNE_PKT_FUSED"); return e ? atoi(e) : 1; }();
+    const int fused_env = ctx->knobs.pkt_fused;   // knob pkt_fused (measurements)
     if (fused_env && t >= 5 && t <= 12) {
         int frc = QK_OK;
         if (int e = ensure_scratch(ctx, (size_t)nchunks * 32 * sizeof(uint64_t), s)) return e;

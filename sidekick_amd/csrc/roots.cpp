@@ -1,0 +1,448 @@
+// roots.cpp — host root finding for the decode-missing root test.
+//
+// The reference decode (media_client.rs:304-313) evaluates the monic
+// polynomial P(z) = z^d + c_1 z^(d-1) + ... + c_d of diff.to_coeffs() at every
+// entry x of the sender's log and keeps the entries with P(x) == 0.  Over
+// GF(p), P(x) == 0  <=>  (x mod p) is one of P's roots in GF(p), so the same
+// hit list follows from the (at most d) roots of P and a set-membership scan
+// of the log (decode.hip k_root_scan_*): O(d^2 log p) host work once, then
+// O(1) per candidate instead of d Horner steps.  Bit-exact by construction:
+// the roots found here are exactly {r in GF(p) : P(r) == 0}.
+//
+// Root finding (p = p32 = 2^32 - 5 or p64 = 2^64 - 59):
+//   1. factors z^k of P give the root 0; divide them out (then P(0) != 0)
+//   2. g = gcd(P, z^(p-1) - 1): the product of (z - r) over P's distinct
+//      nonzero roots r in GF(p).  z^(p-1) is not formed directly:
+//      z^(2^w) mod P takes w squarings (w = 32 / 64), and 2^w = p + c
+//      (c = 5 / 59), so z^(2^w) - z^(c+1) = z^(c+1) (z^(p-1) - 1) and, z being
+//      prime to P, gcd(P, z^(2^w) - z^(c+1)) = g
+//   3. Cantor-Zassenhaus equal-degree splitting of g into linear factors:
+//      for a random a, gcd(g, (z + a)^((p-1)/2) - 1) holds the roots r with
+//      r + a a quadratic residue — about half of them; recurse on both parts;
+//      quadratics by the root formula.
+// In the decode case P is a product of linear factors (the missing ids), so
+// step 3 runs on P itself first (the fast path, no z^(2^w) exponentiation);
+// only a P that will not split that way (roots outside GF(p): a corrupt or
+// mismatched difference) takes steps 2-3.
+// Polynomial products accumulate folded 64x64 (u64 field: 128-bit) products
+// lazily and reduce each coefficient once; reduction by the monic modulus
+// runs top-down with the negated modulus coefficients, so a squaring mod a
+// degree-m polynomial is ~1.5 m^2 multiply-adds.
+#include "quack_hip.h"
+#include "field.h"
+
+#include <string.h>
+
+#include <immintrin.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+namespace {
+
+using namespace qk;
+
+#define QK_AVX512 __attribute__((target("avx512f,avx512vl,avx512dq")))
+
+static bool cpu_has_avx512() {
+    static const int ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
+                          __builtin_cpu_supports("avx512dq");
+    return ok;
+}
+
+// l + 5 h of each 64-bit lane (2^32 == 5): a product < 2^64 -> < 6 * 2^32
+QK_AVX512 static inline __m512i fold512(__m512i m) {
+    const __m512i h = _mm512_srli_epi64(m, 32);
+    return _mm512_add_epi64(_mm512_and_si512(m, _mm512_set1_epi64(0xFFFFFFFFll)),
+                            _mm512_add_epi64(h, _mm512_slli_epi64(h, 2)));
+}
+
+// GF(p32) squaring mod a monic f of degree m on AVX-512: the same lazy sums
+// as the scalar ModRing::sqr (folded products < 6 * 2^32, at most 2m per
+// coefficient), eight 32x32 products per vpmuludq.  a64 / nf64 hold a and
+// -f zero-extended to 64 bits and zero-padded to a multiple of 8 past m, so
+// the vector loops run over whole blocks (padding lanes add 0); acc has
+// 2m + 16 slots.
+QK_AVX512 static void sqr32_avx512(uint32_t *a, size_t m, const uint64_t *nf64, uint64_t *a64, uint64_t *acc) {
+    const size_t mb = (m + 7) & ~(size_t)7;
+    for (size_t i = 0; i < m; ++i) a64[i] = a[i];
+    for (size_t i = m; i < mb + 8; ++i) a64[i] = 0;
+    for (size_t i = 0; i < 2 * m + 16; ++i) acc[i] = 0;
+    for (size_t i = 0; i < m; ++i) {
+        const uint64_t ai = a[i];
+        if (!ai) continue;
+        const uint64_t sq = ai * ai;
+        acc[2 * i] += (sq >> 32) * C32 + (uint32_t)sq;
+        const uint64_t a2 = add32((uint32_t)ai, (uint32_t)ai);
+        const __m512i b = _mm512_set1_epi64((long long)a2);
+        for (size_t j = i + 1; j < m; j += 8) {
+            const __m512i x = _mm512_loadu_si512(a64 + j);
+            __m512i *dst = reinterpret_cast<__m512i *>(acc + i + j);
+            _mm512_storeu_si512(dst, _mm512_add_epi64(_mm512_loadu_si512(dst), fold512(_mm512_mul_epu32(b, x))));
+        }
+    }
+    for (size_t k = 2 * m - 1; k-- > m;) {
+        const uint32_t q = canon32(fold64_32(acc[k]));
+        if (!q) continue;
+        const __m512i b = _mm512_set1_epi64((long long)q);
+        uint64_t *base = acc + k - m;
+        for (size_t i = 0; i < m; i += 8) {
+            __m512i *dst = reinterpret_cast<__m512i *>(base + i);
+            const __m512i y = _mm512_loadu_si512(nf64 + i);
+            _mm512_storeu_si512(dst, _mm512_add_epi64(_mm512_loadu_si512(dst), fold512(_mm512_mul_epu32(b, y))));
+        }
+    }
+    for (size_t i = 0; i < m; ++i) a[i] = canon32(fold64_32(acc[i]));
+}
+
+// Field policies: canonical elements T, lazy accumulator A (sums of folded
+// products: < 2^35 (u32) / < 2^70 (u64) each, at most 2^11 of them).
+struct F32 {
+    using T = uint32_t;
+    using A = uint64_t;
+    static constexpr int W = 32;         // 2^W = p + C
+    static constexpr uint64_t C = C32;
+    static constexpr uint64_t HALF = (P32 - 1) / 2;
+    static T add(T a, T b) { return add32(a, b); }
+    static T sub(T a, T b) { return sub32(a, b); }
+    static T mul(T a, T b) { return mul32(a, b); }
+    static T neg(T a) { return neg32(a); }
+    static T inv(T a) { return inv32(a); }
+    static T canon_any(T a) { return canon32(a); }
+    static void mac(A &acc, T a, T b) {
+        const uint64_t p = (uint64_t)a * b;
+        acc += (p >> 32) * C32 + (uint32_t)p;   // < 6 * 2^32
+    }
+    static T red(A acc) { return canon32(fold64_32(acc)); }
+    // a square root of n, or false for a non-residue: p32 = 3 (mod 4), so
+    // n^((p+1)/4) squares to n whenever n is a residue
+    static bool sqrt(T n, T &r) {
+        r = pow32(n, (uint64_t)(P32 + 1) / 4);
+        return mul32(r, r) == n;
+    }
+};
+
+struct F64 {
+    using T = uint64_t;
+    using A = unsigned __int128;
+    static constexpr int W = 64;
+    static constexpr uint64_t C = C64;
+    static constexpr uint64_t HALF = (P64 - 1) / 2;
+    static T add(T a, T b) { return add64(a, b); }
+    static T sub(T a, T b) { return sub64(a, b); }
+    static T mul(T a, T b) { return mul64(a, b); }
+    static T neg(T a) { return neg64(a); }
+    static T inv(T a) { return inv64(a); }
+    static T canon_any(T a) { return canon64(a); }
+    static void mac(A &acc, T a, T b) {
+        const unsigned __int128 p = (unsigned __int128)a * b;
+        acc += (unsigned __int128)(uint64_t)(p >> 64) * C64 + (uint64_t)p;   // < 60 * 2^64
+    }
+    static T red(A acc) {
+        // acc < 2^81: acc = H 2^64 + L == 59 H + L  (< 2^64 + 2^23), twice
+        unsigned __int128 t = (unsigned __int128)(uint64_t)(acc >> 64) * C64 + (uint64_t)acc;
+        unsigned __int128 u = (unsigned __int128)(uint64_t)(t >> 64) * C64 + (uint64_t)t;
+        return canon64((uint64_t)u + C64 * (uint64_t)(u >> 64));
+    }
+    // Tonelli-Shanks: p64 - 1 = 4 Q (Q odd); z = 2 is a non-residue mod p64
+    // (p64 = 3 mod 8), so c = 2^Q has order 4
+    static bool sqrt(T n, T &r) {
+        if (n == 0) {
+            r = 0;
+            return true;
+        }
+        constexpr uint64_t Q = (P64 - 1) / 4;
+        if (pow64(n, (P64 - 1) / 2) != 1) return false;
+        T c = pow64(2, Q), t = pow64(n, Q);
+        r = pow64(n, (Q + 1) / 2);
+        int M = 2;
+        while (t != 1) {
+            int i = 1;
+            for (T t2 = mul64(t, t); t2 != 1; t2 = mul64(t2, t2)) ++i;
+            T b = c;
+            for (int j = 0; j < M - i - 1; ++j) b = mul64(b, b);
+            M = i;
+            c = mul64(b, b);
+            t = mul64(t, c);
+            r = mul64(r, b);
+        }
+        return true;
+    }
+};
+
+// Polynomials: coefficient vectors low degree first, canonical, no trailing
+// zeros (the zero polynomial is empty).
+template <class F> using Poly = std::vector<typename F::T>;
+
+template <class F> void trim(Poly<F> &a) {
+    while (!a.empty() && a.back() == 0) a.pop_back();
+}
+
+// a * inv(lead) (monic); a nonzero
+template <class F> void make_monic(Poly<F> &a) {
+    const typename F::T li = F::inv(a.back());
+    for (auto &v : a) v = F::mul(v, li);
+}
+
+// a mod b (b monic, deg b >= 1), in place
+template <class F> void rem_monic(Poly<F> &a, const Poly<F> &b) {
+    const size_t m = b.size() - 1;
+    for (size_t k = a.size(); k-- > m;) {
+        const typename F::T q = a[k];
+        if (q)
+            for (size_t i = 0; i < m; ++i) a[k - m + i] = F::sub(a[k - m + i], F::mul(q, b[i]));
+        a[k] = 0;
+    }
+    trim<F>(a);
+}
+
+// a / b (b monic), exact division assumed
+template <class F> Poly<F> div_monic(Poly<F> a, const Poly<F> &b) {
+    const size_t m = b.size() - 1;
+    if (a.size() <= m) return {};
+    Poly<F> q(a.size() - m);
+    for (size_t k = a.size(); k-- > m;) {
+        const typename F::T c = a[k];
+        q[k - m] = c;
+        if (c)
+            for (size_t i = 0; i < m; ++i) a[k - m + i] = F::sub(a[k - m + i], F::mul(c, b[i]));
+    }
+    return q;
+}
+
+// a <- a mod b up to a nonzero scalar, fraction-free: each step cancels a's
+// leading term as lead(b) a - lead(a) z^s b (no inversion; a field inverse
+// costs ~60 multiplications, more than the extra row of products here)
+template <class F> void rem_ff(Poly<F> &a, const Poly<F> &b) {
+    const size_t m = b.size() - 1;
+    const typename F::T lb = b.back();
+    while (a.size() > m) {
+        const typename F::T la = a.back();
+        const size_t s = a.size() - 1 - m;
+        for (size_t i = 0; i < s; ++i) a[i] = F::mul(a[i], lb);
+        for (size_t i = 0; i < m; ++i) a[s + i] = F::sub(F::mul(a[s + i], lb), F::mul(la, b[i]));
+        a.pop_back();
+        trim<F>(a);
+    }
+}
+
+// monic gcd(a, b)
+template <class F> Poly<F> gcd(Poly<F> a, Poly<F> b) {
+    trim<F>(a);
+    trim<F>(b);
+    while (!b.empty()) {
+        rem_ff<F>(a, b);
+        std::swap(a, b);
+    }
+    if (!a.empty()) make_monic<F>(a);
+    return a;
+}
+
+// Arithmetic modulo a fixed monic f of degree m >= 1: residues are vectors of
+// exactly m coefficients.
+template <class F> struct ModRing {
+    using T = typename F::T;
+    using A = typename F::A;
+    size_t m;
+    std::vector<T> nf;       // -f_i, i < m
+    std::vector<A> acc;      // 2m - 1 lazy accumulators
+    // the AVX-512 form (u32 field, m >= 8): -f and a widened and padded
+    bool vec = false;
+    std::vector<uint64_t> nf64, a64, acc64;
+
+    explicit ModRing(const Poly<F> &f) : m(f.size() - 1), nf(m), acc(2 * m) {
+        for (size_t i = 0; i < m; ++i) nf[i] = F::neg(f[i]);
+        if constexpr (F::W == 32) {
+            vec = m >= 8 && cpu_has_avx512();
+            if (vec) {
+                const size_t mb = (m + 7) & ~(size_t)7;
+                nf64.assign(mb + 8, 0);
+                for (size_t i = 0; i < m; ++i) nf64[i] = nf[i];
+                a64.assign(mb + 8, 0);
+                acc64.assign(2 * m + 16, 0);
+            }
+        }
+    }
+    // acc[0 .. 2m-1) (degree <= 2m-2) -> r (m coefficients): top-down, each
+    // top coefficient q adds q * (-f_i) below it
+    void reduce_acc(std::vector<T> &r) {
+        for (size_t k = 2 * m - 1; k-- > m;) {
+            const T q = F::red(acc[k]);
+            if (q)
+                for (size_t i = 0; i < m; ++i) F::mac(acc[k - m + i], q, nf[i]);
+        }
+        for (size_t i = 0; i < m; ++i) r[i] = F::red(acc[i]);
+    }
+    void sqr(std::vector<T> &a) {
+        if constexpr (F::W == 32) {
+            if (vec) {
+                sqr32_avx512(a.data(), m, nf64.data(), a64.data(), acc64.data());
+                return;
+            }
+        }
+        std::fill(acc.begin(), acc.end(), A(0));
+        for (size_t i = 0; i < m; ++i) {
+            const T ai = a[i];
+            if (!ai) continue;
+            F::mac(acc[2 * i], ai, ai);
+            const T a2 = F::add(ai, ai);
+            for (size_t j = i + 1; j < m; ++j) F::mac(acc[i + j], a2, a[j]);
+        }
+        reduce_acc(a);
+    }
+    // a <- a * (z + c)
+    void mul_lin(std::vector<T> &a, T c) {
+        const T top = a[m - 1];                       // coefficient of z^m after the shift
+        for (size_t i = m; i-- > 0;) {
+            const T lower = i ? a[i - 1] : 0;
+            a[i] = F::add(lower, F::mul(c, a[i]));
+        }
+        if (top)
+            for (size_t i = 0; i < m; ++i) a[i] = F::add(a[i], F::mul(top, nf[i]));
+    }
+    // (z + c)^e mod f
+    std::vector<T> pow_lin(T c, uint64_t e) {
+        std::vector<T> r(m, 0);
+        r[0] = 1;
+        bool started = false;
+        for (int b = 63; b >= 0; --b) {
+            if (started) sqr(r);
+            if ((e >> b) & 1) {
+                mul_lin(r, c);
+                started = true;
+            }
+        }
+        return r;
+    }
+};
+
+template <class F> Poly<F> to_poly(std::vector<typename F::T> r) {
+    Poly<F> p(std::move(r));
+    trim<F>(p);
+    return p;
+}
+
+// Split g into linear factors, appending their roots.  exact: g is monic,
+// squarefree, and all its roots lie in GF(p)*: always succeeds.  !exact
+// (the fast path, any monic g with g(0) != 0): every leaf that is reached is a
+// genuine linear factor of g (split products are exact divisions), so the
+// roots appended are roots of g and, when it returns true, all of them; it
+// returns false when a factor will not split into linear ones (an
+// irreducible factor of degree >= 2, i.e. roots outside GF(p)), after a
+// quadratic with a non-residue discriminant or 24 failed attempts on one
+// factor (for a product of >= 3 linear factors a random attempt fails with
+// probability <= 1/4).
+template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out, bool exact) {
+    using T = typename F::T;
+    const T inv2 = F::inv(2);
+    std::vector<Poly<F>> todo{g0};
+    uint64_t s = 0x243F6A8885A308D3ull;   // fixed seed: a deterministic sequence of a's
+    while (!todo.empty()) {
+        Poly<F> g = std::move(todo.back());
+        todo.pop_back();
+        const size_t k = g.size() - 1;
+        if (k == 0) continue;
+        if (k == 1) {
+            out.push_back(F::neg(g[0]));
+            continue;
+        }
+        if (k == 2) {   // z^2 + b z + c: (-b +- sqrt(b^2 - 4c)) / 2
+            const T b = g[1], c = g[0];
+            const T disc = F::sub(F::mul(b, b), F::mul(4, c));
+            T sq;
+            if (!F::sqrt(disc, sq)) {
+                if (!exact) return false;
+                continue;   // (cannot happen for an exact-mode factor)
+            }
+            const T nb = F::neg(b);
+            out.push_back(F::mul(F::add(nb, sq), inv2));
+            out.push_back(F::mul(F::sub(nb, sq), inv2));
+            continue;
+        }
+        ModRing<F> R(g);
+        for (int fails = 0;; ++fails) {
+            if (!exact && fails >= 24) return false;
+            s += GAMMA;
+            const T a = F::canon_any((T)splitmix_mix(s));
+            std::vector<T> w = R.pow_lin(a, F::HALF);
+            w[0] = F::sub(w[0], 1);
+            Poly<F> h = gcd<F>(g, to_poly<F>(std::move(w)));
+            const size_t dh = h.empty() ? 0 : h.size() - 1;
+            if (dh == 0 || dh == k) continue;
+            todo.push_back(div_monic<F>(g, h));
+            todo.push_back(std::move(h));
+            break;
+        }
+    }
+    return true;
+}
+
+// the distinct roots of z^d + c_1 z^(d-1) + ... + c_d in GF(p), ascending
+template <class F> std::vector<typename F::T> roots(const typename F::T *c, uint32_t d) {
+    using T = typename F::T;
+    std::vector<T> out;
+    if (d == 0) return out;
+    Poly<F> f(d + 1);
+    f[d] = 1;
+    for (uint32_t i = 1; i <= d; ++i) f[d - i] = F::canon_any(c[i - 1]);
+    // 1. the root 0
+    size_t z = 0;
+    while (z < f.size() && f[z] == 0) ++z;
+    if (z) {
+        out.push_back(0);
+        f.erase(f.begin(), f.begin() + z);
+    }
+    if (f.size() > 1) {
+        // fast path: the decode case (f a product of linear factors, the
+        // missing ids) splits without step 2
+        std::vector<T> r;
+        if (!split<F>(f, r, false)) {
+            // 2. g = gcd(f, z^(2^W) - z^(C+1)), then 3. split it
+            r.clear();
+            ModRing<F> R(f);
+            std::vector<T> h(R.m, 0);
+            if (R.m == 1) h[0] = F::neg(f[0]);          // z mod (z + f0)
+            else h[1] = 1;
+            for (int i = 0; i < F::W; ++i) R.sqr(h);    // z^(2^W)
+            const std::vector<T> zc = R.pow_lin(0, F::C + 1);   // z^(C+1)
+            for (size_t i = 0; i < R.m; ++i) h[i] = F::sub(h[i], zc[i]);
+            Poly<F> g = gcd<F>(f, to_poly<F>(std::move(h)));
+            if (g.size() > 1) split<F>(g, r, true);
+        }
+        out.insert(out.end(), r.begin(), r.end());
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
+template <class F>
+int roots_abi(const typename F::T *coeffs, uint32_t d, typename F::T *out, uint32_t cap, uint32_t *k) {
+    if (!k || (d && !coeffs)) return QK_E_INVAL;
+    *k = 0;
+    std::vector<typename F::T> r;
+    try {
+        r = roots<F>(coeffs, d);
+    } catch (const std::bad_alloc &) {
+        return QK_E_NOMEM;
+    }
+    *k = (uint32_t)r.size();
+    if (r.size() > cap || (!r.empty() && !out)) return QK_E_CAPACITY;
+    std::copy(r.begin(), r.end(), out);
+    return QK_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int qk_u32_roots(const uint32_t *coeffs, uint32_t d, uint32_t *roots, uint32_t cap, uint32_t *k) {
+    return roots_abi<F32>(coeffs, d, roots, cap, k);
+}
+
+int qk_u64_roots(const uint64_t *coeffs, uint32_t d, uint64_t *roots, uint32_t cap, uint32_t *k) {
+    return roots_abi<F64>(coeffs, d, roots, cap, k);
+}
+
+} // extern "C"

@@ -73,6 +73,10 @@ class Context:
     def set_grid(self, blocks: int):
         check(lib().qk_ctx_set_grid(self.handle, int(blocks)))
 
+    def set_knob(self, name: str, value: int):
+        """A measurement knob of this context (qk_ctx_set_knob)."""
+        check(lib().qk_ctx_set_knob(self.handle, name.encode(), int(value)), f"set_knob({name}={value})")
+
     def trim(self):
         """Free grown-out scratch buffers (synchronises the device)."""
         check(lib().qk_ctx_trim(self.handle), "trim")
@@ -150,6 +154,19 @@ arithmetic = _Arithmetic()
 # --------------------------------------------------------------------------
 # Array plumbing (torch device tensors, numpy host arrays)
 # --------------------------------------------------------------------------
+def roots(coeffs, bits: int = 32) -> list:
+    """The distinct roots in GF(p), ascending, of z^d + c_1 z^(d-1) + ... + c_d
+    (qk_u32_roots / qk_u64_roots, roots.cpp): a log entry is a root-test hit
+    exactly when it is congruent to one of them."""
+    d = len(coeffs)
+    T = C.c_uint32 if bits == 32 else C.c_uint64
+    c = (T * max(d, 1))(*[int(v) for v in coeffs])
+    out = (T * max(d, 1))()
+    k = C.c_uint32()
+    check(getattr(lib(), f"qk_u{bits}_roots")(c, d, out, d, C.byref(k)), "roots")
+    return [int(v) for v in out[:k.value]]
+
+
 def _device_array(a, bits: int):
     """(ptr, n, device_index, stream_ptr) of a contiguous CUDA tensor, or None."""
     try:

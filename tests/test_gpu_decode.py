@@ -24,6 +24,73 @@ def QT(bits):
     return sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
 
 
+@pytest.fixture(autouse=True, params=["horner", "scan"])
+def root_test_mode(request):
+    """Every test of this module runs twice: the root test by Horner per
+    candidate (k_root_test_*) and by host root finding + the root-set scan
+    (roots.cpp, k_root_scan; forced for 2 <= d <= 256): the same hit lists."""
+    ctx = sk.get_context(0)
+    ctx.set_knob("root_test", 1 if request.param == "horner" else 2)
+    yield request.param
+    ctx.set_knob("root_test", 0)
+
+
+def _poly_mul(a, b, p):
+    A, B = [1] + list(a), [1] + list(b)
+    out = [0] * (len(A) + len(B) - 1)
+    for i, x in enumerate(A):
+        for j, y in enumerate(B):
+            out[i + j] = (out[i + j] + x * y) % p
+    return out[1:]
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+def test_root_test_non_splitting_polynomials(bits):
+    """Coefficient vectors that are not a product of linear factors over
+    GF(p): planted log roots times irreducible quadratics, and random
+    vectors.  Hits = the oracle's evaluation, whichever path runs."""
+    p = qo.MOD[bits]
+    rng = np.random.default_rng(bits)
+    n = 40_003
+    log = coracle.splitmix_u32(77, n) if bits == 32 else coracle.splitmix_u64(77, n)
+    for trial in range(4):
+        planted = [int(log[i]) for i in rng.choice(n, size=3 + trial, replace=False)]
+        q = QT(bits)(len(planted))
+        for x in planted:
+            q.insert(x)
+        c = list(q.to_coeffs())
+        for _ in range(1 + trial % 2):
+            while True:
+                nr = int(rng.integers(2, min(p, 1 << 62)))
+                if pow(nr, (p - 1) // 2, p) == p - 1:
+                    break
+            s0 = int(rng.integers(0, min(p, 1 << 62)))
+            c = _poly_mul(c, [(-2 * s0) % p, (s0 * s0 - nr) % p], p)
+        want = qo.root_test_indices(c, log.tolist(), p)
+        got = QT(bits)(1).root_test(c, dev(log, bits))
+        assert got == want and len(got) >= len(planted)
+    for d in (5, 12, 31):
+        c = [int(v) for v in rng.integers(0, min(p, 1 << 62), size=d)]
+        assert QT(bits)(1).root_test(c, dev(log, bits)) == qo.root_test_indices(c, log.tolist(), p)
+
+
+def test_root_test_u32_aliases_and_zero():
+    """Roots 0 and 1: log entries 0, p, 1, p + 1 all hit (x mod p); 2^32 - 1
+    (= 4 mod p) does not unless 4 is a root."""
+    p = qo.MOD[32]
+    log = coracle.splitmix_u32(5, 10_007)
+    specials = [0, p, 1, p + 1, 2**32 - 1, 4, p - 1]
+    pos = [10, 999, 1000, 4097, 5000, 7001, 10_006]
+    log[pos] = specials
+    q = sk.PowerSumQuackU32(3)
+    for x in (0, 1, p - 1):
+        q.insert(x)
+    c = q.to_coeffs()
+    got = q.root_test(c, dev(log))
+    assert got == qo.root_test_indices(c, log.tolist(), p)
+    assert {10, 999, 1000, 4097, 10_006} <= set(got) and 5000 not in got
+
+
 def test_golden_decodes(golden):
     for g in golden["decodes"]:
         bits, n, t = g["bits"], g["n"], g["t"]

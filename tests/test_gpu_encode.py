@@ -100,8 +100,8 @@ def test_u32_multipass_edges(golden, t):
     """Thresholds above 80 run as baby-step/giant-step passes (80 powers, then
     offset passes of <= 48 with giants from x^base): ids at the field edges,
     the lazy-fold wrap ids of the shared baby chain, misaligned starts, and
-    equality with the power chain (QK_TUNE_U32_PASSES=0 is a process-wide
-    switch, so the chain side is the oracle here)."""
+    equality with the power chain (the oracle here; knob u32_passes = 0
+    selects the chain on the device)."""
     P32 = 4294967291
     ids = coracle.splitmix_u32(0x77 + t, 30_011)
     edge = np.array([0, 1, P32 - 1, P32, P32 + 1, 2**32 - 1, 2**31], dtype=np.uint32)

@@ -88,33 +88,55 @@ def run_decode(args, ctx, bits=32):
     keep[torch.from_numpy(drops).to(DEV)] = False
     kept = log[keep].contiguous()
     torch.cuda.synchronize()
-    # the timed decode step: encode both sides, subtract, to_coeffs, root test
-    reps = []
-    for r in range(args.steps + 1):
+    # host root finding alone (the root-set scan's host step, roots.cpp)
+    sent, recv = cls(t), cls(t)
+    sent.insert_batch(log)
+    recv.insert_batch(kept)
+    diff = sent.clone()
+    diff.sub_assign(recv)
+    c = diff.to_coeffs()
+    rt = []
+    for _ in range(max(5, args.steps)):
         t0 = time.perf_counter()
-        sent, recv = cls(t), cls(t)
-        sent.insert_batch(log)
-        recv.insert_batch(kept)
-        diff = sent.clone()
-        diff.sub_assign(recv)
-        t1 = time.perf_counter()
-        c = diff.to_coeffs()
-        t2 = time.perf_counter()
-        ctx.set_profiling(True)
-        hits = diff.root_test(c, log)
-        ctx.set_profiling(False)
-        t3 = time.perf_counter()
-        ms, k = ctx.kernel_stats()
-        if r:
-            reps.append((t1 - t0, t2 - t1, t3 - t2, ms / 1e3))
-    a = np.median(np.array(reps), axis=0)
-    ok = set(drops.tolist()) <= set(hits)
-    b = bits // 8
-    emit({"config": f"decode-missing u{bits} n=1e8 d=32" + (" (configs[4])" if bits == 32 else ""), "n": n,
-          "hits": len(hits), "drops_recovered": ok,
-          "encode_both_s": a[0], "to_coeffs_s": a[1], "root_test_wall_s": a[2], "root_test_kernel_s": a[3],
-          "root_test_candidates_per_s": n / a[3], "root_test_GBps": b * n / a[3] / 1e9,
-          "frac_hbm_8TBs": b * n / a[3] / 8e12, "total_s": a[0] + a[1] + a[2]})
+        r = sk.roots(c, bits)
+        rt.append(time.perf_counter() - t0)
+    emit({"config": f"host root finding u{bits} d={len(c)} (roots.cpp)", "roots": len(r),
+          "median_s": float(np.median(rt)), "min_s": min(rt)})
+    # the timed decode step: encode both sides, subtract, to_coeffs, root test
+    # (mode 1: Horner per candidate; 2: host roots + root-set scan; 0: automatic)
+    results = {}
+    for mode in args.rt_modes:
+        ctx.set_knob("root_test", mode)
+        reps = []
+        for r in range(args.steps + 1):
+            t0 = time.perf_counter()
+            sent, recv = cls(t), cls(t)
+            sent.insert_batch(log)
+            recv.insert_batch(kept)
+            diff = sent.clone()
+            diff.sub_assign(recv)
+            t1 = time.perf_counter()
+            c = diff.to_coeffs()
+            t2 = time.perf_counter()
+            ctx.set_profiling(True)
+            hits = diff.root_test(c, log)
+            ctx.set_profiling(False)
+            t3 = time.perf_counter()
+            ms, k = ctx.kernel_stats()
+            if r:
+                reps.append((t1 - t0, t2 - t1, t3 - t2, ms / 1e3))
+        ctx.set_knob("root_test", 0)
+        results[mode] = hits
+        a = np.median(np.array(reps), axis=0)
+        ok = set(drops.tolist()) <= set(hits)
+        b = bits // 8
+        name = {0: "auto", 1: "horner", 2: "root-set scan"}[mode]
+        emit({"config": f"decode-missing u{bits} n=1e8 d=32" + (" (configs[4])" if bits == 32 else "")
+                        + f", root test: {name}", "n": n,
+              "hits": len(hits), "drops_recovered": ok, "same_hits_as_first_mode": hits == results[args.rt_modes[0]],
+              "encode_both_s": a[0], "to_coeffs_s": a[1], "root_test_wall_s": a[2], "root_test_kernel_s": a[3],
+              "root_test_candidates_per_s": n / a[3], "root_test_GBps": b * n / a[3] / 1e9,
+              "frac_hbm_8TBs": b * n / a[3] / 8e12, "total_s": a[0] + a[1] + a[2]})
     if args.cpu:
         from oracle import coracle
         m = int(args.cpu_sample_dec)
@@ -306,7 +328,7 @@ def run_sweep64(args, ctx):
     n = int(args.nsweep)
     ids = torch.empty(n, dtype=torch.int64, device=DEV)
     fill_splitmix(ctx, ids, 0x5EED0003, bits=64)
-    path = "chain" if os.environ.get("QK_TUNE_BSGS64_OFF") == "1" else "default"
+    path = "chain" if "bsgs64_off=1" in args.knob else "default"
     for t in (8, 9, 16, 17, 24, 32, 40, 48, 56, 64, 72, 80, 81, 128, 160, 256, 512, 1024):
         wall, kern = time_encode(ctx, ids, t, 64, max(3, args.steps // 2))
         emit({"config": f"encode u64 t={t} ({path})", "n": n, "ids_per_s": n / kern,
@@ -326,8 +348,14 @@ def main():
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--cpu-sample64", type=float, default=5e6)
     ap.add_argument("--cpu-sample-dec", type=float, default=2e7)
+    ap.add_argument("--rt-modes", default="1,2", help="decode: root-test modes to time (0 auto, 1 Horner, 2 scan)")
+    ap.add_argument("--knob", action="append", default=[], help="NAME=VALUE measurement knob (qk_ctx_set_knob)")
     args = ap.parse_args()
+    args.rt_modes = [int(x) for x in args.rt_modes.split(",")]
     ctx = sk.get_context(0)
+    for kv in args.knob:
+        k, v = kv.split("=")
+        ctx.set_knob(k, int(v))
     for w in args.what:
         {"u64": run_u64, "decode": run_decode, "decode64": run_decode64, "host": run_host, "sweep": run_sweep, "sweep64": run_sweep64,
          "packets": run_packets, "flows": run_flows, "micro": run_micro}[w](args, ctx)

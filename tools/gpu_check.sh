@@ -29,13 +29,13 @@ for s in $STEPS; do
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
     sgsweep)
       for g in ${SG_LIST:-0 2 4 6 8}; do
-        QK_TUNE_BSGS_SG=$g step sg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 || exit 3
+        step sg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
       done ;;
     configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
     pktab)  # packet batch: fused extract+encode vs the two-pass path
       step pkt_fused 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 || exit 3
-      QK_TUNE_PKT_FUSED=0 step pkt_twopass 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 || exit 3 ;;
-    configs20) QK_TUNE_U64_KMAX=20 step configs20 900 python3 -u tools/bench_configs.py u64 || exit 3 ;;
+      step pkt_twopass 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 --knob pkt_fused=0 || exit 3 ;;
+    configs20) step configs20 900 python3 -u tools/bench_configs.py u64 --knob u64_kmax=20 || exit 3 ;;
     prof)
       export TMPDIR=/tmp
       step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 1 --cpu-sample 0 || exit 3 ;;
@@ -53,8 +53,8 @@ for s in $STEPS; do
     pmcab)  # SQ stall/issue counters for two BSGS variants (A/B), two counter passes each
       export TMPDIR=/tmp
       for g in ${SG_AB:-0 8}; do
-        QK_TUNE_BSGS_SG=$g step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
-        QK_TUNE_BSGS_SG=$g step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 || exit 3
+        step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
+        step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
       done ;;
     profcfg)  # kernel stats for the secondary configs' kernels (u64 encode, u32/u64 root test)
       export TMPDIR=/tmp
@@ -68,11 +68,11 @@ for s in $STEPS; do
     flowsbench) step flowsbench 600 python3 -u tools/bench_configs.py flows --steps 6 || exit 3 ;;
     flowswg)
       for w in ${WG_LIST:-4 6 8}; do
-        QK_TUNE_FLOW_WGPC=$w step flowswg$w 300 python3 -u tools/bench_configs.py flows --steps 6 || exit 3
+        step flowswg$w 300 python3 -u tools/bench_configs.py flows --steps 6 --knob flow_wgpc=$w || exit 3
       done ;;
     dec64)  # u64 root test: BSGS (default) vs Horner
       step dec64_bsgs 300 python3 -u tools/bench_configs.py decode64 --steps 10 --cpu || exit 3
-      QK_TUNE_RT64_HORNER=1 step dec64_horner 300 python3 -u tools/bench_configs.py decode64 --steps 10 || exit 3 ;;
+      step dec64_horner 300 python3 -u tools/bench_configs.py decode64 --steps 10 --knob rt64_horner=1 || exit 3 ;;
     fig2)  # the reference's figure-2 command lines against the drop-in programs (host and --gpu)
       step fig2_host 600 python3 -u tools/run_fig2.py "$OUT/fig2_host" --trials 100 || exit 3
       step fig2_gpu 600 python3 -u tools/run_fig2.py "$OUT/fig2_gpu" --trials 20 --gpu || exit 3 ;;
@@ -80,7 +80,7 @@ for s in $STEPS; do
       NCCL_DEBUG=WARN step dist2rccl 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29544 bench.py --gpus 2 --steps 3 --warmup 1 --ids-per-gpu 1e8 --cpu-sample 0 || exit 3 ;;
     passes)  # u32 t > 80: BSGS passes (default) vs the power chain
       step sweep_passes 300 python3 -u tools/bench_configs.py sweep --steps 6 || exit 3
-      QK_TUNE_U32_PASSES=0 step sweep_chain 300 python3 -u tools/bench_configs.py sweep --steps 6 || exit 3 ;;
+      step sweep_chain 300 python3 -u tools/bench_configs.py sweep --steps 6 --knob u32_passes=0 || exit 3 ;;
     pmc)
       export TMPDIR=/tmp
       step pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;

@@ -1,3 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-for L in 4 2 8; do QK_TUNE_FLOW_LOAD=$L timeout -k 10 300 python -u tools/bench_configs.py flows --steps 6 > gpurun_out/flows_load$L.log 2>&1 || exit 1; done
+for L in 4 2 8; do timeout -k 10 300 python -u tools/bench_configs.py flows --steps 6 --knob flow_load=$L > gpurun_out/flows_load$L.log 2>&1 || exit 1; done
