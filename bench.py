@@ -90,6 +90,79 @@ def valu_roofline(bits: int, t: int, n: int, kern_avg_ms: float):
     }
 
 
+# The published crate at the metric's threshold: benchmark_construct on one
+# core of a Xeon E5 (rdtsc ~2.256 GHz), t = 32 interpolated between the t = 30
+# and t = 40 rows (zip:nsdi24/quack/threshold_vs_encode_time/32.txt:9,12;
+# BASELINE.md).
+PUBLISHED_NS_PER_ID = {(32, 32): 125.8, (32, 16): 58.6, (64, 80): 461.0}
+
+
+def host_cpu():
+    """(model name, current MHz of cpu0, logical CPUs) of this host."""
+    model, mhz = "unknown", None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name") and model == "unknown":
+                    model = line.split(":", 1)[1].strip()
+                elif line.startswith("cpu MHz") and mhz is None:
+                    mhz = float(line.split(":", 1)[1])
+    except OSError:
+        pass
+    return model, mhz, os.cpu_count() or 1
+
+
+def cpu_baselines(args, bits, t, start, cnt, ids):
+    """The oracle's scalar restatement of the reference insert loop, timed on
+    this host over a bounded prefix of the same stream, with the ids
+    pre-generated (the crate's benchmark_construct times inserts of
+    pre-generated ids): one core, then every core of this process's share."""
+    import numpy as np
+    import sidekick_amd as sk
+    from oracle import coracle
+    m = int(min(args.cpu_sample, cnt))
+    host_ids = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(args.seed, m, start)
+    tc = time.perf_counter()
+    cpu_S = (coracle.encode_u32 if bits == 32 else coracle.encode_u64)(host_ids, t)
+    cpu_s = time.perf_counter() - tc
+    q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
+    q.insert_batch(ids[:m])                    # GPU on the same prefix: bit-exact parity check
+    parity = q.power_sums() == cpu_S
+    if not parity:
+        log("PARITY FAILURE: GPU power sums differ from the CPU oracle on the sample prefix")
+    model, mhz, ncpu = host_cpu()
+    pub = PUBLISHED_NS_PER_ID.get((bits, t))
+    host = f"host {model}, {ncpu} logical CPUs" + (f", cpu0 at {mhz:.0f} MHz" if mhz else "")
+    one = {
+        "value": m / cpu_s, "unit": "identifiers/s", "cores": 1, "kind": "port",
+        "ns_per_id": cpu_s / m * 1e9,
+        "sample": f"first {m} ids of the same stream (seed {hex(args.seed)}), pre-generated, inserted by the "
+                  f"scalar C restatement of the reference insert loop (oracle/quack_oracle.c qo_encode_u{bits}), "
+                  f"1 core, {cpu_s:.1f} s = {cpu_s / m * 1e9:.1f} ns/id; {host}"
+                  + (f"; the published crate: {pub} ns/id at u{bits} t={t} on one Xeon E5 core at ~2.26 GHz "
+                     f"(BASELINE.md)" if pub else ""),
+        "published_crate_ns_per_id": pub,
+        "parity_with_gpu": parity,
+    }
+    thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or ncpu
+    thr = max(1, min(thr, 64))
+    mm = int(min(m * thr // 3, cnt))           # ~1/3 of the 1-core sample per thread
+    host_mm = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(args.seed, mm, start)
+    tc = time.perf_counter()
+    mt_S = coracle.encode_mt(host_mm, t, thr)
+    mt_s = time.perf_counter() - tc
+    del host_mm
+    q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
+    q.insert_batch(ids[:mm])
+    allc = {
+        "value": mm / mt_s, "unit": "identifiers/s", "cores": thr, "kind": "port",
+        "sample": f"first {mm} ids of the same stream, pre-generated, {thr} threads x {mm // thr} ids, one partial "
+                  f"sketch per thread merged (oracle/quack_oracle.c qo_encode_mt), {mt_s:.1f} s; {host}",
+        "parity_with_gpu": q.power_sums() == mt_S,
+    }
+    return one, allc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -267,42 +340,7 @@ def main():
     }
 
     if world == 1 and args.cpu_sample > 0:
-        from oracle import coracle
-        m = int(min(args.cpu_sample, cnt))
-        tc = time.perf_counter()
-        if bits == 32:
-            cpu_S = coracle.encode_u32_seed(args.seed, m, t, start=start)
-        else:
-            cpu_S = coracle.encode_u64_seed(args.seed, m, t, start=start)
-        cpu_s = time.perf_counter() - tc
-        # GPU on the same prefix: bit-exact parity check
-        q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
-        q.insert_batch(ids[:m])
-        parity = q.power_sums() == cpu_S
-        out["cpu_baseline"] = {
-            "value": m / cpu_s, "unit": "identifiers/s", "cores": 1, "kind": "port",
-            "sample": f"first {m} ids of the same stream (seed {hex(args.seed)}), scalar C restatement of the "
-                      f"reference insert loop (oracle/quack_oracle.c), 1 host core, {cpu_s:.1f} s",
-            "parity_with_gpu": parity,
-        }
-        if not parity:
-            log("PARITY FAILURE: GPU power sums differ from the CPU oracle on the sample prefix")
-        # all host cores of this process's share: the same loop,
-        # one partial per thread, merged; the same per-thread sample size
-        thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        thr = max(1, min(thr, 64))
-        mm = int(min(m * thr // 3, cnt))  # ~1/3 of the 1-core sample per thread
-        tc = time.perf_counter()
-        mt_S = coracle.encode_seed_mt(bits, args.seed, mm, t, thr, start=start)
-        mt_s = time.perf_counter() - tc
-        q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
-        q.insert_batch(ids[:mm])
-        out["cpu_baseline_all_cores"] = {
-            "value": mm / mt_s, "unit": "identifiers/s", "cores": thr, "kind": "port",
-            "sample": f"first {mm} ids of the same stream, {thr} threads x {mm // thr} ids, one partial sketch "
-                      f"per thread merged (oracle/quack_oracle.c qo_encode_seed_mt), {mt_s:.1f} s",
-            "parity_with_gpu": q.power_sums() == mt_S,
-        }
+        out["cpu_baseline"], out["cpu_baseline_all_cores"] = cpu_baselines(args, bits, t, start, cnt, ids)
     print(json.dumps(out), flush=True)
     if comm is not None and world == 1:
         comm.close()

@@ -38,6 +38,7 @@ def lib():
             "qo_encode_u64_seed": (None, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
             "qo_encode_seed_mt": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
                                             C.c_void_p]),
+            "qo_encode_mt": (C.c_int, [C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]),
             "qo_to_coeffs_u32": (None, [u32p, C.c_uint32, u32p]),
             "qo_to_coeffs_u64": (None, [u64p, C.c_uint32, u64p]),
             "qo_eval_u32": (C.c_uint32, [u32p, C.c_uint32, C.c_uint32]),
@@ -91,6 +92,18 @@ def encode_seed_mt(bits, seed, n, t, threads, start=0):
     rc = lib().qo_encode_seed_mt(bits, seed, start, n, t, threads, S.ctypes.data)
     if rc:
         raise RuntimeError(f"qo_encode_seed_mt rc={rc}")
+    return [int(v) for v in S]
+
+
+def encode_mt(ids, t, threads):
+    """All-cores restatement over a pre-generated id array (one partial per
+    thread over a contiguous slice, merged)."""
+    bits = 32 if ids.dtype == np.uint32 else 64
+    ids = np.ascontiguousarray(ids)
+    S = np.zeros(t, dtype=np.uint32 if bits == 32 else np.uint64)
+    rc = lib().qo_encode_mt(bits, ids.ctypes.data, len(ids), t, threads, S.ctypes.data)
+    if rc:
+        raise RuntimeError(f"qo_encode_mt rc={rc}")
     return [int(v) for v in S]
 
 

@@ -174,18 +174,24 @@ typedef struct {
     uint64_t seed, start, n;
     uint32_t t, bits;
     void *S;
+    const void *ids;   /* pre-generated ids (slice [start, start + n)), or NULL: splitmix inline */
 } qo_job;
 
 static void *qo_worker(void *arg) {
     qo_job *j = (qo_job *)arg;
-    if (j->bits == 32) qo_encode_u32_seed(j->seed, j->start, j->n, j->t, (uint32_t *)j->S);
-    else qo_encode_u64_seed(j->seed, j->start, j->n, j->t, (uint64_t *)j->S);
+    if (j->ids) {
+        if (j->bits == 32) qo_encode_u32((const uint32_t *)j->ids + j->start, j->n, j->t, (uint32_t *)j->S);
+        else qo_encode_u64((const uint64_t *)j->ids + j->start, j->n, j->t, (uint64_t *)j->S);
+    } else if (j->bits == 32) {
+        qo_encode_u32_seed(j->seed, j->start, j->n, j->t, (uint32_t *)j->S);
+    } else {
+        qo_encode_u64_seed(j->seed, j->start, j->n, j->t, (uint64_t *)j->S);
+    }
     return 0;
 }
 
-/* returns 0 on success */
-int qo_encode_seed_mt(uint32_t bits, uint64_t seed, uint64_t start, uint64_t n, uint32_t t, uint32_t nthreads,
-                      void *S) {
+static int qo_encode_mt_impl(uint32_t bits, const void *ids, uint64_t seed, uint64_t start, uint64_t n, uint32_t t,
+                             uint32_t nthreads, void *S) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -196,7 +202,7 @@ int qo_encode_seed_mt(uint32_t bits, uint64_t seed, uint64_t start, uint64_t n, 
     uint32_t started = 0;
     for (uint32_t i = 0; i < nthreads; ++i, ++started) {
         const uint64_t b = n * i / nthreads, e = n * (i + 1) / nthreads;
-        job[i] = (qo_job){seed, start + b, e - b, t, bits, parts + (size_t)i * t * esz};
+        job[i] = (qo_job){seed, start + b, e - b, t, bits, parts + (size_t)i * t * esz, ids};
         if (pthread_create(&th[i], 0, qo_worker, &job[i])) break;
     }
     for (uint32_t i = 0; i < started; ++i) pthread_join(th[i], 0);
@@ -208,6 +214,17 @@ int qo_encode_seed_mt(uint32_t bits, uint64_t seed, uint64_t start, uint64_t n, 
         }
     free(parts);
     return 0;
+}
+
+/* returns 0 on success */
+int qo_encode_seed_mt(uint32_t bits, uint64_t seed, uint64_t start, uint64_t n, uint32_t t, uint32_t nthreads,
+                      void *S) {
+    return qo_encode_mt_impl(bits, 0, seed, start, n, t, nthreads, S);
+}
+/* over a pre-generated id array (the crate's benchmark times inserts of
+ * pre-generated ids) */
+int qo_encode_mt(uint32_t bits, const void *ids, uint64_t n, uint32_t t, uint32_t nthreads, void *S) {
+    return qo_encode_mt_impl(bits, ids, 0, 0, n, t, nthreads, S);
 }
 
 /* ---- reference-shape microbenchmark (BASELINE.md "Reference-shape row"):

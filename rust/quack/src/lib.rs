@@ -62,6 +62,26 @@ fn ok(rc: c_int) {
 }
 
 /// Library version string (`quack-hip …`).
+/// The distinct roots in GF(p32), ascending, of the polynomial `coeffs`
+/// describes (`to_coeffs`): a log entry is a root-test hit (`media_client.rs:310`)
+/// exactly when it is congruent to one of them (`qk_u32_roots`).
+pub fn roots_u32(coeffs: &[u32]) -> Result<Vec<u32>> {
+    let mut out = vec![0u32; coeffs.len().max(1)];
+    let mut k = 0u32;
+    check(unsafe { ffi::qk_u32_roots(coeffs.as_ptr(), coeffs.len() as u32, out.as_mut_ptr(), out.len() as u32, &mut k) })?;
+    out.truncate(k as usize);
+    Ok(out)
+}
+
+/// [`roots_u32`] over GF(p64) (`qk_u64_roots`).
+pub fn roots_u64(coeffs: &[u64]) -> Result<Vec<u64>> {
+    let mut out = vec![0u64; coeffs.len().max(1)];
+    let mut k = 0u32;
+    check(unsafe { ffi::qk_u64_roots(coeffs.as_ptr(), coeffs.len() as u32, out.as_mut_ptr(), out.len() as u32, &mut k) })?;
+    out.truncate(k as usize);
+    Ok(out)
+}
+
 pub fn version() -> String {
     unsafe { CStr::from_ptr(ffi::qk_version()) }.to_string_lossy().into_owned()
 }

@@ -140,6 +140,14 @@ def lib():
     """Load libquack_hip.so; raises if it has not been built (no fallback)."""
     global _lib
     if _lib is None:
+        # torch first when it is installed: it brings its own HIP runtime
+        # (libamdhip64.so.7), and the library must bind to that same copy —
+        # loaded the other way round, torch finds the /opt/rocm runtime
+        # already mapped under its soname and reports no GPU
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

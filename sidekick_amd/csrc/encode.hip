@@ -5,20 +5,29 @@
 // benchmark_construct, figures/fig2_microbenchmarks.py:220-228) for an id
 // array resident in HBM.
 //
-// Work decomposition:
-//   * A lane group of G lanes owns one id at a time; lane j of the group
-//     computes the powers j+1, j+1+G, ..., j+1+(K-1)G of x = id (mod p) with
-//     a step of x^G, keeping K lazy accumulators in VGPRs.  G*K >= t.
-//     t = 32 (the headline) is G = 1, K = 32: each lane streams its own ids
-//     with 16-byte loads and runs 31 dependent lazy modmuls per id.
-//   * The ids are never reduced mod p up front: x^k is congruent either way
-//     and the lazy accumulators are folded once per lane at the end.
-//   * Lane partials -> wavefront butterfly (shfl_xor over lanes with equal
-//     lane % G) -> LDS across the 4 waves -> one partial per block per power,
-//     stored [power][block] -> a finalize kernel (t workgroups) sums the
-//     block partials and writes the canonical partial vector.
-// Integer VALU bound (no MFMA: nothing here is a contraction); the HBM read
-// of 4 B/id is ~5% of the roofline at t = 32.
+// Kernels and dispatch (`enc32` / `enc64` below):
+//   * 5 <= t <= 80 (u32) — the headline kernel k_encode_u32_bsgs<NB,NA,SG>
+//     (bsgs.h): baby steps x^1..x^NB and giant steps x^(NB a) per id, lane
+//     private, then S_(NB a + b) += A_a * B_b as 64-bit multiply-accumulates
+//     whose wraps are counted per wave on the scalar unit.  t = 32 is
+//     (NB, NA) = (8, 4): 9 lazy modmuls + 24 MACs + 8 row-0 mads per id,
+//     1.19 VALU + 0.76 SALU wave-instructions per id, ~0.75 of the
+//     integer-issue roofline (tools/issue_roofline.py) and ~0.19 of the HBM
+//     read roofline (4 B/id).
+//   * 21 <= t <= 80 (u64) — k_encode_u64_bsgs<NA,MODE,SG> (bsgs64.h): the
+//     same split with the babies/giants of a 256-id tile shared through LDS,
+//     each wave owning two babies' MAC rows.
+//   * t > 80 — passes of the BSGS kernels (offset giants x^(base + 8a)).
+//   * small t (u32 t <= 4, u64 t <= 20) — power chains: a lane group of G
+//     lanes owns one id, lane j computes powers j+1, j+1+G, ... with step
+//     x^G and K lazy accumulators (G K >= t).
+//   The ids are never reduced mod p up front (x^k is congruent either way).
+//   Lane partials -> wavefront butterfly -> LDS across the waves -> one
+//   partial per (power, block), stored [power][block] -> a finalize kernel
+//   (one workgroup per power) writes the canonical partial vector.
+// Integer-issue bound; no MFMA in this library (north_star).  The int8
+// matrix-core variants (mfma8.h / mfma64.h) compile only into
+// the opt-in libquack_hip_mfma.so (QK_WITH_MATRIX_CORES).
 #include "ctx.h"
 #include "field.h"
 #include "bsgs.h"

@@ -16,10 +16,11 @@
 //      z^(2^w) mod P takes w squarings (w = 32 / 64), and 2^w = p + c
 //      (c = 5 / 59), so z^(2^w) - z^(c+1) = z^(c+1) (z^(p-1) - 1) and, z being
 //      prime to P, gcd(P, z^(2^w) - z^(c+1)) = g
-//   3. Cantor-Zassenhaus equal-degree splitting of g into linear factors:
-//      for a random a, gcd(g, (z + a)^((p-1)/2) - 1) holds the roots r with
-//      r + a a quadratic residue — about half of them; recurse on both parts;
-//      quadratics by the root formula.
+//   3. Cantor-Zassenhaus equal-degree splitting of g into linear factors,
+//      L ways at once: for a random a, w = (z + a)^((p-1)/L) mod g takes the
+//      value chi_L(r + a) (an L-th root of unity) at each root r, and
+//      gcd(g, w - zeta^j) collects the roots of class j; recurse on the
+//      classes; quadratics by the root formula.
 // In the decode case P is a product of linear factors (the missing ids), so
 // step 3 runs on P itself first (the fast path, no z^(2^w) exponentiation);
 // only a P that will not split that way (roots outside GF(p): a corrupt or
@@ -96,6 +97,16 @@ QK_AVX512 static void sqr32_avx512(uint32_t *a, size_t m, const uint64_t *nf64, 
     for (size_t i = 0; i < m; ++i) a[i] = canon32(fold64_32(acc[i]));
 }
 
+// splitting arity per field (a divisor of p - 1; measured on d = 8..64,
+// 2-way 203 / 877 us at d = 32 (u32 / u64), 10-way 116 /
+// 11-way 447, 19-way 95 / 22-way 230, 38-way 128 / 44-way 368)
+#ifndef SPLIT32
+#define SPLIT32 19
+#endif
+#ifndef SPLIT64
+#define SPLIT64 22
+#endif
+
 // Field policies: canonical elements T, lazy accumulator A (sums of folded
 // products: < 2^35 (u32) / < 2^70 (u64) each, at most 2^11 of them).
 struct F32 {
@@ -103,7 +114,9 @@ struct F32 {
     using A = uint64_t;
     static constexpr int W = 32;         // 2^W = p + C
     static constexpr uint64_t C = C32;
-    static constexpr uint64_t HALF = (P32 - 1) / 2;
+    static constexpr uint64_t PM1 = P32 - 1;       // = 2 * 5 * 19 * 22605091
+    static constexpr uint32_t L = SPLIT32;         // splitting arity: L | p - 1
+    static T pow(T a, uint64_t e) { return pow32(a, e); }
     static T add(T a, T b) { return add32(a, b); }
     static T sub(T a, T b) { return sub32(a, b); }
     static T mul(T a, T b) { return mul32(a, b); }
@@ -128,7 +141,9 @@ struct F64 {
     using A = unsigned __int128;
     static constexpr int W = 64;
     static constexpr uint64_t C = C64;
-    static constexpr uint64_t HALF = (P64 - 1) / 2;
+    static constexpr uint64_t PM1 = P64 - 1;       // = 4 * 11 * 137 * 547 * 5594472617641
+    static constexpr uint32_t L = SPLIT64;
+    static T pow(T a, uint64_t e) { return pow64(a, e); }
     static T add(T a, T b) { return add64(a, b); }
     static T sub(T a, T b) { return sub64(a, b); }
     static T mul(T a, T b) { return mul64(a, b); }
@@ -323,6 +338,25 @@ template <class F> Poly<F> to_poly(std::vector<typename F::T> r) {
     return p;
 }
 
+// a primitive L-th root of unity of GF(p) (L | p - 1)
+template <class F> typename F::T root_of_unity() {
+    using T = typename F::T;
+    static const T z = [] {
+        for (T c = 2;; ++c) {
+            const T w = F::pow(c, F::PM1 / F::L);
+            bool prim = w != 1;
+            uint32_t l = F::L;
+            for (uint32_t q = 2; q <= l && prim; ++q)
+                if (l % q == 0) {
+                    prim = F::pow(w, F::L / q) != 1;
+                    while (l % q == 0) l /= q;
+                }
+            if (prim) return w;
+        }
+    }();
+    return z;
+}
+
 // Split g into linear factors, appending their roots.  exact: g is monic,
 // squarefree, and all its roots lie in GF(p)*: always succeeds.  !exact
 // (the fast path, any monic g with g(0) != 0): every leaf that is reached is a
@@ -331,11 +365,15 @@ template <class F> Poly<F> to_poly(std::vector<typename F::T> r) {
 // returns false when a factor will not split into linear ones (an
 // irreducible factor of degree >= 2, i.e. roots outside GF(p)), after a
 // quadratic with a non-residue discriminant or 24 failed attempts on one
-// factor (for a product of >= 3 linear factors a random attempt fails with
-// probability <= 1/4).
+// factor.
+// A factor of degree k >= 3 is split L ways at once (Cantor-Zassenhaus with
+// the L-th power character): w = (z + a)^((p-1)/L) mod g takes at a root r
+// the L-th root of unity chi(r + a) (0 for r = -a), so gcd(g, w - zeta^j),
+// j = 0..L-1, sort the roots into L groups — one exponentiation for ~log_L k
+// levels instead of log_2 k (L = 19 for p32, 22 for p64).
 template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out, bool exact) {
     using T = typename F::T;
-    const T inv2 = F::inv(2);
+    const T inv2 = F::inv(2), zeta = root_of_unity<F>();
     std::vector<Poly<F>> todo{g0};
     uint64_t s = 0x243F6A8885A308D3ull;   // fixed seed: a deterministic sequence of a's
     while (!todo.empty()) {
@@ -365,13 +403,24 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
             if (!exact && fails >= 24) return false;
             s += GAMMA;
             const T a = F::canon_any((T)splitmix_mix(s));
-            std::vector<T> w = R.pow_lin(a, F::HALF);
-            w[0] = F::sub(w[0], 1);
-            Poly<F> h = gcd<F>(g, to_poly<F>(std::move(w)));
-            const size_t dh = h.empty() ? 0 : h.size() - 1;
-            if (dh == 0 || dh == k) continue;
-            todo.push_back(div_monic<F>(g, h));
-            todo.push_back(std::move(h));
+            const Poly<F> w = to_poly<F>(R.pow_lin(a, F::PM1 / F::L));
+            Poly<F> rem = g;
+            std::vector<Poly<F>> parts;
+            T zj = 1;
+            for (uint32_t j = 0; j < F::L && rem.size() > 2; ++j, zj = F::mul(zj, zeta)) {
+                Poly<F> wr = w;
+                if (parts.size()) rem_monic<F>(wr, rem);      // w mod rem (rem == g: w is reduced)
+                if (wr.empty()) wr.push_back(0);
+                wr[0] = F::sub(wr[0], zj);
+                Poly<F> h = gcd<F>(rem, std::move(wr));
+                if (h.size() > 1) {
+                    rem = div_monic<F>(rem, h);
+                    parts.push_back(std::move(h));
+                }
+            }
+            if (rem.size() > 1) parts.push_back(std::move(rem));   // the last group, r = -a, or an unsplit rest
+            if (parts.size() < 2) continue;
+            for (auto &p : parts) todo.push_back(std::move(p));
             break;
         }
     }

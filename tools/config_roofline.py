@@ -6,14 +6,18 @@ the committed rocprofv3 CSVs of one round (not part of the product):
   <round>/configs_pmc_fetch_size.csv --pmc FETCH_SIZE
   <round>/configs_pmc_sq.csv         --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE
 
-all three collected on `tools/bench_configs.py u64 decode decode64`.
+all three collected on `tools/bench_configs.py u64 decode decode64`, plus
+the integer-issue roofline of each kernel from <round>/issue_roofline.json
+(tools/issue_roofline.py: VALU instructions per unit x the mean issue cost
+of the kernel's hot-loop mix, against the SIMD-cycles per unit of the
+profiled launch at its GRBM_GUI_ACTIVE clock).
 Algorithmic bytes: 8 B per u64 id (encode), 4 / 8 B per u32 / u64 candidate
 (root test), one launch = the whole array.  HBM traffic =
 FETCH_SIZE KiB x 1024 x 2 (the gfx950 correction of MI355X_MICROARCH.md, as
 tools/update_profiles.py).  Instruction counts are wave-instructions; x64 =
 lane operations.
 
-    python tools/config_roofline.py profiles/r02 > profiles/r02/configs_roofline.json
+    python tools/config_roofline.py profiles/r03 > profiles/r03/configs_roofline.json
 """
 import collections
 import csv
@@ -23,12 +27,17 @@ import sys
 
 PEAK_GBPS = 8000.0
 # (kernel name prefix, grid size of the config's launch, units, bytes per unit, config)
+# (kernel name prefix, grid, units, bytes per unit, config, issue_roofline.json key)
 ROWS = [("void qk::k_encode_u64_bsgs<10, 1, 0>", "196608", 1_000_000_000, 8,
-         "configs[2]: encode 1e9 u64 ids, t=80"),
+         "configs[2]: encode 1e9 u64 ids, t=80", "encode_u64_t80"),
+        ("void qk::k_root_scan<unsigned int, 1>", "524288", 100_000_000, 4,
+         "configs[4]: root test of 1e8 u32 candidates, d=32 — root-set scan (the default)", "root_scan_u32_d32"),
         ("void qk::k_root_test_u32<32>", "458752", 100_000_000, 4,
-         "configs[4]: root test of 1e8 u32 candidates, d=32"),
-        ("qk::k_root_test_u64", "524288", 100_000_000, 8,
-         "root test of 1e8 u64 candidates, d=32 (u64 twin of configs[4])")]
+         "configs[4]: root test of 1e8 u32 candidates, d=32 — Horner", "root_test_u32_d32"),
+        ("void qk::k_root_scan<unsigned long, 1>", "524288", 100_000_000, 8,
+         "root test of 1e8 u64 candidates, d=32 — root-set scan (the default)", "root_scan_u64_d32"),
+        ("void qk::k_root_test_u64_bsgs<0>", "458752", 100_000_000, 8,
+         "root test of 1e8 u64 candidates, d=32 — baby-step/giant-step Horner", "root_test_u64_d32")]
 
 
 def main(d):
@@ -37,8 +46,12 @@ def main(d):
     for f in ("configs_pmc_fetch_size.csv", "configs_pmc_sq.csv"):
         for r in csv.DictReader(open(os.path.join(d, f))):
             ctr[(r["Kernel_Name"].split("(")[0], r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    issue = {}
+    ip = os.path.join(d, "issue_roofline.json")
+    if os.path.exists(ip):
+        issue = json.load(open(ip))["kernels"]
     out = []
-    for name, grid, units, bpu, cfg in ROWS:
+    for name, grid, units, bpu, cfg, ikey in ROWS:
         s = stats[name]
         c = {k: sum(v) / len(v) for k, v in ctr[(name, grid)].items()}
         avg_s = float(s["AverageNs"]) * 1e-9
@@ -54,6 +67,13 @@ def main(d):
                     "valu_lane_ops_per_unit": round(c["SQ_INSTS_VALU"] / units * 64, 1),
                     "salu_wave_insts_per_unit": round(c["SQ_INSTS_SALU"] / units, 3),
                     "lds_wave_insts_per_unit": round(c["SQ_INSTS_LDS"] / units, 3)})
+        if ikey in issue:
+            k = issue[ikey]
+            out[-1]["valu"] = {"bound": "valu-issue", "unit": "SIMD-cycles/unit",
+                               "peak": k["issue_cycles_per_unit_peak"],
+                               "achieved": k["issue_cycles_per_unit_achieved"], "frac": k["frac"],
+                               "mean_issue_cycles_per_valu": k["mean_issue_cycles_per_valu"],
+                               "clock_ghz": k["clock_ghz"], "salu_busy": k["salu_busy"]}
     json.dump(out, sys.stdout, indent=1)
     print()
 

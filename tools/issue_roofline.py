@@ -52,18 +52,28 @@ CUS = 256
 COST_SIMPLE = 17.97 / 8
 COST_HEAVY = 33.52 / 8
 
-# kernel -> (asm file, symbol prefix, pmc csv, kernel-name substring, units per launch,
-#            units per loop iteration per wave, config label)
+# kernel -> (asm file, symbol prefix, pmc csv, kernel-name substring, grid of the
+#            measured launch, units per launch, units per hot-loop iteration per
+#            wave, config label)
 KERNELS = {
-    "encode_u32_t32": ("encode.s", "_ZN2qk17k_encode_u32_bsgsILi8ELi4ELi8E", "profiles/r02/encode_pmc_sq.csv",
-                       "k_encode_u32_bsgs<8, 4, 8>", 1e9, 256,
+    "encode_u32_t32": ("encode.s", "_ZN2qk17k_encode_u32_bsgsILi8ELi4ELi8E", "profiles/r03/encode_pmc_sq.csv",
+                       "k_encode_u32_bsgs<8, 4, 8>", "327680", 1e9, 256,
                        "configs[1]: encode 1e9 u32 ids, t=32 (the bench line)"),
-    "encode_u64_t80": ("encode.s", "_ZN2qk17k_encode_u64_bsgsILi10ELi1ELi0E", "profiles/r02/configs_pmc_sq.csv",
-                       "k_encode_u64_bsgs<10, 1, 0>", 1e9, 64,
+    "encode_u64_t80": ("encode.s", "_ZN2qk17k_encode_u64_bsgsILi10ELi1ELi0E", "profiles/r03/configs_pmc_sq.csv",
+                       "k_encode_u64_bsgs<10, 1, 0>", "196608", 1e9, 64,
                        "configs[2]: encode 1e9 u64 ids, t=80"),
-    "root_test_u32_d32": ("decode.s", "_ZN2qk15k_root_test_u32ILi32E", "profiles/r02/configs_pmc_sq.csv",
-                          "k_root_test_u32<32>", 1e8, 256,
+    "root_scan_u32_d32": ("decode.s", "_ZN2qk11k_root_scanIjLi1E", "profiles/r03/configs_pmc_sq.csv",
+                          "k_root_scan<unsigned int, 1>", "524288", 1e8, 512,
+                          "configs[4]: root test of 1e8 u32 candidates, d=32 (root-set scan, the default)"),
+    "root_test_u32_d32": ("decode.s", "_ZN2qk15k_root_test_u32ILi32E", "profiles/r03/configs_pmc_sq.csv",
+                          "k_root_test_u32<32>", "458752", 1e8, 256,
                           "configs[4]: root test of 1e8 u32 candidates, d=32 (Horner)"),
+    "root_scan_u64_d32": ("decode.s", "_ZN2qk11k_root_scanImLi1E", "profiles/r03/configs_pmc_sq.csv",
+                          "k_root_scan<unsigned long, 1>", "524288", 1e8, 256,
+                          "root test of 1e8 u64 candidates, d=32 (root-set scan, the default)"),
+    "root_test_u64_d32": ("decode.s", "_ZN2qk20k_root_test_u64_bsgsILi0E", "profiles/r03/configs_pmc_sq.csv",
+                          "k_root_test_u64_bsgs<0>", "458752", 1e8, 128,
+                          "root test of 1e8 u64 candidates, d=32 (baby-step/giant-step Horner)"),
 }
 
 
@@ -126,12 +136,12 @@ def pick_loop(ls, dyn_valu_per_iter):
     return best
 
 
-def pmc_row(path, kname):
-    """Counters and duration (ns) of the last profiled dispatch of kname."""
+def pmc_row(path, kname, grid):
+    """Counters and duration (ns) of the last profiled dispatch of kname at grid."""
     disp = collections.defaultdict(dict)
     with open(os.path.join(ROOT, path)) as f:
         for r in csv.DictReader(f):
-            if kname in r["Kernel_Name"]:
+            if kname in r["Kernel_Name"] and r["Grid_Size"] == grid:
                 d = disp[r["Dispatch_Id"]]
                 d[r["Counter_Name"]] = float(r["Counter_Value"])
                 d["_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
@@ -142,9 +152,9 @@ def pmc_row(path, kname):
 
 
 def analyse(name, asm_dir):
-    asm, sym, csvp, kname, units, per_iter, label = KERNELS[name]
+    asm, sym, csvp, kname, grid, units, per_iter, label = KERNELS[name]
     lines = open(os.path.join(asm_dir, asm)).read().split("\n")
-    c = pmc_row(csvp, kname)
+    c = pmc_row(csvp, kname, grid)
     valu_pu = c["SQ_INSTS_VALU"] / units
     salu_pu = c["SQ_INSTS_SALU"] / units
     err, n_static, cost_static, loop_name = pick_loop(loops(lines, sym), valu_pu * per_iter)
