@@ -267,7 +267,7 @@ static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t,
 // pass; Horner costs d multiply steps per candidate.  Cost model in
 // microseconds from the measurements in DESIGN.md §3.4 (MI355X kernels,
 // EPYC host root finding): the scan is taken when it is cheaper.
-template <typename T> static bool rt_use_scan(qk_ctx *ctx, uint32_t d, size_t n) {
+template <typename T> static bool rt_use_scan(const qk_ctx *ctx, uint32_t d, size_t n) {
     if (d < 2 || d > RT_SCAN_MAXD) return false;          // d = 1: the root is -c_1, Horner is one step
     if (ctx->knobs.root_test == 1) return false;
     if (ctx->knobs.root_test == 2) return true;
@@ -278,36 +278,37 @@ template <typename T> static bool rt_use_scan(qk_ctx *ctx, uint32_t d, size_t n)
     return scan < horner;
 }
 
+template <typename T> int root_test_plan(const qk_ctx *ctx, const T *coeffs, uint32_t d, size_t n, RtPlan<T> &plan) {
+    plan = RtPlan<T>{};
+    if (!n || !rt_use_scan<T>(ctx, d, n)) return QK_OK;
+    std::vector<T> r(d);
+    uint32_t k = 0;
+    int rc;
+    if constexpr (sizeof(T) == 4) rc = qk_u32_roots(coeffs, d, r.data(), d, &k);
+    else rc = qk_u64_roots(coeffs, d, r.data(), d, &k);
+    if (rc) return rc;
+    plan.scan = rt_scan_table<T>(r.data(), k, plan.set, plan.tab) && plan.set.words * sizeof(T) <= SMALL_NHITS * 8;
+    if (!plan.scan) plan.tab.clear();
+    return QK_OK;
+}
+
 template <typename T>
-int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
-                    hipStream_t s) {
+int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_t d, const T *d_log, size_t n,
+                    int use_stop, T stop_value, hipStream_t s) {
     // layout of d_small: [0, SMALL_NHITS) coefficients (or the root set), [SMALL_NHITS] hit count,
     // [SMALL_STOP] stop index
     uint64_t *d_counters = ctx->d_small + SMALL_NHITS;
     T *d_c = (T *)ctx->d_small;
-    bool scan = n && rt_use_scan<T>(ctx, d, n);
-    RtScanSet set;
+    const bool scan = n && plan.scan;
     size_t cbytes = (size_t)d * sizeof(T);
     if (scan) {
-        std::vector<T> r(d), tab;
-        uint32_t k = 0;
-        int rc;
-        if constexpr (sizeof(T) == 4) rc = qk_u32_roots(coeffs, d, r.data(), d, &k);
-        else rc = qk_u64_roots(coeffs, d, r.data(), d, &k);
-        if (rc) return rc;
-        scan = rt_scan_table<T>(r.data(), k, set, tab) && set.words * sizeof(T) <= SMALL_NHITS * 8;
-        if (scan) {
-            cbytes = (size_t)set.words * sizeof(T);
-            memcpy(ctx->h_small, tab.data(), cbytes);
-        }
-    }
-    if (!scan) {
-        if constexpr (sizeof(T) == 8) {
-            if (rt64_use_bsgs(ctx, d)) cbytes = rt64_bsgs_table(coeffs, d, ctx->h_small) * 8;   // limb-shifted table
-            else memcpy(ctx->h_small, coeffs, cbytes);
-        } else {
-            memcpy(ctx->h_small, coeffs, cbytes);
-        }
+        cbytes = (size_t)plan.set.words * sizeof(T);
+        memcpy(ctx->h_small, plan.tab.data(), cbytes);
+    } else if constexpr (sizeof(T) == 8) {
+        if (rt64_use_bsgs(ctx, d)) cbytes = rt64_bsgs_table(coeffs, d, ctx->h_small) * 8;   // limb-shifted table
+        else memcpy(ctx->h_small, coeffs, cbytes);
+    } else {
+        memcpy(ctx->h_small, coeffs, cbytes);
     }
     if (cbytes) QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, cbytes, hipMemcpyHostToDevice, s));
     if (int rc = ensure_hits(ctx, 4096, s)) return rc;
@@ -315,7 +316,7 @@ int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, si
     if (n) {
         int rc;
         if (scan) {
-            rc = launch_root_scan<T>(ctx, d_c, set, d_log, n, use_stop, stop_value, ctx->d_hits,
+            rc = launch_root_scan<T>(ctx, d_c, plan.set, d_log, n, use_stop, stop_value, ctx->d_hits,
                                      (uint64_t)ctx->hits_cap, d_counters, s);
         } else {
             int (*launch)(qk_ctx *, const T *, uint32_t, const T *, size_t, int, T, uint64_t *, uint64_t, uint64_t *,
@@ -336,13 +337,13 @@ int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, si
 }
 
 template <typename T>
-int root_test_finish(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
-                     hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index) {
+int root_test_finish(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_t d, const T *d_log, size_t n,
+                     int use_stop, T stop_value, hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index) {
     QK_HIP_TRY(hipStreamSynchronize(s));
     uint64_t cnt = ctx->h_small[SMALL_NHITS];
     if (cnt > ctx->hits_cap) {   // grow and rerun once (the kernel counts every hit)
         if (int rc = ensure_hits(ctx, (size_t)cnt, s)) return rc;
-        if (int rc = root_test_begin<T>(ctx, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
+        if (int rc = root_test_begin<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
         QK_HIP_TRY(hipStreamSynchronize(s));
         cnt = ctx->h_small[SMALL_NHITS];
         if (cnt > ctx->hits_cap) return QK_E_HIP;
@@ -359,14 +360,18 @@ int root_test_finish(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, s
     stop_index = use_stop ? std::min<uint64_t>(stop, (uint64_t)n) : (uint64_t)n;
     return QK_OK;
 }
-template int root_test_begin<uint32_t>(qk_ctx *, const uint32_t *, uint32_t, const uint32_t *, size_t, int, uint32_t,
-                                       hipStream_t);
-template int root_test_begin<uint64_t>(qk_ctx *, const uint64_t *, uint32_t, const uint64_t *, size_t, int, uint64_t,
-                                       hipStream_t);
-template int root_test_finish<uint32_t>(qk_ctx *, const uint32_t *, uint32_t, const uint32_t *, size_t, int, uint32_t,
-                                        hipStream_t, std::vector<uint64_t> &, uint64_t &);
-template int root_test_finish<uint64_t>(qk_ctx *, const uint64_t *, uint32_t, const uint64_t *, size_t, int, uint64_t,
-                                        hipStream_t, std::vector<uint64_t> &, uint64_t &);
+template int root_test_plan<uint32_t>(const qk_ctx *, const uint32_t *, uint32_t, size_t, RtPlan<uint32_t> &);
+template int root_test_plan<uint64_t>(const qk_ctx *, const uint64_t *, uint32_t, size_t, RtPlan<uint64_t> &);
+template int root_test_begin<uint32_t>(qk_ctx *, const RtPlan<uint32_t> &, const uint32_t *, uint32_t,
+                                       const uint32_t *, size_t, int, uint32_t, hipStream_t);
+template int root_test_begin<uint64_t>(qk_ctx *, const RtPlan<uint64_t> &, const uint64_t *, uint32_t,
+                                       const uint64_t *, size_t, int, uint64_t, hipStream_t);
+template int root_test_finish<uint32_t>(qk_ctx *, const RtPlan<uint32_t> &, const uint32_t *, uint32_t,
+                                        const uint32_t *, size_t, int, uint32_t, hipStream_t, std::vector<uint64_t> &,
+                                        uint64_t &);
+template int root_test_finish<uint64_t>(qk_ctx *, const RtPlan<uint64_t> &, const uint64_t *, uint32_t,
+                                        const uint64_t *, size_t, int, uint64_t, hipStream_t, std::vector<uint64_t> &,
+                                        uint64_t &);
 
 template <typename T>
 static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop,
@@ -386,10 +391,12 @@ static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_l
     std::lock_guard<std::mutex> g(ctx->mu);
     QK_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = pick_stream(ctx, stream);
-    if (int rc = root_test_begin<T>(ctx, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
+    RtPlan<T> plan;
+    if (int rc = root_test_plan<T>(ctx, coeffs, d, n, plan)) return rc;
+    if (int rc = root_test_begin<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
     std::vector<uint64_t> h;
     uint64_t stop = n;
-    if (int rc = root_test_finish<T>(ctx, coeffs, d, d_log, n, use_stop, stop_value, s, h, stop)) return rc;
+    if (int rc = root_test_finish<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s, h, stop)) return rc;
     const size_t m = (size_t)(std::lower_bound(h.begin(), h.end(), stop) - h.begin());
     if (stop_index) *stop_index = stop;
     *n_hits = m;

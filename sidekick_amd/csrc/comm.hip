@@ -373,27 +373,48 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
         if (!ls[i] && hdr[i][0]) ls[i] = (int)(int64_t)hdr[i][0];   // the root's status
     }
 
-    // 2. root test of every local shard, all GPUs in flight
+    // 2. root test of every local shard, all GPUs in flight; the plan (the
+    //    host roots for the root-set scan) once per call for every local rank
     std::vector<std::vector<uint64_t>> lh(nl);
     std::vector<uint64_t> lstop(nl, 0);
-    std::vector<T> coeffs;
     std::vector<char> began(nl, 0);
+    std::vector<T> coeffs;
+    RtPlan<T> plan;
+    uint32_t d = 0;
+    int use_stop = 0;
+    T stop_value = 0;
+    {
+        size_t first = nl, nmax = 0;
+        for (size_t i = 0; i < nl; ++i)
+            if (!ls[i]) {
+                if (first == nl) first = i;
+                nmax = std::max(nmax, n[i]);
+            }
+        if (first < nl) {   // every local rank holds the same broadcast header
+            const uint64_t *hd = hdr[first].data();
+            d = (uint32_t)std::min<uint64_t>(hd[1], QK_MAX_THRESHOLD);
+            use_stop = (int)hd[2];
+            stop_value = (T)hd[3];
+            coeffs.assign(std::max<uint32_t>(d, 1), 0);
+            for (uint32_t k = 0; k < d; ++k) coeffs[k] = (T)hd[4 + k];
+            if (d > 0 && nmax)
+                if (int e = root_test_plan<T>(c->local[first].ctx, coeffs.data(), d, nmax, plan))
+                    for (size_t i = 0; i < nl; ++i)
+                        if (!ls[i]) ls[i] = e;
+        }
+    }
     for (size_t i = 0; i < nl; ++i) {
         Local &L = c->local[i];
         lstop[i] = n ? n[i] : 0;
         if (ls[i]) continue;
-        const uint64_t *hd = hdr[i].data();
-        const uint32_t d = (uint32_t)std::min<uint64_t>(hd[1], QK_MAX_THRESHOLD);
-        const int use_stop = (int)hd[2];
-        coeffs.assign(std::max<uint32_t>(d, 1), 0);
-        for (uint32_t k = 0; k < d; ++k) coeffs[k] = (T)hd[4 + k];
         if (!(d > 0 || use_stop) || !n[i]) continue;
         std::lock_guard<std::mutex> g(L.ctx->mu);
-        if (int e = hipSetDevice(L.device) == hipSuccess ? QK_OK : QK_E_HIP) {
-            ls[i] = e;
+        if (hipSetDevice(L.device) != hipSuccess) {
+            ls[i] = QK_E_HIP;
             continue;
         }
-        if (int e = root_test_begin<T>(L.ctx, coeffs.data(), d, d_log[i], n[i], use_stop, (T)hd[3], L.ctx->stream))
+        if (int e = root_test_begin<T>(L.ctx, plan, coeffs.data(), d, d_log[i], n[i], use_stop, stop_value,
+                                       L.ctx->stream))
             ls[i] = e;
         else
             began[i] = 1;
@@ -401,14 +422,10 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
     for (size_t i = 0; i < nl; ++i) {
         if (!began[i]) continue;
         Local &L = c->local[i];
-        const uint64_t *hd = hdr[i].data();
-        const uint32_t d = (uint32_t)std::min<uint64_t>(hd[1], QK_MAX_THRESHOLD);
-        coeffs.assign(std::max<uint32_t>(d, 1), 0);
-        for (uint32_t k = 0; k < d; ++k) coeffs[k] = (T)hd[4 + k];
         std::lock_guard<std::mutex> g(L.ctx->mu);
         (void)hipSetDevice(L.device);
-        if (int e = root_test_finish<T>(L.ctx, coeffs.data(), d, d_log[i], n[i], (int)hd[2], (T)hd[3], L.ctx->stream,
-                                        lh[i], lstop[i])) {
+        if (int e = root_test_finish<T>(L.ctx, plan, coeffs.data(), d, d_log[i], n[i], use_stop, stop_value,
+                                        L.ctx->stream, lh[i], lstop[i])) {
             ls[i] = e;
             lh[i].clear();
             continue;

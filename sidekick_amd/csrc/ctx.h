@@ -150,13 +150,22 @@ template <typename T>
 int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
                      T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, hipStream_t s);
 
-// root test in two phases (api.hip): enqueue on s, then wait + collect the
+// root test in two phases (api.hip): root_test_plan picks Horner or the
+// root-set scan for (d, n) and, for the scan, finds the roots on the host and
+// builds the set (once per call, shared by every shard of a sharded decode);
+// root_test_begin enqueues on s; root_test_finish waits and collects the
 // sorted hit positions (all of them) and the first stop position
+template <typename T> struct RtPlan {
+    bool scan = false;
+    RtScanSet set;
+    std::vector<T> tab;   // the root set (scan)
+};
+template <typename T> int root_test_plan(const qk_ctx *ctx, const T *coeffs, uint32_t d, size_t n, RtPlan<T> &plan);
 template <typename T>
-int root_test_begin(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
-                    hipStream_t s);
+int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_t d, const T *d_log, size_t n,
+                    int use_stop, T stop_value, hipStream_t s);
 template <typename T>
-int root_test_finish(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop, T stop_value,
-                     hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index);
+int root_test_finish(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_t d, const T *d_log, size_t n,
+                     int use_stop, T stop_value, hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index);
 
 } // namespace qk

@@ -97,6 +97,79 @@ QK_AVX512 static void sqr32_avx512(uint32_t *a, size_t m, const uint64_t *nf64, 
     for (size_t i = 0; i < m; ++i) a[i] = canon32(fold64_32(acc[i]));
 }
 
+// ---- row operations of the Euclid / division loops, u32 on AVX-512 -------
+// canonical a * b over eight 64-bit lanes (a, b < p): two folds leave
+// < 2^32 + 25, one conditional subtraction makes it canonical
+QK_AVX512 static inline __m512i mulc512(__m512i a, __m512i b) {
+    const __m512i P = _mm512_set1_epi64(P32);
+    const __m512i r = fold512(fold512(_mm512_mul_epu32(a, b)));
+    return _mm512_mask_sub_epi64(r, _mm512_cmpge_epu64_mask(r, P), r, P);
+}
+QK_AVX512 static inline __m512i subc512(__m512i a, __m512i b) {   // canonical a - b
+    const __m512i d = _mm512_sub_epi64(a, b);
+    return _mm512_mask_add_epi64(d, _mm512_cmplt_epu64_mask(a, b), d, _mm512_set1_epi64(P32));
+}
+QK_AVX512 static inline __m512i addc512(__m512i a, __m512i b) {   // canonical a + b
+    const __m512i P = _mm512_set1_epi64(P32);
+    const __m512i r = _mm512_add_epi64(a, b);
+    return _mm512_mask_sub_epi64(r, _mm512_cmpge_epu64_mask(r, P), r, P);
+}
+QK_AVX512 static inline __m512i ld8(const uint32_t *p, size_t rem) {
+    const __mmask8 m = rem >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << rem) - 1u);
+    return _mm512_cvtepu32_epi64(_mm256_maskz_loadu_epi32(m, p));
+}
+QK_AVX512 static inline void st8(uint32_t *p, size_t rem, __m512i v) {
+    const __mmask8 m = rem >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << rem) - 1u);
+    _mm512_mask_cvtepi64_storeu_epi32(p, m, v);
+}
+// d[i] = alpha d[i] - beta s[i], i < m (alpha = 1: d[i] - beta s[i])
+QK_AVX512 static void axmy32_avx512(uint32_t *d, const uint32_t *s, size_t m, uint32_t alpha, uint32_t beta) {
+    const __m512i A = _mm512_set1_epi64(alpha), B = _mm512_set1_epi64(beta);
+    for (size_t i = 0; i < m; i += 8) {
+        const size_t r = m - i;
+        __m512i x = ld8(d + i, r);
+        if (alpha != 1) x = mulc512(x, A);
+        st8(d + i, r, subc512(x, mulc512(ld8(s + i, r), B)));
+    }
+}
+QK_AVX512 static void scale32_avx512(uint32_t *d, size_t m, uint32_t alpha) {
+    const __m512i A = _mm512_set1_epi64(alpha);
+    for (size_t i = 0; i < m; i += 8) st8(d + i, m - i, mulc512(ld8(d + i, m - i), A));
+}
+// a <- a (z + c) mod f: out[i] = a[i-1] + c a[i] + top nf[i]  (a[-1] = 0)
+QK_AVX512 static void mullin32_avx512(uint32_t *a, size_t m, uint32_t c, const uint32_t *nf, uint32_t *tmp) {
+    const uint32_t top = a[m - 1];
+    tmp[0] = 0;
+    for (size_t i = 1; i < m; ++i) tmp[i] = a[i - 1];
+    const __m512i C = _mm512_set1_epi64(c), Tp = _mm512_set1_epi64(top);
+    for (size_t i = 0; i < m; i += 8) {
+        const size_t r = m - i;
+        __m512i v = addc512(ld8(tmp + i, r), mulc512(ld8(a + i, r), C));
+        if (top) v = addc512(v, mulc512(ld8(nf + i, r), Tp));
+        st8(a + i, r, v);
+    }
+}
+
+template <class F> static inline bool vec32(size_t m) {
+    if constexpr (F::W == 32) return m >= 8 && cpu_has_avx512();
+    else return false;
+}
+
+// d[i] = alpha d[i] - beta s[i] mod p, i < m
+template <class F>
+static void axmy(typename F::T *d, const typename F::T *s, size_t m, typename F::T alpha, typename F::T beta) {
+    if constexpr (F::W == 32) {
+        if (vec32<F>(m)) return axmy32_avx512(d, s, m, alpha, beta);
+    }
+    for (size_t i = 0; i < m; ++i) d[i] = F::sub(alpha == 1 ? d[i] : F::mul(d[i], alpha), F::mul(beta, s[i]));
+}
+template <class F> static void scale(typename F::T *d, size_t m, typename F::T alpha) {
+    if constexpr (F::W == 32) {
+        if (vec32<F>(m)) return scale32_avx512(d, m, alpha);
+    }
+    for (size_t i = 0; i < m; ++i) d[i] = F::mul(d[i], alpha);
+}
+
 // splitting arity per field (a divisor of p - 1; measured on d = 8..64,
 // 2-way 203 / 877 us at d = 32 (u32 / u64), 10-way 116 /
 // 11-way 447, 19-way 95 / 22-way 230, 38-way 128 / 44-way 368)
@@ -205,8 +278,7 @@ template <class F> void rem_monic(Poly<F> &a, const Poly<F> &b) {
     const size_t m = b.size() - 1;
     for (size_t k = a.size(); k-- > m;) {
         const typename F::T q = a[k];
-        if (q)
-            for (size_t i = 0; i < m; ++i) a[k - m + i] = F::sub(a[k - m + i], F::mul(q, b[i]));
+        if (q) axmy<F>(a.data() + k - m, b.data(), m, 1, q);
         a[k] = 0;
     }
     trim<F>(a);
@@ -220,8 +292,7 @@ template <class F> Poly<F> div_monic(Poly<F> a, const Poly<F> &b) {
     for (size_t k = a.size(); k-- > m;) {
         const typename F::T c = a[k];
         q[k - m] = c;
-        if (c)
-            for (size_t i = 0; i < m; ++i) a[k - m + i] = F::sub(a[k - m + i], F::mul(c, b[i]));
+        if (c) axmy<F>(a.data() + k - m, b.data(), m, 1, c);
     }
     return q;
 }
@@ -235,8 +306,8 @@ template <class F> void rem_ff(Poly<F> &a, const Poly<F> &b) {
     while (a.size() > m) {
         const typename F::T la = a.back();
         const size_t s = a.size() - 1 - m;
-        for (size_t i = 0; i < s; ++i) a[i] = F::mul(a[i], lb);
-        for (size_t i = 0; i < m; ++i) a[s + i] = F::sub(F::mul(a[s + i], lb), F::mul(la, b[i]));
+        scale<F>(a.data(), s, lb);
+        axmy<F>(a.data() + s, b.data(), m, lb, la);
         a.pop_back();
         trim<F>(a);
     }
@@ -265,6 +336,7 @@ template <class F> struct ModRing {
     // the AVX-512 form (u32 field, m >= 8): -f and a widened and padded
     bool vec = false;
     std::vector<uint64_t> nf64, a64, acc64;
+    std::vector<T> tmp;
 
     explicit ModRing(const Poly<F> &f) : m(f.size() - 1), nf(m), acc(2 * m) {
         for (size_t i = 0; i < m; ++i) nf[i] = F::neg(f[i]);
@@ -276,6 +348,7 @@ template <class F> struct ModRing {
                 for (size_t i = 0; i < m; ++i) nf64[i] = nf[i];
                 a64.assign(mb + 8, 0);
                 acc64.assign(2 * m + 16, 0);
+                tmp.assign(m, 0);
             }
         }
     }
@@ -308,6 +381,12 @@ template <class F> struct ModRing {
     }
     // a <- a * (z + c)
     void mul_lin(std::vector<T> &a, T c) {
+        if constexpr (F::W == 32) {
+            if (vec) {
+                mullin32_avx512(a.data(), m, c, nf.data(), tmp.data());
+                return;
+            }
+        }
         const T top = a[m - 1];                       // coefficient of z^m after the shift
         for (size_t i = m; i-- > 0;) {
             const T lower = i ? a[i - 1] : 0;
