@@ -169,3 +169,99 @@ def test_sharded_root_test_gpu_two_ranks(bits, stop_at):
     """The same merge with each rank's shard tested by the gfx950 root test
     (two processes on one GPU, gloo for the small collectives)."""
     _run_decode(2, bits, 100_000, 20, stop_at, use_gpu=True)
+
+
+# ---------------------------------------------------------------- host channels
+# The collectives comm.hip delegates to a host channel (qk_comm_init_host):
+# LoopbackHub (threads of one process) and ProcessGroupChannel (a
+# torch.distributed group), called the way the C side calls them — through
+# the ctypes function pointers of qk_comm_host_ops.
+import ctypes as C  # noqa: E402
+import threading  # noqa: E402
+
+
+def _call_ops(ch, op, a, b=None, root=0):
+    ops = ch._ops()
+    p = lambda x: x.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
+    if op == "reduce":
+        return ops.reduce_sum_u64(None, p(a), len(a), root)
+    if op == "bcast":
+        return ops.broadcast_u64(None, p(a), len(a), root)
+    return ops.allgather_u64(None, p(a), p(b), len(a))
+
+
+def test_loopback_hub_collectives_through_ctypes():
+    from sidekick_amd.dist import LoopbackHub
+    world, n = 3, 5
+    hub = LoopbackHub(world, timeout=30)
+    res = [None] * world
+
+    def rank(r):
+        ch = hub.channel(r)
+        red = np.arange(n, dtype=np.uint64) + np.uint64(10 * r)
+        red[0] = np.uint64(2**64 - 1)                       # the sum wraps mod 2^64, as RCCL's
+        rc1 = _call_ops(ch, "reduce", red, root=1)
+        bc = np.full(n, r, dtype=np.uint64)
+        rc2 = _call_ops(ch, "bcast", bc, root=2)
+        send = np.full(n, 100 + r, dtype=np.uint64)
+        recv = np.zeros(n * world, dtype=np.uint64)
+        rc3 = _call_ops(ch, "gather", send, recv)
+        res[r] = (rc1, rc2, rc3, red.copy(), bc.copy(), recv.copy())
+    ths = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(60)
+    for r in range(world):
+        rc1, rc2, rc3, red, bc, recv = res[r]
+        assert (rc1, rc2, rc3) == (0, 0, 0)
+        assert (bc == 2).all()
+        assert recv.tolist() == [100 + q for q in range(world) for _ in range(n)]
+    want = (np.arange(n, dtype=np.uint64) * world + np.uint64(30)).tolist()
+    want[0] = (3 * (2**64 - 1)) % 2**64
+    assert res[1][3].tolist() == want
+
+
+def test_loopback_missing_peer_fails_the_call_not_the_process():
+    from sidekick_amd.dist import LoopbackHub
+    hub = LoopbackHub(2, timeout=1)
+    a = np.zeros(4, dtype=np.uint64)
+    assert _call_ops(hub.channel(0), "reduce", a) == -1   # BrokenBarrierError -> nonzero to C
+
+
+def _pg_channel_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sidekick_amd.dist import ProcessGroupChannel
+        ch = ProcessGroupChannel()
+        red = np.array([rank + 1, 2**40, 7], dtype=np.uint64)
+        rc1 = _call_ops(ch, "reduce", red, root=0)
+        bc = np.array([rank, rank], dtype=np.uint64)
+        rc2 = _call_ops(ch, "bcast", bc, root=1)
+        send = np.array([rank * 10, rank * 10 + 1], dtype=np.uint64)
+        recv = np.zeros(2 * world, dtype=np.uint64)
+        rc3 = _call_ops(ch, "gather", send, recv)
+        q.put((rank, rc1, rc2, rc3, red.tolist(), bc.tolist(), recv.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_process_group_channel_collectives():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pg_channel_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r[0]: r[1:] for r in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        rc1, rc2, rc3, red, bc, recv = res[r]
+        assert (rc1, rc2, rc3) == (0, 0, 0)
+        assert bc == [1, 1] and recv == [0, 1, 10, 11]
+    assert res[0][3] == [3, 2**41, 14]
