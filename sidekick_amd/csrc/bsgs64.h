@@ -128,6 +128,34 @@ __device__ __forceinline__ uint64_t shift32(uint64_t B) {
     "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
     "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
 
+// half: the C0 carries (P0, P2) on the scalar unit, the C1 carries (P1, P3)
+// per lane into kv — two VALU and four SALU per MAC.  Each v_addc reads its
+// carry >= 2 wait states after the mad that wrote it.
+#define QK_MAC64H(P0, P1, P2, P3, T)                                                                    \
+    "v_mad_u64_u32 %[C0], " P0 ", %[bl], %[a0], %[C0]\n\t"                                             \
+    "v_mad_u64_u32 %[C1], " P1 ", %[bh], %[a0], %[C1]\n\t"                                             \
+    "v_mad_u64_u32 %[C0], " P2 ", %[sl], %[a1], %[C0]\n\t"                                             \
+    "v_mad_u64_u32 %[C1], " P3 ", %[sh], %[a1], %[C1]\n\t"                                             \
+    "s_bcnt1_i32_b64 " T ", " P0 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
+    "v_addc_co_u32_e64 %[kv], " P1 ", %[kv], 0, " P1 "\n\t"                                            \
+    "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
+    "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
+
+template <int SET>
+__device__ __forceinline__ void mac_h(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &kv, uint32_t a0,
+                                      uint32_t a1, uint4 b) {
+    if constexpr (SET == 0)
+        asm volatile(QK_EXPAND(QK_MAC64H, QK_SET0T)
+                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [kv] "+v"(kv)
+                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
+                     : "scc", "s56", QK_CLOB0);
+    else
+        asm volatile(QK_EXPAND(QK_MAC64H, QK_SET1T)
+                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [kv] "+v"(kv)
+                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
+                     : "scc", "s57", QK_CLOB1);
+}
+
 template <int SET>
 __device__ __forceinline__ void mac_m(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &k1, uint32_t &kv,
                                       uint32_t a0, uint32_t a1, uint4 b) {
@@ -207,10 +235,20 @@ __device__ __forceinline__ uint64_t mod_p128(unsigned __int128 v) {
 
 // The workgroup's operands of one tile in LDS, [value][id] so that lanes read
 // consecutive ids: babies (B.lo, B.hi, Bsh.lo, Bsh.hi) and giants (a0, a1).
-template <int NA>
+// BSH: the babies' B * 2^32 are not stored but recomputed by the wave that
+// owns the baby (each baby has one owner, so the VALU work is the same), and
+// the first giant x^8 is not stored twice (it is baby 8) — 32 KB instead of
+// 50 KB per workgroup at t = 80: 5 workgroups per CU instead of 3.
+// NG = giant rows stored.
+template <int NG, bool BSH = false>
 struct Smem {
     uint4 bb[NB][BLOCK];
-    uint2 ga[NA - 1][BLOCK];
+    uint2 ga[NG][BLOCK];
+};
+template <int NG>
+struct Smem<NG, true> {
+    uint2 bb[NB][BLOCK];
+    uint2 ga[NG > 0 ? NG : 1][BLOCK];
 };
 
 // The kernel body.  Tiles of 256 consecutive ids, grid-stride over tiles;
@@ -222,6 +260,8 @@ struct Smem {
 //   MODE 0  the first SG MACs of a wave's tile count all four carries on the
 //           scalar unit, the rest per lane (v_addc)
 //   MODE 1  every MAC: three carries on the scalar unit, one per lane
+//   MODE 3  every MAC: the two C0 carries on the scalar unit, the two C1
+//           carries per lane
 // Writes, per block, partials[(2 m + limb) * gridDim.x + blockIdx.x] for
 // powers m < T (32-bit limbs of canonical lane values summed: < 2^40).
 // ABL (ablations for tools/tune_u64.hip only; the product uses 0): 1 skips
@@ -230,12 +270,21 @@ struct Smem {
 //           base+8NA with giants x^(base+8a), a = 0..NA-1 — every row a MAC
 //           row, no a = 0 row; x^base by square-and-multiply from x^8 over
 //           the uniform exponent base/8 (base a multiple of 8)
-template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false>
+//   BSH     B * 2^32 recomputed by the owner wave in step 3 (see Smem)
+//   LD      giant operands read one row ahead instead of all rows at once
+template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
                                      uint64_t *__restrict__ partials, uint32_t base = 0) {
     static_assert(NA >= 2 && NA <= 10, "giant rows");
+    static_assert(!(BSH && PF) && !(LD && PF), "prefetch form: stored B * 2^32, all rows");
     constexpr int NR = OFF ? NA : NA - 1;        // MAC rows (giants x^8 .. x^(8 NR), or x^base ..)
-    __shared__ Smem<NR + 1> sm;
+    constexpr bool G8 = BSH && !OFF;             // giant row 0 (x^8) read from baby 8
+    constexpr int NG = G8 ? NR - 1 : NR;
+    __shared__ Smem<NG, BSH> sm;
+    auto giant = [&](int r, int j) -> uint2 {
+        if constexpr (G8) return r ? sm.ga[r - 1][j] : sm.bb[NB - 1][j];
+        else return sm.ga[r][j];
+    };
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cb = 2 * wave;                     // this wave's babies (b = cb+1, cb+2)
@@ -262,8 +311,12 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 if (b && ABL != 2) mulv(V, x0, x1);
-                const uint64_t sh = shift32(V);
-                sm.bb[b][tid] = make_uint4((uint32_t)V, (uint32_t)(V >> 32), (uint32_t)sh, (uint32_t)(sh >> 32));
+                if constexpr (BSH) {
+                    sm.bb[b][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
+                } else {
+                    const uint64_t sh = shift32(V);
+                    sm.bb[b][tid] = make_uint4((uint32_t)V, (uint32_t)(V >> 32), (uint32_t)sh, (uint32_t)(sh >> 32));
+                }
             }
             const uint32_t g0 = (uint32_t)V, g1 = (uint32_t)(V >> 32);   // x^8
             if constexpr (OFF) {
@@ -284,11 +337,11 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 }
                 V = r;
             }
-            sm.ga[0][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
+            if constexpr (!G8) sm.ga[0][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
 #pragma unroll
             for (int a = 1; a < NR; ++a) {
                 if (ABL != 2) mulv(V, g0, g1);
-                sm.ga[a][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
+                sm.ga[G8 ? a - 1 : a][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
             }
         }
         __syncthreads();
@@ -325,19 +378,42 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                     for (int r = 0; r < NR; ++r) ng[r] = sm.ga[r][j + 64];
                 }
             } else {
-                bv[0] = sm.bb[cb][j];
-                bv[1] = sm.bb[cb + 1][j];
+                if constexpr (BSH) {
 #pragma unroll
-                for (int r = 0; r < NR; ++r) g[r] = sm.ga[r][j];
+                    for (int c = 0; c < 2; ++c) {
+                        const uint2 B = sm.bb[cb + c][j];
+                        const uint64_t sh = shift32(((uint64_t)B.y << 32) | B.x);
+                        bv[c] = make_uint4(B.x, B.y, (uint32_t)sh, (uint32_t)(sh >> 32));
+                    }
+                } else {
+                    bv[0] = sm.bb[cb][j];
+                    bv[1] = sm.bb[cb + 1][j];
+                }
+                if constexpr (!LD) {
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) g[r] = giant(r, j);
+                }
             }
             if constexpr (!OFF) row2<1>(r0lo, r0hi, bv);
+            // LD: one giant row's operands in flight while the previous row's
+            // MACs run (2 rows live instead of NR: fewer VGPRs)
+            uint2 gn;
+            if constexpr (LD) gn = giant(0, j);
             if (ABL != 1) {
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
+                    if constexpr (LD) {
+                        g[r] = gn;
+                        if (r + 1 < NR) gn = giant(r + 1, j);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
                         const int m = r * 2 + c;   // MAC index in the tile: parity picks the SGPR set
-                        if constexpr (MODE == 1) {
+                        if constexpr (MODE == 3) {
+                            if (m % 2 == 0) mac_h<0>(C0[r][c], C1[r][c], K0[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
+                            else mac_h<1>(C0[r][c], C1[r][c], K0[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
+                        } else if constexpr (MODE == 1) {
                             if (m % 2 == 0) mac_m<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                             else mac_m<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                         } else if (m < SG) {
@@ -358,7 +434,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     // the tile operands are dead after the loop's last barrier: the reduction
     // reuses their LDS (a separate array pushes the offset pass with NA = 10
     // past 1/3 of the CU's LDS, i.e. to 2 workgroups per CU)
-    static_assert(sizeof(Smem<NR + 1>) >= 2 * NB * NA * sizeof(unsigned long long), "reduction space");
+    static_assert(sizeof(Smem<NG, BSH>) >= 2 * NB * NA * sizeof(unsigned long long), "reduction space");
     unsigned long long *red = reinterpret_cast<unsigned long long *>(&sm);
     for (int i = tid; i < 2 * NB * NA; i += BLOCK) red[i] = 0;
     __syncthreads();
@@ -385,10 +461,11 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             const int m = r * 2 + c;
             unsigned __int128 v = (unsigned __int128)C0[r][c] + ((unsigned __int128)C1[r][c] << 32);
             // scalar counts are the wave's totals: added once, by lane 0
-            const bool s0 = MODE == 1 || m < SG, s1 = MODE == 0 && m < SG;
+            const bool s0 = MODE != 0 || m < SG, s1 = MODE == 0 && m < SG;
             const uint32_t k0 = s0 ? (lane == 0 ? K0[r][c] : 0u) : K0[r][c];
             uint64_t k1 = s1 ? (lane == 0 ? K1[r][c] : 0u) : K1[r][c];
             if (MODE == 1) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];
+            if (MODE == 3) k1 = KV[r][c];
             v += (unsigned __int128)k0 * C64 + (unsigned __int128)k1 * W1;
             put((r + (OFF ? 0 : 1)) * NB + cb + c, mod_p128(v));
         }

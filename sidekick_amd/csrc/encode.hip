@@ -587,25 +587,28 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restri
 }
 
 // u64 baby-step / giant-step (bsgs64.h): 256-id tiles, babies and giants
-// shared through LDS, the MAC powers split over the 4 waves.  50 KB of LDS
-// per workgroup: 3 per CU.
-template <int NA, int MODE, int SG>
-__global__ __launch_bounds__(bsgs64::BLOCK, 3) void k_encode_u64_bsgs(const uint64_t *__restrict__ ids, uint64_t n,
+// shared through LDS, the MAC powers split over the 4 waves.  The babies'
+// B * 2^32 are recomputed by their owner wave instead of stored (BSH) and x^8
+// is read from baby 8: 32 KB of LDS per workgroup at t = 80, 4 per CU
+// (tools/tune_u64.hip: 24.1 vs 25.6 ms per 1e9 ids with 50 KB at 3 per CU).
+// The first SG MACs of a wave's tile count their carries on the scalar unit.
+template <int NA, int SG>
+__global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs(const uint64_t *__restrict__ ids, uint64_t n,
                                                                       uint32_t head, uint32_t T,
                                                                       uint64_t *__restrict__ partials) {
     (void)head;
-    bsgs64::body<NA, MODE, SG>(ids, n, T, partials);
+    bsgs64::body<NA, 0, SG, 0, 0, false, true, 1>(ids, n, T, partials);
 }
 
 // Offset pass for u64 thresholds > 80: powers base+1 .. base+8NA with giants
 // x^(base + 8a) (bsgs64.h OFF); the ids are read once per pass.
 template <int NA>
-__global__ __launch_bounds__(bsgs64::BLOCK, 3) void k_encode_u64_bsgs_off(const uint64_t *__restrict__ ids,
+__global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_off(const uint64_t *__restrict__ ids,
                                                                           uint64_t n, uint32_t head, uint32_t T,
                                                                           uint32_t base,
                                                                           uint64_t *__restrict__ partials) {
     (void)head;
-    bsgs64::body<NA, 1, 0, 0, 0, true>(ids, n, T, partials, base);
+    bsgs64::body<NA, 0, 16, 0, 0, true, true, 1>(ids, n, T, partials, base);
 }
 
 // ------------------------------------------------------------- dispatch
@@ -801,7 +804,7 @@ static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t hea
                         int acc, hipStream_t s) {
     uint64_t *meta = out + 2 * T;
     {   // pass 0: powers 1..80
-        auto kern = k_encode_u64_bsgs<10, 1, 0>;
+        auto kern = k_encode_u64_bsgs<10, 16>;
         const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
         if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 80 * sizeof(uint64_t), s)) return rc;
         uint64_t *partials = (uint64_t *)ctx->d_scratch;
@@ -1021,24 +1024,23 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     const int no64 = ctx->knobs.bsgs64_off;
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     if (T >= 21 && T <= 80 && !no64 && n / min_grid64 < (1ull << 30)) {
-#define QK_BSGS64(NA_, MODE_, SG_)                                                                    \
-    run_encode<uint64_t>(ctx, k_encode_u64_bsgs<NA_, MODE_, SG_>, k_finalize_u64, 8 * NA_, 2, ids, n, head, T, \
+#define QK_BSGS64(NA_, SG_)                                                                           \
+    run_encode<uint64_t>(ctx, k_encode_u64_bsgs<NA_, SG_>, k_finalize_u64, 8 * NA_, 2, ids, n, head, T,     \
                          (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
-        switch ((T + 7) / 8) {
-        case 3: return QK_BSGS64(3, 1, 0);
-        case 4: return QK_BSGS64(4, 1, 0);
-        case 5: return QK_BSGS64(5, 1, 0);
-        case 6: return QK_BSGS64(6, 1, 0);
-        case 7: return QK_BSGS64(7, 1, 0);
-        case 8: return QK_BSGS64(8, 1, 0);
-        case 9: return QK_BSGS64(9, 1, 0);
+        switch ((T + 7) / 8) {   // NA <= 9: a wave's <= 16 MACs all scalar-counted
+        case 3: return QK_BSGS64(3, 16);
+        case 4: return QK_BSGS64(4, 16);
+        case 5: return QK_BSGS64(5, 16);
+        case 6: return QK_BSGS64(6, 16);
+        case 7: return QK_BSGS64(7, 16);
+        case 8: return QK_BSGS64(8, 16);
+        case 9: return QK_BSGS64(9, 16);
         default:
-            switch (sg64) {
-            case 0: return QK_BSGS64(10, 0, 0);
-            case 8: return QK_BSGS64(10, 0, 8);
-            case 12: return QK_BSGS64(10, 0, 12);
-            case 18: return QK_BSGS64(10, 0, 18);
-            default: return QK_BSGS64(10, 1, 0);   // 3 scalar + 1 lane carry per MAC (sg64 = -1, the default)
+            switch (sg64) {   // knob bsgs64_sg (measurements): scalar-counted MACs of the 18
+            case 8: return QK_BSGS64(10, 8);
+            case 12: return QK_BSGS64(10, 12);
+            case 18: return QK_BSGS64(10, 18);
+            default: return QK_BSGS64(10, 16);   // sg64 = -1, the default
             }
         }
 #undef QK_BSGS64

@@ -28,12 +28,12 @@ __global__ void k_fill(uint64_t *out, uint64_t n, uint64_t seed) {
         out[i] = splitmix_mix(seed + (i + 1) * GAMMA);
 }
 
-template <int NA, int MODE, int SG, int ABL, int OCC, int PF = 0>
+template <int NA, int MODE, int SG, int ABL, int OCC, int PF = 0, bool BSH = false, int LD = 0>
 __global__ __launch_bounds__(256, OCC) void k_var(const uint64_t *ids, uint64_t n, uint32_t T, uint64_t *partials,
                                                   uint64_t *clk) {
     uint64_t t0 = 0, r0 = 0;
     if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
-    bsgs64::body<NA, MODE, SG, ABL, PF>(ids, n, T, partials);
+    bsgs64::body<NA, MODE, SG, ABL, PF, false, BSH, LD>(ids, n, T, partials);
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
         clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
@@ -44,6 +44,7 @@ struct Var {
     const char *name;
     void (*fn)(const uint64_t *, uint64_t, uint32_t, uint64_t *, uint64_t *);
     int occ;
+    int abl = 0;   // ablation: results not compared
 };
 
 int main() {
@@ -56,23 +57,23 @@ int main() {
     int cus = 0;
     CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     std::vector<Var> vars = {
-        {"mode1 (3 scalar + 1 lane carry)", k_var<10, 1, 0, 0, 3>, 3},
-        {"mode0 sg8", k_var<10, 0, 8, 0, 3>, 3},
-        {"mode0 sg18 (all scalar)", k_var<10, 0, 18, 0, 3>, 3},
-        {"mode0 sg12", k_var<10, 0, 12, 0, 3>, 3},
-        {"mode0 sg0 (all lane)", k_var<10, 0, 0, 0, 3>, 3},
-        {"mode1 occ2", k_var<10, 1, 0, 0, 2>, 2},
-        {"mode1 prefetch", k_var<10, 1, 0, 0, 3, 1>, 3},
-        {"mode0 sg18 prefetch", k_var<10, 0, 18, 0, 3, 1>, 3},
-        {"mode0 sg12 prefetch", k_var<10, 0, 12, 0, 3, 1>, 3},
-        {"mode1 prefetch occ2", k_var<10, 1, 0, 0, 2, 1>, 2},
-        {"ablate: no MACs", k_var<10, 1, 0, 1, 3>, 3},
-        {"ablate: no modmuls", k_var<10, 1, 0, 2, 3>, 3},
+        {"mode1 occ3 (product before)", k_var<10, 1, 0, 0, 3>, 3},
+        {"mode0 sg16 bsh occ4 ld", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
+        {"mode0 sg14 bsh occ4 ld", k_var<10, 0, 14, 0, 4, 0, true, 1>, 4},
+        {"mode0 sg15 bsh occ4 ld", k_var<10, 0, 15, 0, 4, 0, true, 1>, 4},
+        {"mode0 sg17 bsh occ4 ld", k_var<10, 0, 17, 0, 4, 0, true, 1>, 4},
+        {"mode0 sg18 bsh occ4 ld", k_var<10, 0, 18, 0, 4, 0, true, 1>, 4},
+        {"mode0 sg16 bsh occ3 ld", k_var<10, 0, 16, 0, 3, 0, true, 1>, 3},
+        {"mode0 sg12 bsh occ3 ld", k_var<10, 0, 12, 0, 3, 0, true, 1>, 3},
+        {"mode0 sg16 bsh occ4", k_var<10, 0, 16, 0, 4, 0, true>, 4},
+        {"mode0 sg8 occ3 (old layout)", k_var<10, 0, 8, 0, 3>, 3},
     };
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
     std::vector<double> best(vars.size(), 1e30), ghz(vars.size(), 0);
+    std::vector<uint64_t> ref;
+    std::vector<bool> ok(vars.size(), true);
     for (int round = 0; round < 4; ++round) {
         for (size_t v = 0; v < vars.size(); ++v) {
             const uint32_t grid = cus * vars[v].occ;
@@ -82,6 +83,22 @@ int main() {
             CHK(hipEventSynchronize(b));
             float ms = 0;
             CHK(hipEventElapsedTime(&ms, a, b));
+            {   // per power: (sum of lo limbs, sum of hi limbs) over the blocks, folded mod p
+                std::vector<uint64_t> pp((size_t)2 * 80 * grid);
+                CHK(hipMemcpy(pp.data(), part, pp.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<uint64_t> sums(80);
+                for (int m = 0; m < 80; ++m) {
+                    unsigned __int128 lo = 0, hi = 0;
+                    for (uint32_t b = 0; b < grid; ++b) {
+                        lo += pp[(size_t)(2 * m) * grid + b];
+                        hi += pp[(size_t)(2 * m + 1) * grid + b];
+                    }
+                    const unsigned __int128 P = (unsigned __int128)0xFFFFFFFFFFFFFFC5ull;
+                    sums[m] = (uint64_t)(((lo % P) + ((hi % P) << 32) % P) % P);
+                }
+                if (v == 0 && round == 0) ref = sums;
+                if (vars[v].abl == 0 && sums != ref) ok[v] = false;
+            }
             std::vector<uint64_t> h(2 * grid);
             CHK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
             double c = 0, r = 0;
@@ -91,8 +108,9 @@ int main() {
     }
     printf("{\"n\": %llu, \"t\": 80, \"variants\": [", (unsigned long long)n);
     for (size_t v = 0; v < vars.size(); ++v)
-        printf("%s{\"name\": \"%s\", \"ms\": %.3f, \"ids_per_s\": %.4g, \"shader_ghz\": %.3f}", v ? ", " : "",
-               vars[v].name, best[v], n / (best[v] * 1e-3), ghz[v]);
+        printf("%s{\"name\": \"%s\", \"ms\": %.3f, \"ids_per_s\": %.4g, \"shader_ghz\": %.3f, \"bit_exact\": %s}",
+               v ? ", " : "", vars[v].name, best[v], n / (best[v] * 1e-3), ghz[v],
+               vars[v].abl ? "null" : ok[v] ? "true" : "false");
     printf("]}\n");
     return 0;
 }
