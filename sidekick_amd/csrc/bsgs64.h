@@ -19,13 +19,14 @@
 // so the powers are split over the 4 waves of a workgroup and the babies and
 // giants of an id are computed ONCE and shared through LDS:
 //   step 1  each thread takes one id of the 256-id tile: 7 baby and NA - 2
-//           giant modmuls (exact, hand-scheduled p64 step), Bsh per baby,
-//           and writes (B, Bsh) per baby and A per giant to LDS
-//   step 3  wave w takes babies 2w+1, 2w+2: their a = 0 row (S_b += B_b)
-//           and their MACs with every giant, over all 256 ids of the tile
-//           (4 per lane), reading the operands from LDS
-// LDS: 256 ids x (8 x 16 B + 9 x 8 B) = 50 KB per workgroup, 3 workgroups
-// per CU.  Integer-VALU (+SALU) bound; the ids are read once (8 B each).
+//           giant modmuls (exact, hand-scheduled p64 step), and writes B per
+//           baby and A per giant (x^8 = baby 8 is not stored twice) to LDS
+//   step 3  wave w takes babies 2w+1, 2w+2: computes their Bsh, runs their
+//           a = 0 row (S_b += B_b) and their MACs with every giant, over all
+//           256 ids of the tile (4 per lane), reading the operands from LDS
+// LDS: 256 ids x (8 + 8) x 8 B = 32 KB per workgroup at t = 80, 4 workgroups
+// per CU (the product form, BSH; storing Bsh too takes 50 KB, 3 per CU, and
+// measured 6 % slower).  Integer-VALU (+SALU) bound; the ids are read once.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -127,34 +128,6 @@ __device__ __forceinline__ uint64_t shift32(uint64_t B) {
     "s_bcnt1_i32_b64 " T ", " P1 "\n\ts_add_u32 %[k1], %[k1], " T "\n\t"                                \
     "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
     "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
-
-// half: the C0 carries (P0, P2) on the scalar unit, the C1 carries (P1, P3)
-// per lane into kv — two VALU and four SALU per MAC.  Each v_addc reads its
-// carry >= 2 wait states after the mad that wrote it.
-#define QK_MAC64H(P0, P1, P2, P3, T)                                                                    \
-    "v_mad_u64_u32 %[C0], " P0 ", %[bl], %[a0], %[C0]\n\t"                                             \
-    "v_mad_u64_u32 %[C1], " P1 ", %[bh], %[a0], %[C1]\n\t"                                             \
-    "v_mad_u64_u32 %[C0], " P2 ", %[sl], %[a1], %[C0]\n\t"                                             \
-    "v_mad_u64_u32 %[C1], " P3 ", %[sh], %[a1], %[C1]\n\t"                                             \
-    "s_bcnt1_i32_b64 " T ", " P0 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
-    "v_addc_co_u32_e64 %[kv], " P1 ", %[kv], 0, " P1 "\n\t"                                            \
-    "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
-    "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
-
-template <int SET>
-__device__ __forceinline__ void mac_h(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &kv, uint32_t a0,
-                                      uint32_t a1, uint4 b) {
-    if constexpr (SET == 0)
-        asm volatile(QK_EXPAND(QK_MAC64H, QK_SET0T)
-                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [kv] "+v"(kv)
-                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
-                     : "scc", "s56", QK_CLOB0);
-    else
-        asm volatile(QK_EXPAND(QK_MAC64H, QK_SET1T)
-                     : [C0] "+v"(C0), [C1] "+v"(C1), [k0] "+s"(k0), [kv] "+v"(kv)
-                     : [a0] "v"(a0), [a1] "v"(a1), [bl] "v"(b.x), [bh] "v"(b.y), [sl] "v"(b.z), [sh] "v"(b.w)
-                     : "scc", "s57", QK_CLOB1);
-}
 
 template <int SET>
 __device__ __forceinline__ void mac_m(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &k1, uint32_t &kv,
@@ -260,8 +233,6 @@ struct Smem<NG, true> {
 //   MODE 0  the first SG MACs of a wave's tile count all four carries on the
 //           scalar unit, the rest per lane (v_addc)
 //   MODE 1  every MAC: three carries on the scalar unit, one per lane
-//   MODE 3  every MAC: the two C0 carries on the scalar unit, the two C1
-//           carries per lane
 // Writes, per block, partials[(2 m + limb) * gridDim.x + blockIdx.x] for
 // powers m < T (32-bit limbs of canonical lane values summed: < 2^40).
 // ABL (ablations for tools/tune_u64.hip only; the product uses 0): 1 skips
@@ -410,10 +381,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
                         const int m = r * 2 + c;   // MAC index in the tile: parity picks the SGPR set
-                        if constexpr (MODE == 3) {
-                            if (m % 2 == 0) mac_h<0>(C0[r][c], C1[r][c], K0[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
-                            else mac_h<1>(C0[r][c], C1[r][c], K0[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
-                        } else if constexpr (MODE == 1) {
+                        if constexpr (MODE == 1) {
                             if (m % 2 == 0) mac_m<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                             else mac_m<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                         } else if (m < SG) {
@@ -461,11 +429,10 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             const int m = r * 2 + c;
             unsigned __int128 v = (unsigned __int128)C0[r][c] + ((unsigned __int128)C1[r][c] << 32);
             // scalar counts are the wave's totals: added once, by lane 0
-            const bool s0 = MODE != 0 || m < SG, s1 = MODE == 0 && m < SG;
+            const bool s0 = MODE == 1 || m < SG, s1 = MODE == 0 && m < SG;
             const uint32_t k0 = s0 ? (lane == 0 ? K0[r][c] : 0u) : K0[r][c];
             uint64_t k1 = s1 ? (lane == 0 ? K1[r][c] : 0u) : K1[r][c];
             if (MODE == 1) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];
-            if (MODE == 3) k1 = KV[r][c];
             v += (unsigned __int128)k0 * C64 + (unsigned __int128)k1 * W1;
             put((r + (OFF ? 0 : 1)) * NB + cb + c, mod_p128(v));
         }

@@ -57,16 +57,18 @@ int main() {
     int cus = 0;
     CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     std::vector<Var> vars = {
-        {"mode1 occ3 (product before)", k_var<10, 1, 0, 0, 3>, 3},
-        {"mode0 sg16 bsh occ4 ld", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
-        {"mode0 sg14 bsh occ4 ld", k_var<10, 0, 14, 0, 4, 0, true, 1>, 4},
+        {"product: mode0 sg16, B*2^32 recomputed, occ4, row-ahead giants", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
+        {"mode0 sg16 bsh occ4 (all giant rows loaded at once)", k_var<10, 0, 16, 0, 4, 0, true, 0>, 4},
+        {"mode0 sg12 bsh occ4 ld", k_var<10, 0, 12, 0, 4, 0, true, 1>, 4},
         {"mode0 sg15 bsh occ4 ld", k_var<10, 0, 15, 0, 4, 0, true, 1>, 4},
-        {"mode0 sg17 bsh occ4 ld", k_var<10, 0, 17, 0, 4, 0, true, 1>, 4},
         {"mode0 sg18 bsh occ4 ld", k_var<10, 0, 18, 0, 4, 0, true, 1>, 4},
         {"mode0 sg16 bsh occ3 ld", k_var<10, 0, 16, 0, 3, 0, true, 1>, 3},
-        {"mode0 sg12 bsh occ3 ld", k_var<10, 0, 12, 0, 3, 0, true, 1>, 3},
-        {"mode0 sg16 bsh occ4", k_var<10, 0, 16, 0, 4, 0, true>, 4},
-        {"mode0 sg8 occ3 (old layout)", k_var<10, 0, 8, 0, 3>, 3},
+        {"mode1 bsh occ3", k_var<10, 1, 0, 0, 3, 0, true>, 3},
+        {"round 2: mode1, B*2^32 in LDS (50 KB), occ3", k_var<10, 1, 0, 0, 3>, 3},
+        {"round 2 layout: mode0 sg8 occ3", k_var<10, 0, 8, 0, 3>, 3},
+        {"round 2 layout: mode0 sg12 prefetch occ3", k_var<10, 0, 12, 0, 3, 1>, 3},
+        {"ablate: no MACs (product)", k_var<10, 0, 16, 1, 4, 0, true, 1>, 4, 1},
+        {"ablate: no modmuls (product)", k_var<10, 0, 16, 2, 4, 0, true, 1>, 4, 2},
     };
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
