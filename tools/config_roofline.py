@@ -28,7 +28,7 @@ import sys
 PEAK_GBPS = 8000.0
 # (kernel name prefix, grid size of the config's launch, units, bytes per unit, config)
 # (kernel name prefix, grid, units, bytes per unit, config, issue_roofline.json key)
-ROWS = [("void qk::k_encode_u64_bsgs<10, 1, 0>", "196608", 1_000_000_000, 8,
+ROWS = [("void qk::k_encode_u64_bsgs<10, 16>", "262144", 1_000_000_000, 8,
          "configs[2]: encode 1e9 u64 ids, t=80", "encode_u64_t80"),
         ("void qk::k_root_scan<unsigned int, 1>", "524288", 100_000_000, 4,
          "configs[4]: root test of 1e8 u32 candidates, d=32 — root-set scan (the default)", "root_scan_u32_d32"),

@@ -59,8 +59,8 @@ KERNELS = {
     "encode_u32_t32": ("encode.s", "_ZN2qk17k_encode_u32_bsgsILi8ELi4ELi8E", "profiles/r03/encode_pmc_sq.csv",
                        "k_encode_u32_bsgs<8, 4, 8>", "327680", 1e9, 256,
                        "configs[1]: encode 1e9 u32 ids, t=32 (the bench line)"),
-    "encode_u64_t80": ("encode.s", "_ZN2qk17k_encode_u64_bsgsILi10ELi1ELi0E", "profiles/r03/configs_pmc_sq.csv",
-                       "k_encode_u64_bsgs<10, 1, 0>", "196608", 1e9, 64,
+    "encode_u64_t80": ("encode.s", "_ZN2qk17k_encode_u64_bsgsILi10ELi16E", "profiles/r03/configs_pmc_sq.csv",
+                       "k_encode_u64_bsgs<10, 16>", "262144", 1e9, 64,
                        "configs[2]: encode 1e9 u64 ids, t=80"),
     "root_scan_u32_d32": ("decode.s", "_ZN2qk11k_root_scanIjLi1E", "profiles/r03/configs_pmc_sq.csv",
                           "k_root_scan<unsigned int, 1>", "524288", 1e8, 512,
