@@ -211,7 +211,7 @@ __device__ __forceinline__ uint64_t mod_p128(unsigned __int128 v) {
 // BSH: the babies' B * 2^32 are not stored but recomputed by the wave that
 // owns the baby (each baby has one owner, so the VALU work is the same), and
 // the first giant x^8 is not stored twice (it is baby 8) — 32 KB instead of
-// 50 KB per workgroup at t = 80: 5 workgroups per CU instead of 3.
+// 50 KB per workgroup at t = 80: 4 workgroups per CU instead of 3.
 // NG = giant rows stored.
 template <int NG, bool BSH = false>
 struct Smem {
