@@ -229,10 +229,15 @@ __device__ __forceinline__ void row2m(uint64_t &a0, uint64_t &a1, uint32_t b0, u
 //          giants are x^(base + a*NB) for a = 0..NA-1 with a runtime base
 //          (a multiple of NB), so every row is a MAC row (no a = 0 sum row)
 //          and the pass yields powers base+1 .. base+NB*NA
-template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false, bool OFF_ = false>
+//  XC      offset passes: bit 0 — x^base per id read from the previous pass's
+//          cache instead of square-and-multiply; bit 1 — x^(base + NB*NA)
+//          written for the next pass (one more product per id)
+template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false, bool OFF_ = false,
+          int XC_ = 0>
 struct Cfg {
-    static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_;
+    static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_, XC = XC_;
     static constexpr bool PAIR = PAIR_, OFF = OFF_;
+    static_assert(!XC_ || OFF_, "the x^base cache is for offset passes");
     static constexpr int ROWS = OFF_ ? NA_ : NA_ - 1;   // MAC rows
     static constexpr int ROW1 = OFF_ ? 0 : 1;           // group-row number of the first MAC row
     static_assert(NB % 2 == 0 && NA >= 2, "NB even, NA >= 2");
@@ -276,7 +281,7 @@ __device__ __forceinline__ uint32_t pow_uniform(uint32_t xn, uint32_t q, MUL mul
 // caller then recomputes exactly).  OFF: A[a] = x^(base + a*NB).
 template <class C>
 __device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], uint32_t (&A)[C::ROWS],
-                                           uint32_t base = 0) {
+                                           uint32_t base = 0, uint32_t xb = 0, uint32_t *xnext = nullptr) {
     constexpr int NB = C::NB, NA = C::NA;
     B[0] = id;
     if constexpr (C::OFF) {
@@ -284,9 +289,11 @@ __device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], ui
 #pragma unroll
         for (int b = 1; b < NB; ++b) B[b] = mulfold32_min(B[b - 1], B[0], mn);
         const uint32_t xn = B[NB - 1];                                   // x^NB (B[b] = x^(b+1))
-        A[0] = pow_uniform(xn, base / NB, [&](uint32_t u, uint32_t v) { return mulfold32_min(u, v, mn); });
+        if constexpr (C::XC & 1) A[0] = xb;
+        else A[0] = pow_uniform(xn, base / NB, [&](uint32_t u, uint32_t v) { return mulfold32_min(u, v, mn); });
 #pragma unroll
         for (int a = 1; a < NA; ++a) A[a] = mulfold32_min(A[a - 1], xn, mn);
+        if constexpr ((C::XC & 2) != 0) *xnext = mulfold32_min(A[NA - 1], xn, mn);
         return mn < 25u;
     } else if constexpr (C::FOLD == 0) {
         uint32_t wrapped = 0;
@@ -307,14 +314,17 @@ __device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], ui
     }
 }
 template <class C>
-__device__ __forceinline__ void powers_exact(uint32_t (&B)[C::NB], uint32_t (&A)[C::ROWS], uint32_t base = 0) {
+__device__ __forceinline__ void powers_exact(uint32_t (&B)[C::NB], uint32_t (&A)[C::ROWS], uint32_t base = 0,
+                                             uint32_t xb = 0, uint32_t *xnext = nullptr) {
 #pragma unroll
     for (int b = 1; b < C::NB; ++b) B[b] = mulfold32_exact(B[b - 1], B[0]);
     if constexpr (C::OFF) {
         const uint32_t xn = B[C::NB - 1];
-        A[0] = pow_uniform(xn, base / C::NB, [](uint32_t u, uint32_t v) { return mulfold32_exact(u, v); });
+        if constexpr (C::XC & 1) A[0] = xb;
+        else A[0] = pow_uniform(xn, base / C::NB, [](uint32_t u, uint32_t v) { return mulfold32_exact(u, v); });
 #pragma unroll
         for (int a = 1; a < C::NA; ++a) A[a] = mulfold32_exact(A[a - 1], xn);
+        if constexpr ((C::XC & 2) != 0) *xnext = mulfold32_exact(A[C::NA - 1], xn);
         return;
     }
     A[0] = B[C::NB - 1];
@@ -381,12 +391,14 @@ __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA, C::ROWS> &S, const 
     }
 }
 
+// xb / xnext: an offset pass's cached x^base and the next pass's (Cfg XC)
 template <class C>
-__device__ __forceinline__ void one(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id, uint32_t base = 0) {
+__device__ __forceinline__ void one(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id, uint32_t base = 0, uint32_t xb = 0,
+                                    uint32_t *xnext = nullptr) {
     uint32_t B[C::NB], A[C::ROWS];
-    const uint32_t w = powers<C>(id, B, A, base);
+    const uint32_t w = powers<C>(id, B, A, base, xb, xnext);
     if (__builtin_expect(__any(w), 0)) {
-        if (w) powers_exact<C>(B, A, base);
+        if (w) powers_exact<C>(B, A, base, xb, xnext);
     }
     accumulate<C>(S, B, A);
 }
@@ -408,15 +420,18 @@ __device__ __forceinline__ void two(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id0,
 }
 
 template <class C>
-__device__ __forceinline__ void four(Acc<C::NB, C::NA, C::ROWS> &S, uint4 w, uint32_t base) {
+__device__ __forceinline__ void four(Acc<C::NB, C::NA, C::ROWS> &S, uint4 w, uint32_t base,
+                                     uint4 xb = make_uint4(0, 0, 0, 0), uint4 *xn = nullptr) {
     if constexpr (C::PAIR) {
         two<C>(S, w.x, w.y);
         two<C>(S, w.z, w.w);
     } else {
-        one<C>(S, w.x, base);
-        one<C>(S, w.y, base);
-        one<C>(S, w.z, base);
-        one<C>(S, w.w, base);
+        uint4 t = make_uint4(0, 0, 0, 0);
+        one<C>(S, w.x, base, xb.x, &t.x);
+        one<C>(S, w.y, base, xb.y, &t.y);
+        one<C>(S, w.z, base, xb.z, &t.z);
+        one<C>(S, w.w, base, xb.w, &t.w);
+        if constexpr ((C::XC & 2) != 0) *xn = t;
     }
 }
 
@@ -486,9 +501,14 @@ __device__ __forceinline__ void clear(Acc<C::NB, C::NA, C::ROWS> &S) {
     }
 }
 
+// XC (offset passes): xin / xout are per-id arrays indexed like ids whose
+// address is congruent to ids' modulo 16 (the same 16-byte groups).
 template <class C, class Out>
 __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
-                                         uint64_t gtid, uint64_t nthr, Out out, uint32_t base = 0) {
+                                         uint64_t gtid, uint64_t nthr, Out out, uint32_t base = 0,
+                                         const uint32_t *__restrict__ xin = nullptr,
+                                         uint32_t *__restrict__ xout = nullptr) {
+    constexpr bool XI = (C::XC & 1) != 0, XO = (C::XC & 2) != 0;
     Acc<C::NB, C::NA, C::ROWS> S;
     clear<C>(S);
     const uint64_t h = head < n ? head : n;
@@ -498,25 +518,56 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
     const uint32_t tmax = (uint32_t)__builtin_amdgcn_readfirstlane(iters);           // lane 0: most trips
     const uint32_t tmin = (uint32_t)__builtin_amdgcn_readlane((int)iters, 63);       // lane 63: fewest
     const uint4 *__restrict__ p = v + gtid;
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (iters) nxt = *p;
+    const uint4 *__restrict__ pc = XI ? reinterpret_cast<const uint4 *>(xin + h) + gtid : nullptr;
+    uint4 *__restrict__ po = XO ? reinterpret_cast<uint4 *>(xout + h) + gtid : nullptr;
+    uint4 nxt = make_uint4(0, 0, 0, 0), nxc = make_uint4(0, 0, 0, 0), xo = make_uint4(0, 0, 0, 0);
+    if (iters) {
+        nxt = *p;
+        if constexpr (XI) nxc = *pc;
+    }
     uint32_t it = 0;
     for (; it + 1 < tmin; ++it) {
-        const uint4 w = nxt;
+        const uint4 w = nxt, c = nxc;
         p += nthr;
         nxt = *p;
-        four<C>(S, w, base);
+        if constexpr (XI) {
+            pc += nthr;
+            nxc = *pc;
+        }
+        four<C>(S, w, base, c, &xo);
+        if constexpr (XO) {
+            *po = xo;
+            po += nthr;
+        }
     }
     for (; it < tmax; ++it) {
-        const uint4 w = nxt;
+        const uint4 w = nxt, c = nxc;
         p += nthr;
         nxt = make_uint4(0, 0, 0, 0);
         if (it + 1 < iters) nxt = *p;
-        four<C>(S, w, base);
+        if constexpr (XI) {
+            pc += nthr;
+            if (it + 1 < iters) nxc = *pc;
+        }
+        four<C>(S, w, base, c, &xo);
+        if constexpr (XO) {
+            if (it < iters) *po = xo;
+            po += nthr;
+        }
     }
     const uint64_t tail0 = h + (nbody << 2);
-    one<C>(S, gtid < h ? ids[gtid] : 0u, base);
-    one<C>(S, gtid < n - tail0 ? ids[tail0 + gtid] : 0u, base);
+    {
+        const bool in = gtid < h;
+        uint32_t xn = 0;
+        one<C>(S, in ? ids[gtid] : 0u, base, XI && in ? xin[gtid] : 0u, &xn);
+        if (XO && in) xout[gtid] = xn;
+    }
+    {
+        const bool in = gtid < n - tail0;
+        uint32_t xn = 0;
+        one<C>(S, in ? ids[tail0 + gtid] : 0u, base, XI && in ? xin[tail0 + gtid] : 0u, &xn);
+        if (XO && in) xout[tail0 + gtid] = xn;
+    }
 
     finish<C>(S, T, out);
 }
@@ -525,10 +576,11 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
 // stored [power][block]
 template <class C>
 __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
-                                     uint64_t *__restrict__ partials, uint32_t base = 0) {
+                                     uint64_t *__restrict__ partials, uint32_t base = 0,
+                                     const uint32_t *__restrict__ xin = nullptr, uint32_t *__restrict__ xout = nullptr) {
     body_gen<C>(
         ids, n, head, T, (uint64_t)blockIdx.x * BLOCK + threadIdx.x, (uint64_t)gridDim.x * BLOCK,
-        [=](uint32_t m, uint64_t s) { partials[(size_t)m * gridDim.x + blockIdx.x] = s; }, base);
+        [=](uint32_t m, uint64_t s) { partials[(size_t)m * gridDim.x + blockIdx.x] = s; }, base, xin, xout);
 }
 
 } // namespace bsgs

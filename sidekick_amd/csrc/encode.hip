@@ -165,11 +165,13 @@ __global__ __launch_bounds__(64) void k_mfma32_fix(const uint64_t *__restrict__ 
 
 // Offset pass for thresholds > 80 (several passes over the ids): powers
 // base+1 .. base+8*NA with giants x^(base + 8a), a = 0..NA-1 (bsgs.h OFF).
-template <int NA, int SG>
+// XC: x^base from the previous pass's per-id cache (bit 0) / x^(base + 8 NA)
+// to the next pass's (bit 1) instead of square-and-multiply per pass.
+template <int NA, int SG, int XC = 0>
 __global__ __launch_bounds__(BLOCK, (NA > 6 ? 2 : NA > 5 ? 3 : 4)) void k_encode_u32_bsgs_off(
     const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T, uint32_t base,
-    uint64_t *__restrict__ partials) {
-    bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true>>(ids, n, head, T, partials, base);
+    uint64_t *__restrict__ partials, const uint32_t *__restrict__ xin, uint32_t *__restrict__ xout) {
+    bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true, XC>>(ids, n, head, T, partials, base, xin, xout);
 }
 
 // lane j of a G-group: start = x^(j+1), step = x^G (square-and-multiply).
@@ -657,17 +659,20 @@ int launch_finalize_powers_u32(const uint64_t *partials, uint32_t nblocks, uint3
 // kernel (powers 1..80), each further pass the offset kernel with giants
 // from x^base (the ids are read once per pass; HBM has the bandwidth, the
 // passes are integer-issue bound like the single-pass kernels).
+// xcache (offset passes): the per-id x^base cache (xin / xout), placed in
+// the scratch after the partials (run_pass32_cached sizes the scratch once)
 template <bool OFF, class KernelT>
 static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_ids, size_t n,
                     uint32_t head, uint32_t Tp, uint32_t base, uint64_t *out, uint64_t *meta, int acc,
-                    hipStream_t s) {
+                    hipStream_t s, const uint32_t *xin = nullptr, uint32_t *xout = nullptr) {
     const uint32_t nb = grid_for(ctx, kern, (n + 3) / 4, BLOCK);
     if (int rc = ensure_scratch(ctx, (size_t)nb * GK * sizeof(uint64_t), s)) return rc;
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
     if (int rc = scratch_acquire(ctx, s)) return rc;
     hipEvent_t e0 = prof_begin(ctx, s);
     if constexpr (OFF)
-        hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, base, partials);
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, base, partials, xin,
+                           xout);
     else
         hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, partials);
     prof_end(ctx, s, e0);
@@ -761,16 +766,51 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
     // <= 48 powers with the offset (8,6) kernel (142 VGPRs, 3 waves/SIMD;
     // every row of an offset pass is a MAC row: the 80-power form spills, a
     // 64-power (8,8) form at 2 waves/SIMD measured the same as 48)
-    for (uint32_t base = 0; base < T;) {
+    //
+    // With two or more offset passes, each pass hands x^(next base) to the
+    // next one through a per-id cache (4 B per id read + 4 B written per
+    // pass) instead of every pass raising x^8 to base/8 (~5-8 of its ~22
+    // modmuls per id).  The cache lives in the scratch after the partials,
+    // sized once for every pass (a regrow between passes would drop it), with
+    // the ids' address modulo 16 so that both are read in the same 16-byte
+    // groups; knob u32_xcache = 0 keeps the square-and-multiply form.
+    const uint32_t npass = T <= 80 ? 0 : (T - 80 + 47) / 48;   // offset passes
+    uint32_t *xc = nullptr;
+    if (npass >= 2 && ctx->knobs.u32_xcache) {
+        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u32_bsgs<8, 10, 16>, (n + 3) / 4, BLOCK),
+                                         grid_for(ctx, k_encode_u32_bsgs_off<6, 12, 3>, (n + 3) / 4, BLOCK),
+                                         grid_for(ctx, k_encode_u32_bsgs_off<5, 10, 1>, (n + 3) / 4, BLOCK)});
+        const size_t poff = ((size_t)nbmax * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
+        if (ensure_scratch(ctx, poff + 16 + (size_t)n * 4, s) == QK_OK)
+            xc = (uint32_t *)((char *)ctx->d_scratch + poff + ((uintptr_t)ids & 15));
+        // else: no room for the cache, each pass raises x^8 itself
+    }
+    uint32_t pass = 0;
+    for (uint32_t base = 0; base < T; ++pass) {
         const uint32_t Tp = std::min<uint32_t>(base == 0 ? 80 : 48, T - base);
         uint64_t *meta = base == 0 ? out + T : nullptr;
+        // XC: pass 1 writes the cache, the middle passes read and write it, the last reads it
+        const int xcm = !xc || pass == 0 ? 0 : (pass > 1 ? 1 : 0) | (pass < npass ? 2 : 0);
         int rc;
         if (base == 0)
             rc = run_pass<false>(ctx, k_encode_u32_bsgs<8, 10, 16>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
-        else if (Tp <= 40)
-            rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10>, 40, ids, n, head, Tp, base, out + base, meta, acc, s);
-        else
-            rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12>, 48, ids, n, head, Tp, base, out + base, meta, acc, s);
+        else if (Tp <= 40) {   // the last pass (npass >= 1)
+            rc = xcm & 1 ? run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10, 1>, 40, ids, n, head, Tp, base, out + base,
+                                          meta, acc, s, xc, nullptr)
+                         : run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10, 0>, 40, ids, n, head, Tp, base, out + base,
+                                          meta, acc, s);
+        } else {
+            switch (xcm) {
+            case 1: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 1>, 48, ids, n, head, Tp, base, out + base,
+                                        meta, acc, s, xc, nullptr); break;
+            case 2: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 2>, 48, ids, n, head, Tp, base, out + base,
+                                        meta, acc, s, nullptr, xc); break;
+            case 3: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 3>, 48, ids, n, head, Tp, base, out + base,
+                                        meta, acc, s, xc, xc); break;
+            default: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 0>, 48, ids, n, head, Tp, base, out + base,
+                                         meta, acc, s); break;
+            }
+        }
         if (rc) return rc;
         base += Tp;
     }

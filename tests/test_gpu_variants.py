@@ -2,7 +2,8 @@
 
 The measurement knobs of a context (qk_ctx_set_knob): bsgs_sg
 — how many 4-wide BSGS accumulator groups (the a = 0 add row first, then the
-multiply-accumulate rows) count their wraps on the scalar unit; u64_kmax —
+multiply-accumulate rows) count their wraps on the scalar unit; u32_xcache —
+the per-id x^base cache of the u32 offset passes; u64_kmax —
 u64 accumulators per lane; bsgs64_sg — the u64 BSGS MAC carry mode;
 bsgs64_off — the u64 power chain.  Each variant runs on the shared context of
 device 0 with the knob set and restored afterwards.  Inputs cover ragged
@@ -15,7 +16,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0}
+DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "u32_xcache": 1}
 
 
 @contextlib.contextmanager
@@ -78,7 +79,7 @@ def test_u64_lane_split(kmax):
     assert all(res.values()), res
 
 
-@pytest.mark.parametrize("sg", [-1, 0, 8, 12, 18])
+@pytest.mark.parametrize("sg", [-1, 8, 12, 18])
 def test_u64_bsgs_scalar_carry_macs(sg):
     """The u64 baby-step/giant-step kernel (bsgs64.h) with the first sg MACs
     of each wave's tile counting carries on the scalar unit, the rest per
@@ -86,6 +87,21 @@ def test_u64_bsgs_scalar_carry_macs(sg):
     cases = [("t80", 300_001, 80, 1), ("t73", 100_003, 73, 0), ("t77", 4099, 77, 1), ("t79_tiny", 37, 79, 0)]
     with knob("bsgs64_sg", sg):
         res = _run(64, cases)
+    assert all(res.values()), res
+
+
+@pytest.mark.parametrize("xcache", [1, 0])
+def test_u32_passes_xbase_cache(xcache):
+    """u32 thresholds > 128 run two or more offset passes; with the per-id
+    x^base cache (the default) pass 1 writes x^128 per id, the middle passes
+    read and write it, the last one reads it — against the oracle with an
+    unaligned head, ragged tails, a partial last pass (t = 129, 250, 300) and
+    the 20-pass maximum (t = 1024); knob u32_xcache = 0 is the
+    square-and-multiply form."""
+    cases = [("t129", 300_001, 129, 1), ("t176", 100_003, 176, 3), ("t250", 65_537, 250, 2), ("t300", 40_009, 300, 0),
+             ("t1024", 20_011, 1024, 1), ("t1024_tiny", 9, 1024, 3)]
+    with knob("u32_xcache", xcache):
+        res = _run(32, cases)
     assert all(res.values()), res
 
 
