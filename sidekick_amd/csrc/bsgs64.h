@@ -243,9 +243,15 @@ struct Smem<NG, true> {
 //           the uniform exponent base/8 (base a multiple of 8)
 //   BSH     B * 2^32 recomputed by the owner wave in step 3 (see Smem)
 //   LD      giant operands read one row ahead instead of all rows at once
-template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0>
+//   XC      offset passes: bit 0 — x^base per id from the previous pass's
+//           cache xin (no square-and-multiply); bit 1 — x^(base + 8 NA) per
+//           id written to xout for the next pass
+template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0,
+          int XC = 0>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
-                                     uint64_t *__restrict__ partials, uint32_t base = 0) {
+                                     uint64_t *__restrict__ partials, uint32_t base = 0,
+                                     const uint64_t *__restrict__ xin = nullptr, uint64_t *__restrict__ xout = nullptr) {
+    static_assert(!XC || OFF, "the x^base cache is for offset passes");
     static_assert(NA >= 2 && NA <= 10, "giant rows");
     static_assert(!(BSH && PF) && !(LD && PF), "prefetch form: stored B * 2^32, all rows");
     constexpr int NR = OFF ? NA : NA - 1;        // MAC rows (giants x^8 .. x^(8 NR), or x^base ..)
@@ -271,8 +277,11 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 
     const uint64_t ntiles = (n + BLOCK - 1) / BLOCK;
     uint64_t tile = blockIdx.x;
-    uint64_t nxt = 0;
-    if (tile < ntiles && tile * BLOCK + tid < n) nxt = ids[tile * BLOCK + tid];
+    uint64_t nxt = 0, nxc = 0;
+    if (tile < ntiles && tile * BLOCK + tid < n) {
+        nxt = ids[tile * BLOCK + tid];
+        if constexpr ((XC & 1) != 0) nxc = xin[tile * BLOCK + tid];
+    }
     for (; tile < ntiles; tile += gridDim.x) {
         // ---- step 1: this thread's id -> babies (+ B * 2^32), giants -> LDS
         {
@@ -290,7 +299,9 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 }
             }
             const uint32_t g0 = (uint32_t)V, g1 = (uint32_t)(V >> 32);   // x^8
-            if constexpr (OFF) {
+            if constexpr ((XC & 1) != 0) {
+                V = nxc;   // x^base from the previous pass
+            } else if constexpr (OFF) {
                 // x^base = (x^8)^(base/8): square-and-multiply, uniform exponent
                 uint32_t q = base / NB;
                 uint64_t r = 0, sq = V;
@@ -314,12 +325,19 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 if (ABL != 2) mulv(V, g0, g1);
                 sm.ga[G8 ? a - 1 : a][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
             }
+            if constexpr ((XC & 2) != 0) {   // x^(base + 8 NR) for the next pass
+                mulv(V, g0, g1);
+                if (tile * BLOCK + tid < n) xout[tile * BLOCK + tid] = V;
+            }
         }
         __syncthreads();
         // next tile's id in flight during step 3
         const uint64_t tn = tile + gridDim.x;
         nxt = 0;
-        if (tn < ntiles && tn * BLOCK + tid < n) nxt = ids[tn * BLOCK + tid];
+        if (tn < ntiles && tn * BLOCK + tid < n) {
+            nxt = ids[tn * BLOCK + tid];
+            if constexpr ((XC & 1) != 0) nxc = xin[tn * BLOCK + tid];
+        }
         // ---- step 3: this wave's 2 x NR MACs over the 256 ids (4 per lane)
         // PF: the next chunk's operands are read from LDS while this chunk's
         // MACs run (double-buffered registers, the chunk loop unrolled)

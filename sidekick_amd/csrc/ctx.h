@@ -17,6 +17,7 @@ struct qk_knobs {
     int bsgs64_sg = -1;    // u64 BSGS MAC mode override (-1: default)
     int bsgs64_off = 0;    // 1: u64 on the power chain instead of BSGS
     int u64_passes = 1;    // 0: u64 t > 80 on the power chain instead of BSGS passes
+    int u64_xcache = 1;    // 0: u64 offset passes raise x^8 to base/8 themselves (no per-id x^base cache)
     int u64_kmax = 40;     // u64 power chain: accumulators per lane
     int flow_load = 4;     // flow-table slots per expected flow
     int flow_wgpc = 12;    // flow extract: workgroups per CU

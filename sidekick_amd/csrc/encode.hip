@@ -604,13 +604,16 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs(const uint
 
 // Offset pass for u64 thresholds > 80: powers base+1 .. base+8NA with giants
 // x^(base + 8a) (bsgs64.h OFF); the ids are read once per pass.
-template <int NA>
+// XC: the per-id x^base cache between passes (bsgs64.h)
+template <int NA, int XC = 0>
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_off(const uint64_t *__restrict__ ids,
                                                                           uint64_t n, uint32_t head, uint32_t T,
                                                                           uint32_t base,
-                                                                          uint64_t *__restrict__ partials) {
+                                                                          uint64_t *__restrict__ partials,
+                                                                          const uint64_t *__restrict__ xin,
+                                                                          uint64_t *__restrict__ xout) {
     (void)head;
-    bsgs64::body<NA, 0, 16, 0, 0, true, true, 1>(ids, n, T, partials, base);
+    bsgs64::body<NA, 0, 16, 0, 0, true, true, 1, XC>(ids, n, T, partials, base, xin, xout);
 }
 
 // ------------------------------------------------------------- dispatch
@@ -822,16 +825,17 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
 // x^(base + 8a), every row a MAC row; NA = ceil(Tp / 8)).  Each pass reads the
 // 8-byte ids once more: at ~25 ms of integer issue per pass over 1e9 ids, the
 // extra 1 ms of HBM reads is noise.
-template <int NA>
+template <int NA, int XC = 0>
 static int run_pass64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t Tp, uint32_t base,
-                      uint64_t *out, uint64_t *meta, int acc, hipStream_t s) {
-    auto kern = k_encode_u64_bsgs_off<NA>;
+                      uint64_t *out, uint64_t *meta, int acc, hipStream_t s, uint64_t *xc = nullptr) {
+    auto kern = k_encode_u64_bsgs_off<NA, XC>;
     const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
     if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 8 * NA * sizeof(uint64_t), s)) return rc;
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
     if (int rc = scratch_acquire(ctx, s)) return rc;
     hipEvent_t e0 = prof_begin(ctx, s);
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, Tp, base, partials);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, Tp, base, partials,
+                       (const uint64_t *)xc, xc);
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_finalize_u64_pass, dim3(Tp), dim3(BLOCK), 0, s, partials, nb, Tp, ids, (uint64_t)n, out,
@@ -843,6 +847,19 @@ static int run_pass64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head,
 static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
                         int acc, hipStream_t s) {
     uint64_t *meta = out + 2 * T;
+    // With two or more offset passes, x^(next base) goes from pass to pass
+    // through a per-id cache (8 B read + 8 B written per id and pass) instead
+    // of each pass raising x^8 to base/8 (as enc32_passes; knob u64_xcache).
+    // The cache follows the partials in the scratch, sized once.
+    const uint32_t npass = (T - 80 + 79) / 80;
+    uint64_t *xc = nullptr;
+    if (npass >= 2 && ctx->knobs.u64_xcache) {
+        const uint64_t tiles = (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK;
+        const uint32_t nbmax = std::max(grid_for(ctx, k_encode_u64_bsgs<10, 16>, tiles, 1),
+                                        grid_for(ctx, k_encode_u64_bsgs_off<10, 3>, tiles, 1));
+        const size_t poff = ((size_t)nbmax * 2 * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
+        if (ensure_scratch(ctx, poff + (size_t)n * 8, s) == QK_OK) xc = (uint64_t *)((char *)ctx->d_scratch + poff);
+    }
     {   // pass 0: powers 1..80
         auto kern = k_encode_u64_bsgs<10, 16>;
         const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
@@ -858,21 +875,34 @@ static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t hea
         QK_HIP_TRY(hipGetLastError());
         if (int rc = scratch_release(ctx, s)) return rc;
     }
-    for (uint32_t base = 80; base < T;) {
+    uint32_t pass = 1;
+    for (uint32_t base = 80; base < T; ++pass) {
         const uint32_t Tp = std::min<uint32_t>(80, T - base);
         uint64_t *o = out + 2 * base;
+        // pass 1 writes the cache, the middle passes read and write it (all
+        // full 80-power passes), the last one reads it
+        const int xcm = !xc ? 0 : (pass > 1 ? 1 : 0) | (pass < npass ? 2 : 0);
         int rc;
-        switch (std::max<uint32_t>(2, (Tp + 7) / 8)) {
-        case 2: rc = run_pass64<2>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        case 3: rc = run_pass64<3>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        case 4: rc = run_pass64<4>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        case 5: rc = run_pass64<5>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        case 6: rc = run_pass64<6>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        case 7: rc = run_pass64<7>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        case 8: rc = run_pass64<8>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        case 9: rc = run_pass64<9>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
-        default: rc = run_pass64<10>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s); break;
+#define QK_PASS64(NA_)                                                                              \
+    (xcm & 1 ? run_pass64<NA_, 1>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc)           \
+             : run_pass64<NA_, 0>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s))
+        if (xcm & 2) {
+            rc = xcm & 1 ? run_pass64<10, 3>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc)
+                         : run_pass64<10, 2>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc);
+        } else {
+            switch (std::max<uint32_t>(2, (Tp + 7) / 8)) {
+            case 2: rc = QK_PASS64(2); break;
+            case 3: rc = QK_PASS64(3); break;
+            case 4: rc = QK_PASS64(4); break;
+            case 5: rc = QK_PASS64(5); break;
+            case 6: rc = QK_PASS64(6); break;
+            case 7: rc = QK_PASS64(7); break;
+            case 8: rc = QK_PASS64(8); break;
+            case 9: rc = QK_PASS64(9); break;
+            default: rc = QK_PASS64(10); break;
+            }
         }
+#undef QK_PASS64
         if (rc) return rc;
         base += Tp;
     }

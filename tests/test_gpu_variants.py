@@ -3,7 +3,8 @@
 The measurement knobs of a context (qk_ctx_set_knob): bsgs_sg
 — how many 4-wide BSGS accumulator groups (the a = 0 add row first, then the
 multiply-accumulate rows) count their wraps on the scalar unit; u32_xcache —
-the per-id x^base cache of the u32 offset passes; u64_kmax —
+the per-id x^base cache of the u32 offset passes (u64_xcache: of the u64
+ones); u64_kmax —
 u64 accumulators per lane; bsgs64_sg — the u64 BSGS MAC carry mode;
 bsgs64_off — the u64 power chain.  Each variant runs on the shared context of
 device 0 with the knob set and restored afterwards.  Inputs cover ragged
@@ -16,7 +17,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "u32_xcache": 1}
+DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "u32_xcache": 1, "u64_xcache": 1}
 
 
 @contextlib.contextmanager
@@ -102,6 +103,19 @@ def test_u32_passes_xbase_cache(xcache):
              ("t1024", 20_011, 1024, 1), ("t1024_tiny", 9, 1024, 3)]
     with knob("u32_xcache", xcache):
         res = _run(32, cases)
+    assert all(res.values()), res
+
+
+@pytest.mark.parametrize("xcache", [1, 0])
+def test_u64_passes_xbase_cache(xcache):
+    """u64 thresholds > 160: offset passes of 80 powers hand x^(next base)
+    on through the per-id cache (knob u64_xcache; 0 = square-and-multiply per
+    pass): a partial last pass (t = 161, 250), full passes only (t = 240) and
+    the 13-pass maximum (t = 1024), with ragged tails and a head offset."""
+    cases = [("t161", 100_003, 161, 1), ("t240", 50_001, 240, 0), ("t250", 30_011, 250, 2), ("t1024", 8_009, 1024, 1),
+             ("t1024_tiny", 5, 1024, 0)]
+    with knob("u64_xcache", xcache):
+        res = _run(64, cases)
     assert all(res.values()), res
 
 
