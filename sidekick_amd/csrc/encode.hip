@@ -797,11 +797,19 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
         int rc;
         if (base == 0)
             rc = run_pass<false>(ctx, k_encode_u32_bsgs<8, 10, 16>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
-        else if (Tp <= 40) {   // the last pass (npass >= 1)
-            rc = xcm & 1 ? run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10, 1>, 40, ids, n, head, Tp, base, out + base,
-                                          meta, acc, s, xc, nullptr)
-                         : run_pass<true>(ctx, k_encode_u32_bsgs_off<5, 10, 0>, 40, ids, n, head, Tp, base, out + base,
-                                          meta, acc, s);
+        else if (Tp <= 40) {   // the last pass (npass >= 1): NA = ceil(Tp / 8) giant rows
+#define QK_LAST32(NA_)                                                                                       \
+    (xcm & 1 ? run_pass<true>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 1>, 8 * NA_, ids, n, head, Tp, base,      \
+                              out + base, meta, acc, s, xc, nullptr)                                          \
+             : run_pass<true>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 0>, 8 * NA_, ids, n, head, Tp, base,      \
+                              out + base, meta, acc, s))
+            switch ((Tp + 7) / 8) {
+            case 0: case 1: case 2: rc = QK_LAST32(2); break;
+            case 3: rc = QK_LAST32(3); break;
+            case 4: rc = QK_LAST32(4); break;
+            default: rc = QK_LAST32(5); break;
+            }
+#undef QK_LAST32
         } else {
             switch (xcm) {
             case 1: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 1>, 48, ids, n, head, Tp, base, out + base,
