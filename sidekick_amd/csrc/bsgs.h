@@ -229,15 +229,17 @@ __device__ __forceinline__ void row2m(uint64_t &a0, uint64_t &a1, uint32_t b0, u
 //          giants are x^(base + a*NB) for a = 0..NA-1 with a runtime base
 //          (a multiple of NB), so every row is a MAC row (no a = 0 sum row)
 //          and the pass yields powers base+1 .. base+NB*NA
-//  XC      offset passes: bit 0 — x^base per id read from the previous pass's
-//          cache instead of square-and-multiply; bit 1 — x^(base + NB*NA)
-//          written for the next pass (one more product per id)
+//  XC      bit 0 (offset passes) — x^base per id read from the previous
+//          pass's cache instead of square-and-multiply; bit 1 — the next
+//          pass's x^base written per id (one more product): x^(base + NB*NA)
+//          after an offset pass, x^(NB*NA) after a plain one (pass 0)
 template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false, bool OFF_ = false,
           int XC_ = 0>
 struct Cfg {
     static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_, XC = XC_;
     static constexpr bool PAIR = PAIR_, OFF = OFF_;
-    static_assert(!XC_ || OFF_, "the x^base cache is for offset passes");
+    static_assert(OFF_ || (XC_ & 1) == 0, "only an offset pass reads x^base");
+    static_assert(!XC_ || FOLD_ == 1, "the x^base cache goes with min-tracked folds");
     static constexpr int ROWS = OFF_ ? NA_ : NA_ - 1;   // MAC rows
     static constexpr int ROW1 = OFF_ ? 0 : 1;           // group-row number of the first MAC row
     static_assert(NB % 2 == 0 && NA >= 2, "NB even, NA >= 2");
@@ -310,6 +312,7 @@ __device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], ui
         A[0] = B[NB - 1];
 #pragma unroll
         for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_min(A[a - 1], A[0], mn);
+        if constexpr ((C::XC & 2) != 0) *xnext = mulfold32_min(A[NA - 2], A[0], mn);   // x^(NB NA)
         return mn < 25u;
     }
 }
@@ -330,6 +333,7 @@ __device__ __forceinline__ void powers_exact(uint32_t (&B)[C::NB], uint32_t (&A)
     A[0] = B[C::NB - 1];
 #pragma unroll
     for (int a = 1; a < C::NA - 1; ++a) A[a] = mulfold32_exact(A[a - 1], A[0]);
+    if constexpr ((C::XC & 2) != 0) *xnext = mulfold32_exact(A[C::NA - 2], A[0]);
 }
 
 // Groups are issued in the order row 0, row 1, ... and alternate carry-SGPR

@@ -163,6 +163,18 @@ __global__ __launch_bounds__(64) void k_mfma32_fix(const uint64_t *__restrict__ 
 }
 #endif // QK_WITH_MATRIX_CORES
 
+// Pass 0 of a multi-pass encode (powers 1..80) that also writes x^80 per id
+// for pass 1 (the x^base cache, enc32_passes)
+template <int SG>
+__global__ __launch_bounds__(BLOCK, 2) void k_encode_u32_bsgs_x80(const uint32_t *__restrict__ ids, uint64_t n,
+                                                                 uint32_t head, uint32_t T,
+                                                                 uint64_t *__restrict__ partials,
+                                                                 const uint32_t *__restrict__ xin,
+                                                                 uint32_t *__restrict__ xout) {
+    (void)xin;
+    bsgs::body<bsgs::Cfg<8, 10, SG, 1, 1, false, false, 2>>(ids, n, head, T, partials, 0, nullptr, xout);
+}
+
 // Offset pass for thresholds > 80 (several passes over the ids): powers
 // base+1 .. base+8*NA with giants x^(base + 8a), a = 0..NA-1 (bsgs.h OFF).
 // XC: x^base from the previous pass's per-id cache (bit 0) / x^(base + 8 NA)
@@ -664,7 +676,10 @@ int launch_finalize_powers_u32(const uint64_t *partials, uint32_t nblocks, uint3
 // passes are integer-issue bound like the single-pass kernels).
 // xcache (offset passes): the per-id x^base cache (xin / xout), placed in
 // the scratch after the partials (run_pass32_cached sizes the scratch once)
-template <bool OFF, class KernelT>
+// KIND 0: a plain kernel (ids, n, head, T, partials); 1: an offset pass
+// (+ base, xin, xout); 2: a plain kernel that writes the x^base cache
+// (+ xin, xout)
+template <int KIND, class KernelT>
 static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_ids, size_t n,
                     uint32_t head, uint32_t Tp, uint32_t base, uint64_t *out, uint64_t *meta, int acc,
                     hipStream_t s, const uint32_t *xin = nullptr, uint32_t *xout = nullptr) {
@@ -673,9 +688,11 @@ static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_id
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
     if (int rc = scratch_acquire(ctx, s)) return rc;
     hipEvent_t e0 = prof_begin(ctx, s);
-    if constexpr (OFF)
+    if constexpr (KIND == 1)
         hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, base, partials, xin,
                            xout);
+    else if constexpr (KIND == 2)
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, partials, xin, xout);
     else
         hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, d_ids, (uint64_t)n, head, Tp, partials);
     prof_end(ctx, s, e0);
@@ -770,17 +787,18 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
     // every row of an offset pass is a MAC row: the 80-power form spills, a
     // 64-power (8,8) form at 2 waves/SIMD measured the same as 48)
     //
-    // With two or more offset passes, each pass hands x^(next base) to the
-    // next one through a per-id cache (4 B per id read + 4 B written per
-    // pass) instead of every pass raising x^8 to base/8 (~5-8 of its ~22
-    // modmuls per id).  The cache lives in the scratch after the partials,
-    // sized once for every pass (a regrow between passes would drop it), with
-    // the ids' address modulo 16 so that both are read in the same 16-byte
-    // groups; knob u32_xcache = 0 keeps the square-and-multiply form.
+    // Each pass hands x^(next base) to the next one through a per-id cache
+    // (4 B per id read + 4 B written per pass) instead of every offset pass
+    // raising x^8 to base/8 (~4-8 of its ~16-22 modmuls per id): pass 0
+    // writes x^80, the middle passes read and write, the last one reads.  The
+    // cache lives in the scratch after the partials, sized once for every
+    // pass (a regrow between passes would drop it), with the ids' address
+    // modulo 16 so that both are read in the same 16-byte groups; knob
+    // u32_xcache = 0 keeps the square-and-multiply form.
     const uint32_t npass = T <= 80 ? 0 : (T - 80 + 47) / 48;   // offset passes
     uint32_t *xc = nullptr;
-    if (npass >= 2 && ctx->knobs.u32_xcache) {
-        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u32_bsgs<8, 10, 16>, (n + 3) / 4, BLOCK),
+    if (npass >= 1 && ctx->knobs.u32_xcache) {
+        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u32_bsgs_x80<16>, (n + 3) / 4, BLOCK),
                                          grid_for(ctx, k_encode_u32_bsgs_off<6, 12, 3>, (n + 3) / 4, BLOCK),
                                          grid_for(ctx, k_encode_u32_bsgs_off<5, 10, 1>, (n + 3) / 4, BLOCK)});
         const size_t poff = ((size_t)nbmax * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
@@ -792,16 +810,18 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
     for (uint32_t base = 0; base < T; ++pass) {
         const uint32_t Tp = std::min<uint32_t>(base == 0 ? 80 : 48, T - base);
         uint64_t *meta = base == 0 ? out + T : nullptr;
-        // XC: pass 1 writes the cache, the middle passes read and write it, the last reads it
-        const int xcm = !xc || pass == 0 ? 0 : (pass > 1 ? 1 : 0) | (pass < npass ? 2 : 0);
+        // XC: pass 0 writes the cache, the middle passes read and write it, the last reads it
+        const int xcm = !xc ? 0 : (pass > 0 ? 1 : 0) | (pass < npass ? 2 : 0);
         int rc;
-        if (base == 0)
-            rc = run_pass<false>(ctx, k_encode_u32_bsgs<8, 10, 16>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
+        if (base == 0 && xc)
+            rc = run_pass<2>(ctx, k_encode_u32_bsgs_x80<16>, 80, ids, n, head, Tp, 0, out, meta, acc, s, nullptr, xc);
+        else if (base == 0)
+            rc = run_pass<0>(ctx, k_encode_u32_bsgs<8, 10, 16>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
         else if (Tp <= 40) {   // the last pass (npass >= 1): NA = ceil(Tp / 8) giant rows
 #define QK_LAST32(NA_)                                                                                       \
-    (xcm & 1 ? run_pass<true>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 1>, 8 * NA_, ids, n, head, Tp, base,      \
+    (xcm & 1 ? run_pass<1>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 1>, 8 * NA_, ids, n, head, Tp, base,      \
                               out + base, meta, acc, s, xc, nullptr)                                          \
-             : run_pass<true>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 0>, 8 * NA_, ids, n, head, Tp, base,      \
+             : run_pass<1>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 0>, 8 * NA_, ids, n, head, Tp, base,      \
                               out + base, meta, acc, s))
             switch ((Tp + 7) / 8) {
             case 0: case 1: case 2: rc = QK_LAST32(2); break;
@@ -812,13 +832,13 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
 #undef QK_LAST32
         } else {
             switch (xcm) {
-            case 1: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 1>, 48, ids, n, head, Tp, base, out + base,
+            case 1: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 1>, 48, ids, n, head, Tp, base, out + base,
                                         meta, acc, s, xc, nullptr); break;
-            case 2: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 2>, 48, ids, n, head, Tp, base, out + base,
+            case 2: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 2>, 48, ids, n, head, Tp, base, out + base,
                                         meta, acc, s, nullptr, xc); break;
-            case 3: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 3>, 48, ids, n, head, Tp, base, out + base,
+            case 3: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 3>, 48, ids, n, head, Tp, base, out + base,
                                         meta, acc, s, xc, xc); break;
-            default: rc = run_pass<true>(ctx, k_encode_u32_bsgs_off<6, 12, 0>, 48, ids, n, head, Tp, base, out + base,
+            default: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 0>, 48, ids, n, head, Tp, base, out + base,
                                          meta, acc, s); break;
             }
         }
