@@ -243,15 +243,16 @@ struct Smem<NG, true> {
 //           the uniform exponent base/8 (base a multiple of 8)
 //   BSH     B * 2^32 recomputed by the owner wave in step 3 (see Smem)
 //   LD      giant operands read one row ahead instead of all rows at once
-//   XC      offset passes: bit 0 — x^base per id from the previous pass's
-//           cache xin (no square-and-multiply); bit 1 — x^(base + 8 NA) per
-//           id written to xout for the next pass
+//   XC      bit 0 (offset passes) — x^base per id from the previous pass's
+//           cache xin (no square-and-multiply); bit 1 — the next pass's
+//           x^base per id written to xout: x^(base + 8 NA) after an offset
+//           pass, x^(8 NA) after pass 0
 template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0,
           int XC = 0>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
                                      uint64_t *__restrict__ partials, uint32_t base = 0,
                                      const uint64_t *__restrict__ xin = nullptr, uint64_t *__restrict__ xout = nullptr) {
-    static_assert(!XC || OFF, "the x^base cache is for offset passes");
+    static_assert(OFF || (XC & 1) == 0, "only an offset pass reads x^base");
     static_assert(NA >= 2 && NA <= 10, "giant rows");
     static_assert(!(BSH && PF) && !(LD && PF), "prefetch form: stored B * 2^32, all rows");
     constexpr int NR = OFF ? NA : NA - 1;        // MAC rows (giants x^8 .. x^(8 NR), or x^base ..)
@@ -325,7 +326,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 if (ABL != 2) mulv(V, g0, g1);
                 sm.ga[G8 ? a - 1 : a][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
             }
-            if constexpr ((XC & 2) != 0) {   // x^(base + 8 NR) for the next pass
+            if constexpr ((XC & 2) != 0) {   // x^(base + 8 NR), or x^(8 NA) after pass 0, for the next pass
                 mulv(V, g0, g1);
                 if (tile * BLOCK + tid < n) xout[tile * BLOCK + tid] = V;
             }

@@ -614,6 +614,15 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs(const uint
     bsgs64::body<NA, 0, SG, 0, 0, false, true, 1>(ids, n, T, partials);
 }
 
+// Pass 0 of a u64 multi-pass encode that also writes x^80 per id for pass 1
+__global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_x80(const uint64_t *__restrict__ ids,
+                                                                          uint64_t n, uint32_t head, uint32_t T,
+                                                                          uint64_t *__restrict__ partials,
+                                                                          uint64_t *__restrict__ xout) {
+    (void)head;
+    bsgs64::body<10, 0, 16, 0, 0, false, true, 1, 2>(ids, n, T, partials, 0, nullptr, xout);
+}
+
 // Offset pass for u64 thresholds > 80: powers base+1 .. base+8NA with giants
 // x^(base + 8a) (bsgs64.h OFF); the ids are read once per pass.
 // XC: the per-id x^base cache between passes (bsgs64.h)
@@ -875,27 +884,32 @@ static int run_pass64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head,
 static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
                         int acc, hipStream_t s) {
     uint64_t *meta = out + 2 * T;
-    // With two or more offset passes, x^(next base) goes from pass to pass
-    // through a per-id cache (8 B read + 8 B written per id and pass) instead
-    // of each pass raising x^8 to base/8 (as enc32_passes; knob u64_xcache).
-    // The cache follows the partials in the scratch, sized once.
+    // x^(next base) goes from pass to pass through a per-id cache (8 B read +
+    // 8 B written per id and pass; pass 0 writes x^80) instead of each offset
+    // pass raising x^8 to base/8 (as enc32_passes; knob u64_xcache).  The
+    // cache follows the partials in the scratch, sized once.
     const uint32_t npass = (T - 80 + 79) / 80;
     uint64_t *xc = nullptr;
-    if (npass >= 2 && ctx->knobs.u64_xcache) {
+    if (npass >= 1 && ctx->knobs.u64_xcache) {
         const uint64_t tiles = (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK;
-        const uint32_t nbmax = std::max(grid_for(ctx, k_encode_u64_bsgs<10, 16>, tiles, 1),
-                                        grid_for(ctx, k_encode_u64_bsgs_off<10, 3>, tiles, 1));
+        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u64_bsgs<10, 16>, tiles, 1),
+                                         grid_for(ctx, k_encode_u64_bsgs_x80, tiles, 1),
+                                         grid_for(ctx, k_encode_u64_bsgs_off<10, 3>, tiles, 1)});
         const size_t poff = ((size_t)nbmax * 2 * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
         if (ensure_scratch(ctx, poff + (size_t)n * 8, s) == QK_OK) xc = (uint64_t *)((char *)ctx->d_scratch + poff);
     }
-    {   // pass 0: powers 1..80
+    {   // pass 0: powers 1..80 (+ x^80 per id for pass 1 when the cache is on)
         auto kern = k_encode_u64_bsgs<10, 16>;
         const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
         if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 80 * sizeof(uint64_t), s)) return rc;
         uint64_t *partials = (uint64_t *)ctx->d_scratch;
         if (int rc = scratch_acquire(ctx, s)) return rc;
         hipEvent_t e0 = prof_begin(ctx, s);
-        hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, 80u, partials);
+        if (xc)
+            hipLaunchKernelGGL(k_encode_u64_bsgs_x80, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, 80u,
+                               partials, xc);
+        else
+            hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, 80u, partials);
         prof_end(ctx, s, e0);
         QK_HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_finalize_u64_pass, dim3(80), dim3(BLOCK), 0, s, partials, nb, 80u, ids, (uint64_t)n,
@@ -907,16 +921,15 @@ static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t hea
     for (uint32_t base = 80; base < T; ++pass) {
         const uint32_t Tp = std::min<uint32_t>(80, T - base);
         uint64_t *o = out + 2 * base;
-        // pass 1 writes the cache, the middle passes read and write it (all
+        // pass 0 wrote the cache; the middle passes read and write it (all
         // full 80-power passes), the last one reads it
-        const int xcm = !xc ? 0 : (pass > 1 ? 1 : 0) | (pass < npass ? 2 : 0);
+        const int xcm = !xc ? 0 : 1 | (pass < npass ? 2 : 0);
         int rc;
 #define QK_PASS64(NA_)                                                                              \
     (xcm & 1 ? run_pass64<NA_, 1>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc)           \
              : run_pass64<NA_, 0>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s))
-        if (xcm & 2) {
-            rc = xcm & 1 ? run_pass64<10, 3>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc)
-                         : run_pass64<10, 2>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc);
+        if (xcm & 2) {   // a middle pass: Tp = 80
+            rc = run_pass64<10, 3>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc);
         } else {
             switch (std::max<uint32_t>(2, (Tp + 7) / 8)) {
             case 2: rc = QK_PASS64(2); break;
