@@ -157,10 +157,6 @@ __global__ void k_fill_u64(uint64_t *out, uint64_t n, uint64_t seed, uint64_t st
         out[i] = splitmix_mix(seed + (start + i + 1) * GAMMA);
 }
 
-__global__ void k_init_counters(uint64_t *c) {
-    c[0] = 0;
-    c[1] = ~0ull;
-}
 
 // Pageable -> pinned staging copy, split over a few host threads: one core's
 // memcpy (~24 GB/s) is under half of the PCIe Gen5 rate the DMA can take.
@@ -310,9 +306,13 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
     } else {
         memcpy(ctx->h_small, coeffs, cbytes);
     }
-    if (cbytes) QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, cbytes, hipMemcpyHostToDevice, s));
+    // one copy carries the table (or coefficients) and the zeroed hit
+    // counter / stop index (no counter-initialising launch)
+    ctx->h_small[SMALL_NHITS] = 0;
+    ctx->h_small[SMALL_STOP] = ~0ull;
+    QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, (SMALL_STOP + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    (void)cbytes;
     if (int rc = ensure_hits(ctx, 4096, s)) return rc;
-    hipLaunchKernelGGL(k_init_counters, dim3(1), dim3(1), 0, s, d_counters);
     if (n) {
         int rc;
         if (scan) {
