@@ -789,8 +789,8 @@ static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, ui
 
 #endif // QK_WITH_MATRIX_CORES
 
-static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
-                        int acc, hipStream_t s) {
+static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                              int acc, hipStream_t s) {
     // pass 0: powers 1..80 with the single-pass (8,10) kernel; then passes of
     // <= 48 powers with the offset (8,6) kernel (142 VGPRs, 3 waves/SIMD;
     // every row of an offset pass is a MAC row: the 80-power form spills, a
@@ -857,6 +857,21 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
     return QK_OK;
 }
 
+// The x^base cache holds 4 B per id for the whole array: above XC_CHUNK32 ids
+// the passes run chunk by chunk (each chunk all its passes, the later chunks
+// accumulating into out), so the scratch stays <= 1 GiB.
+constexpr size_t XC_CHUNK32 = (size_t)1 << 28;
+static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                        int acc, hipStream_t s) {
+    if (n <= XC_CHUNK32 || !ctx->knobs.u32_xcache) return enc32_passes_chunk(ctx, ids, n, head, T, out, acc, s);
+    for (size_t c0 = 0; c0 < n; c0 += XC_CHUNK32) {
+        const uint32_t *p = ids + c0;
+        const uint32_t hd = (uint32_t)(((16 - ((uintptr_t)p & 15)) & 15) / 4);
+        if (int rc = enc32_passes_chunk(ctx, p, std::min(XC_CHUNK32, n - c0), hd, T, out, c0 ? 1 : acc, s)) return rc;
+    }
+    return QK_OK;
+}
+
 // u64 thresholds > 80: pass 0 is the single-pass (8 babies, 10 giants)
 // kernel for powers 1..80, then offset passes of <= 80 powers (giants
 // x^(base + 8a), every row a MAC row; NA = ceil(Tp / 8)).  Each pass reads the
@@ -881,8 +896,8 @@ static int run_pass64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head,
     return scratch_release(ctx, s);
 }
 
-static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
-                        int acc, hipStream_t s) {
+static int enc64_passes_chunk(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                              int acc, hipStream_t s) {
     uint64_t *meta = out + 2 * T;
     // x^(next base) goes from pass to pass through a per-id cache (8 B read +
     // 8 B written per id and pass; pass 0 writes x^80) instead of each offset
@@ -946,6 +961,19 @@ static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t hea
 #undef QK_PASS64
         if (rc) return rc;
         base += Tp;
+    }
+    return QK_OK;
+}
+
+// as enc32_passes: 8 B of cache per id, chunks of XC_CHUNK64 ids (1 GiB)
+constexpr size_t XC_CHUNK64 = (size_t)1 << 27;
+static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
+                        int acc, hipStream_t s) {
+    if (n <= XC_CHUNK64 || !ctx->knobs.u64_xcache) return enc64_passes_chunk(ctx, ids, n, head, T, out, acc, s);
+    for (size_t c0 = 0; c0 < n; c0 += XC_CHUNK64) {
+        const uint64_t *p = ids + c0;
+        const uint32_t hd = (uint32_t)(((16 - ((uintptr_t)p & 15)) & 15) / 8);
+        if (int rc = enc64_passes_chunk(ctx, p, std::min(XC_CHUNK64, n - c0), hd, T, out, c0 ? 1 : acc, s)) return rc;
     }
     return QK_OK;
 }
