@@ -21,6 +21,7 @@ struct qk_knobs {
     int u64_kmax = 40;     // u64 power chain: accumulators per lane
     int flow_load = 4;     // flow-table slots per expected flow
     int flow_wgpc = 12;    // flow extract: workgroups per CU
+    int flow_hist = 1;     // 0: few-flow batches grouped by the radix sort instead of per-workgroup slot histograms
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)

@@ -423,6 +423,80 @@ __global__ void k_rank_perm(const FlowSlot *__restrict__ tab, const uint32_t *__
     info[4 * (uint64_t)r + 1] = ft_dst(e);
 }
 
+// ---- histogram grouping (few flows: a table of <= HIST_MAX slots) ----------
+// Instead of radix-sorting the packets, workgroup w takes the contiguous
+// packets [w chunk, (w + 1) chunk): k_hist_count counts its packets per slot
+// in LDS and writes the nonzero counts to hist[slot * nwg + w] (zeroed
+// before) and the slot's last packet index (+1) with one atomicMax per
+// (workgroup, slot); an exclusive sum of hist in that slot-major order gives
+// every (slot, workgroup) its place, and k_hist_scatter sends each id there
+// (+ its rank within the workgroup's run of that slot, from an LDS counter).
+// Segments come out in slot order; the order inside a segment is arbitrary
+// (power sums are order-independent) and last_value comes from the last
+// packet index, so nothing depends on it.
+constexpr uint32_t HIST_MAX = 8192;   // slots (LDS counters per workgroup: 32 KB)
+
+__global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__ slots, uint64_t n, uint64_t chunk,
+                                                    uint32_t C, uint32_t nwg, uint32_t *__restrict__ hist,
+                                                    uint32_t *__restrict__ last) {
+    extern __shared__ uint32_t lh[];   // C counts, C last indices (+1)
+    uint32_t *lc = lh, *ll = lh + C;
+    for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) { lc[j] = 0; ll[j] = 0; }
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+        const uint32_t sl = slots[i];
+        if (sl != SLOT_NONE) {
+            atomicAdd(&lc[sl], 1u);
+            atomicMax(&ll[sl], (uint32_t)i + 1u);   // n < 2^32
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) {
+        if (lc[j]) {
+            hist[(size_t)j * nwg + blockIdx.x] = lc[j];
+            atomicMax(&last[j], ll[j]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict__ slots,
+                                                      const uint32_t *__restrict__ ids, uint64_t n, uint64_t chunk,
+                                                      uint32_t C, uint32_t nwg, const uint32_t *__restrict__ base,
+                                                      uint32_t *__restrict__ grouped) {
+    extern __shared__ uint32_t lc[];   // C running counts
+    for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) lc[j] = 0;
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+        const uint32_t sl = slots[i];
+        if (sl != SLOT_NONE) {
+            const uint32_t r = atomicAdd(&lc[sl], 1u);
+            grouped[base[(size_t)sl * nwg + blockIdx.x] + r] = ids[i];
+        }
+    }
+}
+
+// histogram grouping: segment p = the p-th occupied slot (ascending), its
+// start = the place of (slot, workgroup 0)
+__global__ void k_hist_offsets(const uint32_t *__restrict__ used, uint32_t nf, const uint32_t *__restrict__ base,
+                               uint32_t nwg, uint64_t inserted, uint64_t *__restrict__ offs) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < nf) offs[p] = base[(size_t)used[p] * nwg];
+    if (p == 0) offs[nf] = inserted;
+}
+
+// histogram grouping: info[4r+2] = count, [4r+3] = the id of the flow's last packet
+__global__ void k_hist_info(const uint32_t *__restrict__ perm, const uint64_t *__restrict__ offs, uint32_t nf,
+                            const uint32_t *__restrict__ used, const uint32_t *__restrict__ last,
+                            const uint32_t *__restrict__ ids, uint64_t *__restrict__ info) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nf) return;
+    const uint32_t g = perm[r];   // rank -> segment (slot order)
+    info[4 * (uint64_t)r + 2] = offs[g + 1] - offs[g];
+    info[4 * (uint64_t)r + 3] = ids[last[used[g]] - 1];
+}
+
 // by-slot grouping: segment starts of the slot-sorted packets
 // Segment starts of the sorted keys: position i starts a segment when
 // key[i] != key[i-1].  Each thread compares 4 keys of one 16-byte load (key
@@ -895,7 +969,25 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 rc = QK_E_HIP;
             tb2 = std::max(tb2, b);
         }
+        // histogram grouping: few flows (a table of <= HIST_MAX slots)
+        const bool hist = C <= HIST_MAX && ctx->knobs.flow_hist;
+        const uint32_t hnwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->num_cus * 4,
+                                                                                  (n_eff + 4095) / 4096));
+        const uint64_t hchunk = (n_eff + hnwg - 1) / hnwg;
+        uint32_t *hcnt = nullptr, *hlast = nullptr, *hbase = nullptr;
+        void *temp3 = nullptr;
+        size_t tb3 = 0;
+        if (hist) {
+            uint32_t *u = nullptr;
+            if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, u, u, (int)(C * hnwg), s) != hipSuccess) rc = QK_E_HIP;
+        }
         auto layout1 = [&](Carve &c) {
+            if (hist) {
+                hcnt = c.take<uint32_t>((size_t)C * hnwg);
+                hbase = c.take<uint32_t>((size_t)C * hnwg);
+                hlast = c.take<uint32_t>(C);
+                temp3 = c.take<char>(tb3);
+            }
             info = c.take<uint64_t>((size_t)nf * 4);
             acc = c.take<unsigned long long>((size_t)nf * T);
             d_items = c.take<SegItem>(items_max);
@@ -949,7 +1041,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         if (!rc && hipcub::DeviceRadixSort::SortPairs(temp2, tb2, ks, ks2, sl2, sl3, nf, 0, 48, s2) != hipSuccess)
             rc = QK_E_HIP;
         if (!rc) {
-            if (by_slot) {
+            if (by_slot || hist) {
                 hipLaunchKernelGGL(k_slot_pos, dim3(fblocks), dim3(256), 0, s2, used, nf, rank_of_slot);
                 hipLaunchKernelGGL(k_rank_perm, dim3(fblocks), dim3(256), 0, s2, tab, sl3, nf, rank_of_slot, perm, info);
             } else {
@@ -957,7 +1049,30 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             }
             if (hipGetLastError() != hipSuccess || hipEventRecord(ctx->flow_ev[1], s2) != hipSuccess) rc = QK_E_HIP;
         }
-        if (!rc && by_slot) {
+        if (!rc && hist) {
+            if (hipMemsetAsync(hcnt, 0, (size_t)C * hnwg * 4, s) != hipSuccess ||
+                hipMemsetAsync(hlast, 0, (size_t)C * 4, s) != hipSuccess)
+                rc = QK_E_HIP;
+            if (!rc) {
+                hipLaunchKernelGGL(k_hist_count, dim3(hnwg), dim3(256), (size_t)C * 8, s, slots, n_eff, hchunk, (uint32_t)C,
+                                   hnwg, hcnt, hlast);
+                if (hipGetLastError() != hipSuccess ||
+                    hipcub::DeviceScan::ExclusiveSum(temp3, tb3, hcnt, hbase, (int)(C * hnwg), s) != hipSuccess)
+                    rc = QK_E_HIP;
+            }
+            if (!rc) {
+                hipLaunchKernelGGL(k_hist_scatter, dim3(hnwg), dim3(256), (size_t)C * 4, s, slots, ids, n_eff, hchunk,
+                                   (uint32_t)C, hnwg, hbase, id_s);
+                if (hipGetLastError() != hipSuccess || hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess)
+                    rc = QK_E_HIP;
+            }
+            if (!rc) {
+                hipLaunchKernelGGL(k_hist_offsets, dim3(fblocks), dim3(256), 0, s, used, nf, hbase, hnwg, inserted,
+                                   d_offs);
+                hipLaunchKernelGGL(k_hist_info, dim3(fblocks), dim3(256), 0, s, perm, d_offs, nf, used, hlast, ids, info);
+                if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+            }
+        } else if (!rc && by_slot) {
             if (hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, cbits, s) !=
                     hipSuccess ||
                 hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess)
@@ -1008,7 +1123,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nf * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);
             hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info,
-                               by_slot ? (const uint32_t *)perm : nullptr, (uint64_t)nf, T, d_rec, d_keys);
+                               by_slot || hist ? (const uint32_t *)perm : nullptr, (uint64_t)nf, T, d_rec, d_keys);
             if (hipGetLastError() != hipSuccess)
                 rc = QK_E_HIP;
             else if (!dev_out && (hipMemcpyAsync(sketches, d_rec, (size_t)nf * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||

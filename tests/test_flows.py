@@ -254,6 +254,39 @@ def test_gpu_flows_group_by_slot_and_by_rank():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nflows,t,p_reset,skew", [(1, 32, 0.0, False), (16, 32, 0.01, False), (300, 16, 0.0, True),
+                                                   (1500, 48, 0.005, False)])
+def test_gpu_flows_histogram_grouping(nflows, t, p_reset, skew):
+    """Few flows (a table of <= 8192 slots): the batch is grouped by
+    per-workgroup slot histograms and a scatter instead of the radix sort; the
+    order inside a flow is arbitrary, so the counts, last ids (from the last
+    packet index) and sums must match the oracle, and the records must be the
+    radix-sort path's (knob flow_hist = 0) byte for byte — one flow, skewed
+    flows, resets, and the work-item path (t > 32) included."""
+    import torch
+    from sidekick_amd.quack import Context, encode_flows
+    bufs, meta = make_flows(250_000 + nflows, nflows, seed=nflows + t, p_reset=p_reset, skew=skew)
+    want, nres, _ = vector_flows(bufs, meta)
+    d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
+    d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
+    recs = {}
+    for mode in (1, 0):
+        ctx = Context(0)
+        ctx.set_knob("flow_hist", mode)
+        keys, qs, st = encode_flows(d_bufs, t, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
+        assert st["resets"] == nres and st["inserted"] == sum(len(v) for v in want.values())
+        assert keys == sorted(want)
+        for k, q in zip(keys, qs):
+            ids = want[k]
+            assert q.count() == len(ids) and q.last_value() == ids[-1], k.hex()
+        for i in range(0, len(keys), max(1, len(keys) // 40)):
+            assert qs[i].power_sums() == coracle.encode_u32(np.array(want[keys[i]], dtype=np.uint32), t)
+        recs[mode] = [bytes(q._buf.raw) for q in qs]
+        ctx.close()
+    assert recs[1] == recs[0]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("where", ["first", "middle", "last", "none"])
 def test_gpu_flows_reset_wipes_table(where):
     """A Reset anywhere in the batch wipes every flow made before it, the
