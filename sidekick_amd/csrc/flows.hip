@@ -443,14 +443,21 @@ __global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__
     uint32_t *lc = lh, *ll = lh + C;
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) { lc[j] = 0; ll[j] = 0; }
     __syncthreads();
+    // four packets per thread and step (chunk is a multiple of 4, the arrays
+    // are arena buffers: 16-byte aligned): independent loads in flight
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
-    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
-        const uint32_t sl = slots[i];
+    auto one = [&](uint32_t sl, uint64_t i) {
         if (sl != SLOT_NONE) {
             atomicAdd(&lc[sl], 1u);
             atomicMax(&ll[sl], (uint32_t)i + 1u);   // n < 2^32
         }
+    };
+    const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
+    for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
+        const uint4 sv = *reinterpret_cast<const uint4 *>(slots + i);
+        one(sv.x, i); one(sv.y, i + 1); one(sv.z, i + 2); one(sv.w, i + 3);
     }
+    for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) one(slots[i], i);
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) {
         if (lc[j]) {
@@ -468,13 +475,19 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) lc[j] = 0;
     __syncthreads();
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
-    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
-        const uint32_t sl = slots[i];
+    auto one = [&](uint32_t sl, uint32_t id) {
         if (sl != SLOT_NONE) {
             const uint32_t r = atomicAdd(&lc[sl], 1u);
-            grouped[base[(size_t)sl * nwg + blockIdx.x] + r] = ids[i];
+            grouped[base[(size_t)sl * nwg + blockIdx.x] + r] = id;
         }
+    };
+    const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
+    for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
+        const uint4 sv = *reinterpret_cast<const uint4 *>(slots + i);
+        const uint4 iv = *reinterpret_cast<const uint4 *>(ids + i);
+        one(sv.x, iv.x); one(sv.y, iv.y); one(sv.z, iv.z); one(sv.w, iv.w);
     }
+    for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) one(slots[i], ids[i]);
 }
 
 // histogram grouping: segment p = the p-th occupied slot (ascending), its
@@ -973,7 +986,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const bool hist = C <= HIST_MAX && ctx->knobs.flow_hist;
         const uint32_t hnwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->num_cus * 4,
                                                                                   (n_eff + 4095) / 4096));
-        const uint64_t hchunk = (n_eff + hnwg - 1) / hnwg;
+        const uint64_t hchunk = ((n_eff + hnwg - 1) / hnwg + 3) & ~(uint64_t)3;   // a multiple of 4 (16-byte reads)
         uint32_t *hcnt = nullptr, *hlast = nullptr, *hbase = nullptr;
         void *temp3 = nullptr;
         size_t tb3 = 0;
