@@ -1105,6 +1105,12 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     if (T >= 5 && T <= 8 && sg(1)) return QK_BSGS(4, 2, 1);
     if (T >= 9 && T <= 12) return sg(3) ? QK_BSGS(4, 3, 3) : QK_BSGS(4, 3, 0);
     if (T >= 13 && T <= 16) return sg(4) ? QK_BSGS(4, 4, 4) : QK_BSGS(4, 4, 0);
+    // 17..28: four babies and NA = ceil(T / 4) giant rows — 3 + (NA - 2)
+    // modmuls and 4 (NA - 1) MACs per id, every group 4 wide (scalar-counted);
+    // the (6,4) / (8,4) shapes that covered them compute 24 / 32 powers
+    if (T >= 17 && T <= 20 && sg(5)) return QK_BSGS(4, 5, 5);
+    if (T >= 21 && T <= 24 && sg(6)) return QK_BSGS(4, 6, 6);
+    if (T >= 25 && T <= 28 && sg(7)) return QK_BSGS(4, 7, 7);
     if (T >= 17 && T <= 24) return sg(4) ? QK_BSGS(6, 4, 4) : QK_BSGS(6, 4, 0);
     if (T >= 25 && T <= 32) {
         switch (sg(QK_BSGS_SG_T32)) {
