@@ -1105,12 +1105,20 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     if (T >= 5 && T <= 8 && sg(1)) return QK_BSGS(4, 2, 1);
     if (T >= 9 && T <= 12) return sg(3) ? QK_BSGS(4, 3, 3) : QK_BSGS(4, 3, 0);
     if (T >= 13 && T <= 16) return sg(4) ? QK_BSGS(4, 4, 4) : QK_BSGS(4, 4, 0);
-    // 17..28: four babies and NA = ceil(T / 4) giant rows — 3 + (NA - 2)
-    // modmuls and 4 (NA - 1) MACs per id, every group 4 wide (scalar-counted);
-    // the (6,4) / (8,4) shapes that covered them compute 24 / 32 powers
-    if (T >= 17 && T <= 20 && sg(5)) return QK_BSGS(4, 5, 5);
-    if (T >= 21 && T <= 24 && sg(6)) return QK_BSGS(4, 6, 6);
-    if (T >= 25 && T <= 28 && sg(7)) return QK_BSGS(4, 7, 7);
+    // Round-3 shapes (knob bsgs_shapes = 0: the round-2 ones): the (NB, NA)
+    // with the fewest issue cycles for the powers actually needed — modmuls
+    // NB - 1 + NA - 2 at ~17 cycles, MACs NB (NA - 1) and row-0 adds NB at
+    // ~4.2, measured: 17..28 four babies and ceil(T / 4)
+    // giant rows (every group 4 wide, scalar-counted; (6,4) / (8,4) computed
+    // 24 / 32 powers), 29..30 (6,5), 33..36 (6,6), 41..42 (6,7), 65..72 (8,9)
+    const bool r3 = ctx->knobs.bsgs_shapes;
+    if (r3 && T >= 17 && T <= 20 && sg(5)) return QK_BSGS(4, 5, 5);
+    if (r3 && T >= 21 && T <= 24 && sg(6)) return QK_BSGS(4, 6, 6);
+    if (r3 && T >= 25 && T <= 28 && sg(7)) return QK_BSGS(4, 7, 7);
+    if (r3 && T >= 29 && T <= 30 && sg(5)) return QK_BSGS(6, 5, 5);
+    if (r3 && T >= 33 && T <= 36 && sg(6)) return QK_BSGS(6, 6, 6);
+    if (r3 && T >= 41 && T <= 42 && sg(7)) return QK_BSGS(6, 7, 7);
+    if (r3 && T >= 65 && T <= 72 && sg(14)) return QK_BSGS(8, 9, 14);
     if (T >= 17 && T <= 24) return sg(4) ? QK_BSGS(6, 4, 4) : QK_BSGS(6, 4, 0);
     if (T >= 25 && T <= 32) {
         switch (sg(QK_BSGS_SG_T32)) {

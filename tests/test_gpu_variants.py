@@ -17,7 +17,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "u32_xcache": 1, "u64_xcache": 1}
+DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "u32_xcache": 1, "u64_xcache": 1,
+            "bsgs_shapes": 1}
 
 
 @contextlib.contextmanager
@@ -88,6 +89,18 @@ def test_u64_bsgs_scalar_carry_macs(sg):
     cases = [("t80", 300_001, 80, 1), ("t73", 100_003, 73, 0), ("t77", 4099, 77, 1), ("t79_tiny", 37, 79, 0)]
     with knob("bsgs64_sg", sg):
         res = _run(64, cases)
+    assert all(res.values()), res
+
+
+@pytest.mark.parametrize("shapes", [1, 0])
+def test_u32_bsgs_shapes(shapes):
+    """The round-3 (NB, NA) shapes — (4,5..7) for t 17..28, (6,5) 29..30,
+    (6,6) 33..36, (6,7) 41..42, (8,9) 65..72 — and the round-2 ones they
+    replaced (knob bsgs_shapes = 0), against the oracle at both ends of each
+    range, ragged and misaligned."""
+    cases = [(f"t{t}", 100_003 + t, t, t % 4) for t in (17, 20, 21, 24, 25, 28, 29, 30, 33, 36, 41, 42, 65, 72)]
+    with knob("bsgs_shapes", shapes):
+        res = _run(32, cases)
     assert all(res.values()), res
 
 

@@ -319,7 +319,8 @@ def run_sweep(args, ctx):
     n = int(args.nsweep)
     ids = torch.empty(n, dtype=torch.int32, device=DEV)
     fill_splitmix(ctx, ids, 0x5EED0002)
-    for t in (1, 4, 8, 10, 16, 17, 20, 24, 25, 28, 30, 32, 40, 48, 56, 64, 80, 96, 128, 176, 256, 300, 512, 1024):
+    for t in (1, 4, 8, 10, 16, 17, 20, 24, 25, 28, 30, 32, 33, 36, 40, 42, 48, 50, 56, 60, 64, 70, 72, 80, 96, 128,
+              176, 256, 300, 512, 1024):
         wall, kern = time_encode(ctx, ids, t, 32, max(3, args.steps // 2))
         emit({"config": f"encode u32 t={t}", "n": n, "ids_per_s": n / kern, "ns_per_id_per_power": kern / n / t * 1e9 * 1})
 
