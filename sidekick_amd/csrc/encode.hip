@@ -14,11 +14,11 @@
 //     1.19 VALU + 0.76 SALU wave-instructions per id, ~0.75 of the
 //     integer-issue roofline (tools/issue_roofline.py) and ~0.19 of the HBM
 //     read roofline (4 B/id).
-//   * 21 <= t <= 80 (u64) — k_encode_u64_bsgs<NA,MODE,SG> (bsgs64.h): the
+//   * 14 <= t <= 80 (u64) — k_encode_u64_bsgs<NA,MODE,SG> (bsgs64.h): the
 //     same split with the babies/giants of a 256-id tile shared through LDS,
 //     each wave owning two babies' MAC rows.
 //   * t > 80 — passes of the BSGS kernels (offset giants x^(base + 8a)).
-//   * small t (u32 t <= 4, u64 t <= 20) — power chains: a lane group of G
+//   * small t (u32 t <= 4, u64 t <= 13) — power chains: a lane group of G
 //     lanes owns one id, lane j computes powers j+1, j+1+G, ... with step
 //     x^G and K lazy accumulators (G K >= t).
 //   The ids are never reduced mod p up front (x^k is congruent either way).
@@ -1162,9 +1162,10 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     const uintptr_t a = (uintptr_t)ids;
     if (a & 7) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
-    // baby-step / giant-step for 21 <= T <= 80 (configs[2] is T = 80; below
-    // ~20 powers the 15-odd modmuls of the babies and giants cost more than
-    // the chain they save, tools/bench_configs.py sweep64): NA = ceil(T / 8)
+    // baby-step / giant-step for 14 <= T <= 80 (configs[2] is T = 80; below
+    // 14 powers the 8 modmuls of the babies and x^8 cost more than the chain
+    // they save: knob bsgs64_tmin, profiles/r03/shapes/sweep64_tmin_ab.jsonl —
+    // 21 before round 3, BSGS +3..9 % at t = 14..20): NA = ceil(T / 8)
     // giant rows; its per-wave 32-bit carry totals need < 2^31 ids per
     // workgroup.  knob bsgs64_sg (T > 72 only) picks a carry mode
     // for measurements (tools/tune_u64.hip); knob bsgs64_off = 1 forces the
@@ -1176,11 +1177,12 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     const int sg64 = ctx->knobs.bsgs64_sg;
     const int no64 = ctx->knobs.bsgs64_off;
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
-    if (T >= 21 && T <= 80 && !no64 && n / min_grid64 < (1ull << 30)) {
+    if (T >= (uint32_t)ctx->knobs.bsgs64_tmin && T <= 80 && !no64 && n / min_grid64 < (1ull << 30)) {
 #define QK_BSGS64(NA_, SG_)                                                                           \
     run_encode<uint64_t>(ctx, k_encode_u64_bsgs<NA_, SG_>, k_finalize_u64, 8 * NA_, 2, ids, n, head, T,     \
                          (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
         switch ((T + 7) / 8) {   // NA <= 9: a wave's <= 16 MACs all scalar-counted
+        case 2: return QK_BSGS64(2, 16);
         case 3: return QK_BSGS64(3, 16);
         case 4: return QK_BSGS64(4, 16);
         case 5: return QK_BSGS64(5, 16);

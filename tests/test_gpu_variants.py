@@ -17,7 +17,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "u32_xcache": 1, "u64_xcache": 1,
+DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "bsgs64_tmin": 14, "u32_xcache": 1, "u64_xcache": 1,
             "bsgs_shapes": 1}
 
 
@@ -136,6 +136,16 @@ def test_u64_bsgs_off_matches_chain():
     """The power-chain path the u64 BSGS kernel replaced gives the same sums."""
     with knob("bsgs64_off", 1):
         res = _run(64, [("t80", 200_001, 80, 1), ("t75", 3001, 75, 0)])
+    assert all(res.values()), res
+
+
+@pytest.mark.parametrize("tmin", [9, 81])
+def test_u64_bsgs_small_thresholds(tmin):
+    """u64 t = 9..20 on the baby-step/giant-step kernel (NA = 2, 3; knob
+    bsgs64_tmin = 9) and on the power chain (81), against the oracle."""
+    cases = [(f"t{t}", 50_003 + t, t, t % 2) for t in (9, 12, 13, 14, 16, 17, 20, 21)]
+    with knob("bsgs64_tmin", tmin):
+        res = _run(64, cases)
     assert all(res.values()), res
 
 

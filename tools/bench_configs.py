@@ -315,12 +315,16 @@ def run_micro(args, ctx):
           "cpu_port_1core_ids_per_s": m / cs, "parity": q.power_sums() == S})
 
 
+def sweep_ts(args, default):
+    return tuple(int(x) for x in args.sweep_t.split(",")) if args.sweep_t else default
+
+
 def run_sweep(args, ctx):
     n = int(args.nsweep)
     ids = torch.empty(n, dtype=torch.int32, device=DEV)
     fill_splitmix(ctx, ids, 0x5EED0002)
-    for t in (1, 4, 8, 10, 16, 17, 20, 24, 25, 28, 30, 32, 33, 36, 40, 42, 48, 50, 56, 60, 64, 70, 72, 80, 96, 128,
-              176, 256, 300, 512, 1024):
+    for t in sweep_ts(args, (1, 4, 8, 10, 16, 17, 20, 24, 25, 28, 30, 32, 33, 36, 40, 42, 48, 50, 56, 60, 64, 70, 72, 80,
+                             96, 128, 176, 256, 300, 512, 1024)):
         wall, kern = time_encode(ctx, ids, t, 32, max(3, args.steps // 2))
         emit({"config": f"encode u32 t={t}", "n": n, "ids_per_s": n / kern, "ns_per_id_per_power": kern / n / t * 1e9 * 1})
 
@@ -330,7 +334,7 @@ def run_sweep64(args, ctx):
     ids = torch.empty(n, dtype=torch.int64, device=DEV)
     fill_splitmix(ctx, ids, 0x5EED0003, bits=64)
     path = "chain" if "bsgs64_off=1" in args.knob else "default"
-    for t in (8, 9, 16, 17, 24, 32, 40, 48, 56, 64, 72, 80, 81, 128, 160, 256, 512, 1024):
+    for t in sweep_ts(args, (8, 9, 12, 16, 17, 20, 24, 32, 40, 48, 56, 64, 72, 80, 81, 128, 160, 256, 512, 1024)):
         wall, kern = time_encode(ctx, ids, t, 64, max(3, args.steps // 2))
         emit({"config": f"encode u64 t={t} ({path})", "n": n, "ids_per_s": n / kern,
               "ns_per_id_per_power": kern / n / t * 1e9})
@@ -346,6 +350,7 @@ def main():
     ap.add_argument("--ndec", type=float, default=1e8)
     ap.add_argument("--nhost", type=float, default=1e9)
     ap.add_argument("--nsweep", type=float, default=2.5e8)
+    ap.add_argument("--sweep-t", default="", help="sweep / sweep64: thresholds (comma list) instead of the default set")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--cpu-sample64", type=float, default=5e6)
     ap.add_argument("--cpu-sample-dec", type=float, default=2e7)
