@@ -242,7 +242,7 @@ struct Cfg {
     static_assert(!XC_ || FOLD_ == 1, "the x^base cache goes with min-tracked folds");
     static constexpr int ROWS = OFF_ ? NA_ : NA_ - 1;   // MAC rows
     static constexpr int ROW1 = OFF_ ? 0 : 1;           // group-row number of the first MAC row
-    static_assert(NB % 2 == 0 && NA >= 2, "NB even, NA >= 2");
+    static_assert(NB % 2 == 0 && (NA >= 2 || (OFF_ && NA == 1)), "NB even, NA >= 2 (1: offset pass)");
     static_assert(!OFF_ || FOLD_ == 1, "offset passes use min-tracked folds");
 };
 

@@ -253,7 +253,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                                      uint64_t *__restrict__ partials, uint32_t base = 0,
                                      const uint64_t *__restrict__ xin = nullptr, uint64_t *__restrict__ xout = nullptr) {
     static_assert(OFF || (XC & 1) == 0, "only an offset pass reads x^base");
-    static_assert(NA >= 2 && NA <= 10, "giant rows");
+    static_assert((NA >= 2 || (OFF && NA == 1)) && NA <= 10, "giant rows");
     static_assert(!(BSH && PF) && !(LD && PF), "prefetch form: stored B * 2^32, all rows");
     constexpr int NR = OFF ? NA : NA - 1;        // MAC rows (giants x^8 .. x^(8 NR), or x^base ..)
     constexpr bool G8 = BSH && !OFF;             // giant row 0 (x^8) read from baby 8

@@ -833,7 +833,8 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
              : run_pass<1>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 0>, 8 * NA_, ids, n, head, Tp, base,      \
                               out + base, meta, acc, s))
             switch ((Tp + 7) / 8) {
-            case 0: case 1: case 2: rc = QK_LAST32(2); break;
+            case 1: rc = QK_LAST32(1); break;   // <= 8 powers: one giant row (x^base)
+            case 2: rc = QK_LAST32(2); break;
             case 3: rc = QK_LAST32(3); break;
             case 4: rc = QK_LAST32(4); break;
             default: rc = QK_LAST32(5); break;
@@ -946,7 +947,8 @@ static int enc64_passes_chunk(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32
         if (xcm & 2) {   // a middle pass: Tp = 80
             rc = run_pass64<10, 3>(ctx, ids, n, head, Tp, base, o, nullptr, acc, s, xc);
         } else {
-            switch (std::max<uint32_t>(2, (Tp + 7) / 8)) {
+            switch ((Tp + 7) / 8) {   // a last pass of <= 8 powers: one giant row (x^base)
+            case 1: rc = QK_PASS64(1); break;
             case 2: rc = QK_PASS64(2); break;
             case 3: rc = QK_PASS64(3); break;
             case 4: rc = QK_PASS64(4); break;

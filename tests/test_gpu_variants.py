@@ -109,10 +109,12 @@ def test_u32_passes_xbase_cache(xcache):
     """u32 thresholds > 128 run two or more offset passes; with the per-id
     x^base cache (the default) pass 1 writes x^128 per id, the middle passes
     read and write it, the last one reads it — against the oracle with an
-    unaligned head, ragged tails, a partial last pass (t = 129, 250, 300) and
+    unaligned head, ragged tails, a partial last pass (t = 129, 250, 300; one
+    giant row at t = 81, 88, 129, 136) and
     the 20-pass maximum (t = 1024); knob u32_xcache = 0 is the
     square-and-multiply form."""
-    cases = [("t129", 300_001, 129, 1), ("t176", 100_003, 176, 3), ("t250", 65_537, 250, 2), ("t300", 40_009, 300, 0),
+    cases = [("t129", 300_001, 129, 1), ("t81", 70_001, 81, 2), ("t88", 50_021, 88, 0), ("t136", 30_011, 136, 1),
+             ("t176", 100_003, 176, 3), ("t250", 65_537, 250, 2), ("t300", 40_009, 300, 0),
              ("t1024", 20_011, 1024, 1), ("t1024_tiny", 9, 1024, 3)]
     with knob("u32_xcache", xcache):
         res = _run(32, cases)
@@ -123,9 +125,10 @@ def test_u32_passes_xbase_cache(xcache):
 def test_u64_passes_xbase_cache(xcache):
     """u64 thresholds > 160: offset passes of 80 powers hand x^(next base)
     on through the per-id cache (knob u64_xcache; 0 = square-and-multiply per
-    pass): a partial last pass (t = 161, 250), full passes only (t = 240) and
+    pass): a partial last pass (t = 161, 250; one giant row at t = 81, 88, 161), full passes only (t = 240) and
     the 13-pass maximum (t = 1024), with ragged tails and a head offset."""
-    cases = [("t161", 100_003, 161, 1), ("t240", 50_001, 240, 0), ("t250", 30_011, 250, 2), ("t1024", 8_009, 1024, 1),
+    cases = [("t161", 100_003, 161, 1), ("t81", 70_001, 81, 0), ("t88", 60_013, 88, 1), ("t89", 20_011, 89, 1),
+             ("t240", 50_001, 240, 0), ("t250", 30_011, 250, 2), ("t1024", 8_009, 1024, 1),
              ("t1024_tiny", 5, 1024, 0)]
     with knob("u64_xcache", xcache):
         res = _run(64, cases)
