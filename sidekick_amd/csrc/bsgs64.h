@@ -196,6 +196,15 @@ __device__ __forceinline__ void row2(uint64_t (&lo)[2], uint64_t (&hi)[2], const
                      : QK_CLOB1);
 }
 
+// one baby's a = 0 row (a wave owning one baby, NBT = 4)
+__device__ __forceinline__ void row1(uint64_t &lo, uint64_t &hi, uint4 b) {
+    uint64_t c0, c1;
+    asm volatile("v_mad_u64_u32 %0, %2, %4, 1, %0\n\t"
+                 "v_mad_u64_u32 %1, %3, %5, 1, %1"
+                 : "+v"(lo), "+v"(hi), "=&s"(c0), "=&s"(c1)
+                 : "v"(b.x), "v"(b.y));
+}
+
 // (u128 value) mod p, canonical
 __device__ __forceinline__ uint64_t mod_p128(unsigned __int128 v) {
     // v = H 2^64 + L == 59 H + L; twice brings it below 2^64 + 59^2
@@ -213,14 +222,14 @@ __device__ __forceinline__ uint64_t mod_p128(unsigned __int128 v) {
 // the first giant x^8 is not stored twice (it is baby 8) — 32 KB instead of
 // 50 KB per workgroup at t = 80: 4 workgroups per CU instead of 3.
 // NG = giant rows stored.
-template <int NG, bool BSH = false>
+template <int NG, bool BSH = false, int NBB = NB>
 struct Smem {
-    uint4 bb[NB][BLOCK];
+    uint4 bb[NBB][BLOCK];
     uint2 ga[NG][BLOCK];
 };
-template <int NG>
-struct Smem<NG, true> {
-    uint2 bb[NB][BLOCK];
+template <int NG, int NBB>
+struct Smem<NG, true, NBB> {
+    uint2 bb[NBB][BLOCK];
     uint2 ga[NG > 0 ? NG : 1][BLOCK];
 };
 
@@ -247,34 +256,39 @@ struct Smem<NG, true> {
 //           cache xin (no square-and-multiply); bit 1 — the next pass's
 //           x^base per id written to xout: x^(base + 8 NA) after an offset
 //           pass, x^(8 NA) after pass 0
+//   NBT     babies per id: 8 (two per wave), or 4 (one per wave: thresholds
+//           t <= 40 waste fewer powers in 4-wide rows, and the babies and
+//           giants of an id cost 3 + NA - 2 products instead of 7 + NA - 2)
 template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0,
-          int XC = 0>
+          int XC = 0, int NBT = NB>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
                                      uint64_t *__restrict__ partials, uint32_t base = 0,
                                      const uint64_t *__restrict__ xin = nullptr, uint64_t *__restrict__ xout = nullptr) {
     static_assert(OFF || (XC & 1) == 0, "only an offset pass reads x^base");
     static_assert((NA >= 2 || (OFF && NA == 1)) && NA <= 10, "giant rows");
     static_assert(!(BSH && PF) && !(LD && PF), "prefetch form: stored B * 2^32, all rows");
+    static_assert(NBT == 8 || (NBT == 4 && BSH && !PF && XC == 0), "babies per id: 8, or 4 (plain BSH form)");
+    constexpr int CW = NBT / 4;                  // babies per wave
     constexpr int NR = OFF ? NA : NA - 1;        // MAC rows (giants x^8 .. x^(8 NR), or x^base ..)
     constexpr bool G8 = BSH && !OFF;             // giant row 0 (x^8) read from baby 8
     constexpr int NG = G8 ? NR - 1 : NR;
-    __shared__ Smem<NG, BSH> sm;
+    __shared__ Smem<NG, BSH, NBT> sm;
     auto giant = [&](int r, int j) -> uint2 {
-        if constexpr (G8) return r ? sm.ga[r - 1][j] : sm.bb[NB - 1][j];
+        if constexpr (G8) return r ? sm.ga[r - 1][j] : sm.bb[NBT - 1][j];
         else return sm.ga[r][j];
     };
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int cb = 2 * wave;                     // this wave's babies (b = cb+1, cb+2)
+    const int cb = CW * wave;                    // this wave's babies (b = cb+1 .. cb+CW)
 
     // a = 0 row: 64-bit sums of the halves; MAC tile: C0/C1 + carry counters
     uint64_t r0lo[2] = {0, 0}, r0hi[2] = {0, 0};
-    uint64_t C0[NR][2], C1[NR][2];
-    uint32_t K0[NR][2], K1[NR][2], KV[NR][2];
+    uint64_t C0[NR][CW], C1[NR][CW];
+    uint32_t K0[NR][CW], K1[NR][CW], KV[NR][CW];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) { C0[r][c] = 0; C1[r][c] = 0; K0[r][c] = 0; K1[r][c] = 0; KV[r][c] = 0; }
+        for (int c = 0; c < CW; ++c) { C0[r][c] = 0; C1[r][c] = 0; K0[r][c] = 0; K1[r][c] = 0; KV[r][c] = 0; }
 
     const uint64_t ntiles = (n + BLOCK - 1) / BLOCK;
     uint64_t tile = blockIdx.x;
@@ -290,7 +304,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
             uint64_t V = x;
 #pragma unroll
-            for (int b = 0; b < NB; ++b) {
+            for (int b = 0; b < NBT; ++b) {
                 if (b && ABL != 2) mulv(V, x0, x1);
                 if constexpr (BSH) {
                     sm.bb[b][tid] = make_uint2((uint32_t)V, (uint32_t)(V >> 32));
@@ -299,12 +313,12 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                     sm.bb[b][tid] = make_uint4((uint32_t)V, (uint32_t)(V >> 32), (uint32_t)sh, (uint32_t)(sh >> 32));
                 }
             }
-            const uint32_t g0 = (uint32_t)V, g1 = (uint32_t)(V >> 32);   // x^8
+            const uint32_t g0 = (uint32_t)V, g1 = (uint32_t)(V >> 32);   // x^NBT
             if constexpr ((XC & 1) != 0) {
                 V = nxc;   // x^base from the previous pass
             } else if constexpr (OFF) {
                 // x^base = (x^8)^(base/8): square-and-multiply, uniform exponent
-                uint32_t q = base / NB;
+                uint32_t q = base / NBT;
                 uint64_t r = 0, sq = V;
                 bool have = false;
                 for (;;) {
@@ -342,7 +356,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
         // ---- step 3: this wave's 2 x NR MACs over the 256 ids (4 per lane)
         // PF: the next chunk's operands are read from LDS while this chunk's
         // MACs run (double-buffered registers, the chunk loop unrolled)
-        uint4 nbv[2];
+        uint4 nbv[CW];
         uint2 ng[NR];
         if constexpr (PF) {
             nbv[0] = sm.bb[cb][lane];
@@ -354,7 +368,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
 #pragma unroll UNR
         for (int q = 0; q < BLOCK / 64; ++q) {
             const int j = q * 64 + lane;
-            uint4 bv[2];
+            uint4 bv[CW];
             uint2 g[NR];
             if constexpr (PF) {
                 bv[0] = nbv[0];
@@ -370,7 +384,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             } else {
                 if constexpr (BSH) {
 #pragma unroll
-                    for (int c = 0; c < 2; ++c) {
+                    for (int c = 0; c < CW; ++c) {
                         const uint2 B = sm.bb[cb + c][j];
                         const uint64_t sh = shift32(((uint64_t)B.y << 32) | B.x);
                         bv[c] = make_uint4(B.x, B.y, (uint32_t)sh, (uint32_t)(sh >> 32));
@@ -384,7 +398,8 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                     for (int r = 0; r < NR; ++r) g[r] = giant(r, j);
                 }
             }
-            if constexpr (!OFF) row2<1>(r0lo, r0hi, bv);
+            if constexpr (!OFF && CW == 2) row2<1>(r0lo, r0hi, bv);
+            if constexpr (!OFF && CW == 1) row1(r0lo[0], r0hi[0], bv[0]);
             // LD: one giant row's operands in flight while the previous row's
             // MACs run (2 rows live instead of NR: fewer VGPRs)
             uint2 gn;
@@ -398,8 +413,8 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                         __builtin_amdgcn_sched_barrier(0);
                     }
 #pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int m = r * 2 + c;   // MAC index in the tile: parity picks the SGPR set
+                    for (int c = 0; c < CW; ++c) {
+                        const int m = r * CW + c;   // MAC index in the tile: parity picks the SGPR set
                         if constexpr (MODE == 1) {
                             if (m % 2 == 0) mac_m<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                             else mac_m<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
@@ -421,9 +436,9 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     // the tile operands are dead after the loop's last barrier: the reduction
     // reuses their LDS (a separate array pushes the offset pass with NA = 10
     // past 1/3 of the CU's LDS, i.e. to 2 workgroups per CU)
-    static_assert(sizeof(Smem<NG, BSH>) >= 2 * NB * NA * sizeof(unsigned long long), "reduction space");
+    static_assert(sizeof(Smem<NG, BSH, NBT>) >= 2 * NBT * NA * sizeof(unsigned long long), "reduction space");
     unsigned long long *red = reinterpret_cast<unsigned long long *>(&sm);
-    for (int i = tid; i < 2 * NB * NA; i += BLOCK) red[i] = 0;
+    for (int i = tid; i < 2 * NBT * NA; i += BLOCK) red[i] = 0;
     __syncthreads();
     auto put = [&](int m, uint64_t v) {   // v canonical; m = power - 1
         uint64_t lo = (uint32_t)v, hi = v >> 32;
@@ -439,13 +454,13 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     };
     const uint64_t W1 = 59ull << 32;   // 2^96 mod p
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < CW; ++c)
         if constexpr (!OFF) put(cb + c, mod_p128((unsigned __int128)r0lo[c] + ((unsigned __int128)r0hi[c] << 32)));
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int m = r * 2 + c;
+        for (int c = 0; c < CW; ++c) {
+            const int m = r * CW + c;
             unsigned __int128 v = (unsigned __int128)C0[r][c] + ((unsigned __int128)C1[r][c] << 32);
             // scalar counts are the wave's totals: added once, by lane 0
             const bool s0 = MODE == 1 || m < SG, s1 = MODE == 0 && m < SG;
@@ -453,7 +468,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             uint64_t k1 = s1 ? (lane == 0 ? K1[r][c] : 0u) : K1[r][c];
             if (MODE == 1) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];
             v += (unsigned __int128)k0 * C64 + (unsigned __int128)k1 * W1;
-            put((r + (OFF ? 0 : 1)) * NB + cb + c, mod_p128(v));
+            put((r + (OFF ? 0 : 1)) * NBT + cb + c, mod_p128(v));
         }
     }
     __syncthreads();

@@ -614,6 +614,16 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs(const uint
     bsgs64::body<NA, 0, SG, 0, 0, false, true, 1>(ids, n, T, partials);
 }
 
+// the same with four babies per id (one per wave) and NA giant rows of 4
+// powers: t <= 40 (bsgs64.h NBT)
+template <int NA>
+__global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs4(const uint64_t *__restrict__ ids, uint64_t n,
+                                                                       uint32_t head, uint32_t T,
+                                                                       uint64_t *__restrict__ partials) {
+    (void)head;
+    bsgs64::body<NA, 0, 16, 0, 0, false, true, 1, 0, 4>(ids, n, T, partials);
+}
+
 // Pass 0 of a u64 multi-pass encode that also writes x^80 per id for pass 1
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_x80(const uint64_t *__restrict__ ids,
                                                                           uint64_t n, uint32_t head, uint32_t T,
@@ -1183,6 +1193,21 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
 #define QK_BSGS64(NA_, SG_)                                                                           \
     run_encode<uint64_t>(ctx, k_encode_u64_bsgs<NA_, SG_>, k_finalize_u64, 8 * NA_, 2, ids, n, head, T,     \
                          (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
+#define QK_BSGS64_4(NA_)                                                                              \
+    run_encode<uint64_t>(ctx, k_encode_u64_bsgs4<NA_>, k_finalize_u64, 4 * NA_, 2, ids, n, head, T,         \
+                         (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
+        // four babies per id and ceil(T/4) giant rows (knob bsgs64_shapes)
+        if (ctx->knobs.bsgs64_shapes && T <= 40) switch ((T + 3) / 4) {
+            case 4: return QK_BSGS64_4(4);
+            case 5: return QK_BSGS64_4(5);
+            case 6: return QK_BSGS64_4(6);
+            case 7: return QK_BSGS64_4(7);
+            case 8: return QK_BSGS64_4(8);
+            case 9: return QK_BSGS64_4(9);
+            case 10: return QK_BSGS64_4(10);
+            default: break;
+            }
+#undef QK_BSGS64_4
         switch ((T + 7) / 8) {   // NA <= 9: a wave's <= 16 MACs all scalar-counted
         case 2: return QK_BSGS64(2, 16);
         case 3: return QK_BSGS64(3, 16);
