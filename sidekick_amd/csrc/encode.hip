@@ -1197,14 +1197,14 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     run_encode<uint64_t>(ctx, k_encode_u64_bsgs4<NA_>, k_finalize_u64, 4 * NA_, 2, ids, n, head, T,         \
                          (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
         // four babies per id and ceil(T/4) giant rows (knob bsgs64_shapes)
-        if (ctx->knobs.bsgs64_shapes && T <= 40) switch ((T + 3) / 4) {
+        // where 8 babies would compute 4+ powers more: t = 14..20, 25..28,
+        // 33..36 (+8..17 %, profiles/r03/shapes/sweep64_four_babies_ab.jsonl;
+        // at t = 21..24, 29..32 even, at 37..40 7 % slower: not used)
+        if (ctx->knobs.bsgs64_shapes && T <= 36) switch ((T + 3) / 4) {
             case 4: return QK_BSGS64_4(4);
             case 5: return QK_BSGS64_4(5);
-            case 6: return QK_BSGS64_4(6);
             case 7: return QK_BSGS64_4(7);
-            case 8: return QK_BSGS64_4(8);
             case 9: return QK_BSGS64_4(9);
-            case 10: return QK_BSGS64_4(10);
             default: break;
             }
 #undef QK_BSGS64_4

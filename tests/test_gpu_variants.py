@@ -17,7 +17,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "bsgs64_tmin": 14, "bsgs64_shapes": 0, "u32_xcache": 1, "u64_xcache": 1,
+DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "bsgs64_tmin": 14, "bsgs64_shapes": 1, "u32_xcache": 1, "u64_xcache": 1,
             "bsgs_shapes": 1}
 
 
@@ -154,9 +154,10 @@ def test_u64_bsgs_small_thresholds(tmin):
 
 @pytest.mark.parametrize("shapes", [1, 0])
 def test_u64_bsgs_four_babies(shapes):
-    """u64 t = 14..40 with four babies per id and ceil(t/4) giant rows (one
-    baby per wave) and with the 8-baby kernel it replaced (knob
-    bsgs64_shapes = 0), against the oracle at both ends of each row count."""
+    """u64 t = 14..20, 25..28, 33..36 with four babies per id and ceil(t/4)
+    giant rows (one baby per wave) and with the 8-baby kernel it replaced
+    (knob bsgs64_shapes = 0), against the oracle at both ends of each range
+    and at the thresholds that stay on 8 babies."""
     cases = [(f"t{t}", 40_009 + t, t, t % 2) for t in (14, 16, 17, 20, 21, 24, 25, 28, 32, 33, 36, 37, 40, 41)]
     with knob("bsgs64_shapes", shapes):
         res = _run(64, cases)
