@@ -24,9 +24,16 @@ Rank 0 prints ONE JSON line.  Alongside the metric it reports
                 u32 id) over its average launch duration, measured with HIP
                 events on the launch stream, against the 8 TB/s HBM3E peak;
                 and `valu`, the integer-issue roofline that actually binds
-                (tools/issue_roofline.py: the kernel's measured VALU
-                instructions per id x their issue cost, against the SIMD
-                cycles the launch spent per id);
+                (tools/issue_model.py: the decomposition's VALU work per id
+                at the measured issue costs, against the SIMD cycles the
+                launch spent per id at this run's shader clock, read by
+                qk_clock_probe beside the running kernel after the timed
+                region);
+  parity        N > 1: after the timed region, the N = 1 stream cut into N
+                shards and encoded through the same communicator; its digest
+                against rank 0's single-GPU encode and the recorded N = 1
+                digest; `rccl` / `ranks`: what RCCL reports on every rank
+                (ncclCommCount, ncclCommCuDevice, ncclCommUserRank);
   cpu_baseline  the oracle's scalar C restatement of the reference insert
                 loop on ONE host core over a bounded prefix of the same
                 stream (rank 0, N = 1 only), with a GPU/CPU parity check on
@@ -63,31 +70,80 @@ def load_traffic(bits: int, t: int, n: int):
         return None, None
 
 
-def valu_roofline(bits: int, t: int, n: int, kern_avg_ms: float):
-    """The integer-issue roofline of the encode kernel (tools/issue_roofline.py,
-    profiles/r03/issue_roofline.json): peak = the measured VALU
-    wave-instructions per id x the mean issue cost of the kernel's hot-loop
-    mix; achieved = the SIMD-cycles per id of THIS run's kernel time at the
-    effective clock of the committed counter run (GRBM_GUI_ACTIVE / 8 / its
-    kernel time)."""
-    path = os.path.join(ROOT, "profiles", "r03", "issue_roofline.json")
-    key = {(32, 32): "encode_u32_t32", (64, 80): "encode_u64_t80"}.get((bits, t))
+def valu_roofline(bits: int, t: int, n: int, kern_avg_ms: float, clock_ghz):
+    """The integer-issue roofline (tools/issue_model.py): the decomposition's
+    VALU work per id at the measured per-class issue costs — fixed per t, so
+    instruction bloat lowers the fraction — against the SIMD-cycles per id of
+    THIS run's kernel time at THIS run's shader clock (measure_clock)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import issue_model
+    return issue_model.roofline(bits, t, n, kern_avg_ms, clock_ghz)
+
+
+def measure_clock(ctx, step, dev_index, kern_avg_ms, steps=10):
+    """The shader clock the chip holds under this kernel, in this run: after
+    the timed region, qk_clock_probe's one wave spins on a side stream for
+    ~90 % of `steps` further (untimed) steps and reads s_memtime against
+    s_memrealtime (100 MHz).  Returns GHz or None."""
+    import torch
     try:
-        with open(path) as f:
-            k = json.load(f)["kernels"][key]
-    except Exception:
+        out = torch.zeros(2, dtype=torch.int64, device=f"cuda:{dev_index}")
+        side = torch.cuda.Stream(device=dev_index)
+        for _ in range(2):
+            step()                                   # the chip busy before the probe lands
+        us = max(1000, int(kern_avg_ms * steps * 0.9 * 1e3))
+        ctx.clock_probe_async(us, out, side.cuda_stream)
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        c, r = (int(v) for v in out.cpu().tolist())
+        return c / r * 0.1 if r > 0 else None
+    except Exception as e:  # noqa: BLE001 — a measurement aid, never fatal
+        log(f"clock probe failed: {e!r}")
         return None
-    clock = k["clock_ghz"] * 1e9
-    achieved = clock * kern_avg_ms * 1e-3 * 1024 / n
-    peak = k["issue_cycles_per_unit_peak"]
-    return {
-        "bound": "valu-issue", "unit": "SIMD-cycles/id",
-        "valu_insts_per_id": k["valu_insts_per_unit"], "salu_insts_per_id": k["salu_insts_per_unit"],
-        "mean_issue_cycles_per_valu": k["mean_issue_cycles_per_valu"],
-        "peak": peak, "achieved": achieved, "frac": peak / achieved,
-        "clock_ghz": k["clock_ghz"], "frac_counter_run": k["frac"], "salu_busy_counter_run": k["salu_busy"],
-        "source": os.path.relpath(path, ROOT),
-    }
+
+
+# Digest of the folded power sums of the N = 1 stream (configs[1]: 1e9 u32
+# ids, t = 32, seed 0x5EED0002): unchanged since round 1 (BENCH_r01..r03).
+RECORDED_DIGESTS = {(32, 32, 1_000_000_000, 0x5EED0002): "523499db79543cdf"}
+
+
+def digest_of(S, count) -> str:
+    import hashlib
+    return hashlib.sha256((",".join(str(v) for v in S) + f"|{count}").encode()).hexdigest()[:16]
+
+
+def strong_scaling_check(args, comm, ctx, ids, rank, world, dev_index, bits, t):
+    """N > 1, untimed: the N = 1 stream (--ids-per-gpu ids, the same seed) cut
+    into `world` contiguous shards, each filled on its own GPU and encoded
+    through the same communicator (one reduce to rank 0); rank 0 then encodes
+    the whole stream alone on its GPU.  Returns (on rank 0) the sharded digest,
+    the single-GPU digest and the recorded N = 1 digest."""
+    import torch
+    import sidekick_amd as sk
+    from sidekick_amd import dist as skd
+    from sidekick_amd.quack import fill_splitmix
+    Q = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+    n1 = int(args.ids_per_gpu)
+    s, c = skd.shard(n1, rank, world)
+    view = ids[:c]
+    fill_splitmix(ctx, view, args.seed, s, bits=bits)
+    torch.cuda.synchronize()
+    q = Q(t)
+    comm.encode_sharded([view], q)
+    if rank != 0:
+        return None
+    sharded = digest_of(q.power_sums(), q.count())
+    fill_splitmix(ctx, ids[:n1], args.seed, 0, bits=bits)
+    q1 = Q(t)
+    q1.insert_batch(ids[:n1], ctx=ctx)
+    single = digest_of(q1.power_sums(), q1.count())
+    rec = RECORDED_DIGESTS.get((bits, t, n1, args.seed))
+    return {"workload": f"strong scaling, untimed: the N=1 stream ({n1:.0e} u{bits} ids, seed {hex(args.seed)}) in "
+                        f"{world} contiguous shards, one per rank, encoded through the same communicator",
+            "digest": sharded, "digest_single_gpu": single, "equals_n1": sharded == single,
+            "recorded_n1_digest": rec, "equals_recorded": (sharded == rec) if rec else None,
+            "last_value_equal": q.last_value() == q1.last_value()}
 
 
 # The published crate at the metric's threshold: benchmark_construct on one
@@ -112,6 +168,24 @@ def host_cpu():
     return model, mhz, os.cpu_count() or 1
 
 
+def usable_cpus():
+    """(CPUs this process may run on, how that was derived): its CPU affinity,
+    capped by the cgroup CPU quota when one is set (a GPU box's share of a
+    256-CPU host is 16 CPUs; os.cpu_count() shows the whole host)."""
+    aff = len(os.sched_getaffinity(0))
+    n, how = aff, f"sched_getaffinity: {aff}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            how += f", cgroup cpu.max quota {int(quota) / int(period):g} CPUs"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    return n, how
+
+
 def cpu_baselines(args, bits, t, start, cnt, ids):
     """The oracle's scalar restatement of the reference insert loop, timed on
     this host over a bounded prefix of the same stream, with the ids
@@ -133,19 +207,26 @@ def cpu_baselines(args, bits, t, start, cnt, ids):
     model, mhz, ncpu = host_cpu()
     pub = PUBLISHED_NS_PER_ID.get((bits, t))
     host = f"host {model}, {ncpu} logical CPUs" + (f", cpu0 at {mhz:.0f} MHz" if mhz else "")
+    ns_id = cpu_s / m * 1e9
+    cpp = ns_id * mhz * 1e-3 / t if mhz else None          # cycles per power at cpu0's reported clock
+    pub_cpp = pub * 2.256 / t if pub else None              # the crate: rdtsc ~2.256 GHz
     one = {
         "value": m / cpu_s, "unit": "identifiers/s", "cores": 1, "kind": "port",
-        "ns_per_id": cpu_s / m * 1e9,
+        "ns_per_id": ns_id, "cycles_per_power": cpp,
         "sample": f"first {m} ids of the same stream (seed {hex(args.seed)}), pre-generated, inserted by the "
                   f"scalar C restatement of the reference insert loop (oracle/quack_oracle.c qo_encode_u{bits}), "
-                  f"1 core, {cpu_s:.1f} s = {cpu_s / m * 1e9:.1f} ns/id; {host}"
+                  f"1 core, {cpu_s:.1f} s = {ns_id:.1f} ns/id"
+                  + (f" = {cpp:.1f} cycles per power at cpu0's {mhz:.0f} MHz" if cpp else "") + f"; {host}"
                   + (f"; the published crate: {pub} ns/id at u{bits} t={t} on one Xeon E5 core at ~2.26 GHz "
-                     f"(BASELINE.md)" if pub else ""),
+                     f"= {pub_cpp:.1f} cycles per power (BASELINE.md), so per clock this port is "
+                     f"{cpp / pub_cpp:.1f}x slower than the crate and GPU/CPU ratios against it overstate the "
+                     f"gap to the crate by that factor" if pub and cpp else ""),
         "published_crate_ns_per_id": pub,
+        "published_crate_cycles_per_power": pub_cpp,
         "parity_with_gpu": parity,
     }
-    thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or ncpu
-    thr = max(1, min(thr, 64))
+    thr, how = usable_cpus()
+    thr = max(1, min(thr, 256))
     mm = int(min(m * thr // 3, cnt))           # ~1/3 of the 1-core sample per thread
     host_mm = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(args.seed, mm, start)
     tc = time.perf_counter()
@@ -157,7 +238,8 @@ def cpu_baselines(args, bits, t, start, cnt, ids):
     allc = {
         "value": mm / mt_s, "unit": "identifiers/s", "cores": thr, "kind": "port",
         "sample": f"first {mm} ids of the same stream, pre-generated, {thr} threads x {mm // thr} ids, one partial "
-                  f"sketch per thread merged (oracle/quack_oracle.c qo_encode_mt), {mt_s:.1f} s; {host}",
+                  f"sketch per thread merged (oracle/quack_oracle.c qo_encode_mt), {mt_s:.1f} s; threads = the "
+                  f"CPUs this process may use ({how}); {host}",
         "parity_with_gpu": q.power_sums() == mt_S,
     }
     return one, allc
@@ -281,8 +363,26 @@ def main():
         else:
             S, count = skd.fold_partial_sum(part_host, t, bits)
         log(f"encode result: count={count} S[0..3]={S[:3]}")
-        import hashlib
-        digest = hashlib.sha256((",".join(str(v) for v in S) + f"|{count}").encode()).hexdigest()[:16]
+        digest = digest_of(S, count)
+
+    # untimed, after the timed region: this run's shader clock under the
+    # kernel (roofline.valu), and for N > 1 the strong-scaling parity pass and
+    # what RCCL itself reports on every rank
+    clock_ghz = measure_clock(ctx, step, dev_index, kern_avg_ms)
+    if comm is not None:   # drain the probe's steps (the root merges into a throwaway sketch)
+        comm.encode_sharded_wait((sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t))
+    strong = None
+    ranks = None
+    if world > 1:
+        strong = strong_scaling_check(args, comm, ctx, ids, rank, world, dev_index, bits, t)
+        info = comm.rccl_info()
+        props = torch.cuda.get_device_properties(dev_index)
+        mine = {"rank": rank, "local_rank": local, "device": dev_index,
+                "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")),
+                "rccl_count": info[0] if info else None, "rccl_device": info[1] if info else None,
+                "rccl_rank": info[2] if info else None}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
 
     if rank != 0:
         if world > 1:
@@ -296,7 +396,7 @@ def main():
     value = n_total * args.steps / elapsed
     achieved_gbs = bytes_per_id * cnt / (kern_avg_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(bits, t, cnt)
-    valu = valu_roofline(bits, t, cnt, kern_avg_ms)
+    valu = valu_roofline(bits, t, cnt, kern_avg_ms, clock_ghz)
 
     out = {
         "metric": f"quACK encode identifiers/s (device-resident), u{bits} ids, threshold t={t}",
@@ -335,9 +435,22 @@ def main():
             "valu": valu,
         },
         "cpu_baseline": None,
+        "clock_ghz": clock_ghz,
         "result": {"count": count, "power_sums_head": S[:4], "digest": digest,
-                   "note": "sha256 of the folded power sums of the whole global stream (identical for any N)"},
+                   "note": "sha256 of the folded power sums of the whole global stream of this run "
+                           "(N x ids-per-gpu ids)"},
     }
+    rec = RECORDED_DIGESTS.get((bits, t, n_total, args.seed))
+    if rec:
+        out["result"]["equals_recorded"] = digest == rec
+    if world > 1:
+        out["parity"] = strong
+        out["ranks"] = ranks
+        if data_path == "rccl":
+            out["rccl"] = {"ranks_reported": sorted({r["rccl_count"] for r in ranks}),
+                           "all_ranks_joined": all(r["rccl_count"] == world for r in ranks),
+                           "devices": [r["rccl_device"] for r in ranks],
+                           "user_ranks": [r["rccl_rank"] for r in ranks]}
 
     if world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"], out["cpu_baseline_all_cores"] = cpu_baselines(args, bits, t, start, cnt, ids)

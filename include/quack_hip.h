@@ -160,9 +160,16 @@ int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
  * "bsgs_sg", "bsgs_shapes", "u32_passes", "u32_xcache", "bsgs64_sg", "bsgs64_off", "bsgs64_tmin", "bsgs64_shapes", "u64_passes",
  * "u64_xcache", "u64_kmax", "flow_load" (2..64), "flow_wgpc", "flow_hist",
  * "pkt_fused", "rt64_horner",
- * "root_test" (0 automatic, 1 Horner, 2 root-set scan).  Unknown name or
- * out-of-range value -> QK_E_INVAL. */
+ * "root_test" (0 automatic, 1 Horner, 2 root-set scan), "comm_fault" (tests:
+ * the k-th collective's payload staging of this context's rank fails once).
+ * Unknown name or out-of-range value -> QK_E_INVAL. */
 int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value);
+/* Shader-clock probe (measurement): one wave on `stream` spins for
+ * `microseconds` of wall time and writes d_out[0] = shader-clock ticks
+ * (s_memtime) and d_out[1] = 100 MHz ticks (s_memrealtime) elapsed, so the
+ * clock is d_out[0] / d_out[1] * 100 MHz.  Launched beside running kernels it
+ * reads the clock the chip holds under their load. */
+int qk_clock_probe(qk_ctx *ctx, uint32_t microseconds, uint64_t *d_out, void *stream);
 /* Pinned host memory for the host-input path: ids written here by the
  * sniffer are DMA'd without a staging copy. */
 int qk_host_alloc(size_t bytes, void **out);
@@ -330,11 +337,17 @@ int qk_u64_decode_device(qk_ctx *ctx, const qk_u64 *diff, const uint64_t *d_log,
  * stream, and the given stream is ordered after it.  Every rank of the
  * communicator must make the same sequence of collective calls with the same
  * threshold and root.
- * Failure semantics: a rank whose own arguments or local work fail still
- * takes part in every collective of the call (its failure travels as data),
- * so no peer is left blocked; see each call for what every rank returns.  A
- * failed collective aborts the communicator (ncclCommAbort): that call and
- * every later one return QK_E_COMM; destroy it.
+ * Failure semantics: a rank whose own arguments or local work fail — including
+ * the staging copy of its payload into a collective — still takes part in
+ * every collective of the call (its failure travels as data), so no peer is
+ * left blocked; see each call for what every rank returns.  A failed
+ * collective, or a rank that cannot read what a collective delivered, aborts
+ * the communicator (ncclCommAbort): that call and every later one return
+ * QK_E_COMM; destroy it.  An abort releases this process's ranks only; a peer
+ * in another process is released by its own timeout: every wait on an RCCL
+ * collective polls ncclCommGetAsyncError and aborts after the communicator's
+ * timeout (qk_comm_set_timeout; a host channel's callbacks time out
+ * themselves).
  * ---------------------------------------------------------------------- */
 typedef struct qk_comm qk_comm;
 #define QK_COMM_ID_BYTES 128
@@ -364,6 +377,15 @@ int qk_comm_info(const qk_comm *comm, int *world, int *nlocal, int *first_rank);
 int qk_comm_context(qk_comm *comm, int local, qk_ctx **out);
 /* all ranks reach this point (one 8-byte reduce), then the local streams drain */
 int qk_comm_barrier(qk_comm *comm);
+/* Waits on RCCL collectives give up after `ms` milliseconds (0: never;
+ * default 300 000), abort the communicator and return QK_E_COMM — the bound
+ * on how long a rank waits for a peer that failed in another process. */
+int qk_comm_set_timeout(qk_comm *comm, int64_t ms);
+/* What RCCL itself reports for local rank `local`: ncclCommCount (ranks),
+ * ncclCommCuDevice (device), ncclCommUserRank (rank) — e.g. to check that a
+ * multi-process launch joined one communicator of the expected size.
+ * QK_E_INVAL for a host-channel communicator (no RCCL communicator). */
+int qk_comm_rccl_info(const qk_comm *comm, int local, int *count, int *device, int *rank);
 
 /* Sharded encode: local rank i encodes d_ids[i][0 .. n[i]) on its GPU, then
  * one ncclReduce(sum, uint64) of its partial to global rank `root`:

@@ -153,6 +153,7 @@ extern "C" {
     pub fn qk_ctx_trim(ctx: *mut qk_ctx) -> c_int;
     pub fn qk_ctx_set_grid(ctx: *mut qk_ctx, blocks: u32) -> c_int;
     pub fn qk_ctx_set_knob(ctx: *mut qk_ctx, name: *const c_char, value: i64) -> c_int;
+    pub fn qk_clock_probe(ctx: *mut qk_ctx, microseconds: u32, d_out: *mut u64, stream: *mut c_void) -> c_int;
     pub fn qk_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
     pub fn qk_host_free(p: *mut c_void) -> c_int;
 
@@ -216,6 +217,9 @@ extern "C" {
     pub fn qk_comm_info(comm: *const qk_comm, world: *mut c_int, nlocal: *mut c_int, first_rank: *mut c_int) -> c_int;
     pub fn qk_comm_context(comm: *mut qk_comm, local: c_int, out: *mut *mut qk_ctx) -> c_int;
     pub fn qk_comm_barrier(comm: *mut qk_comm) -> c_int;
+    pub fn qk_comm_set_timeout(comm: *mut qk_comm, ms: i64) -> c_int;
+    pub fn qk_comm_rccl_info(comm: *const qk_comm, local: c_int, count: *mut c_int, device: *mut c_int,
+                             rank: *mut c_int) -> c_int;
     pub fn qk_u32_encode_sharded_async(comm: *mut qk_comm, d_ids: *const *const u32, n: *const usize, threshold: u32,
                                        root: c_int, streams: *const *mut c_void) -> c_int;
     pub fn qk_u64_encode_sharded_async(comm: *mut qk_comm, d_ids: *const *const u64, n: *const usize, threshold: u32,

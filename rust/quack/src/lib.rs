@@ -568,6 +568,17 @@ impl Comm {
     pub fn barrier(&self) -> Result<()> {
         check(unsafe { ffi::qk_comm_barrier(self.raw) })
     }
+    /// Bound (ms, 0 = none) on every wait for an RCCL collective; past it the
+    /// communicator aborts and the call returns QK_E_COMM.
+    pub fn set_timeout(&self, ms: i64) -> Result<()> {
+        check(unsafe { ffi::qk_comm_set_timeout(self.raw, ms) })
+    }
+    /// (ranks, device, rank) as RCCL reports them for local rank `local`.
+    pub fn rccl_info(&self, local: i32) -> Result<(i32, i32, i32)> {
+        let (mut k, mut d, mut r) = (0, 0, 0);
+        check(unsafe { ffi::qk_comm_rccl_info(self.raw, local, &mut k, &mut d, &mut r) })?;
+        Ok((k, d, r))
+    }
     fn check_local(&self, a: usize, b: usize) -> Result<()> {
         if a != self.nlocal || b != self.nlocal {
             return Err(QuackError { status: ffi::QK_E_INVAL });

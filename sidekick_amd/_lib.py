@@ -75,6 +75,7 @@ SIGNATURES = {
     "qk_ctx_kernel_stats": (C.c_int, [vp, C.POINTER(C.c_double), u64p]),
     "qk_ctx_set_grid": (C.c_int, [vp, C.c_uint32]),
     "qk_ctx_set_knob": (C.c_int, [vp, C.c_char_p, C.c_int64]),
+    "qk_clock_probe": (C.c_int, [vp, C.c_uint32, vp, vp]),
     "qk_ctx_trim": (C.c_int, [vp]),
     "qk_host_alloc": (C.c_int, [sz, C.POINTER(vp)]),
     "qk_host_free": (C.c_int, [vp]),
@@ -109,6 +110,8 @@ SIGNATURES = {
     "qk_comm_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "qk_comm_context": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
     "qk_comm_barrier": (C.c_int, [vp]),
+    "qk_comm_set_timeout": (C.c_int, [vp, C.c_int64]),
+    "qk_comm_rccl_info": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "qk_u32_encode_sharded_async": (C.c_int, [vp, vpp, szp, C.c_uint32, C.c_int, vpp]),
     "qk_u64_encode_sharded_async": (C.c_int, [vp, vpp, szp, C.c_uint32, C.c_int, vpp]),
     "qk_u32_encode_sharded_wait": (C.c_int, [vp, vp]),

@@ -543,7 +543,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"u64_xcache", &qk_knobs::u64_xcache, 0, 1},   {"u64_kmax", &qk_knobs::u64_kmax, 4, 40},
         {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
         {"flow_hist", &qk_knobs::flow_hist, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
-        {"root_test", &qk_knobs::root_test, 0, 2},
+        {"root_test", &qk_knobs::root_test, 0, 2},      {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
 #ifdef QK_WITH_MATRIX_CORES
         {"matrix_cores", &qk_knobs::matrix_cores, 0, 1},
 #endif
@@ -556,6 +556,31 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
             return QK_OK;
         }
     return QK_E_INVAL;
+}
+
+// one wave: wall time from s_memrealtime (100 MHz), shader cycles from
+// s_memtime; s_sleep between samples keeps the probe off the issue ports
+__global__ void k_clock_probe(uint64_t *out, uint64_t ticks) {
+    const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t c1, r1;
+    do {
+        __builtin_amdgcn_s_sleep(32);
+        c1 = __builtin_amdgcn_s_memtime();
+        r1 = __builtin_amdgcn_s_memrealtime();
+    } while (r1 - r0 < ticks);
+    if (threadIdx.x == 0) {
+        out[0] = c1 - c0;
+        out[1] = r1 - r0;
+    }
+}
+
+int qk_clock_probe(qk_ctx *ctx, uint32_t microseconds, uint64_t *d_out, void *stream) {
+    if (!ctx || !d_out || !microseconds || microseconds > 10000000u) return QK_E_INVAL;
+    if (!is_device_ptr(d_out)) return QK_E_INVAL;
+    QK_HIP_TRY(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, d_out, (uint64_t)microseconds * 100);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
 }
 
 int qk_host_alloc(size_t bytes, void **out) {

@@ -36,14 +36,20 @@
 // every collective of an operation; the only early returns precede the first
 // collective and test arguments every rank passes alike by contract
 // (threshold, root).  A local failure travels as data — the failed word of
-// the encode payload, the status word of the decode gather — and the gathered
-// statuses decide, identically on every rank, whether a further collective
-// runs.  No buffer is allocated between collectives (the payload buffer is
+// the encode payload, the status word of every decode exchange — and the
+// gathered statuses decide, identically on every rank, whether a further
+// collective runs: a rank that fails to stage its payload (the local copy
+// into the collective buffer) sends the failure marker instead and keeps
+// joining.  No buffer is allocated between collectives (the payload buffer is
 // sized for the largest operation at init; hits travel in fixed-size chunks).
-// A collective that fails leaves the communicator in an unknown state: its
-// RCCL communicators are aborted (ncclCommAbort, which also releases peers
-// blocked on them) and every later call returns QK_E_COMM.
-//
+// A collective that fails, or a rank that cannot read what a collective
+// delivered (so cannot follow the rest of the protocol), marks the
+// communicator broken: its RCCL communicators are aborted (ncclCommAbort) and
+// every later call returns QK_E_COMM.  An abort releases only this process's
+// ranks: peers in other processes are released by their own timeout — every
+// wait on an RCCL collective polls ncclCommGetAsyncError and gives up after
+// the communicator's timeout (qk_comm_set_timeout, default 300 s), aborting
+// in turn; a host channel's callbacks carry their own timeout.
 // Collectives go through RCCL (device buffers, the context's stream) or,
 // for a communicator made by qk_comm_init_host, through the caller's host
 // callbacks on the pinned mirror of the payload buffer: the same protocol
@@ -56,7 +62,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <rccl/rccl.h>
 #include <vector>
 
@@ -83,6 +91,8 @@ struct qk_comm {
     bool host = false;                // collectives through ops (qk_comm_init_host)
     qk_comm_host_ops ops{};
     bool broken = false;              // a collective failed: unusable
+    int64_t timeout_ms = 300000;      // waits on RCCL collectives give up (and abort) after this; 0: never
+    int step = 0;                     // collectives of the operation in progress (fault injection)
     // sharded encode in flight (qk_*_encode_sharded_async -> _wait)
     int pend_bits = 0;
     uint32_t pend_t = 0;
@@ -128,6 +138,25 @@ __global__ void k_comm_fail(uint64_t *buf, uint32_t words) {
     for (uint32_t j = threadIdx.x; j < words; j += blockDim.x) buf[j] = j + 1 == words ? 1 : 0;
 }
 
+static int init_local(Local &L, int device, int world) {
+    L.device = device;
+    if (int rc = qk_ctx_create(device, &L.ctx)) return rc;
+    QK_HIP_TRY(hipSetDevice(device));
+    QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_in, hipEventDisableTiming));
+    QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_out, hipEventDisableTiming));
+    const size_t w = coll_cap(world);
+    if (hipMalloc(&L.d_coll, w * 8) != hipSuccess) return QK_E_NOMEM;
+    if (hipHostMalloc(&L.h_coll, w * 8, hipHostMallocDefault) != hipSuccess) return QK_E_NOMEM;
+    return QK_OK;
+}
+
+enum class Op { Bcast, Gather };
+
+// a rank's failure marker in a decode exchange payload: the status word
+__global__ void k_comm_mark(uint64_t *buf, uint32_t idx, uint64_t value) {
+    if (threadIdx.x == 0) buf[idx] = value;
+}
+
 // order the local rank's stream after the caller's stream
 static int enter(Local &L) {
     QK_HIP_TRY(hipSetDevice(L.device));
@@ -143,24 +172,6 @@ static int leave(Local &L) {
     return QK_OK;
 }
 
-static int sync_local(Local &L) {
-    QK_HIP_TRY(hipSetDevice(L.device));
-    QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
-    return QK_OK;
-}
-
-static int init_local(Local &L, int device, int world) {
-    L.device = device;
-    if (int rc = qk_ctx_create(device, &L.ctx)) return rc;
-    QK_HIP_TRY(hipSetDevice(device));
-    QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_in, hipEventDisableTiming));
-    QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_out, hipEventDisableTiming));
-    const size_t w = coll_cap(world);
-    if (hipMalloc(&L.d_coll, w * 8) != hipSuccess) return QK_E_NOMEM;
-    if (hipHostMalloc(&L.h_coll, w * 8, hipHostMallocDefault) != hipSuccess) return QK_E_NOMEM;
-    return QK_OK;
-}
-
 static int abort_comm(qk_comm *c) {
     c->broken = true;
     for (auto &L : c->local)
@@ -171,57 +182,143 @@ static int abort_comm(qk_comm *c) {
     return QK_E_COMM;
 }
 
-// Collectives over every local rank, in place on d_coll:
-//   Reduce:  d_coll[0..w) summed over ranks into the root's
-//   Bcast:   the root's d_coll[0..w) to every rank
-//   Gather:  rank r's d_coll[0..w) to d_coll[w + r*w .. w + (r+1)*w) everywhere
-// Enqueued on the local streams (RCCL) or run now through the host callbacks
-// (staged through h_coll).  A failed collective aborts the communicator.
-enum class Op { Reduce, Bcast, Gather };
+// Drain the local rank's stream.  With RCCL work in it, the wait polls the
+// communicator's asynchronous error and gives up after the timeout (a peer
+// that never reaches the collective): the communicator is aborted, QK_E_COMM.
+static int wait_local(qk_comm *c, Local &L) {
+    QK_HIP_TRY(hipSetDevice(L.device));
+    if (c->host || !L.nc) {
+        QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
+        return QK_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+        const hipError_t q = hipStreamQuery(L.ctx->stream);
+        if (q == hipSuccess) return QK_OK;
+        if (q != hipErrorNotReady) return QK_E_HIP;
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(L.nc, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress))
+            return abort_comm(c);
+        if (c->timeout_ms > 0 &&
+            std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
+                c->timeout_ms)
+            return abort_comm(c);
+        if (spin >= 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
 
-static int collective(qk_comm *c, Op op, size_t w, int root) {
+// Test knob comm_fault = k on a local rank's context (qk_ctx_set_knob): the
+// staging of that rank's payload for the k-th collective of its next
+// operation fails, once — the path a failed local copy takes.
+static bool fault_now(qk_comm *c, Local &L) {
+    int &k = L.ctx->knobs.comm_fault;
+    if (k > 0 && k == c->step) {
+        k = 0;
+        return true;
+    }
+    return false;
+}
+
+// Sum-reduce of d_coll[0..w) to the root (the encode payload; the barrier's
+// one word).  A rank whose payload cannot be staged (host channel: the copy
+// to the pinned mirror) sends the failed payload instead — zeros, last word 1
+// (k_comm_fail's layout) — and reports the error in lerr[i].  The result is
+// in the root's d_coll (RCCL) or h_coll (host channel).  Returns QK_E_COMM
+// when the collective itself fails (the communicator is then broken).
+static int reduce_payload(qk_comm *c, size_t w, int root, std::vector<int> &lerr) {
     if (c->broken) return QK_E_COMM;
+    ++c->step;
     if (c->host) {
         Local &L = c->local[0];
         hipStream_t s = L.ctx->stream;
-        int e = QK_OK;
-        if (hipSetDevice(L.device) != hipSuccess ||
+        if (fault_now(c, L) || hipSetDevice(L.device) != hipSuccess ||
             hipMemcpyAsync(L.h_coll, L.d_coll, w * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
             memset(L.h_coll, 0, w * 8);   // still take part: the peers are in the collective
-            e = QK_E_HIP;
+            L.h_coll[w - 1] = 1;
+            if (!lerr[0]) lerr[0] = QK_E_HIP;
         }
-        int cb = -1;
-        switch (op) {
-        case Op::Reduce: cb = c->ops.reduce_sum_u64(c->ops.user, L.h_coll, w, root); break;
-        case Op::Bcast: cb = c->ops.broadcast_u64(c->ops.user, L.h_coll, w, root); break;
-        case Op::Gather: cb = c->ops.allgather_u64(c->ops.user, L.h_coll, L.h_coll + w, w); break;
-        }
-        if (cb != 0) {
+        if (c->ops.reduce_sum_u64(c->ops.user, L.h_coll, w, root) != 0) {
             c->broken = true;
             return QK_E_COMM;
         }
-        const size_t off = op == Op::Gather ? w : 0, words = op == Op::Gather ? w * (size_t)c->world : w;
-        if (!e && (hipMemcpyAsync(L.d_coll + off, L.h_coll + off, words * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-                   hipStreamSynchronize(s) != hipSuccess))
-            e = QK_E_HIP;
-        return e;
+        return QK_OK;
+    }
+    for (size_t i = 0; i < c->local.size(); ++i) {
+        Local &L = c->local[i];
+        if (fault_now(c, L)) {
+            (void)hipSetDevice(L.device);
+            hipLaunchKernelGGL(k_comm_fail, dim3(1), dim3(256), 0, L.ctx->stream, L.d_coll, (uint32_t)w);
+            (void)hipGetLastError();
+            if (!lerr[i]) lerr[i] = QK_E_HIP;
+        }
     }
     bool ok = ncclGroupStart() == ncclSuccess;
     for (auto &L : c->local) {
         if (!ok) break;
-        ncclResult_t r = ncclSuccess;
-        switch (op) {
-        case Op::Reduce:
-            r = ncclReduce(L.d_coll, L.d_coll, w, ncclUint64, ncclSum, root, L.nc, L.ctx->stream);
-            break;
-        case Op::Bcast: r = ncclBroadcast(L.d_coll, L.d_coll, w, ncclUint64, root, L.nc, L.ctx->stream); break;
-        case Op::Gather: r = ncclAllGather(L.d_coll, L.d_coll + w, w, ncclUint64, L.nc, L.ctx->stream); break;
-        }
-        ok = r == ncclSuccess;
+        ok = ncclReduce(L.d_coll, L.d_coll, w, ncclUint64, ncclSum, root, L.nc, L.ctx->stream) == ncclSuccess;
     }
     if (ncclGroupEnd() != ncclSuccess) ok = false;
     return ok ? QK_OK : abort_comm(c);
+}
+
+// Broadcast / all-gather of host payloads (the decode's exchanges): every
+// local rank's h_coll[0..w) is sent; a broadcast delivers the root's into
+// h_coll[0..w), an all-gather rank r's into h_coll[w + r*w .. w + (r+1)*w).
+// Word `sidx` of a payload is its rank's status: a rank whose payload cannot
+// be staged (RCCL: the copy to the device buffer) sends QK_E_HIP there
+// (k_comm_mark) and records it in ls[i] — it keeps joining.  A rank that
+// cannot read what the collective delivered cannot follow the rest of the
+// protocol: the communicator is broken (abort; peers are released by their
+// own timeout).  Returns QK_OK or QK_E_COMM.
+static int exchange(qk_comm *c, Op op, size_t w, int root, size_t sidx, std::vector<int> &ls) {
+    if (c->broken) return QK_E_COMM;
+    ++c->step;
+    if (c->host) {
+        Local &L = c->local[0];
+        if (fault_now(c, L)) {
+            L.h_coll[sidx] = (uint64_t)(int64_t)QK_E_HIP;
+            if (!ls[0]) ls[0] = QK_E_HIP;
+        }
+        const int cb = op == Op::Bcast ? c->ops.broadcast_u64(c->ops.user, L.h_coll, w, root)
+                                       : c->ops.allgather_u64(c->ops.user, L.h_coll, L.h_coll + w, w);
+        if (cb != 0) {
+            c->broken = true;
+            return QK_E_COMM;
+        }
+        return QK_OK;
+    }
+    for (size_t i = 0; i < c->local.size(); ++i) {
+        Local &L = c->local[i];
+        (void)hipSetDevice(L.device);
+        if (fault_now(c, L) ||
+            hipMemcpyAsync(L.d_coll, L.h_coll, w * 8, hipMemcpyHostToDevice, L.ctx->stream) != hipSuccess) {
+            hipLaunchKernelGGL(k_comm_mark, dim3(1), dim3(64), 0, L.ctx->stream, L.d_coll, (uint32_t)sidx,
+                               (uint64_t)(int64_t)QK_E_HIP);
+            (void)hipGetLastError();
+            if (!ls[i]) ls[i] = QK_E_HIP;
+        }
+    }
+    bool ok = ncclGroupStart() == ncclSuccess;
+    for (auto &L : c->local) {
+        if (!ok) break;
+        const ncclResult_t r = op == Op::Bcast
+                                   ? ncclBroadcast(L.d_coll, L.d_coll, w, ncclUint64, root, L.nc, L.ctx->stream)
+                                   : ncclAllGather(L.d_coll, L.d_coll + w, w, ncclUint64, L.nc, L.ctx->stream);
+        ok = r == ncclSuccess;
+    }
+    if (ncclGroupEnd() != ncclSuccess) ok = false;
+    if (!ok) return abort_comm(c);
+    const size_t off = op == Op::Gather ? w : 0, words = op == Op::Gather ? w * (size_t)c->world : w;
+    for (auto &L : c->local) {
+        (void)hipSetDevice(L.device);
+        if (hipMemcpyAsync(L.h_coll + off, L.d_coll + off, words * 8, hipMemcpyDeviceToHost, L.ctx->stream) !=
+            hipSuccess)
+            return abort_comm(c);
+    }
+    for (auto &L : c->local)
+        if (int e = wait_local(c, L)) return e == QK_E_COMM ? e : abort_comm(c);
+    return QK_OK;
 }
 
 template <int BITS>
@@ -232,11 +329,12 @@ static int encode_sharded_async(qk_comm *c, const void *const *d_ids, const size
     // them returns before any collective, on every rank
     if (t == 0 || t > QK_MAX_THRESHOLD) return QK_E_THRESHOLD;
     if (root < 0 || root >= c->world) return QK_E_INVAL;
+    c->step = 0;
     const size_t esz = BITS == 32 ? 4 : 8;
     const size_t R = reduce_words(BITS, t), W = R + 2 * (size_t)c->world + 1;
     // per-rank arguments and local work: a failure still joins the reduce,
     // with the failed payload
-    int rc = QK_OK;
+    std::vector<int> lerr(c->local.size(), QK_OK);
     for (size_t i = 0; i < c->local.size(); ++i) {
         Local &L = c->local[i];
         L.user = streams ? (hipStream_t)streams[i] : nullptr;
@@ -262,21 +360,25 @@ static int encode_sharded_async(qk_comm *c, const void *const *d_ids, const size
             (void)hipSetDevice(L.device);
             hipLaunchKernelGGL(k_comm_fail, dim3(1), dim3(256), 0, L.ctx->stream, L.d_coll, (uint32_t)W);
             (void)hipGetLastError();
-            if (!rc) rc = e;
+            lerr[i] = e;
         }
     }
-    const int crc = collective(c, Op::Reduce, W, root);
-    for (auto &L : c->local) {
+    const int crc = reduce_payload(c, W, root, lerr);
+    int rc = QK_OK;
+    for (size_t i = 0; i < c->local.size(); ++i) {
+        Local &L = c->local[i];
+        if (lerr[i] && !rc) rc = lerr[i];
         (void)hipSetDevice(L.device);
-        if (L.rank == root && hipMemcpyAsync(L.h_coll, L.d_coll, W * 8, hipMemcpyDeviceToHost, L.ctx->stream) !=
-                                  hipSuccess && !rc)
+        // the root's sum to its pinned mirror (a host channel left it there)
+        if (!crc && !c->host && L.rank == root &&
+            hipMemcpyAsync(L.h_coll, L.d_coll, W * 8, hipMemcpyDeviceToHost, L.ctx->stream) != hipSuccess && !rc)
             rc = QK_E_HIP;
         if (int e = leave(L); e && !rc) rc = e;
     }
     c->pend_bits = BITS;
     c->pend_t = t;
     c->pend_root = root;
-    c->pend_rc = rc ? rc : crc;
+    c->pend_rc = crc ? crc : rc;
     return c->pend_rc;
 }
 
@@ -288,7 +390,7 @@ static int encode_sharded_wait(qk_comm *c, Q *q) {
     c->pend_bits = 0;
     int rc = QK_OK;
     for (auto &L : c->local)
-        if (int e = sync_local(L); e && !rc) rc = e;
+        if (int e = wait_local(c, L); e && !rc) rc = e;
     if (prc) return prc;                           // q untouched
     if (rc) return rc;
     for (auto &L : c->local) {
@@ -297,7 +399,7 @@ static int encode_sharded_wait(qk_comm *c, Q *q) {
         if (q->threshold != t) return QK_E_MISMATCH;
         const size_t R = reduce_words(BITS, t);
         const uint64_t *h = L.h_coll;
-        if (h[R + 2 * (size_t)c->world]) return QK_E_PEER;   // another rank failed: q untouched
+        if (h[R + 2 * (size_t)c->world]) return QK_E_PEER;   // a rank failed: q untouched
         int has = 0;
         uint64_t last = 0;
         for (int r = c->world - 1; r >= 0; --r)
@@ -312,14 +414,23 @@ static int encode_sharded_wait(qk_comm *c, Q *q) {
     return QK_OK;   // not the root: q is untouched
 }
 
+// the lowest failing rank's status among W gathered payloads of `w` words
+// with the status at word sidx (0 if none failed) — the same on every rank
+static int gathered_status(const uint64_t *g, size_t W, size_t w, size_t sidx) {
+    for (size_t r = 0; r < W; ++r)
+        if (g[r * w + sidx]) return (int)(int64_t)g[r * w + sidx];
+    return QK_OK;
+}
+
 template <typename T, typename Q>
 static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d_log, const size_t *n,
                           int stop_at_last, uint64_t *hits, size_t cap, size_t *n_hits, void *const *streams) {
     if (c->broken) return QK_E_COMM;
     if (root < 0 || root >= c->world) return QK_E_INVAL;   // alike on every rank
+    c->step = 0;
     if (n_hits) *n_hits = 0;
     const size_t nl = c->local.size(), W = (size_t)c->world, B = 4 + QK_MAX_THRESHOLD;
-    // local status per local rank: travels in the status gather of step 3
+    // local status per local rank: travels in the status word of every exchange
     std::vector<int> ls(nl, QK_OK);
     for (size_t i = 0; i < nl; ++i) {
         Local &L = c->local[i];
@@ -329,13 +440,19 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
             ls[i] = QK_E_INVAL;
         if (int e = enter(L); e && !ls[i]) ls[i] = e;
     }
+    auto finish = [&](int status) {
+        int rc = status;
+        for (auto &L : c->local)
+            if (int e = leave(L); e && !rc) rc = e;
+        return rc;
+    };
 
-    // 1. coefficients from the root (its status travels with them)
+    // 1. [status, d, stop flag, stop value, c_1..c_d] from the root
     for (size_t i = 0; i < nl; ++i) {
         Local &L = c->local[i];
-        if (L.rank != root) continue;
         uint64_t *h = L.h_coll;
         memset(h, 0, B * 8);
+        if (L.rank != root) continue;
         int64_t status = ls[i];
         uint32_t d = 0;
         if (!status && !diff) status = QK_E_INVAL;
@@ -351,25 +468,11 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
         h[1] = status == QK_OK ? d : 0;
         h[2] = !status && stop_at_last && diff->has_last ? 1 : 0;
         h[3] = !status ? (uint64_t)diff->last_value : 0;
-        (void)hipSetDevice(L.device);
-        if (hipMemcpyAsync(L.d_coll, h, B * 8, hipMemcpyHostToDevice, L.ctx->stream) != hipSuccess && !ls[i])
-            ls[i] = QK_E_HIP;
     }
-    int crc = collective(c, Op::Bcast, B, root);
-    if (crc) return crc;
+    if (int e = exchange(c, Op::Bcast, B, root, 0, ls)) return finish(e);
     std::vector<std::vector<uint64_t>> hdr(nl);
     for (size_t i = 0; i < nl; ++i) {
-        Local &L = c->local[i];
-        int e = sync_local(L);
-        if (!e && hipMemcpyAsync(L.h_coll, L.d_coll, B * 8, hipMemcpyDeviceToHost, L.ctx->stream) != hipSuccess)
-            e = QK_E_HIP;
-        if (!e) e = sync_local(L);
-        if (e) {
-            if (!ls[i]) ls[i] = e;
-            hdr[i].assign(B, 0);
-        } else {
-            hdr[i].assign(L.h_coll, L.h_coll + B);
-        }
+        hdr[i].assign(c->local[i].h_coll, c->local[i].h_coll + B);
         if (!ls[i] && hdr[i][0]) ls[i] = (int)(int64_t)hdr[i][0];   // the root's status
     }
 
@@ -436,56 +539,35 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
 
     // 3. (n, stop, hits, status) of every rank
     for (size_t i = 0; i < nl; ++i) {
-        Local &L = c->local[i];
-        uint64_t *h = L.h_coll;
+        uint64_t *h = c->local[i].h_coll;
         h[0] = ls[i] ? 0 : n[i];
         h[1] = ls[i] ? 0 : lstop[i];
         h[2] = ls[i] ? 0 : lh[i].size();
         h[3] = (uint64_t)(int64_t)ls[i];
-        (void)hipSetDevice(L.device);
-        if (hipMemcpyAsync(L.d_coll, h, 32, hipMemcpyHostToDevice, L.ctx->stream) != hipSuccess)
-            ls[i] = QK_E_HIP;   // (sent anyway: the peers are in the collective)
     }
-    if ((crc = collective(c, Op::Gather, 4, root))) return crc;
-    Local &L0 = c->local[0];
-    int rc = sync_local(L0);
-    if (!rc && hipMemcpyAsync(L0.h_coll, L0.d_coll + 4, 4 * W * 8, hipMemcpyDeviceToHost, L0.ctx->stream) != hipSuccess)
-        rc = QK_E_HIP;
-    if (!rc) rc = sync_local(L0);
-    for (size_t i = 1; i < nl; ++i)
-        if (int e = sync_local(c->local[i]); e && !rc) rc = e;
-    // every rank gathered the same words (RCCL) — unless its own copies
-    // failed, which only it sees: it reports that error alone
-    if (rc) {
-        for (auto &L : c->local) leave(L);
-        return rc;
-    }
+    if (int e = exchange(c, Op::Gather, 4, root, 3, ls)) return finish(e);
+    // every local rank received the same words
+    const uint64_t *m = c->local[0].h_coll + 4;
+    int gstatus = gathered_status(m, W, 4, 3);
+    if (gstatus) return finish(gstatus);
     std::vector<uint64_t> base(W + 1, 0), cnt(W, 0);
     uint64_t gstop = UINT64_MAX, M = 0;
-    int gstatus = QK_OK;
-    {
-        const uint64_t *m = L0.h_coll;
-        for (size_t r = 0; r < W; ++r) {
-            const int st = (int)(int64_t)m[4 * r + 3];
-            if (st && !gstatus) gstatus = st;   // the lowest failing rank's status, on every rank
-            base[r + 1] = base[r] + m[4 * r];
-            if (m[4 * r + 1] < m[4 * r]) gstop = std::min(gstop, base[r] + m[4 * r + 1]);
-            cnt[r] = m[4 * r + 2];
-        }
-        for (size_t r = 0; r < W; ++r) {
-            if (base[r] >= gstop) cnt[r] = 0;   // wholly past the global stop
-            M = std::max(M, cnt[r]);
-        }
+    for (size_t r = 0; r < W; ++r) {
+        base[r + 1] = base[r] + m[4 * r];
+        if (m[4 * r + 1] < m[4 * r]) gstop = std::min(gstop, base[r] + m[4 * r + 1]);
+        cnt[r] = m[4 * r + 2];
     }
-    if (gstatus) {
-        for (auto &L : c->local) leave(L);
-        return gstatus;
+    for (size_t r = 0; r < W; ++r) {
+        if (base[r] >= gstop) cnt[r] = 0;   // wholly past the global stop
+        M = std::max(M, cnt[r]);
     }
 
-    // 4. the hit positions, in rounds of C per rank (padded), C fixed by the
-    //    payload capacity: no allocation between collectives
+    // 4. the hit positions, in rounds of C per rank (padded) plus the rank's
+    //    status word; C fixed by the payload capacity: no allocation between
+    //    collectives.  Every rank joins all rounds (M is known to all); a
+    //    failure in a round travels in its status word.
     std::vector<uint64_t> all;
-    const size_t C = coll_cap(c->world) / (W + 1);
+    const size_t C = coll_cap(c->world) / (W + 1) - 1, w = C + 1;
     for (uint64_t off = 0; off < M; off += C) {
         for (size_t i = 0; i < nl; ++i) {
             Local &L = c->local[i];
@@ -495,29 +577,19 @@ static int decode_sharded(qk_comm *c, const Q *diff, int root, const T *const *d
                 const size_t j = (size_t)off + k;
                 h[k] = j < lh[i].size() && j < cnt[L.rank] ? b + lh[i][j] : UINT64_MAX;
             }
-            (void)hipSetDevice(L.device);
-            if (hipMemcpyAsync(L.d_coll, h, C * 8, hipMemcpyHostToDevice, L.ctx->stream) != hipSuccess && !rc)
-                rc = QK_E_HIP;
+            h[C] = (uint64_t)(int64_t)ls[i];
         }
-        if ((crc = collective(c, Op::Gather, C, root))) return crc;
-        int e = sync_local(L0);
-        if (!e && hipMemcpyAsync(L0.h_coll, L0.d_coll + C, C * W * 8, hipMemcpyDeviceToHost, L0.ctx->stream) !=
-                      hipSuccess)
-            e = QK_E_HIP;
-        if (!e) e = sync_local(L0);
-        for (size_t i = 1; i < nl; ++i)
-            if (int e2 = sync_local(c->local[i]); e2 && !e) e = e2;
-        if (e && !rc) rc = e;
-        if (rc) continue;   // keep joining the remaining rounds
+        if (int e = exchange(c, Op::Gather, w, root, C, ls)) return finish(e);
+        const uint64_t *g = c->local[0].h_coll + w;
+        if (!gstatus) gstatus = gathered_status(g, W, w, C);
+        if (gstatus) continue;   // keep joining the remaining rounds
         for (size_t r = 0; r < W; ++r)
             for (size_t k = 0; k < C && off + k < cnt[r]; ++k) {
-                const uint64_t p = L0.h_coll[r * C + k];
+                const uint64_t p = g[r * w + k];
                 if (p < gstop) all.push_back(p);
             }
     }
-    for (auto &L : c->local)
-        if (int e = leave(L); e && !rc) rc = e;
-    if (rc) return rc;
+    if (int e = finish(gstatus)) return e;
     std::sort(all.begin(), all.end());   // rounds arrive rank-major: restore log order
     *n_hits = all.size();
     if (all.size() > cap || (!all.empty() && !hits)) return QK_E_CAPACITY;
@@ -624,12 +696,8 @@ int qk_comm_init_host(const qk_comm_host_ops *ops, int rank, int world, int devi
 
 void qk_comm_destroy(qk_comm *comm) {
     if (!comm) return;
-    for (auto &L : comm->local) {
-        if (L.ctx) {
-            (void)hipSetDevice(L.device);
-            (void)hipStreamSynchronize(L.ctx->stream);
-        }
-    }
+    for (auto &L : comm->local)
+        if (L.ctx) (void)wait_local(comm, L);   // (a peer that never arrives: the timeout aborts)
     for (auto &L : comm->local) destroy_local(L);
     delete comm;
 }
@@ -652,15 +720,41 @@ int qk_comm_barrier(qk_comm *comm) {
     if (!comm) return QK_E_INVAL;
     std::lock_guard<std::mutex> g(comm->mu);
     if (comm->broken) return QK_E_COMM;
-    int rc = QK_OK;
-    for (auto &L : comm->local) {
+    comm->step = 0;
+    std::vector<int> lerr(comm->local.size(), QK_OK);
+    for (size_t i = 0; i < comm->local.size(); ++i) {
+        Local &L = comm->local[i];
         (void)hipSetDevice(L.device);
-        if (hipMemsetAsync(L.d_coll, 0, 8, L.ctx->stream) != hipSuccess && !rc) rc = QK_E_HIP;
+        if (hipMemsetAsync(L.d_coll, 0, 8, L.ctx->stream) != hipSuccess) lerr[i] = QK_E_HIP;
     }
-    if (int e = collective(comm, Op::Reduce, 1, 0)) return e;
-    for (auto &L : comm->local)
-        if (int e = sync_local(L); e && !rc) rc = e;
+    if (int e = reduce_payload(comm, 1, 0, lerr)) return e;
+    int rc = QK_OK;
+    for (size_t i = 0; i < comm->local.size(); ++i) {
+        if (lerr[i] && !rc) rc = lerr[i];
+        if (int e = wait_local(comm, comm->local[i]); e && !rc) rc = e;
+    }
     return rc;
+}
+
+int qk_comm_set_timeout(qk_comm *comm, int64_t ms) {
+    if (!comm || ms < 0) return QK_E_INVAL;
+    std::lock_guard<std::mutex> g(comm->mu);
+    comm->timeout_ms = ms;
+    return QK_OK;
+}
+
+int qk_comm_rccl_info(const qk_comm *comm, int local, int *count, int *device, int *rank) {
+    if (!comm || local < 0 || local >= (int)comm->local.size()) return QK_E_INVAL;
+    const Local &L = comm->local[local];
+    if (comm->host || !L.nc) return QK_E_INVAL;   // no RCCL communicator (host channel, or aborted)
+    int k = 0, d = 0, r = 0;
+    if (ncclCommCount(L.nc, &k) != ncclSuccess || ncclCommCuDevice(L.nc, &d) != ncclSuccess ||
+        ncclCommUserRank(L.nc, &r) != ncclSuccess)
+        return QK_E_COMM;
+    if (count) *count = k;
+    if (device) *device = d;
+    if (rank) *rank = r;
+    return QK_OK;
 }
 
 int qk_u32_encode_sharded_async(qk_comm *comm, const uint32_t *const *d_ids, const size_t *n, uint32_t threshold,

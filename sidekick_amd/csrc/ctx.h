@@ -29,6 +29,8 @@ struct qk_knobs {
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)
     int matrix_cores = 0;  // 1: the int8-MFMA encode variants (libquack_hip_mfma.so build only)
+    int comm_fault = 0;    // k > 0 (tests): this rank's payload staging for the k-th collective of its
+                           // next sharded operation fails, once (comm.hip fault_now)
 };
 
 struct qk_ctx {

@@ -236,6 +236,21 @@ class Comm:
     def barrier(self):
         check(lib().qk_comm_barrier(self.handle), "qk_comm_barrier")
 
+    def set_timeout(self, ms: int) -> None:
+        """Bound every wait on an RCCL collective (0: never); past it the
+        communicator aborts and the call raises QK_E_COMM."""
+        check(lib().qk_comm_set_timeout(self.handle, int(ms)), "qk_comm_set_timeout")
+
+    def rccl_info(self, local: int = 0):
+        """(ranks, device, rank) as RCCL itself reports them (ncclCommCount,
+        ncclCommCuDevice, ncclCommUserRank); None for a host-channel
+        communicator."""
+        if getattr(self, "_keep", None) is not None:
+            return None
+        k, d, r = C.c_int(), C.c_int(), C.c_int()
+        check(lib().qk_comm_rccl_info(self.handle, local, C.byref(k), C.byref(d), C.byref(r)), "qk_comm_rccl_info")
+        return k.value, d.value, r.value
+
     def context(self, local: int = 0):
         """The (communicator-owned) qk_ctx of a local rank."""
         from .quack import Context

@@ -81,6 +81,12 @@ class Context:
         """Free grown-out scratch buffers (synchronises the device)."""
         check(lib().qk_ctx_trim(self.handle), "trim")
 
+    def clock_probe_async(self, microseconds: int, out, stream) -> None:
+        """Enqueue the shader-clock probe (qk_clock_probe) on `stream` (a raw
+        stream handle): out (a CUDA int64 tensor of 2) receives (s_memtime
+        ticks, 100 MHz ticks) over `microseconds` of wall time."""
+        check(lib().qk_clock_probe(self.handle, int(microseconds), out.data_ptr(), stream), "clock_probe")
+
 
 _ctx_lock = threading.Lock()
 _contexts: dict = {}

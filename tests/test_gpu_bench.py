@@ -32,8 +32,10 @@ def test_bench_contract_and_sharded_parity():
     assert one["n_gpus"] == 1 and one["steps"] == 3 and one["value"] > 0
     rf = one["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
-    v = rf["valu"]                        # the integer-issue roofline (tools/issue_roofline.py)
+    v = rf["valu"]                        # the integer-issue roofline (tools/issue_model.py)
     assert v["bound"] == "valu-issue" and 0 < v["frac"] < 1.5 and abs(v["frac"] - v["peak"] / v["achieved"]) < 1e-9
+    assert 1.0 < one["clock_ghz"] < 3.0 and v["clock_ghz"] == one["clock_ghz"]   # this run's shader clock
+    assert v["anchor"]["ops_per_id"] == {"lazy_modmuls": 9, "macs": 24, "row0_adds": 8}
     cb = one["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["parity_with_gpu"] is True
     want = coracle.encode_u32_seed(seed, n_total, t)
@@ -46,6 +48,15 @@ def test_bench_contract_and_sharded_parity():
     assert two["config"]["collectives"] == "host" and "rehearsal" in two["config"]["workload"]
     assert two["result"]["digest"] == one["result"]["digest"]
     assert two["result"]["count"] == n_total
+    # the untimed strong-scaling pass: the N = 1 stream of --ids-per-gpu ids in 2 shards through the
+    # same communicator equals rank 0's single-GPU encode of it
+    p = two["parity"]
+    assert p["equals_n1"] is True and p["last_value_equal"] is True
+    import hashlib
+    want2 = coracle.encode_u32_seed(seed, n_total // 2, t)
+    assert p["digest"] == hashlib.sha256((",".join(map(str, want2)) + f"|{n_total // 2}").encode()).hexdigest()[:16]
+    assert len(two["ranks"]) == 2 and [r["rank"] for r in two["ranks"]] == [0, 1]
+    assert "rccl" not in two                   # host channel: no RCCL communicator to report
 
 
 def test_bench_native_comm_world1_matches():

@@ -374,3 +374,72 @@ def test_rccl_world1_local_failure_leaves_q_untouched(comm):
     host, ids = _ids(32, 5000, 0x33)
     comm.encode_sharded([ids], q)
     assert q.count() == 5001
+
+
+def test_host_channel_staging_fault_at_every_step_same_status_everywhere():
+    """A rank whose payload staging fails (knob comm_fault = k: the copy into
+    its k-th collective of the call) keeps joining and sends the failure as
+    data.  Sharded encode (one reduce, step 1): that rank returns QK_E_HIP, the
+    root QK_E_PEER, q untouched everywhere.  Sharded decode (broadcast = 1,
+    status gather = 2, hit rounds = 3..): every rank returns the same status,
+    QK_E_HIP, within one call — no rank waits on a peer that left — and the
+    communicator then runs a clean round."""
+    import ctypes as C
+    import time
+    import sidekick_amd as sk
+    from sidekick_amd._lib import QK_E_HIP, QK_E_PEER, QK_OK, lib
+    from sidekick_amd.dist import Comm, LoopbackHub
+    world, t = 4, 16
+    host, ids = _ids(32, 40_000, 0xFA57)
+    bounds = _shards(len(host), world)
+    hub = LoopbackHub(world, timeout=60)
+    comms = [Comm.init_host(hub.channel(r), r, world, 0) for r in range(world)]
+    try:
+        def enc(r, comm, bad, k):
+            if r == bad:
+                comm.context(0).set_knob("comm_fault", k)
+            q = sk.PowerSumQuackU32(t)
+            q.insert(5)
+            s, c = bounds[r]
+            rc = lib().qk_u32_encode_sharded(comm.handle, (C.c_void_p * 1)(ids[s:s + c].data_ptr()),
+                                             (C.c_size_t * 1)(c), q._buf, 0, None)
+            return rc, q.count() == 1 and q.power_sums()[0] == 5
+        for bad in (2, 0):
+            res = _run_ranks(world, lambda r, cm: enc(r, cm, bad, 1), comms=comms)
+            assert all(ok for ok, _ in res), res
+            rcs = [v[0] for _, v in res]
+            assert rcs[bad] == QK_E_HIP
+            assert all(rcs[r] == QK_OK for r in range(1, world) if r != bad)
+            if bad != 0:
+                assert rcs[0] == QK_E_PEER
+            assert all(v[1] for _, v in res)               # q untouched everywhere
+
+        a, log, diff = _decode_case_gpu(32, 80_000, 0xFA58)
+        want = diff.root_test(diff.to_coeffs(), log, stop_value=diff.last_value())
+        assert want
+        dbounds = _shards(80_000, world)
+
+        def dec(r, comm, bad, k):
+            if r == bad:
+                comm.context(0).set_knob("comm_fault", k)
+            s, c = dbounds[r]
+            hits = (C.c_uint64 * 4096)()
+            nh = C.c_size_t()
+            rc = lib().qk_u32_decode_sharded(comm.handle, diff._buf if r == 0 else None, 0,
+                                             (C.c_void_p * 1)(log[s:s + c].data_ptr()), (C.c_size_t * 1)(c), 1,
+                                             hits, 4096, C.byref(nh), None)
+            return rc, [int(h) for h in hits[: nh.value]]
+
+        for k in (1, 2, 3):
+            for bad in (0, 3):
+                t0 = time.time()
+                res = _run_ranks(world, lambda r, cm: dec(r, cm, bad, k), comms=comms)
+                assert time.time() - t0 < 30
+                assert all(ok for ok, _ in res), res
+                assert [v[0] for _, v in res] == [QK_E_HIP] * world, (k, bad, res)
+                # reusable: a clean round gives the single-GPU answer on every rank
+                res = _run_ranks(world, lambda r, cm: dec(r, cm, -1, 0), comms=comms)
+                assert all(v == (QK_OK, want) for _, v in res), (k, bad)
+    finally:
+        for c in comms:
+            c.close()
