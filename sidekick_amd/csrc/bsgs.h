@@ -506,12 +506,15 @@ __device__ __forceinline__ void clear(Acc<C::NB, C::NA, C::ROWS> &S) {
 }
 
 // XC (offset passes): xin / xout are per-id arrays indexed like ids whose
-// address is congruent to ids' modulo 16 (the same 16-byte groups).
+// address is congruent to ids' modulo 16 (the same 16-byte groups).  The
+// middle passes read and write the same cache (xin == xout): not restrict —
+// each element is read one iteration before its own write, and the source
+// order (next load, compute, this store) is the order kept.
 template <class C, class Out>
 __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
                                          uint64_t gtid, uint64_t nthr, Out out, uint32_t base = 0,
-                                         const uint32_t *__restrict__ xin = nullptr,
-                                         uint32_t *__restrict__ xout = nullptr) {
+                                         const uint32_t *xin = nullptr,
+                                         uint32_t *xout = nullptr) {
     constexpr bool XI = (C::XC & 1) != 0, XO = (C::XC & 2) != 0;
     Acc<C::NB, C::NA, C::ROWS> S;
     clear<C>(S);
@@ -522,8 +525,8 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
     const uint32_t tmax = (uint32_t)__builtin_amdgcn_readfirstlane(iters);           // lane 0: most trips
     const uint32_t tmin = (uint32_t)__builtin_amdgcn_readlane((int)iters, 63);       // lane 63: fewest
     const uint4 *__restrict__ p = v + gtid;
-    const uint4 *__restrict__ pc = XI ? reinterpret_cast<const uint4 *>(xin + h) + gtid : nullptr;
-    uint4 *__restrict__ po = XO ? reinterpret_cast<uint4 *>(xout + h) + gtid : nullptr;
+    const uint4 *pc = XI ? reinterpret_cast<const uint4 *>(xin + h) + gtid : nullptr;
+    uint4 *po = XO ? reinterpret_cast<uint4 *>(xout + h) + gtid : nullptr;
     uint4 nxt = make_uint4(0, 0, 0, 0), nxc = make_uint4(0, 0, 0, 0), xo = make_uint4(0, 0, 0, 0);
     if (iters) {
         nxt = *p;
@@ -581,7 +584,7 @@ __device__ __forceinline__ void body_gen(const uint32_t *__restrict__ ids, uint6
 template <class C>
 __device__ __forceinline__ void body(const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T,
                                      uint64_t *__restrict__ partials, uint32_t base = 0,
-                                     const uint32_t *__restrict__ xin = nullptr, uint32_t *__restrict__ xout = nullptr) {
+                                     const uint32_t *xin = nullptr, uint32_t *xout = nullptr) {
     body_gen<C>(
         ids, n, head, T, (uint64_t)blockIdx.x * BLOCK + threadIdx.x, (uint64_t)gridDim.x * BLOCK,
         [=](uint32_t m, uint64_t s) { partials[(size_t)m * gridDim.x + blockIdx.x] = s; }, base, xin, xout);

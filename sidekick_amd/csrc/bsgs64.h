@@ -263,7 +263,7 @@ template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, b
           int XC = 0, int NBT = NB>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
                                      uint64_t *__restrict__ partials, uint32_t base = 0,
-                                     const uint64_t *__restrict__ xin = nullptr, uint64_t *__restrict__ xout = nullptr) {
+                                     const uint64_t *xin = nullptr, uint64_t *xout = nullptr) {
     static_assert(OFF || (XC & 1) == 0, "only an offset pass reads x^base");
     static_assert((NA >= 2 || (OFF && NA == 1)) && NA <= 10, "giant rows");
     static_assert(!(BSH && PF) && !(LD && PF), "prefetch form: stored B * 2^32, all rows");

@@ -169,8 +169,8 @@ template <int SG>
 __global__ __launch_bounds__(BLOCK, 2) void k_encode_u32_bsgs_x80(const uint32_t *__restrict__ ids, uint64_t n,
                                                                  uint32_t head, uint32_t T,
                                                                  uint64_t *__restrict__ partials,
-                                                                 const uint32_t *__restrict__ xin,
-                                                                 uint32_t *__restrict__ xout) {
+                                                                 const uint32_t *xin,
+                                                                 uint32_t *xout) {
     (void)xin;
     bsgs::body<bsgs::Cfg<8, 10, SG, 1, 1, false, false, 2>>(ids, n, head, T, partials, 0, nullptr, xout);
 }
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_encode_u32_bsgs_x80(const uint32_t
 template <int NA, int SG, int XC = 0>
 __global__ __launch_bounds__(BLOCK, (NA > 6 ? 2 : NA > 5 ? 3 : 4)) void k_encode_u32_bsgs_off(
     const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T, uint32_t base,
-    uint64_t *__restrict__ partials, const uint32_t *__restrict__ xin, uint32_t *__restrict__ xout) {
+    uint64_t *__restrict__ partials, const uint32_t *xin, uint32_t *xout) {
     bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true, XC>>(ids, n, head, T, partials, base, xin, xout);
 }
 
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs4(const uin
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_x80(const uint64_t *__restrict__ ids,
                                                                           uint64_t n, uint32_t head, uint32_t T,
                                                                           uint64_t *__restrict__ partials,
-                                                                          uint64_t *__restrict__ xout) {
+                                                                          uint64_t *xout) {
     (void)head;
     bsgs64::body<10, 0, 16, 0, 0, false, true, 1, 2>(ids, n, T, partials, 0, nullptr, xout);
 }
@@ -641,8 +641,8 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_off(const 
                                                                           uint64_t n, uint32_t head, uint32_t T,
                                                                           uint32_t base,
                                                                           uint64_t *__restrict__ partials,
-                                                                          const uint64_t *__restrict__ xin,
-                                                                          uint64_t *__restrict__ xout) {
+                                                                          const uint64_t *xin,
+                                                                          uint64_t *xout) {
     (void)head;
     bsgs64::body<NA, 0, 16, 0, 0, true, true, 1, XC>(ids, n, T, partials, base, xin, xout);
 }

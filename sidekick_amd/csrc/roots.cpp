@@ -234,7 +234,7 @@ struct F64 {
         return canon64((uint64_t)u + C64 * (uint64_t)(u >> 64));
     }
     // Tonelli-Shanks: p64 - 1 = 4 Q (Q odd); z = 2 is a non-residue mod p64
-    // (p64 = 3 mod 8), so c = 2^Q has order 4
+    // (p64 = 5 mod 8), so c = 2^Q has order 4
     static bool sqrt(T n, T &r) {
         if (n == 0) {
             r = 0;
