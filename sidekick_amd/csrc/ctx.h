@@ -25,6 +25,10 @@ struct qk_knobs {
     int flow_load = 4;     // flow-table slots per expected flow
     int flow_wgpc = 12;    // flow extract: workgroups per CU
     int flow_hist = 1;     // 0: few-flow batches grouped by the radix sort instead of per-workgroup slot histograms
+    int flow_sort = 2;     // grouping sort (radix.h, flows.hip rs_sort): 1: 8-bit digits, 256 threads, two arrays
+                           // throughout; 2: pair arrays between the first and last pass; 3 / 4: 512 / 1024
+                           // threads; 5 / 6: 11-bit digits, 512 / 1024 threads; 7-9: as 2, 5, 6 without LDS
+                           // staging (direct scatter); 0: hipCUB's onesweep
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)

@@ -46,6 +46,7 @@
 #include "bsgs.h"
 #include "ctx.h"
 #include "field.h"
+#include "radix.h"
 #include "records.h"
 
 namespace qk {
@@ -824,6 +825,77 @@ extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids,
     return QK_OK;
 }
 
+// The grouping sort (radix.h): chunks of the packets, one per workgroup
+struct RsPlan {
+    uint32_t nwg;
+    uint64_t chunk;   // a multiple of 4
+};
+// wgpc workgroups per CU (at most: one per 4096 packets)
+static RsPlan rs_plan(const qk_ctx *ctx, uint64_t n, uint32_t wgpc) {
+    const uint32_t nwg = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((uint64_t)ctx->num_cus * wgpc, (n + 4095) / 4096));
+    return {nwg, (((n + nwg - 1) / nwg) + 3) & ~(uint64_t)3};
+}
+constexpr uint32_t RS_WGPC_MAX = 4;
+// Stable sort of (key, val) by the low `bits` bits of key, 8 bits per pass,
+// ping-ponging between region X = (k0, v0) and region Y = (k1, v1); each
+// region must also hold n (key, value) pairs from k0 / k1 (arena layout: the
+// value array follows the key array).  The first pass reads two arrays, the
+// last writes two, the passes between use pair arrays (knob flow_sort 2, 3;
+// 1: two arrays throughout).  Returns in `where` the region holding the
+// result: 1 = Y, 0 = X (an even number of passes).
+template <int D, int BLK, int K, bool PAIRS, uint32_t WGPC, bool DIRECT = false>
+static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, uint64_t n, int bits,
+                     uint32_t *cnt, uint32_t *base, void *temp, size_t temp_bytes, hipStream_t s, int &where) {
+    static_assert(WGPC <= RS_WGPC_MAX, "scratch is sized for RS_WGPC_MAX");
+    where = 0;
+    if (n == 0 || bits <= 0) return QK_OK;
+    const RsPlan pl = rs_plan(ctx, n, WGPC);
+    const int passes = (bits + D - 1) / D;
+    const int dd = (bits + passes - 1) / passes;   // the digit width actually used (<= D): balanced passes
+    uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
+    for (int q = 0; q < passes; ++q) {
+        const uint32_t shift = (uint32_t)(q * dd);
+        const int left = bits - q * dd;
+        const uint32_t mask = left >= dd ? (1u << dd) - 1 : (1u << left) - 1;
+        const bool ip = PAIRS && q > 0, op = PAIRS && q + 1 < passes;
+        auto count = ip ? rsort::k_rs_count<D, true> : rsort::k_rs_count<D, false>;
+        hipLaunchKernelGGL(count, dim3(pl.nwg), dim3(256), 0, s, ki, n, pl.chunk, shift, mask, pl.nwg, cnt);
+        if (hipGetLastError() != hipSuccess) return QK_E_HIP;
+        size_t tb = temp_bytes;
+        if (hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, base, (int)((1u << D) * pl.nwg), s) != hipSuccess)
+            return QK_E_HIP;
+        auto kern = ip ? (op ? rsort::k_rs_scatter<D, BLK, K, true, true, DIRECT>
+                             : rsort::k_rs_scatter<D, BLK, K, true, false, DIRECT>)
+                       : (op ? rsort::k_rs_scatter<D, BLK, K, false, true, DIRECT>
+                             : rsort::k_rs_scatter<D, BLK, K, false, false, DIRECT>);
+        hipLaunchKernelGGL(kern, dim3(pl.nwg), dim3(BLK), 0, s, ki, vi, n, pl.chunk, shift, mask, pl.nwg, base, ko, vo);
+        if (hipGetLastError() != hipSuccess) return QK_E_HIP;
+        std::swap(ki, ko);
+        std::swap(vi, vo);
+    }
+    where = passes % 2;
+    return QK_OK;
+}
+static int rs_sort(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, uint64_t n, int bits,
+                   uint32_t *cnt, uint32_t *base, void *temp, size_t temp_bytes, hipStream_t s, int &where) {
+#define QK_RS(D, BLK, K, PAIRS, WGPC, ...)                                                              \
+    return rs_sort_k<D, BLK, K, PAIRS, WGPC, ##__VA_ARGS__>(ctx, k0, v0, k1, v1, n, bits, cnt, base, temp,         \
+                                                           temp_bytes, s, where)
+    switch (ctx->knobs.flow_sort) {
+    case 1: QK_RS(8, 256, 16, false, 4);
+    case 2: QK_RS(8, 256, 16, true, 4);
+    case 3: QK_RS(8, 512, 16, true, 2);
+    case 4: QK_RS(8, 1024, 16, true, 1);
+    case 5: QK_RS(11, 512, 16, true, 1);
+    case 6: QK_RS(11, 1024, 8, true, 1);
+    case 7: QK_RS(8, 256, 16, true, 4, true);
+    case 8: QK_RS(11, 512, 16, true, 1, true);
+    default: QK_RS(11, 1024, 8, true, 1, true);
+    }
+#undef QK_RS
+}
+
 extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
                                           const qk_pkt_meta *d_meta, const uint8_t my_addr[6], uint32_t threshold,
                                           qk_flow_key *keys, uint8_t *sketches, size_t cap, size_t *n_flows,
@@ -872,14 +944,20 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                                      SlotUsed{nullptr}, s) != hipSuccess)
             return QK_E_HIP;
         tb = std::max(tb, b);
+        if (hipcub::DeviceScan::ExclusiveSum(nullptr, b, u, u, (int)(rsort::RMAX * rs_plan(ctx, n, RS_WGPC_MAX).nwg), s) != hipSuccess)
+            return QK_E_HIP;
+        tb = std::max(tb, b);
     }
-    uint32_t *slots = nullptr, *ids = nullptr, *key_s = nullptr, *id_s = nullptr;
+    const uint32_t rs_nwg = rs_plan(ctx, n, RS_WGPC_MAX).nwg;
+    uint32_t *slots = nullptr, *ids = nullptr, *key_s = nullptr, *id_s = nullptr, *rs_cnt = nullptr, *rs_base = nullptr;
     unsigned long long *counters = nullptr, *acc = nullptr;
     void *temp = nullptr;
     auto layout0 = [&](Carve &c) {
         slots = c.take<uint32_t>(n); ids = c.take<uint32_t>(n); key_s = c.take<uint32_t>(n); id_s = c.take<uint32_t>(n);
         counters = c.take<unsigned long long>(5);
         temp = c.take<char>(tb);
+        rs_cnt = c.take<uint32_t>((size_t)rsort::RMAX * rs_nwg);
+        rs_base = c.take<uint32_t>((size_t)rsort::RMAX * rs_nwg);
     };
     {
         Carve probe{nullptr};
@@ -1086,10 +1164,19 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
         } else if (!rc && by_slot) {
-            if (hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, cbits, s) !=
-                    hipSuccess ||
-                hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess)
+            // the grouping sort: radix.h (knob flow_sort = 0: hipCUB's onesweep)
+            if (ctx->knobs.flow_sort) {
+                int where = 0;
+                rc = rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs_cnt, rs_base, temp, tb, s, where);
+                if (!rc && where == 0) {   // even number of passes: the result is in (slots, ids)
+                    std::swap(slots, key_s);
+                    std::swap(ids, id_s);
+                }
+            } else if (hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, cbits,
+                                                          s) != hipSuccess) {
                 rc = QK_E_HIP;
+            }
+            if (!rc && hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess) rc = QK_E_HIP;
             if (!rc) {
                 hipLaunchKernelGGL(k_slot_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted,
                                    rank_of_slot, nf, d_offs);
@@ -1099,10 +1186,18 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         } else if (!rc) {
             if (hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess) rc = QK_E_HIP;
             if (!rc) hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, n_eff, nf);
-            if (!rc && (hipGetLastError() != hipSuccess ||
-                        hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, fbits,
-                                                           s) != hipSuccess))
+            if (!rc && hipGetLastError() != hipSuccess) rc = QK_E_HIP;
+            if (!rc && ctx->knobs.flow_sort) {
+                int where = 0;
+                rc = rs_sort(ctx, slots, ids, key_s, id_s, n_eff, fbits, rs_cnt, rs_base, temp, tb, s, where);
+                if (!rc && where == 0) {
+                    std::swap(slots, key_s);
+                    std::swap(ids, id_s);
+                }
+            } else if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0,
+                                                                 fbits, s) != hipSuccess) {
                 rc = QK_E_HIP;
+            }
             if (!rc) {
                 hipLaunchKernelGGL(k_rank_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted, nf,
                                    d_offs);

@@ -42,6 +42,10 @@ for s in $STEPS; do
     dist2) step dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --ids-per-gpu 2e8 --cpu-sample 0 || exit 3 ;;
     dist2full) step dist2full 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
     dist4full) step dist4full 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29536 bench.py --gpus 4 --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
+    abflows) step abflows 600 python3 -u tools/ab_flows.py ${ABFLOWS_ARGS:-} || exit 3 ;;
+    profabflows)
+      export TMPDIR=/tmp
+      step profabflows 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profabflows" -o run -- python3 "$ROOT/tools/ab_flows.py" ${PROFAB_ARGS:---modes 1 --rounds 2} || exit 3 ;;
     dist4) step dist4 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --steps 3 --warmup 1 --ids-per-gpu 1e8 --cpu-sample 0 || exit 3 ;;
     tune) step tune 600 ./tools/tune_encode ${TUNE_ARGS:-} || exit 3 ;;
     tunebsgs) step tunebsgs 600 ./tools/tune_bsgs ${TUNE_ARGS:-} || exit 3 ;;
