@@ -10,10 +10,12 @@
 //     (bsgs.h): baby steps x^1..x^NB and giant steps x^(NB a) per id, lane
 //     private, then S_(NB a + b) += A_a * B_b as 64-bit multiply-accumulates
 //     whose wraps are counted per wave on the scalar unit.  t = 32 is
-//     (NB, NA) = (8, 4): 9 lazy modmuls + 24 MACs + 8 row-0 mads per id,
-//     1.19 VALU + 0.76 SALU wave-instructions per id, ~0.75 of the
-//     integer-issue roofline (tools/issue_roofline.py) and ~0.19 of the HBM
-//     read roofline (4 B/id).
+//     (NB, NA) = (8, 4): 9 lazy modmuls + 24 MACs + 8 row-0 mads per id =
+//     4.47 SIMD-cycles of VALU issue per id (the algorithmic anchor,
+//     tools/issue_model.py); the kernel issues 1.19 VALU + 0.76 SALU
+//     wave-instructions per id and runs at ~0.76 of the anchor at the
+//     bench run's own shader clock (bench.py roofline.valu)
+//     and ~0.18 of the HBM read roofline (4 B/id).
 //   * 14 <= t <= 80 (u64) — k_encode_u64_bsgs<NA,MODE,SG> (bsgs64.h): the
 //     same split with the babies/giants of a 256-id tile shared through LDS,
 //     each wave owning two babies' MAC rows.

@@ -32,6 +32,14 @@ matches the measured VALU per unit (for a loop nest, the inner loop is
 weighted by the trip count that makes the two agree).
 
     python tools/issue_roofline.py [--asm-dir sidekick_amd/csrc/_build/asm] [--out profiles/r03/issue_roofline.json]
+    python tools/issue_roofline.py --bench profiles/r04/bench_n1.json
+
+The second form is the bench line's figure (round 4 on): the peak is the
+algorithmic anchor of tools/issue_model.py — the decomposition's VALU work,
+fixed per t — not the measured instruction count, and the clock is the one
+bench.py read in the same run (qk_clock_probe).  The counter-based analysis
+above stays as the per-kernel diagnostic (how close the emitted instruction
+stream is to the anchor, and how busy the scalar unit is).
 """
 from __future__ import annotations
 
@@ -178,11 +186,35 @@ def analyse(name, asm_dir):
     }
 
 
+def recompute_bench(path):
+    """The bench line's roofline.valu recomputed from the line's own fields
+    (this run's kernel time and shader clock) and the algorithmic anchor of
+    tools/issue_model.py — the anchor is fixed per t, so a kernel that issued
+    more instructions would take longer and report a lower fraction."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import issue_model
+    with open(path) as f:
+        line = json.loads(next(l for l in f if l.startswith("{")))
+    cfg, rf = line["config"], line["roofline"]
+    got = issue_model.roofline(cfg["bits"], cfg["threshold"], cfg["ids_per_gpu"], rf["kernel_avg_ms"],
+                               line["clock_ghz"])
+    want = rf["valu"]
+    return {"bench": os.path.relpath(path, ROOT), "anchor_cycles_per_id": got["peak"],
+            "achieved_cycles_per_id": got["achieved"], "frac": got["frac"], "frac_on_line": want["frac"],
+            "agree": abs(got["frac"] - want["frac"]) < 1e-9, "clock_ghz": line["clock_ghz"],
+            "kernel_avg_ms": rf["kernel_avg_ms"], "ops_per_id": got["anchor"]["ops_per_id"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--asm-dir", default=os.path.join(ROOT, "sidekick_amd", "csrc", "_build", "asm"))
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03", "issue_roofline.json"))
+    ap.add_argument("--bench", help="recompute a bench line's roofline.valu (tools/issue_model.py) and exit")
     a = ap.parse_args()
+    if a.bench:
+        json.dump(recompute_bench(a.bench), sys.stdout, indent=1)
+        print()
+        return
     res = {"method": __doc__.split("\n\n")[1], "costs": {"simple": COST_SIMPLE, "heavy": COST_HEAVY,
                                                          "source": "profiles/r01/ubench_issue.json"},
            "kernels": {k: analyse(k, a.asm_dir) for k in KERNELS}}
