@@ -233,10 +233,15 @@ __device__ __forceinline__ void row2m(uint64_t &a0, uint64_t &a1, uint32_t b0, u
 //          pass's cache instead of square-and-multiply; bit 1 — the next
 //          pass's x^base written per id (one more product): x^(base + NB*NA)
 //          after an offset pass, x^(NB*NA) after a plain one (pass 0)
+//  TREE    babies by a product tree (x^(h+l) = x^h x^l, h the highest power
+//          of two below): the same NB - 1 lazy modmuls at dependency depth
+//          log2(NB) instead of NB - 1 (plain passes with min-tracked folds)
 template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false, bool OFF_ = false,
-          int XC_ = 0>
+          int XC_ = 0, bool TREE_ = false>
 struct Cfg {
     static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_, XC = XC_;
+    static constexpr bool TREE = TREE_;
+    static_assert(!TREE_ || (!OFF_ && FOLD_ == 1), "product-tree babies: plain passes, min-tracked folds");
     static constexpr bool PAIR = PAIR_, OFF = OFF_;
     static_assert(OFF_ || (XC_ & 1) == 0, "only an offset pass reads x^base");
     static_assert(!XC_ || FOLD_ == 1, "the x^base cache goes with min-tracked folds");
@@ -307,8 +312,17 @@ __device__ __forceinline__ uint32_t powers(uint32_t id, uint32_t (&B)[C::NB], ui
         return wrapped;
     } else {
         uint32_t mn = 0xFFFFFFFFu;
+        if constexpr (C::TREE) {
 #pragma unroll
-        for (int b = 1; b < NB; ++b) B[b] = mulfold32_min(B[b - 1], B[0], mn);
+            for (int b = 1; b < NB; ++b) {   // B[b] = x^(b+1) = x^h * x^(b+1-h)
+                const int h = 1 << (31 - __builtin_clz((unsigned)(b + 1) - 1u));
+                B[b] = (b + 1) == 2 * h ? mulfold32_min(B[h - 1], B[h - 1], mn)
+                                        : mulfold32_min(B[h - 1], B[b - h], mn);
+            }
+        } else {
+#pragma unroll
+            for (int b = 1; b < NB; ++b) B[b] = mulfold32_min(B[b - 1], B[0], mn);
+        }
         A[0] = B[NB - 1];
 #pragma unroll
         for (int a = 1; a < NA - 1; ++a) A[a] = mulfold32_min(A[a - 1], A[0], mn);

@@ -129,6 +129,55 @@ __device__ __forceinline__ uint64_t shift32(uint64_t B) {
     "s_bcnt1_i32_b64 " T ", " P2 "\n\ts_add_u32 %[k0], %[k0], " T "\n\t"                                \
     "v_addc_co_u32_e64 %[kv], " P3 ", %[kv], 0, " P3
 
+// Both MACs of a wave's giant row (its two babies) in one block, the eight
+// mads ordered so that a mad reading an accumulator follows the one writing
+// it by four instructions (in a single MAC the second product into C0 / C1
+// follows the first by two), all eight carries counted on the scalar unit.
+// Operands: %0 C0[0], %1 C0[1], %2 C1[0], %3 C1[1], %4-%7 counters
+// (k0[0], k0[1], k1[0], k1[1]), %8-%11 baby 0 (B.lo, B.hi, Bsh.lo, Bsh.hi),
+// %12-%15 baby 1, %16 a0, %17 a1
+#define QK_MAC64P(Q0, Q1, Q2, Q3, Q4, Q5, Q6, Q7, T)                                                   \
+    "v_mad_u64_u32 %0, " Q0 ", %8, %16, %0\n\t"                                                        \
+    "v_mad_u64_u32 %1, " Q1 ", %12, %16, %1\n\t"                                                       \
+    "v_mad_u64_u32 %2, " Q2 ", %9, %16, %2\n\t"                                                        \
+    "v_mad_u64_u32 %3, " Q3 ", %13, %16, %3\n\t"                                                       \
+    "v_mad_u64_u32 %0, " Q4 ", %10, %17, %0\n\t"                                                       \
+    "v_mad_u64_u32 %1, " Q5 ", %14, %17, %1\n\t"                                                       \
+    "v_mad_u64_u32 %2, " Q6 ", %11, %17, %2\n\t"                                                       \
+    "v_mad_u64_u32 %3, " Q7 ", %15, %17, %3\n\t"                                                       \
+    "s_bcnt1_i32_b64 " T ", " Q0 "\n\ts_add_u32 %4, %4, " T "\n\t"                                       \
+    "s_bcnt1_i32_b64 " T ", " Q1 "\n\ts_add_u32 %5, %5, " T "\n\t"                                       \
+    "s_bcnt1_i32_b64 " T ", " Q2 "\n\ts_add_u32 %6, %6, " T "\n\t"                                       \
+    "s_bcnt1_i32_b64 " T ", " Q3 "\n\ts_add_u32 %7, %7, " T "\n\t"                                       \
+    "s_bcnt1_i32_b64 " T ", " Q4 "\n\ts_add_u32 %4, %4, " T "\n\t"                                       \
+    "s_bcnt1_i32_b64 " T ", " Q5 "\n\ts_add_u32 %5, %5, " T "\n\t"                                       \
+    "s_bcnt1_i32_b64 " T ", " Q6 "\n\ts_add_u32 %6, %6, " T "\n\t"                                       \
+    "s_bcnt1_i32_b64 " T ", " Q7 "\n\ts_add_u32 %7, %7, " T
+#define QK_SETP0 "s[40:41]", "s[42:43]", "s[44:45]", "s[46:47]", "s[48:49]", "s[50:51]", "s[52:53]", "s[54:55]", "s72"
+#define QK_SETP1 "s[56:57]", "s[58:59]", "s[60:61]", "s[62:63]", "s[64:65]", "s[66:67]", "s[68:69]", "s[70:71]", "s73"
+#define QK_CLOBP0 "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", \
+                  "s54", "s55", "s72"
+#define QK_CLOBP1 "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", \
+                  "s70", "s71", "s73"
+template <int SET>
+__device__ __forceinline__ void mac_pair_s(uint64_t (&C0)[2], uint64_t (&C1)[2], uint32_t (&K0)[2], uint32_t (&K1)[2],
+                                           uint32_t a0, uint32_t a1, uint4 b0, uint4 b1) {
+    if constexpr (SET == 0)
+        asm volatile(QK_EXPAND(QK_MAC64P, QK_SETP0)
+                     : "+v"(C0[0]), "+v"(C0[1]), "+v"(C1[0]), "+v"(C1[1]), "+s"(K0[0]), "+s"(K0[1]), "+s"(K1[0]),
+                       "+s"(K1[1])
+                     : "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
+                       "v"(a0), "v"(a1)
+                     : "scc", QK_CLOBP0);
+    else
+        asm volatile(QK_EXPAND(QK_MAC64P, QK_SETP1)
+                     : "+v"(C0[0]), "+v"(C0[1]), "+v"(C1[0]), "+v"(C1[1]), "+s"(K0[0]), "+s"(K0[1]), "+s"(K1[0]),
+                       "+s"(K1[1])
+                     : "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
+                       "v"(a0), "v"(a1)
+                     : "scc", QK_CLOBP1);
+}
+
 template <int SET>
 __device__ __forceinline__ void mac_m(uint64_t &C0, uint64_t &C1, uint32_t &k0, uint32_t &k1, uint32_t &kv,
                                       uint32_t a0, uint32_t a1, uint4 b) {
@@ -242,6 +291,8 @@ struct Smem<NG, true, NBB> {
 //   MODE 0  the first SG MACs of a wave's tile count all four carries on the
 //           scalar unit, the rest per lane (v_addc)
 //   MODE 1  every MAC: three carries on the scalar unit, one per lane
+//   MODE 3  as MODE 0, the two MACs of a giant row issued as one interleaved
+//           block (mac_pair_s) while both are scalar-counted (CW = 2)
 // Writes, per block, partials[(2 m + limb) * gridDim.x + blockIdx.x] for
 // powers m < T (32-bit limbs of canonical lane values summed: < 2^40).
 // ABL (ablations for tools/tune_u64.hip only; the product uses 0): 1 skips
@@ -412,13 +463,25 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                         if (r + 1 < NR) gn = giant(r + 1, j);
                         __builtin_amdgcn_sched_barrier(0);
                     }
+                    if constexpr (MODE == 3 && CW == 2) {
+                        if (r * CW + 1 < SG) {
+                            uint64_t c0[2] = {C0[r][0], C0[r][1]}, c1[2] = {C1[r][0], C1[r][1]};
+                            uint32_t k0[2] = {K0[r][0], K0[r][1]}, k1[2] = {K1[r][0], K1[r][1]};
+                            // (row 0's block follows row2<1>'s SGPRs: start with the disjoint set)
+                            if (r % 2 == 0) mac_pair_s<1>(c0, c1, k0, k1, g[r].x, g[r].y, bv[0], bv[1]);
+                            else mac_pair_s<0>(c0, c1, k0, k1, g[r].x, g[r].y, bv[0], bv[1]);
+                            C0[r][0] = c0[0]; C0[r][1] = c0[1]; C1[r][0] = c1[0]; C1[r][1] = c1[1];
+                            K0[r][0] = k0[0]; K0[r][1] = k0[1]; K1[r][0] = k1[0]; K1[r][1] = k1[1];
+                            continue;
+                        }
+                    }
 #pragma unroll
                     for (int c = 0; c < CW; ++c) {
                         const int m = r * CW + c;   // MAC index in the tile: parity picks the SGPR set
                         if constexpr (MODE == 1) {
                             if (m % 2 == 0) mac_m<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
                             else mac_m<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], KV[r][c], g[r].x, g[r].y, bv[c]);
-                        } else if (m < SG) {
+                        } else if (m < SG && MODE != 3) {
                             if (m % 2 == 0) mac_s<0>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], g[r].x, g[r].y, bv[c]);
                             else mac_s<1>(C0[r][c], C1[r][c], K0[r][c], K1[r][c], g[r].x, g[r].y, bv[c]);
                         } else {
@@ -463,7 +526,8 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             const int m = r * CW + c;
             unsigned __int128 v = (unsigned __int128)C0[r][c] + ((unsigned __int128)C1[r][c] << 32);
             // scalar counts are the wave's totals: added once, by lane 0
-            const bool s0 = MODE == 1 || m < SG, s1 = MODE == 0 && m < SG;
+            const bool sc = MODE == 3 ? r * CW + 1 < SG : m < SG;   // this MAC's carries counted per wave
+            const bool s0 = MODE == 1 || sc, s1 = (MODE == 0 || MODE == 3) && sc;
             const uint32_t k0 = s0 ? (lane == 0 ? K0[r][c] : 0u) : K0[r][c];
             uint64_t k1 = s1 ? (lane == 0 ? K1[r][c] : 0u) : K1[r][c];
             if (MODE == 1) k1 = (lane == 0 ? (uint64_t)K1[r][c] : 0ull) + KV[r][c];

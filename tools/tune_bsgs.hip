@@ -174,6 +174,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void k_sg(const uint32_t *ids, uint64_
     clk_end(clk, c0, r0);
 }
 
+// product-tree babies (bsgs.h Cfg TREE): same modmuls, dependency depth 3
+template <int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void k_tree(const uint32_t *ids, uint64_t n, uint64_t *partials,
+                                                      uint64_t *clk) {
+    uint64_t c0, r0;
+    clk_begin(c0, r0);
+    bsgs::body<bsgs::Cfg<8, 4, 8, 1, 1, false, false, 0, true>>(ids, n, 0, T, partials);
+    clk_end(clk, c0, r0);
+}
+
 __global__ void k_fin(const uint64_t *partials, uint32_t nb, uint32_t *out) {
     const uint32_t m = threadIdx.x;
     if (m >= T) return;
@@ -216,7 +226,10 @@ int main(int argc, char **argv) {
     std::vector<Var> vars = {{"legacy", k_legacy},
                              {"r0f0_sg8_w3", k_sg<8, 0, 0>},
                              {"r1f1_sg8_w4", k_sg<8, 1, 1, false, 4>},
-                             {"r1f1_sg8_w5", k_sg<8, 1, 1, false, 5>}};
+                             {"r1f1_sg8_w5", k_sg<8, 1, 1, false, 5>},
+                             {"tree_sg8_w5", k_tree<5>},
+                             {"tree_sg8_w4", k_tree<4>},
+                             {"r1f1_sg6_w5", k_sg<6, 1, 1, false, 5>}};
     uint32_t ref[T], got[T];
     std::vector<std::vector<float>> times(vars.size());
     std::vector<double> mhz(vars.size(), 0.0);

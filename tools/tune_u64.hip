@@ -58,6 +58,9 @@ int main() {
     CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     std::vector<Var> vars = {
         {"product: mode0 sg16, B*2^32 recomputed, occ4, row-ahead giants", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
+        {"mode3 (paired interleaved MACs) sg16 bsh occ4 ld", k_var<10, 3, 16, 0, 4, 0, true, 1>, 4},
+        {"mode3 (paired interleaved MACs) sg18 bsh occ4 ld", k_var<10, 3, 18, 0, 4, 0, true, 1>, 4},
+        {"mode3 (paired interleaved MACs) sg14 bsh occ4 ld", k_var<10, 3, 14, 0, 4, 0, true, 1>, 4},
         {"mode0 sg16 bsh occ4 (all giant rows loaded at once)", k_var<10, 0, 16, 0, 4, 0, true, 0>, 4},
         {"mode0 sg12 bsh occ4 ld", k_var<10, 0, 12, 0, 4, 0, true, 1>, 4},
         {"mode0 sg15 bsh occ4 ld", k_var<10, 0, 15, 0, 4, 0, true, 1>, 4},
