@@ -32,7 +32,6 @@ struct qk_knobs {
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)
-    int matrix_cores = 0;  // 1: the int8-MFMA encode variants (libquack_hip_mfma.so build only)
     int comm_fault = 0;    // k > 0 (tests): this rank's payload staging for the k-th collective of its
                            // next sharded operation fails, once (comm.hip fault_now)
 };
@@ -134,12 +133,6 @@ int launch_encode_u64_acc(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t
 int launch_root_test_u32(qk_ctx *ctx, const uint32_t *d_c, uint32_t d, const uint32_t *log, size_t n,
                          int use_stop, uint32_t stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters,
                          hipStream_t s);
-#ifdef QK_WITH_MATRIX_CORES
-// u64 encode on the matrix cores for T >= 9 (mfma64.hip; the opt-in
-// libquack_hip_mfma.so build); same output as launch_encode_u64
-int launch_encode_u64_mfma(qk_ctx *ctx, const uint64_t *d_ids, size_t n, uint32_t T, uint64_t *out, int acc,
-                           hipStream_t s);
-#endif
 // canonical power sums out[0..T) from per-block partials [power][block] (encode.hip)
 int launch_finalize_powers_u32(const uint64_t *partials, uint32_t nblocks, uint32_t T, uint64_t *out,
                                hipStream_t s);

@@ -27,16 +27,13 @@
 //   Lane partials -> wavefront butterfly -> LDS across the waves -> one
 //   partial per (power, block), stored [power][block] -> a finalize kernel
 //   (one workgroup per power) writes the canonical partial vector.
-// Integer-issue bound; no MFMA in this library (north_star).  The int8
-// matrix-core variants (mfma8.h / mfma64.h) compile only into
-// the opt-in libquack_hip_mfma.so (QK_WITH_MATRIX_CORES).
+// Integer-issue bound; no MFMA (north_star).  (The int8 matrix-core variant
+// measured in rounds 2-3, DESIGN.md §3.9, was removed from the sources in
+// round 4; it lives in the git history.)
 #include "ctx.h"
 #include "field.h"
 #include "bsgs.h"
 #include "bsgs64.h"
-#ifdef QK_WITH_MATRIX_CORES
-#include "mfma8.h"
-#endif
 
 // scalar-counted wrap groups of the t = 25..32 BSGS kernel (tools/tune_bsgs.hip)
 #ifndef QK_BSGS_SG_T32
@@ -110,60 +107,6 @@ __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB *
     bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD>>(ids, n, head, T, partials);
 }
 
-#ifdef QK_WITH_MATRIX_CORES
-// ---- baby-step / giant-step products on the matrix cores (mfma8.h,
-// DESIGN.md §3.2b): NM blocks of 4 giants x NN blocks of 4 babies
-template <int NM, int NN, int NBU = 4 * NN, int NAU = 4 * NM>
-__global__ __launch_bounds__(mf8::BLOCK) void k_encode_u32_mfma(const uint32_t *__restrict__ ids, uint64_t n,
-                                                               uint64_t *__restrict__ partials) {
-    mf8::body<NM, NN, 0, 1, false, NBU, NAU>(ids, n, partials);
-}
-// offset pass (T > 256): giants x^(base + NB a)
-template <int NM, int NN>
-__global__ __launch_bounds__(mf8::BLOCK) void k_encode_u32_mfma_off(const uint32_t *__restrict__ ids, uint64_t n,
-                                                                   uint64_t *__restrict__ partials, uint32_t base) {
-    mf8::body<NM, NN, 0, 1, true>(ids, n, partials, base);
-}
-
-// The signed-byte corrections of mfma8.h for the pass's powers base + 1 ..
-// base + NB*NA: cw[m] = Cw of power base + m + 1 (canonical), nmod = N mod p
-// (id slots), inv = (1 - 128 R)^-1 mod p.  S holds this batch's canonical
-// power sums (S[P - 1]): the babies' sums S_1..S_NB and, for an offset pass,
-// S_base come from earlier passes; each row uses the previous row's last
-// power as its giants' sum.  The first Tp of the pass go to out[base ..].
-__global__ __launch_bounds__(64) void k_mfma32_fix(const uint64_t *__restrict__ cw, uint32_t NB, uint32_t NA,
-                                                   uint32_t T, uint32_t base, uint32_t Tp, uint32_t nmod,
-                                                   uint32_t inv, const uint32_t *__restrict__ ids, uint64_t n,
-                                                   uint64_t *__restrict__ out, int accumulate,
-                                                   uint64_t *__restrict__ S) {
-    const uint32_t r128 = 0x80808080u;                   // 128 R, R = 0x01010101 (< p)
-    const uint32_t c1 = mul32(r128, nmod);               // 128 R N
-    const uint32_t c2 = mul32(mul32(r128, r128), nmod);  // 16384 R^2 N
-    uint32_t a0 = 0;
-    if (base == 0) {                                     // row 0 solves for its own babies' sums
-        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) S[b] = add32(mul32((uint32_t)cw[b], inv), c1);
-        __syncthreads();
-        a0 = 1;
-    }
-    for (uint32_t a = a0; a < NA; ++a) {
-        const uint32_t ga = (uint32_t)S[base + a * NB - 1];   // sum of giant a = S_(base + NB a)
-        for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) {
-            const uint32_t m = a * NB + b;
-            S[base + m] = sub32(add32((uint32_t)cw[m], mul32(r128, add32(ga, (uint32_t)S[b]))), c2);
-        }
-        __syncthreads();
-    }
-    for (uint32_t m = threadIdx.x; m < Tp; m += blockDim.x) {
-        const uint32_t v = (uint32_t)S[base + m];
-        out[base + m] = accumulate ? (uint64_t)add32((uint32_t)out[base + m], v) : (uint64_t)v;
-    }
-    if (threadIdx.x == 0 && base == 0) {
-        out[T] = accumulate ? out[T] + n : n;
-        if (n) out[T + 1] = ids[n - 1];
-        else if (!accumulate) out[T + 1] = 0;
-    }
-}
-#endif // QK_WITH_MATRIX_CORES
 
 // Pass 0 of a multi-pass encode (powers 1..80) that also writes x^80 per id
 // for pass 1 (the x^base cache, enc32_passes)
@@ -724,82 +667,6 @@ static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_id
     return scratch_release(ctx, s);
 }
 
-#ifdef QK_WITH_MATRIX_CORES
-// One matrix-core pass: powers base + 1 .. base + Tp of T (S = the batch's
-// canonical sums, T + 256 words of scratch).
-template <int NM, int NN, bool OFF, int NBU = 4 * NN, int NAU = 4 * NM>
-static int enc32_mfma_pass(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint32_t base, uint32_t Tp,
-                           uint64_t *out, int acc, uint64_t *partials, uint64_t *cw, uint64_t *S, uint32_t nb,
-                           hipStream_t s) {
-    constexpr int NA = NAU, NB = NBU, NP = NA * NB;
-    static const uint32_t inv = pow32((uint32_t)(((uint64_t)P32 + 1 - 0x80808080u) % P32), P32 - 2);
-    hipEvent_t e0 = prof_begin(ctx, s);
-    if constexpr (OFF)
-        hipLaunchKernelGGL((k_encode_u32_mfma_off<NM, NN>), dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n,
-                           partials, base);
-    else
-        hipLaunchKernelGGL((k_encode_u32_mfma<NM, NN, NBU, NAU>), dim3(nb), dim3(mf8::BLOCK), 0, s, ids, (uint64_t)n,
-                           partials);
-    prof_end(ctx, s, e0);
-    QK_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize_u32_pass, dim3(NP), dim3(BLOCK), 0, s, partials, nb, (uint32_t)NP,
-                       (const uint32_t *)nullptr, (uint64_t)0, cw, (uint64_t *)nullptr, 0);
-    const uint32_t nmod = mul32((uint32_t)(((n + 255) / 256) % P32), 256u);
-    hipLaunchKernelGGL(k_mfma32_fix, dim3(1), dim3(64), 0, s, cw, (uint32_t)NB, (uint32_t)NA, T, base, Tp, nmod, inv,
-                       ids, (uint64_t)n, out, acc, S);
-    QK_HIP_TRY(hipGetLastError());
-    return QK_OK;
-}
-
-template <int NM, int NN, int NBU = 4 * NN, int NAU = 4 * NM>
-static uint32_t mfma_grid(qk_ctx *ctx, size_t n) {
-    return grid_for(ctx, k_encode_u32_mfma<NM, NN, NBU, NAU>, (n + 255) / 256, mf8::WAVES);
-}
-
-// 9 <= T <= 256 in one pass; T > 256 in passes of <= 256 powers (pass 0 the
-// (16 babies, 16 giants) shape, then offset passes with the same 16 babies,
-// NM = the giant tiles the pass needs).  Single-pass shapes: the fewest
-// modmuls (NB - 1 + NA - 2) with NB * NA >= T, ties to fewer tiles.
-static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_t *out, int acc,
-                      hipStream_t s) {
-    const uint32_t nb = std::max(mfma_grid<1, 1>(ctx, n), mfma_grid<4, 4>(ctx, n));
-    if (int rc = ensure_scratch(ctx, ((size_t)nb * 256 + 256 + T + 256) * sizeof(uint64_t), s)) return rc;
-    uint64_t *partials = (uint64_t *)ctx->d_scratch, *cw = partials + (size_t)nb * 256, *S = cw + 256;
-    if (int rc = scratch_acquire(ctx, s)) return rc;
-    int rc = QK_OK;
-    const uint32_t T0 = std::min<uint32_t>(T, 256);
-#define QK_MF(NM_, NN_, OFF_, B_, TP_, ...)                                                             \
-    enc32_mfma_pass<NM_, NN_, OFF_, ##__VA_ARGS__>(ctx, ids, n, T, B_, TP_, out, acc, partials, cw, S, \
-                                                   std::min(nb, mfma_grid<NM_, NN_, ##__VA_ARGS__>(ctx, n)), s)
-    if (T <= 16) rc = QK_MF(1, 1, false, 0, T0);                 // 4 x 4: 5 modmuls
-    else if (T <= 20) rc = QK_MF(1, 2, false, 0, T0, 5, 4);      // 6
-    else if (T <= 24) rc = QK_MF(1, 2, false, 0, T0, 6, 4);      // 7
-    else if (T <= 32) rc = QK_MF(1, 2, false, 0, T0);            // 8 x 4: 9
-    else if (T <= 36) rc = QK_MF(2, 2, false, 0, T0, 6, 6);      // 9
-    else if (T <= 40) rc = QK_MF(2, 2, false, 0, T0, 8, 5);      // 10
-    else if (T <= 48) rc = QK_MF(2, 2, false, 0, T0, 8, 6);      // 11
-    else if (T <= 56) rc = QK_MF(2, 2, false, 0, T0, 8, 7);      // 12
-    else if (T <= 64) rc = QK_MF(2, 2, false, 0, T0);            // 8 x 8: 13
-    else if (T <= 80) rc = QK_MF(2, 3, false, 0, T0, 10, 8);     // 15
-    else if (T <= 96) rc = QK_MF(2, 3, false, 0, T0, 12, 8);     // 17
-    else if (T <= 128) rc = QK_MF(2, 4, false, 0, T0);           // 16 x 8: 21
-    else if (T <= 192) rc = QK_MF(3, 4, false, 0, T0, 16, 12);   // 25
-    else rc = QK_MF(4, 4, false, 0, T0);                         // 16 x 16: 29
-    for (uint32_t base = 256; base < T && !rc; base += 256) {
-        const uint32_t Tp = std::min<uint32_t>(256, T - base);
-        switch ((Tp + 63) / 64) {
-        case 1: rc = QK_MF(1, 4, true, base, Tp); break;
-        case 2: rc = QK_MF(2, 4, true, base, Tp); break;
-        case 3: rc = QK_MF(3, 4, true, base, Tp); break;
-        default: rc = QK_MF(4, 4, true, base, Tp); break;
-        }
-    }
-#undef QK_MF
-    if (int e = scratch_release(ctx, s); e && !rc) rc = e;
-    return rc;
-}
-
-#endif // QK_WITH_MATRIX_CORES
 
 static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
                               int acc, hipStream_t s) {
@@ -1107,12 +974,6 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
     auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
-#ifdef QK_WITH_MATRIX_CORES
-    // matrix-core variant (mfma8.h) for T >= 9: only in the
-    // opt-in libquack_hip_mfma.so build, with knob matrix_cores = 1
-    // (north_star keeps the product on the vector ALUs)
-    if (T >= 9 && ctx->knobs.matrix_cores) return enc32_mfma(ctx, ids, n, T, out, acc, s);
-#endif
 #define QK_BSGS(NB_, NA_, G_)                                                                        \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)
@@ -1184,10 +1045,6 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     // workgroup.  knob bsgs64_sg (T > 72 only) picks a carry mode
     // for measurements (tools/tune_u64.hip); knob bsgs64_off = 1 forces the
     // power chain.
-#ifdef QK_WITH_MATRIX_CORES
-    // matrix-core variant (mfma64.h), opt-in as for u32
-    if (T >= 9 && ctx->knobs.matrix_cores) return launch_encode_u64_mfma(ctx, ids, n, T, out, acc, s);
-#endif
     const int sg64 = ctx->knobs.bsgs64_sg;
     const int no64 = ctx->knobs.bsgs64_off;
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
