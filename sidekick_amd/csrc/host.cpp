@@ -6,6 +6,7 @@
 // kernel launch.  The batch paths live in encode.hip / decode.hip.
 #include "quack_hip.h"
 #include "field.h"
+#include "simd64.h"
 
 #include <string.h>
 
@@ -87,7 +88,6 @@ struct F64 {
 // truncating stores, masked for the last < 8).  Lane values stay < 2^32
 // (lazy), the stored sums canonical: the results are those of the scalar
 // chains bit for bit (tests/test_host_abi.py, every t).
-#define QK_AVX512 __attribute__((target("avx512f,avx512vl,avx512dq")))
 QK_AVX512 static inline __m512i fold512(__m512i m) {   // l + 5 h of each 64-bit lane
     const __m512i h = _mm512_srli_epi64(m, 32);
     return _mm512_add_epi64(_mm512_and_si512(m, _mm512_set1_epi64(0xFFFFFFFFll)),
@@ -139,34 +139,10 @@ QK_AVX512 static void power_walk32_avx512(uint32_t *S, uint32_t t, uint32_t x, b
     }
 }
 
-// u64 twin (p = 2^64 - 59): the lane product a b of two 64-bit values from
-// four vpmuludq (32-bit halves) with the carries of the middle and low sums
-// restored by compares, then hi 2^64 == 59 hi twice as in mul64_lazy; the
-// result < 2^64 (lazy), == a b.  b's halves are the chain step (hoisted).
-QK_AVX512 static inline __m512i mulmod64_512(__m512i a, __m512i b0, __m512i b1) {
-    const __m512i a1 = _mm512_srli_epi64(a, 32);
-    const __m512i p00 = _mm512_mul_epu32(a, b0), p01 = _mm512_mul_epu32(a, b1);
-    const __m512i p10 = _mm512_mul_epu32(a1, b0), p11 = _mm512_mul_epu32(a1, b1);
-    const __m512i mid = _mm512_add_epi64(p01, p10);
-    const __mmask8 cm = _mm512_cmplt_epu64_mask(mid, p01);             // mid wrapped: + 2^96
-    const __m512i lo = _mm512_add_epi64(p00, _mm512_slli_epi64(mid, 32));
-    const __mmask8 cl = _mm512_cmplt_epu64_mask(lo, p00);              // lo wrapped: + 2^64
-    __m512i hi = _mm512_add_epi64(p11, _mm512_srli_epi64(mid, 32));
-    hi = _mm512_mask_add_epi64(hi, cm, hi, _mm512_set1_epi64(1ll << 32));
-    hi = _mm512_mask_add_epi64(hi, cl, hi, _mm512_set1_epi64(1));      // a b = hi 2^64 + lo exactly
-    // 59 hi + lo = c 2^64 + s2 with c <= 66, then s2 + 59 c (one more wrap at most)
-    const __m512i c59 = _mm512_set1_epi64(59);
-    const __m512i x = _mm512_mul_epu32(hi, c59), y = _mm512_mul_epu32(_mm512_srli_epi64(hi, 32), c59);
-    const __m512i s1 = _mm512_add_epi64(x, _mm512_slli_epi64(y, 32));
-    const __mmask8 c1 = _mm512_cmplt_epu64_mask(s1, x);
-    const __m512i s2 = _mm512_add_epi64(s1, lo);
-    const __mmask8 c2 = _mm512_cmplt_epu64_mask(s2, s1);
-    __m512i c = _mm512_srli_epi64(y, 32);
-    c = _mm512_mask_add_epi64(c, c1, c, _mm512_set1_epi64(1));
-    c = _mm512_mask_add_epi64(c, c2, c, _mm512_set1_epi64(1));
-    const __m512i r = _mm512_add_epi64(s2, _mm512_mul_epu32(c, c59));
-    return _mm512_mask_add_epi64(r, _mm512_cmplt_epu64_mask(r, s2), r, c59);
-}
+// u64 twin (p = 2^64 - 59): the lane product of simd64.h (four vpmuludq,
+// carries restored by compares, 2^64 == 59 twice); b's halves are the chain
+// step (hoisted).
+using simd::mulmod64_512;
 QK_AVX512 static inline void acc64_512(uint64_t *S, uint32_t k, uint32_t t, __m512i v, bool add) {
     const __m512i P = _mm512_set1_epi64((long long)P64), c59 = _mm512_set1_epi64(59);
     const uint32_t rem = t - k;

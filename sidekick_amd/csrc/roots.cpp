@@ -31,6 +31,7 @@
 // degree-m polynomial is ~1.5 m^2 multiply-adds.
 #include "quack_hip.h"
 #include "field.h"
+#include "simd64.h"
 
 #include <string.h>
 
@@ -44,7 +45,6 @@ namespace {
 
 using namespace qk;
 
-#define QK_AVX512 __attribute__((target("avx512f,avx512vl,avx512dq")))
 
 static bool cpu_has_avx512() {
     static const int ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
@@ -150,8 +150,247 @@ QK_AVX512 static void mullin32_avx512(uint32_t *a, size_t m, uint32_t c, const u
     }
 }
 
+// ---- the u64 field (p64) on AVX-512: rows and the squaring --------------
+// Lane products by simd64.h's mulmod64_512 (four vpmuludq, lazy < 2^64).
+QK_AVX512 static inline __m512i ld8q(const uint64_t *p, size_t rem) {
+    return rem >= 8 ? _mm512_loadu_si512(p) : _mm512_maskz_loadu_epi64((__mmask8)((1u << rem) - 1u), p);
+}
+QK_AVX512 static inline void st8q(uint64_t *p, size_t rem, __m512i v) {
+    if (rem >= 8) _mm512_storeu_si512(p, v);
+    else _mm512_mask_storeu_epi64(p, (__mmask8)((1u << rem) - 1u), v);
+}
+// d[i] = alpha d[i] - beta s[i], i < m (alpha = 1: d[i] - beta s[i])
+QK_AVX512 static void axmy64_avx512(uint64_t *d, const uint64_t *s, size_t m, uint64_t alpha, uint64_t beta) {
+    const __m512i A0 = simd::lo32x8(alpha), A1 = simd::hi32x8(alpha), B0 = simd::lo32x8(beta),
+                  B1 = simd::hi32x8(beta);
+    for (size_t i = 0; i < m; i += 8) {
+        const size_t r = m - i;
+        __m512i x = ld8q(d + i, r);
+        if (alpha != 1) x = simd::canon64_512(simd::mulmod64_512(x, A0, A1));
+        const __m512i y = simd::canon64_512(simd::mulmod64_512(ld8q(s + i, r), B0, B1));
+        st8q(d + i, r, simd::sub64_512(x, y));
+    }
+}
+QK_AVX512 static void scale64_avx512(uint64_t *d, size_t m, uint64_t alpha) {
+    const __m512i A0 = simd::lo32x8(alpha), A1 = simd::hi32x8(alpha);
+    for (size_t i = 0; i < m; i += 8)
+        st8q(d + i, m - i, simd::canon64_512(simd::mulmod64_512(ld8q(d + i, m - i), A0, A1)));
+}
+// (lo, cnt) lanes += v: a lazy sum lo + cnt 2^64 (the carry restored by a compare)
+QK_AVX512 static inline void addc64_512(uint64_t *lo, uint64_t *cnt, __m512i v) {
+    const __m512i s = _mm512_add_epi64(_mm512_loadu_si512(lo), v);
+    const __mmask8 c = _mm512_cmplt_epu64_mask(s, v);
+    _mm512_storeu_si512(lo, s);
+    const __m512i k = _mm512_loadu_si512(cnt);
+    _mm512_storeu_si512(cnt, _mm512_mask_add_epi64(k, c, k, _mm512_set1_epi64(1)));
+}
+// lo + cnt 2^64 mod p, canonical (cnt small: 2^64 == 59)
+static inline uint64_t red_lc(uint64_t lo, uint64_t cnt) {
+    uint64_t s = lo + C64 * cnt;
+    if (s < lo) s += C64;
+    return canon64(s);
+}
+// GF(p64) squaring mod a monic f of degree m on AVX-512: products a_i a_j
+// (i < j, doubled through 2 a_i) as lazy lane products summed into 64-bit
+// lanes whose carries are counted, the top-down reduction by -f the same
+// way, one canonical reduction per coefficient.  a64 / nf64 hold a and -f
+// zero-padded to a multiple of 8 past m; lo / cnt have 2m + 16 slots.
+QK_AVX512 static void sqr64_avx512(uint64_t *a, size_t m, const uint64_t *nf64, uint64_t *a64, uint64_t *lo,
+                                   uint64_t *cnt) {
+    const size_t mb = (m + 7) & ~(size_t)7;
+    for (size_t i = 0; i < m; ++i) a64[i] = a[i];
+    for (size_t i = m; i < mb + 8; ++i) a64[i] = 0;
+    for (size_t i = 0; i < 2 * m + 16; ++i) lo[i] = cnt[i] = 0;
+    for (size_t i = 0; i < m; ++i) {
+        const uint64_t ai = a[i];
+        if (!ai) continue;
+        const uint64_t sq = mul64_lazy(ai, ai), o = lo[2 * i];
+        lo[2 * i] = o + sq;
+        cnt[2 * i] += lo[2 * i] < sq;
+        const uint64_t a2 = add64(ai, ai);
+        const __m512i A0 = simd::lo32x8(a2), A1 = simd::hi32x8(a2);
+        for (size_t j = i + 1; j < m; j += 8)
+            addc64_512(lo + i + j, cnt + i + j, simd::mulmod64_512(_mm512_loadu_si512(a64 + j), A0, A1));
+    }
+    for (size_t k = 2 * m - 1; k-- > m;) {
+        const uint64_t q = red_lc(lo[k], cnt[k]);
+        if (!q) continue;
+        const __m512i Q0 = simd::lo32x8(q), Q1 = simd::hi32x8(q);
+        for (size_t i = 0; i < m; i += 8)
+            addc64_512(lo + k - m + i, cnt + k - m + i, simd::mulmod64_512(_mm512_loadu_si512(nf64 + i), Q0, Q1));
+    }
+    for (size_t i = 0; i < m; ++i) a[i] = red_lc(lo[i], cnt[i]);
+}
+
+// The same squaring on AVX-512 IFMA (52-bit limbs): a = l0 + l1 2^52
+// (l1 < 2^12), and every product goes into three column sums of weights 1,
+// 2^52 and 2^104 with seven vpmadd52{lo,hi}uq — no reduction per product;
+// one scalar reduction per coefficient (2^104 == 59 2^40).  The products
+// a_i a_j (i < j) are summed once and the columns doubled before the
+// diagonal is added; the top-down reduction adds q (-f_i) the same way.
+// Column sums stay below 2^61 for m <= 1000 (at most 3 (2m + 2) terms of
+// < 2^52 each in the middle column).
+#define QK_IFMA __attribute__((target("avx512f,avx512vl,avx512dq,avx512ifma")))
+static bool cpu_has_ifma() {
+    static const int ok = cpu_has_avx512() && __builtin_cpu_supports("avx512ifma");
+    return ok;
+}
+constexpr uint64_t M52 = (1ull << 52) - 1;
+// the canonical values of column sums c0 + c1 2^52 + c2 2^104 on eight
+// lanes: lo + hi 2^64 = c0 + c1 2^52 + c2 59 2^40 (2^104 == 59 2^40) with
+// the carries restored by compares, then hi 2^64 == 59 hi (hi < 2^50)
+QK_IFMA static inline __m512i red_cols8(__m512i c0, __m512i c1, __m512i c2) {
+    const __m512i one = _mm512_set1_epi64(1), c59 = _mm512_set1_epi64(59);
+    const __m512i lo1 = _mm512_add_epi64(c0, _mm512_slli_epi64(c1, 52));
+    __m512i hi = _mm512_srli_epi64(c1, 12);
+    hi = _mm512_mask_add_epi64(hi, _mm512_cmplt_epu64_mask(lo1, c0), hi, one);
+    const __m512i w = _mm512_mul_epu32(c2, c59);   // c2 < 2^32
+    const __m512i lo = _mm512_add_epi64(lo1, _mm512_slli_epi64(w, 40));
+    hi = _mm512_add_epi64(hi, _mm512_srli_epi64(w, 24));
+    hi = _mm512_mask_add_epi64(hi, _mm512_cmplt_epu64_mask(lo, lo1), hi, one);
+    const __m512i s = _mm512_add_epi64(lo, _mm512_mullo_epi64(hi, c59));
+    __m512i r = _mm512_mask_add_epi64(s, _mm512_cmplt_epu64_mask(s, lo), s, c59);
+    const __m512i P = _mm512_set1_epi64((long long)P64);
+    return _mm512_mask_sub_epi64(r, _mm512_cmpge_epu64_mask(r, P), r, P);
+}
+
+// the aligned columns c[8q .. 8q+8) += x * y over eight lanes (x's limbs
+// broadcast, y a window of limbs): every read-modify-write hits the same
+// aligned 64-byte vectors, so a store forwards to the next load of it
+QK_IFMA static inline void fma52x8(uint64_t *c0, uint64_t *c1, uint64_t *c2, __m512i x0, __m512i x1, __m512i y0,
+                                   __m512i y1) {
+    __m512i a = _mm512_load_si512(c0), b = _mm512_load_si512(c1), c = _mm512_load_si512(c2);
+    a = _mm512_madd52lo_epu64(a, x0, y0);
+    b = _mm512_madd52hi_epu64(b, x0, y0);
+    b = _mm512_madd52lo_epu64(b, x0, y1);
+    b = _mm512_madd52lo_epu64(b, x1, y0);
+    c = _mm512_madd52hi_epu64(c, x0, y1);
+    c = _mm512_madd52hi_epu64(c, x1, y0);
+    c = _mm512_madd52lo_epu64(c, x1, y1);
+    _mm512_store_si512(c0, a);
+    _mm512_store_si512(c1, b);
+    _mm512_store_si512(c2, c);
+}
+constexpr size_t IPAD = 8;   // zero limbs before index 0 of the limb arrays
+// l0 / l1: a's limbs (IPAD zeros, the m limbs, zeros to IPAD + mb + 16);
+// tl0 / tl1: the limbs of z^k mod f, k = m .. 2m-2, one row of mb per k,
+// 64-byte aligned; c0 / c1 / c2: 2 mb + 16 column sums, 64-byte aligned
+QK_IFMA static void sqr64_ifma(uint64_t *a, size_t m, const uint64_t *tl0, const uint64_t *tl1, uint64_t *l0,
+                               uint64_t *l1, uint64_t *c0, uint64_t *c1, uint64_t *c2) {
+    const size_t mb = (m + 7) & ~(size_t)7;
+    for (size_t i = 0; i < m; ++i) {
+        l0[IPAD + i] = a[i] & M52;
+        l1[IPAD + i] = a[i] >> 52;
+    }
+    for (size_t i = 0; i < 2 * mb + 16; ++i) c0[i] = c1[i] = c2[i] = 0;
+    // off-diagonal products a_i a_j, i < j: column vector q gets j = 8q + lane - i
+    for (size_t i = 0; i + 1 < m; ++i) {
+        if (!a[i]) continue;
+        const __m512i x0 = _mm512_set1_epi64((long long)(a[i] & M52)), x1 = _mm512_set1_epi64((long long)(a[i] >> 52));
+        for (size_t q = (2 * i + 1) / 8; 8 * q <= i + m - 1; ++q) {
+            const long long lowest = (long long)(8 * q) - (long long)i;   // j of lane 0
+            // lanes with j <= i take no product
+            const int skip = (int)((long long)i - lowest + 1);
+            const __mmask8 mk = skip <= 0 ? (__mmask8)0xFF : (__mmask8)(0xFFu << skip);
+            const uint64_t *w0 = l0 + IPAD + lowest, *w1 = l1 + IPAD + lowest;
+            fma52x8(c0 + 8 * q, c1 + 8 * q, c2 + 8 * q, x0, x1, _mm512_maskz_loadu_epi64(mk, w0),
+                    _mm512_maskz_loadu_epi64(mk, w1));
+        }
+    }
+    for (size_t k = 0; k < 2 * mb; k += 8) {   // double the off-diagonal sums
+        _mm512_store_si512(c0 + k, _mm512_slli_epi64(_mm512_load_si512(c0 + k), 1));
+        _mm512_store_si512(c1 + k, _mm512_slli_epi64(_mm512_load_si512(c1 + k), 1));
+        _mm512_store_si512(c2 + k, _mm512_slli_epi64(_mm512_load_si512(c2 + k), 1));
+    }
+    for (size_t i = 0; i < m; ++i) {   // the diagonal a_i^2 = l0^2 + 2 l0 l1 2^52 + l1^2 2^104
+        const uint64_t u0 = a[i] & M52, u1 = a[i] >> 52;
+        const unsigned __int128 p0 = (unsigned __int128)u0 * u0;
+        const uint64_t v = u0 * u1;   // < 2^64
+        c0[2 * i] += (uint64_t)p0 & M52;
+        c1[2 * i] += (uint64_t)(p0 >> 52) + 2 * (v & M52);
+        c2[2 * i] += 2 * (v >> 52) + u1 * u1;
+    }
+    // reduction without the top-down chain: z^k mod f for k = m .. 2m-2 is
+    // precomputed (tl0 / tl1: row k - m, mb limbs each), so the result is
+    // the low columns plus sum_k s_k (z^k mod f) — every s_k a canonical
+    // value of the product columns alone, the sums in registers per output
+    // vector
+    alignas(64) uint64_t s0[1024 + 8], s1[1024 + 8];   // (m <= 1024: ModRing)
+    const __m512i mk52 = _mm512_set1_epi64((long long)M52);
+    for (size_t k = m; k + 1 < 2 * m; k += 8) {   // (lanes past 2m - 2 read zero columns)
+        const __m512i v = red_cols8(_mm512_loadu_si512(c0 + k), _mm512_loadu_si512(c1 + k), _mm512_loadu_si512(c2 + k));
+        _mm512_store_si512(s0 + (k - m), _mm512_and_si512(v, mk52));
+        _mm512_store_si512(s1 + (k - m), _mm512_srli_epi64(v, 52));
+    }
+    for (size_t v = 0; 8 * v < m; ++v) {
+        __m512i A = _mm512_load_si512(c0 + 8 * v), B = _mm512_load_si512(c1 + 8 * v), C = _mm512_load_si512(c2 + 8 * v);
+        for (size_t r = 0; r + 1 < m; ++r) {
+            const __m512i x0 = _mm512_set1_epi64((long long)s0[r]), x1 = _mm512_set1_epi64((long long)s1[r]);
+            const __m512i y0 = _mm512_load_si512(tl0 + r * mb + 8 * v), y1 = _mm512_load_si512(tl1 + r * mb + 8 * v);
+            A = _mm512_madd52lo_epu64(A, x0, y0);
+            B = _mm512_madd52hi_epu64(B, x0, y0);
+            B = _mm512_madd52lo_epu64(B, x0, y1);
+            B = _mm512_madd52lo_epu64(B, x1, y0);
+            C = _mm512_madd52hi_epu64(C, x0, y1);
+            C = _mm512_madd52hi_epu64(C, x1, y0);
+            C = _mm512_madd52lo_epu64(C, x1, y1);
+        }
+        const __m512i r = red_cols8(A, B, C);
+        const size_t rem = m - 8 * v;
+        if (rem >= 8) _mm512_storeu_si512(a + 8 * v, r);
+        else _mm512_mask_storeu_epi64(a + 8 * v, (__mmask8)((1u << rem) - 1u), r);
+    }
+}
+
+// axmy / scale for the u64 field on IFMA: alpha d + (p - beta) s as column
+// sums of 52-bit limb products, one red_cols8 per eight coefficients
+QK_IFMA static inline void split52(__m512i v, __m512i &l0, __m512i &l1) {
+    l0 = _mm512_and_si512(v, _mm512_set1_epi64((long long)M52));
+    l1 = _mm512_srli_epi64(v, 52);
+}
+QK_IFMA static inline void prod52(__m512i &A, __m512i &B, __m512i &C, __m512i x0, __m512i x1, __m512i y0,
+                                  __m512i y1) {
+    A = _mm512_madd52lo_epu64(A, x0, y0);
+    B = _mm512_madd52hi_epu64(B, x0, y0);
+    B = _mm512_madd52lo_epu64(B, x0, y1);
+    B = _mm512_madd52lo_epu64(B, x1, y0);
+    C = _mm512_madd52hi_epu64(C, x0, y1);
+    C = _mm512_madd52hi_epu64(C, x1, y0);
+    C = _mm512_madd52lo_epu64(C, x1, y1);
+}
+QK_IFMA static void axmy64_ifma(uint64_t *d, const uint64_t *s, size_t m, uint64_t alpha, uint64_t beta) {
+    const uint64_t nb = beta ? P64 - beta : 0;
+    const __m512i a0 = _mm512_set1_epi64((long long)(alpha & M52)), a1 = _mm512_set1_epi64((long long)(alpha >> 52)),
+                  b0 = _mm512_set1_epi64((long long)(nb & M52)), b1 = _mm512_set1_epi64((long long)(nb >> 52));
+    for (size_t i = 0; i < m; i += 8) {
+        const size_t r = m - i;
+        __m512i d0, d1, s0, s1;
+        split52(ld8q(d + i, r), d0, d1);
+        split52(ld8q(s + i, r), s0, s1);
+        __m512i A = _mm512_setzero_si512(), B = A, C = A;
+        prod52(A, B, C, a0, a1, d0, d1);
+        prod52(A, B, C, b0, b1, s0, s1);
+        st8q(d + i, r, red_cols8(A, B, C));
+    }
+}
+QK_IFMA static void scale64_ifma(uint64_t *d, size_t m, uint64_t alpha) {
+    const __m512i a0 = _mm512_set1_epi64((long long)(alpha & M52)), a1 = _mm512_set1_epi64((long long)(alpha >> 52));
+    for (size_t i = 0; i < m; i += 8) {
+        const size_t r = m - i;
+        __m512i d0, d1;
+        split52(ld8q(d + i, r), d0, d1);
+        __m512i A = _mm512_setzero_si512(), B = A, C = A;
+        prod52(A, B, C, a0, a1, d0, d1);
+        st8q(d + i, r, red_cols8(A, B, C));
+    }
+}
+
 template <class F> static inline bool vec32(size_t m) {
     if constexpr (F::W == 32) return m >= 8 && cpu_has_avx512();
+    else return false;
+}
+template <class F> static inline bool vec64(size_t m) {
+    if constexpr (F::W == 64) return m >= 8 && cpu_has_avx512();
     else return false;
 }
 
@@ -160,12 +399,16 @@ template <class F>
 static void axmy(typename F::T *d, const typename F::T *s, size_t m, typename F::T alpha, typename F::T beta) {
     if constexpr (F::W == 32) {
         if (vec32<F>(m)) return axmy32_avx512(d, s, m, alpha, beta);
+    } else {
+        if (vec64<F>(m)) return cpu_has_ifma() ? axmy64_ifma(d, s, m, alpha, beta) : axmy64_avx512(d, s, m, alpha, beta);
     }
     for (size_t i = 0; i < m; ++i) d[i] = F::sub(alpha == 1 ? d[i] : F::mul(d[i], alpha), F::mul(beta, s[i]));
 }
 template <class F> static void scale(typename F::T *d, size_t m, typename F::T alpha) {
     if constexpr (F::W == 32) {
         if (vec32<F>(m)) return scale32_avx512(d, m, alpha);
+    } else {
+        if (vec64<F>(m)) return cpu_has_ifma() ? scale64_ifma(d, m, alpha) : scale64_avx512(d, m, alpha);
     }
     for (size_t i = 0; i < m; ++i) d[i] = F::mul(d[i], alpha);
 }
@@ -333,23 +576,50 @@ template <class F> struct ModRing {
     size_t m;
     std::vector<T> nf;       // -f_i, i < m
     std::vector<A> acc;      // 2m - 1 lazy accumulators
-    // the AVX-512 form (u32 field, m >= 8): -f and a widened and padded
-    bool vec = false;
-    std::vector<uint64_t> nf64, a64, acc64;
+    // the AVX-512 form (m >= 8): -f (u32: widened) and a zero-padded; lazy
+    // lane sums (u64 field: with carry counts)
+    bool vec = false, ifma = false;
+    std::vector<uint64_t> nf64, a64, acc64, cnt64;
+    std::vector<uint64_t> tab, l0, l1, cols;   // the IFMA form (u64 field)
+    const uint64_t *tl0 = nullptr, *tl1 = nullptr;
     std::vector<T> tmp;
 
     explicit ModRing(const Poly<F> &f) : m(f.size() - 1), nf(m), acc(2 * m) {
         for (size_t i = 0; i < m; ++i) nf[i] = F::neg(f[i]);
-        if constexpr (F::W == 32) {
-            vec = m >= 8 && cpu_has_avx512();
-            if (vec) {
-                const size_t mb = (m + 7) & ~(size_t)7;
-                nf64.assign(mb + 8, 0);
-                for (size_t i = 0; i < m; ++i) nf64[i] = nf[i];
-                a64.assign(mb + 8, 0);
-                acc64.assign(2 * m + 16, 0);
-                tmp.assign(m, 0);
+        vec = m >= 8 && cpu_has_avx512();
+        if (vec) {
+            const size_t mb = (m + 7) & ~(size_t)7;
+            nf64.assign(mb + 8, 0);
+            for (size_t i = 0; i < m; ++i) nf64[i] = nf[i];
+            a64.assign(mb + 8, 0);
+            acc64.assign(2 * m + 16, 0);
+            if constexpr (F::W == 64) {
+                cnt64.assign(2 * m + 16, 0);
+                ifma = cpu_has_ifma();
+                ifma = ifma && m <= 1024;
+                if (ifma) {
+                    // z^k mod f for k = m .. 2m-2 as limb rows (z^m = -f, then
+                    // z^(k+1) = z * z^k: shift, the top coefficient times -f)
+                    tab.assign(2 * (m - 1) * mb + 8, 0);
+                    uint64_t *t0 = tab.data() + ((8 - ((uintptr_t)tab.data() / 8) % 8) % 8), *t1 = t0 + (m - 1) * mb;
+                    std::vector<T> row(nf);
+                    for (size_t r = 0; r + 1 < m; ++r) {
+                        for (size_t i = 0; i < m; ++i) {
+                            t0[r * mb + i] = (uint64_t)row[i] & M52;
+                            t1[r * mb + i] = (uint64_t)row[i] >> 52;
+                        }
+                        const T top = row[m - 1];
+                        for (size_t i = m; i-- > 1;) row[i] = F::add(row[i - 1], F::mul(top, nf[i]));
+                        row[0] = F::mul(top, nf[0]);
+                    }
+                    tl0 = t0;
+                    tl1 = t1;
+                    l0.assign(IPAD + mb + 16, 0);
+                    l1.assign(IPAD + mb + 16, 0);
+                    cols.assign(3 * (2 * mb + 16) + 8, 0);   // + 8: room to align to 64 bytes
+                }
             }
+            tmp.assign(m, 0);
         }
     }
     // acc[0 .. 2m-1) (degree <= 2m-2) -> r (m coefficients): top-down, each
@@ -363,11 +633,17 @@ template <class F> struct ModRing {
         for (size_t i = 0; i < m; ++i) r[i] = F::red(acc[i]);
     }
     void sqr(std::vector<T> &a) {
-        if constexpr (F::W == 32) {
-            if (vec) {
+        if (vec) {
+            if constexpr (F::W == 32) {
                 sqr32_avx512(a.data(), m, nf64.data(), a64.data(), acc64.data());
-                return;
+            } else if (ifma) {
+                const size_t cw = 2 * ((m + 7) & ~(size_t)7) + 16;
+                uint64_t *c = cols.data() + ((8 - ((uintptr_t)cols.data() / 8) % 8) % 8);   // 64-byte aligned
+                sqr64_ifma((uint64_t *)a.data(), m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+            } else {
+                sqr64_avx512((uint64_t *)a.data(), m, nf64.data(), a64.data(), acc64.data(), cnt64.data());
             }
+            return;
         }
         std::fill(acc.begin(), acc.end(), A(0));
         for (size_t i = 0; i < m; ++i) {
