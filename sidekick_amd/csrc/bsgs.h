@@ -237,8 +237,11 @@ __device__ __forceinline__ void row2m(uint64_t &a0, uint64_t &a1, uint32_t b0, u
 //          of two below): the same NB - 1 lazy modmuls at dependency depth
 //          log2(NB) instead of NB - 1 (plain passes with min-tracked folds)
 template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false, bool OFF_ = false,
-          int XC_ = 0, bool TREE_ = false>
+          int XC_ = 0, bool TREE_ = false, int PRIO_ = 0>
 struct Cfg {
+    // PRIO  s_setprio around the MAC phase: 1 raises the priority of a wave
+    //       in its MACs (their scalar wrap counts), 2 of a wave in its modmuls
+    static constexpr int PRIO = PRIO_;
     static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_, XC = XC_;
     static constexpr bool TREE = TREE_;
     static_assert(!TREE_ || (!OFF_ && FOLD_ == 1), "product-tree babies: plain passes, min-tracked folds");
@@ -418,7 +421,11 @@ __device__ __forceinline__ void one(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id, 
     if (__builtin_expect(__any(w), 0)) {
         if (w) powers_exact<C>(B, A, base, xb, xnext);
     }
+    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    if constexpr (C::PRIO == 2) __builtin_amdgcn_s_setprio(0);
     accumulate<C>(S, B, A);
+    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (C::PRIO == 2) __builtin_amdgcn_s_setprio(1);
 }
 
 // two ids at once: their power chains are independent straight-line code, so

@@ -59,40 +59,46 @@ QK_AVX512 static inline __m512i fold512(__m512i m) {
                             _mm512_add_epi64(h, _mm512_slli_epi64(h, 2)));
 }
 
-// GF(p32) squaring mod a monic f of degree m on AVX-512: the same lazy sums
-// as the scalar ModRing::sqr (folded products < 6 * 2^32, at most 2m per
-// coefficient), eight 32x32 products per vpmuludq.  a64 / nf64 hold a and
-// -f zero-extended to 64 bits and zero-padded to a multiple of 8 past m, so
-// the vector loops run over whole blocks (padding lanes add 0); acc has
-// 2m + 16 slots.
-QK_AVX512 static void sqr32_avx512(uint32_t *a, size_t m, const uint64_t *nf64, uint64_t *a64, uint64_t *acc) {
+// GF(p32) squaring mod a monic f of degree m on AVX-512: lazy sums of
+// folded products (< 6 * 2^32 each, at most 2m per coefficient), eight 32x32
+// products per vpmuludq.  The products a_i a_j (i < j, through 2 a_i) go to
+// the aligned coefficient vector q with a window of a (j = 8q + lane - i;
+// a64: IPAD32 zeros, a, zeros), so every read-modify-write hits the same
+// aligned 64-byte vectors; the reduction adds s_k (z^k mod f) for
+// k = m .. 2m-2 from a precomputed table (t64: one row of mb per k) into
+// register sums per output vector — no top-down chain.  acc: 2 mb + 16
+// slots, 64-byte aligned.
+constexpr size_t IPAD32 = 8;
+QK_AVX512 static void sqr32_avx512(uint32_t *a, size_t m, const uint64_t *t64, uint64_t *a64, uint64_t *acc) {
     const size_t mb = (m + 7) & ~(size_t)7;
-    for (size_t i = 0; i < m; ++i) a64[i] = a[i];
-    for (size_t i = m; i < mb + 8; ++i) a64[i] = 0;
-    for (size_t i = 0; i < 2 * m + 16; ++i) acc[i] = 0;
+    for (size_t i = 0; i < m; ++i) a64[IPAD32 + i] = a[i];
+    for (size_t i = 0; i < 2 * mb + 16; i += 8) _mm512_store_si512(acc + i, _mm512_setzero_si512());
     for (size_t i = 0; i < m; ++i) {
         const uint64_t ai = a[i];
         if (!ai) continue;
         const uint64_t sq = ai * ai;
         acc[2 * i] += (sq >> 32) * C32 + (uint32_t)sq;
-        const uint64_t a2 = add32((uint32_t)ai, (uint32_t)ai);
-        const __m512i b = _mm512_set1_epi64((long long)a2);
-        for (size_t j = i + 1; j < m; j += 8) {
-            const __m512i x = _mm512_loadu_si512(a64 + j);
-            __m512i *dst = reinterpret_cast<__m512i *>(acc + i + j);
-            _mm512_storeu_si512(dst, _mm512_add_epi64(_mm512_loadu_si512(dst), fold512(_mm512_mul_epu32(b, x))));
+        if (i + 1 >= m) continue;
+        const __m512i b = _mm512_set1_epi64((long long)add32((uint32_t)ai, (uint32_t)ai));
+        for (size_t q = (2 * i + 1) / 8; 8 * q <= i + m - 1; ++q) {
+            const long long lowest = (long long)(8 * q) - (long long)i;   // j of lane 0
+            const int skip = (int)((long long)i - lowest + 1);          // lanes with j <= i
+            const __mmask8 mk = skip <= 0 ? (__mmask8)0xFF : (__mmask8)(0xFFu << skip);
+            const __m512i x = _mm512_maskz_loadu_epi64(mk, a64 + IPAD32 + lowest);
+            __m512i *dst = reinterpret_cast<__m512i *>(acc + 8 * q);
+            _mm512_store_si512(dst, _mm512_add_epi64(_mm512_load_si512(dst), fold512(_mm512_mul_epu32(b, x))));
         }
     }
-    for (size_t k = 2 * m - 1; k-- > m;) {
-        const uint32_t q = canon32(fold64_32(acc[k]));
-        if (!q) continue;
-        const __m512i b = _mm512_set1_epi64((long long)q);
-        uint64_t *base = acc + k - m;
-        for (size_t i = 0; i < m; i += 8) {
-            __m512i *dst = reinterpret_cast<__m512i *>(base + i);
-            const __m512i y = _mm512_loadu_si512(nf64 + i);
-            _mm512_storeu_si512(dst, _mm512_add_epi64(_mm512_loadu_si512(dst), fold512(_mm512_mul_epu32(b, y))));
+    alignas(64) uint64_t sv[1024 + 8];   // (m <= 1024: ModRing)
+    for (size_t k = m; k + 1 < 2 * m; ++k) sv[k - m] = canon32(fold64_32(acc[k]));
+    for (size_t v = 0; 8 * v < m; ++v) {
+        __m512i s = _mm512_load_si512(acc + 8 * v);
+        for (size_t r = 0; r + 1 < m; ++r) {
+            if (!sv[r]) continue;
+            s = _mm512_add_epi64(s, fold512(_mm512_mul_epu32(_mm512_set1_epi64((long long)sv[r]),
+                                                            _mm512_load_si512(t64 + r * mb + 8 * v))));
         }
+        _mm512_store_si512(acc + 8 * v, s);
     }
     for (size_t i = 0; i < m; ++i) a[i] = canon32(fold64_32(acc[i]));
 }
@@ -132,10 +138,6 @@ QK_AVX512 static void axmy32_avx512(uint32_t *d, const uint32_t *s, size_t m, ui
         st8(d + i, r, subc512(x, mulc512(ld8(s + i, r), B)));
     }
 }
-QK_AVX512 static void scale32_avx512(uint32_t *d, size_t m, uint32_t alpha) {
-    const __m512i A = _mm512_set1_epi64(alpha);
-    for (size_t i = 0; i < m; i += 8) st8(d + i, m - i, mulc512(ld8(d + i, m - i), A));
-}
 // a <- a (z + c) mod f: out[i] = a[i-1] + c a[i] + top nf[i]  (a[-1] = 0)
 QK_AVX512 static void mullin32_avx512(uint32_t *a, size_t m, uint32_t c, const uint32_t *nf, uint32_t *tmp) {
     const uint32_t top = a[m - 1];
@@ -170,11 +172,6 @@ QK_AVX512 static void axmy64_avx512(uint64_t *d, const uint64_t *s, size_t m, ui
         const __m512i y = simd::canon64_512(simd::mulmod64_512(ld8q(s + i, r), B0, B1));
         st8q(d + i, r, simd::sub64_512(x, y));
     }
-}
-QK_AVX512 static void scale64_avx512(uint64_t *d, size_t m, uint64_t alpha) {
-    const __m512i A0 = simd::lo32x8(alpha), A1 = simd::hi32x8(alpha);
-    for (size_t i = 0; i < m; i += 8)
-        st8q(d + i, m - i, simd::canon64_512(simd::mulmod64_512(ld8q(d + i, m - i), A0, A1)));
 }
 // (lo, cnt) lanes += v: a lazy sum lo + cnt 2^64 (the carry restored by a compare)
 QK_AVX512 static inline void addc64_512(uint64_t *lo, uint64_t *cnt, __m512i v) {
@@ -373,17 +370,6 @@ QK_IFMA static void axmy64_ifma(uint64_t *d, const uint64_t *s, size_t m, uint64
         st8q(d + i, r, red_cols8(A, B, C));
     }
 }
-QK_IFMA static void scale64_ifma(uint64_t *d, size_t m, uint64_t alpha) {
-    const __m512i a0 = _mm512_set1_epi64((long long)(alpha & M52)), a1 = _mm512_set1_epi64((long long)(alpha >> 52));
-    for (size_t i = 0; i < m; i += 8) {
-        const size_t r = m - i;
-        __m512i d0, d1;
-        split52(ld8q(d + i, r), d0, d1);
-        __m512i A = _mm512_setzero_si512(), B = A, C = A;
-        prod52(A, B, C, a0, a1, d0, d1);
-        st8q(d + i, r, red_cols8(A, B, C));
-    }
-}
 
 template <class F> static inline bool vec32(size_t m) {
     if constexpr (F::W == 32) return m >= 8 && cpu_has_avx512();
@@ -403,14 +389,6 @@ static void axmy(typename F::T *d, const typename F::T *s, size_t m, typename F:
         if (vec64<F>(m)) return cpu_has_ifma() ? axmy64_ifma(d, s, m, alpha, beta) : axmy64_avx512(d, s, m, alpha, beta);
     }
     for (size_t i = 0; i < m; ++i) d[i] = F::sub(alpha == 1 ? d[i] : F::mul(d[i], alpha), F::mul(beta, s[i]));
-}
-template <class F> static void scale(typename F::T *d, size_t m, typename F::T alpha) {
-    if constexpr (F::W == 32) {
-        if (vec32<F>(m)) return scale32_avx512(d, m, alpha);
-    } else {
-        if (vec64<F>(m)) return cpu_has_ifma() ? scale64_ifma(d, m, alpha) : scale64_avx512(d, m, alpha);
-    }
-    for (size_t i = 0; i < m; ++i) d[i] = F::mul(d[i], alpha);
 }
 
 // splitting arity per field (a divisor of p - 1; measured on d = 8..64,
@@ -543,14 +521,20 @@ template <class F> Poly<F> div_monic(Poly<F> a, const Poly<F> &b) {
 // a <- a mod b up to a nonzero scalar, fraction-free: each step cancels a's
 // leading term as lead(b) a - lead(a) z^s b (no inversion; a field inverse
 // costs ~60 multiplications, more than the extra row of products here)
+// One pass per step over a's coefficients: a_i <- lb a_i - la b_(i-s) with
+// b zero-extended below (bz: a.size() zeros, then b), so the scaling of the
+// low part and the row operation are one vector row.
 template <class F> void rem_ff(Poly<F> &a, const Poly<F> &b) {
     const size_t m = b.size() - 1;
+    if (a.size() <= m) return;
     const typename F::T lb = b.back();
+    const size_t pad = a.size();
+    Poly<F> bz(pad + b.size(), 0);
+    std::copy(b.begin(), b.end(), bz.begin() + pad);
     while (a.size() > m) {
         const typename F::T la = a.back();
         const size_t s = a.size() - 1 - m;
-        scale<F>(a.data(), s, lb);
-        axmy<F>(a.data() + s, b.data(), m, lb, la);
+        axmy<F>(a.data(), bz.data() + pad - s, a.size() - 1, lb, la);   // the top term cancels
         a.pop_back();
         trim<F>(a);
     }
@@ -586,13 +570,29 @@ template <class F> struct ModRing {
 
     explicit ModRing(const Poly<F> &f) : m(f.size() - 1), nf(m), acc(2 * m) {
         for (size_t i = 0; i < m; ++i) nf[i] = F::neg(f[i]);
-        vec = m >= 8 && cpu_has_avx512();
+        vec = m >= 8 && m <= 1024 && cpu_has_avx512();
         if (vec) {
             const size_t mb = (m + 7) & ~(size_t)7;
             nf64.assign(mb + 8, 0);
             for (size_t i = 0; i < m; ++i) nf64[i] = nf[i];
             a64.assign(mb + 8, 0);
             acc64.assign(2 * m + 16, 0);
+            if constexpr (F::W == 32) {
+                // z^k mod f for k = m .. 2m-2 (z^m = -f; z^(k+1) = z z^k: shift,
+                // the top coefficient times -f), one zero-padded row of mb per k
+                tab.assign((m - 1) * mb + 8, 0);
+                uint64_t *t0 = tab.data() + ((8 - ((uintptr_t)tab.data() / 8) % 8) % 8);
+                std::vector<T> row(nf);
+                for (size_t r = 0; r + 1 < m; ++r) {
+                    for (size_t i = 0; i < m; ++i) t0[r * mb + i] = row[i];
+                    const T top = row[m - 1];
+                    for (size_t i = m; i-- > 1;) row[i] = F::add(row[i - 1], F::mul(top, nf[i]));
+                    row[0] = F::mul(top, nf[0]);
+                }
+                tl0 = t0;
+                a64.assign(IPAD32 + mb + 16, 0);
+                acc64.assign(2 * mb + 16 + 8, 0);
+            }
             if constexpr (F::W == 64) {
                 cnt64.assign(2 * m + 16, 0);
                 ifma = cpu_has_ifma();
@@ -635,7 +635,8 @@ template <class F> struct ModRing {
     void sqr(std::vector<T> &a) {
         if (vec) {
             if constexpr (F::W == 32) {
-                sqr32_avx512(a.data(), m, nf64.data(), a64.data(), acc64.data());
+                uint64_t *c = acc64.data() + ((8 - ((uintptr_t)acc64.data() / 8) % 8) % 8);   // 64-byte aligned
+                sqr32_avx512(a.data(), m, tl0, a64.data(), c);
             } else if (ifma) {
                 const size_t cw = 2 * ((m + 7) & ~(size_t)7) + 16;
                 uint64_t *c = cols.data() + ((8 - ((uintptr_t)cols.data() / 8) % 8) % 8);   // 64-byte aligned

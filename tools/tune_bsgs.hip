@@ -174,6 +174,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void k_sg(const uint32_t *ids, uint64_
     clk_end(clk, c0, r0);
 }
 
+// s_setprio around the MAC phase (bsgs.h Cfg PRIO)
+template <int PRIO>
+__global__ __launch_bounds__(BLOCK, 5) void k_prio(const uint32_t *ids, uint64_t n, uint64_t *partials,
+                                                   uint64_t *clk) {
+    uint64_t c0, r0;
+    clk_begin(c0, r0);
+    bsgs::body<bsgs::Cfg<8, 4, 8, 1, 1, false, false, 0, false, PRIO>>(ids, n, 0, T, partials);
+    clk_end(clk, c0, r0);
+}
+
 // product-tree babies (bsgs.h Cfg TREE): same modmuls, dependency depth 3
 template <int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void k_tree(const uint32_t *ids, uint64_t n, uint64_t *partials,
@@ -227,9 +237,9 @@ int main(int argc, char **argv) {
                              {"r0f0_sg8_w3", k_sg<8, 0, 0>},
                              {"r1f1_sg8_w4", k_sg<8, 1, 1, false, 4>},
                              {"r1f1_sg8_w5", k_sg<8, 1, 1, false, 5>},
-                             {"tree_sg8_w5", k_tree<5>},
-                             {"tree_sg8_w4", k_tree<4>},
-                             {"r1f1_sg6_w5", k_sg<6, 1, 1, false, 5>}};
+                             {"prio_mac_w5", k_prio<1>},
+                             {"prio_modmul_w5", k_prio<2>},
+                             {"r1f1_sg8_w5_again", k_sg<8, 1, 1, false, 5>}};
     uint32_t ref[T], got[T];
     std::vector<std::vector<float>> times(vars.size());
     std::vector<double> mhz(vars.size(), 0.0);
