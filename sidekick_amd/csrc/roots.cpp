@@ -19,16 +19,18 @@
 //   3. Cantor-Zassenhaus equal-degree splitting of g into linear factors,
 //      L ways at once: for a random a, w = (z + a)^((p-1)/L) mod g takes the
 //      value chi_L(r + a) (an L-th root of unity) at each root r, and
-//      gcd(g, w - zeta^j) collects the roots of class j; recurse on the
+//      gcd(g, w - zeta^j) collects the roots of class j — first by j mod 4
+//      (or 2) through powers of w, then class by class; recurse on the
 //      classes; quadratics by the root formula.
 // In the decode case P is a product of linear factors (the missing ids), so
 // step 3 runs on P itself first (the fast path, no z^(2^w) exponentiation);
 // only a P that will not split that way (roots outside GF(p): a corrupt or
 // mismatched difference) takes steps 2-3.
-// Polynomial products accumulate folded 64x64 (u64 field: 128-bit) products
-// lazily and reduce each coefficient once; reduction by the monic modulus
-// runs top-down with the negated modulus coefficients, so a squaring mod a
-// degree-m polynomial is ~1.5 m^2 multiply-adds.
+// Polynomial products accumulate lazily (u32: folded 32x32 products in
+// 64-bit lanes; u64: 52-bit-limb column sums on IFMA) and reduce each
+// coefficient once; the reduction mod the degree-m modulus adds the top
+// coefficients times a precomputed table of z^k mod f (k = m .. 2m-2), so a
+// squaring is ~1.5 m^2 multiply-adds with no sequential chain.
 #include "quack_hip.h"
 #include "field.h"
 #include "simd64.h"
@@ -59,6 +61,33 @@ QK_AVX512 static inline __m512i fold512(__m512i m) {
                             _mm512_add_epi64(h, _mm512_slli_epi64(h, 2)));
 }
 
+constexpr size_t IPAD32 = 8;
+// a = acc mod f for lazy product sums acc[0 .. 2m-1) (2 mb + 16 slots,
+// 64-byte aligned): the coefficients k = m .. 2m-2 reduced once, then
+// sum_k s_k (z^k mod f) from the table (t64: one row of mb per k) added into
+// register sums per output vector — no top-down chain
+QK_AVX512 static void red32_tab(uint32_t *a, size_t m, const uint64_t *t64, uint64_t *acc) {
+    const size_t mb = (m + 7) & ~(size_t)7;
+    alignas(64) uint64_t sv[1024 + 8];   // (m <= 1024: ModRing)
+    for (size_t k = m; k + 1 < 2 * m; ++k) sv[k - m] = canon32(fold64_32(acc[k]));
+    for (size_t v0 = 0; 8 * v0 < m; v0 += 4) {   // four independent sums per table row
+        const size_t nv = std::min<size_t>(4, (m - 8 * v0 + 7) / 8);
+        __m512i S[4];
+        for (size_t u = 0; u < 4; ++u) S[u] = _mm512_load_si512(acc + 8 * (v0 + (u < nv ? u : 0)));
+        for (size_t r = 0; r + 1 < m; ++r) {
+            if (!sv[r]) continue;
+            const __m512i x = _mm512_set1_epi64((long long)sv[r]);
+            const uint64_t *t = t64 + r * mb + 8 * v0;
+            for (size_t u = 0; u < 4; ++u) {
+                if (u >= nv) break;
+                S[u] = _mm512_add_epi64(S[u], fold512(_mm512_mul_epu32(x, _mm512_load_si512(t + 8 * u))));
+            }
+        }
+        for (size_t u = 0; u < nv; ++u) _mm512_store_si512(acc + 8 * (v0 + u), S[u]);
+    }
+    for (size_t i = 0; i < m; ++i) a[i] = canon32(fold64_32(acc[i]));
+}
+
 // GF(p32) squaring mod a monic f of degree m on AVX-512: lazy sums of
 // folded products (< 6 * 2^32 each, at most 2m per coefficient), eight 32x32
 // products per vpmuludq.  The products a_i a_j (i < j, through 2 a_i) go to
@@ -68,17 +97,13 @@ QK_AVX512 static inline __m512i fold512(__m512i m) {
 // k = m .. 2m-2 from a precomputed table (t64: one row of mb per k) into
 // register sums per output vector — no top-down chain.  acc: 2 mb + 16
 // slots, 64-byte aligned.
-constexpr size_t IPAD32 = 8;
 QK_AVX512 static void sqr32_avx512(uint32_t *a, size_t m, const uint64_t *t64, uint64_t *a64, uint64_t *acc) {
     const size_t mb = (m + 7) & ~(size_t)7;
     for (size_t i = 0; i < m; ++i) a64[IPAD32 + i] = a[i];
     for (size_t i = 0; i < 2 * mb + 16; i += 8) _mm512_store_si512(acc + i, _mm512_setzero_si512());
-    for (size_t i = 0; i < m; ++i) {
+    for (size_t i = 0; i + 1 < m; ++i) {
         const uint64_t ai = a[i];
         if (!ai) continue;
-        const uint64_t sq = ai * ai;
-        acc[2 * i] += (sq >> 32) * C32 + (uint32_t)sq;
-        if (i + 1 >= m) continue;
         const __m512i b = _mm512_set1_epi64((long long)add32((uint32_t)ai, (uint32_t)ai));
         for (size_t q = (2 * i + 1) / 8; 8 * q <= i + m - 1; ++q) {
             const long long lowest = (long long)(8 * q) - (long long)i;   // j of lane 0
@@ -89,18 +114,33 @@ QK_AVX512 static void sqr32_avx512(uint32_t *a, size_t m, const uint64_t *t64, u
             _mm512_store_si512(dst, _mm512_add_epi64(_mm512_load_si512(dst), fold512(_mm512_mul_epu32(b, x))));
         }
     }
-    alignas(64) uint64_t sv[1024 + 8];   // (m <= 1024: ModRing)
-    for (size_t k = m; k + 1 < 2 * m; ++k) sv[k - m] = canon32(fold64_32(acc[k]));
-    for (size_t v = 0; 8 * v < m; ++v) {
-        __m512i s = _mm512_load_si512(acc + 8 * v);
-        for (size_t r = 0; r + 1 < m; ++r) {
-            if (!sv[r]) continue;
-            s = _mm512_add_epi64(s, fold512(_mm512_mul_epu32(_mm512_set1_epi64((long long)sv[r]),
-                                                            _mm512_load_si512(t64 + r * mb + 8 * v))));
-        }
-        _mm512_store_si512(acc + 8 * v, s);
+    // the diagonal after the vector sums (a scalar store into a vector the
+    // next load reads whole would not forward)
+    for (size_t i = 0; i < m; ++i) {
+        const uint64_t sq = (uint64_t)a[i] * a[i];
+        acc[2 * i] += (sq >> 32) * C32 + (uint32_t)sq;
     }
-    for (size_t i = 0; i < m; ++i) a[i] = canon32(fold64_32(acc[i]));
+    red32_tab(a, m, t64, acc);
+}
+
+// GF(p32) product a <- a b mod f on AVX-512, the same lazy sums with every
+// a_i against a window of b (b64: IPAD32 zeros, b, zeros; j = 8q + lane - i,
+// out-of-range lanes read zeros): m products per coefficient at most
+QK_AVX512 static void mul32_avx512(uint32_t *a, const uint32_t *b, size_t m, const uint64_t *t64, uint64_t *b64,
+                                   uint64_t *acc) {
+    const size_t mb = (m + 7) & ~(size_t)7;
+    for (size_t i = 0; i < m; ++i) b64[IPAD32 + i] = b[i];
+    for (size_t i = 0; i < 2 * mb + 16; i += 8) _mm512_store_si512(acc + i, _mm512_setzero_si512());
+    for (size_t i = 0; i < m; ++i) {
+        if (!a[i]) continue;
+        const __m512i x = _mm512_set1_epi64((long long)a[i]);
+        for (size_t q = i / 8; 8 * q <= i + m - 1; ++q) {
+            const __m512i y = _mm512_loadu_si512(b64 + IPAD32 + (long long)(8 * q) - (long long)i);
+            __m512i *dst = reinterpret_cast<__m512i *>(acc + 8 * q);
+            _mm512_store_si512(dst, _mm512_add_epi64(_mm512_load_si512(dst), fold512(_mm512_mul_epu32(x, y))));
+        }
+    }
+    red32_tab(a, m, t64, acc);
 }
 
 // ---- row operations of the Euclid / division loops, u32 on AVX-512 -------
@@ -219,20 +259,23 @@ QK_AVX512 static void sqr64_avx512(uint64_t *a, size_t m, const uint64_t *nf64, 
     for (size_t i = 0; i < m; ++i) a[i] = red_lc(lo[i], cnt[i]);
 }
 
-// The same squaring on AVX-512 IFMA (52-bit limbs): a = l0 + l1 2^52
+// The same products on AVX-512 IFMA (52-bit limbs): a = l0 + l1 2^52
 // (l1 < 2^12), and every product goes into three column sums of weights 1,
 // 2^52 and 2^104 with seven vpmadd52{lo,hi}uq — no reduction per product;
-// one scalar reduction per coefficient (2^104 == 59 2^40).  The products
-// a_i a_j (i < j) are summed once and the columns doubled before the
-// diagonal is added; the top-down reduction adds q (-f_i) the same way.
-// Column sums stay below 2^61 for m <= 1000 (at most 3 (2m + 2) terms of
-// < 2^52 each in the middle column).
+// one reduction per eight coefficients (2^104 == 59 2^40).  A squaring sums
+// the products a_i a_j (i < j) once and doubles the columns before the
+// diagonal is added; the reduction mod f adds s_k (z^k mod f) from a table.
+// Bounds: a column takes at most 2m products (m from the product, m - 1
+// from the reduction, + the diagonal), i.e. 2m terms of < 2^52 in the
+// low column, 6m in the middle one (< 2^64 needs m <= 682: IFMA_MAX) and 2m
+// of < 2^25 in the top one (< 2^36; red_cols8 takes it as 64 bits).
 #define QK_IFMA __attribute__((target("avx512f,avx512vl,avx512dq,avx512ifma")))
 static bool cpu_has_ifma() {
     static const int ok = cpu_has_avx512() && __builtin_cpu_supports("avx512ifma");
     return ok;
 }
 constexpr uint64_t M52 = (1ull << 52) - 1;
+constexpr size_t IFMA_MAX = 640;   // the largest modulus degree of the IFMA products
 // the canonical values of column sums c0 + c1 2^52 + c2 2^104 on eight
 // lanes: lo + hi 2^64 = c0 + c1 2^52 + c2 59 2^40 (2^104 == 59 2^40) with
 // the carries restored by compares, then hi 2^64 == 59 hi (hi < 2^50)
@@ -241,7 +284,7 @@ QK_IFMA static inline __m512i red_cols8(__m512i c0, __m512i c1, __m512i c2) {
     const __m512i lo1 = _mm512_add_epi64(c0, _mm512_slli_epi64(c1, 52));
     __m512i hi = _mm512_srli_epi64(c1, 12);
     hi = _mm512_mask_add_epi64(hi, _mm512_cmplt_epu64_mask(lo1, c0), hi, one);
-    const __m512i w = _mm512_mul_epu32(c2, c59);   // c2 < 2^32
+    const __m512i w = _mm512_mullo_epi64(c2, c59);   // c2 < 2^58
     const __m512i lo = _mm512_add_epi64(lo1, _mm512_slli_epi64(w, 40));
     hi = _mm512_add_epi64(hi, _mm512_srli_epi64(w, 24));
     hi = _mm512_mask_add_epi64(hi, _mm512_cmplt_epu64_mask(lo, lo1), hi, one);
@@ -269,6 +312,54 @@ QK_IFMA static inline void fma52x8(uint64_t *c0, uint64_t *c1, uint64_t *c2, __m
     _mm512_store_si512(c2, c);
 }
 constexpr size_t IPAD = 8;   // zero limbs before index 0 of the limb arrays
+// a = the columns mod f (c0 / c1 / c2: 2 mb + 16 column sums of the
+// product, 64-byte aligned): z^k mod f for k = m .. 2m-2 is precomputed
+// (tl0 / tl1: row k - m, mb limbs each), so the result is the low columns
+// plus sum_k s_k (z^k mod f) — every s_k a canonical value of the product
+// columns alone, the sums in registers per output vector
+QK_IFMA static void red64_tab(uint64_t *a, size_t m, const uint64_t *tl0, const uint64_t *tl1, const uint64_t *c0,
+                              const uint64_t *c1, const uint64_t *c2) {
+    const size_t mb = (m + 7) & ~(size_t)7;
+    alignas(64) uint64_t s0[1024 + 8], s1[1024 + 8];   // (m <= 1024: ModRing)
+    const __m512i mk52 = _mm512_set1_epi64((long long)M52);
+    for (size_t k = m; k + 1 < 2 * m; k += 8) {   // (lanes past 2m - 2 read zero columns)
+        const __m512i v = red_cols8(_mm512_loadu_si512(c0 + k), _mm512_loadu_si512(c1 + k), _mm512_loadu_si512(c2 + k));
+        _mm512_store_si512(s0 + (k - m), _mm512_and_si512(v, mk52));
+        _mm512_store_si512(s1 + (k - m), _mm512_srli_epi64(v, 52));
+    }
+    // four output vectors at a time: four independent accumulator chains
+    // per table row instead of one (a row's seven IFMAs chain through B / C)
+    for (size_t v0 = 0; 8 * v0 < m; v0 += 4) {
+        const size_t nv = std::min<size_t>(4, (m - 8 * v0 + 7) / 8);
+        __m512i A[4], B[4], C[4];
+        for (size_t u = 0; u < 4; ++u) {
+            const size_t o = 8 * (v0 + (u < nv ? u : 0));
+            A[u] = _mm512_load_si512(c0 + o), B[u] = _mm512_load_si512(c1 + o), C[u] = _mm512_load_si512(c2 + o);
+        }
+        for (size_t r = 0; r + 1 < m; ++r) {
+            const __m512i x0 = _mm512_set1_epi64((long long)s0[r]), x1 = _mm512_set1_epi64((long long)s1[r]);
+            const uint64_t *t0 = tl0 + r * mb + 8 * v0, *t1 = tl1 + r * mb + 8 * v0;
+            for (size_t u = 0; u < 4; ++u) {
+                if (u >= nv) break;
+                const __m512i y0 = _mm512_load_si512(t0 + 8 * u), y1 = _mm512_load_si512(t1 + 8 * u);
+                A[u] = _mm512_madd52lo_epu64(A[u], x0, y0);
+                B[u] = _mm512_madd52hi_epu64(B[u], x0, y0);
+                C[u] = _mm512_madd52hi_epu64(C[u], x0, y1);
+                B[u] = _mm512_madd52lo_epu64(B[u], x0, y1);
+                C[u] = _mm512_madd52hi_epu64(C[u], x1, y0);
+                B[u] = _mm512_madd52lo_epu64(B[u], x1, y0);
+                C[u] = _mm512_madd52lo_epu64(C[u], x1, y1);
+            }
+        }
+        for (size_t u = 0; u < nv; ++u) {
+            const __m512i r = red_cols8(A[u], B[u], C[u]);
+            const size_t v = v0 + u, rem = m - 8 * v;
+            if (rem >= 8) _mm512_storeu_si512(a + 8 * v, r);
+            else _mm512_mask_storeu_epi64(a + 8 * v, (__mmask8)((1u << rem) - 1u), r);
+        }
+    }
+}
+
 // l0 / l1: a's limbs (IPAD zeros, the m limbs, zeros to IPAD + mb + 16);
 // tl0 / tl1: the limbs of z^k mod f, k = m .. 2m-2, one row of mb per k,
 // 64-byte aligned; c0 / c1 / c2: 2 mb + 16 column sums, 64-byte aligned
@@ -307,36 +398,30 @@ QK_IFMA static void sqr64_ifma(uint64_t *a, size_t m, const uint64_t *tl0, const
         c1[2 * i] += (uint64_t)(p0 >> 52) + 2 * (v & M52);
         c2[2 * i] += 2 * (v >> 52) + u1 * u1;
     }
-    // reduction without the top-down chain: z^k mod f for k = m .. 2m-2 is
-    // precomputed (tl0 / tl1: row k - m, mb limbs each), so the result is
-    // the low columns plus sum_k s_k (z^k mod f) — every s_k a canonical
-    // value of the product columns alone, the sums in registers per output
-    // vector
-    alignas(64) uint64_t s0[1024 + 8], s1[1024 + 8];   // (m <= 1024: ModRing)
-    const __m512i mk52 = _mm512_set1_epi64((long long)M52);
-    for (size_t k = m; k + 1 < 2 * m; k += 8) {   // (lanes past 2m - 2 read zero columns)
-        const __m512i v = red_cols8(_mm512_loadu_si512(c0 + k), _mm512_loadu_si512(c1 + k), _mm512_loadu_si512(c2 + k));
-        _mm512_store_si512(s0 + (k - m), _mm512_and_si512(v, mk52));
-        _mm512_store_si512(s1 + (k - m), _mm512_srli_epi64(v, 52));
+    red64_tab(a, m, tl0, tl1, c0, c1, c2);
+}
+
+// a <- a b mod f on IFMA: every a_i against a window of b's limbs (l0 /
+// l1 hold b: IPAD zeros, b, zeros; out-of-range lanes read zeros), then
+// red64_tab
+QK_IFMA static void mul64_ifma(uint64_t *a, const uint64_t *b, size_t m, const uint64_t *tl0, const uint64_t *tl1,
+                               uint64_t *l0, uint64_t *l1, uint64_t *c0, uint64_t *c1, uint64_t *c2) {
+    const size_t mb = (m + 7) & ~(size_t)7;
+    for (size_t i = 0; i < m; ++i) {
+        l0[IPAD + i] = b[i] & M52;
+        l1[IPAD + i] = b[i] >> 52;
     }
-    for (size_t v = 0; 8 * v < m; ++v) {
-        __m512i A = _mm512_load_si512(c0 + 8 * v), B = _mm512_load_si512(c1 + 8 * v), C = _mm512_load_si512(c2 + 8 * v);
-        for (size_t r = 0; r + 1 < m; ++r) {
-            const __m512i x0 = _mm512_set1_epi64((long long)s0[r]), x1 = _mm512_set1_epi64((long long)s1[r]);
-            const __m512i y0 = _mm512_load_si512(tl0 + r * mb + 8 * v), y1 = _mm512_load_si512(tl1 + r * mb + 8 * v);
-            A = _mm512_madd52lo_epu64(A, x0, y0);
-            B = _mm512_madd52hi_epu64(B, x0, y0);
-            B = _mm512_madd52lo_epu64(B, x0, y1);
-            B = _mm512_madd52lo_epu64(B, x1, y0);
-            C = _mm512_madd52hi_epu64(C, x0, y1);
-            C = _mm512_madd52hi_epu64(C, x1, y0);
-            C = _mm512_madd52lo_epu64(C, x1, y1);
+    for (size_t i = 0; i < 2 * mb + 16; ++i) c0[i] = c1[i] = c2[i] = 0;
+    for (size_t i = 0; i < m; ++i) {
+        if (!a[i]) continue;
+        const __m512i x0 = _mm512_set1_epi64((long long)(a[i] & M52)), x1 = _mm512_set1_epi64((long long)(a[i] >> 52));
+        for (size_t q = i / 8; 8 * q <= i + m - 1; ++q) {
+            const long long lowest = (long long)(8 * q) - (long long)i;
+            fma52x8(c0 + 8 * q, c1 + 8 * q, c2 + 8 * q, x0, x1, _mm512_loadu_si512(l0 + IPAD + lowest),
+                    _mm512_loadu_si512(l1 + IPAD + lowest));
         }
-        const __m512i r = red_cols8(A, B, C);
-        const size_t rem = m - 8 * v;
-        if (rem >= 8) _mm512_storeu_si512(a + 8 * v, r);
-        else _mm512_mask_storeu_epi64(a + 8 * v, (__mmask8)((1u << rem) - 1u), r);
     }
+    red64_tab(a, m, tl0, tl1, c0, c1, c2);
 }
 
 // axmy / scale for the u64 field on IFMA: alpha d + (p - beta) s as column
@@ -371,6 +456,27 @@ QK_IFMA static void axmy64_ifma(uint64_t *d, const uint64_t *s, size_t m, uint64
     }
 }
 
+// a <- a (z + c) mod f on IFMA: out[i] = a[i-1] + c a[i] + top nf[i] as
+// column sums (a[i-1]'s limbs added to the low two columns)
+QK_IFMA static void mullin64_ifma(uint64_t *a, size_t m, uint64_t c, const uint64_t *nf, uint64_t *tmp) {
+    const uint64_t top = a[m - 1];
+    tmp[0] = 0;
+    for (size_t i = 1; i < m; ++i) tmp[i] = a[i - 1];
+    const __m512i c0 = _mm512_set1_epi64((long long)(c & M52)), c1 = _mm512_set1_epi64((long long)(c >> 52)),
+                  t0 = _mm512_set1_epi64((long long)(top & M52)), t1 = _mm512_set1_epi64((long long)(top >> 52));
+    for (size_t i = 0; i < m; i += 8) {
+        const size_t r = m - i;
+        __m512i a0, a1, n0, n1, A, B;
+        split52(ld8q(a + i, r), a0, a1);
+        split52(ld8q(nf + i, r), n0, n1);
+        split52(ld8q(tmp + i, r), A, B);
+        __m512i C = _mm512_setzero_si512();
+        prod52(A, B, C, c0, c1, a0, a1);
+        prod52(A, B, C, t0, t1, n0, n1);
+        st8q(a + i, r, red_cols8(A, B, C));
+    }
+}
+
 template <class F> static inline bool vec32(size_t m) {
     if constexpr (F::W == 32) return m >= 8 && cpu_has_avx512();
     else return false;
@@ -391,14 +497,39 @@ static void axmy(typename F::T *d, const typename F::T *s, size_t m, typename F:
     for (size_t i = 0; i < m; ++i) d[i] = F::sub(alpha == 1 ? d[i] : F::mul(d[i], alpha), F::mul(beta, s[i]));
 }
 
-// splitting arity per field (a divisor of p - 1; measured on d = 8..64,
-// 2-way 203 / 877 us at d = 32 (u32 / u64), 10-way 116 /
-// 11-way 447, 19-way 95 / 22-way 230, 38-way 128 / 44-way 368)
+// Field inverses by fixed addition chains on lazy products (every found
+// factor is made monic, so the split pays ~one inverse per root):
+// p32 - 2 = (2^29 - 1) 2^3 + 1: 31 squarings + 8 products (the binary
+// ladder: 31 + 29); p64 - 2 = (2^58 - 1) 2^6 + 3: 63 + 9 (ladder: 63 + 60).
+template <class U, U (*MUL)(U, U)> static inline U sqr_n(U x, int k) {
+    while (k--) x = MUL(x, x);
+    return x;
+}
+static uint32_t inv32_chain(uint32_t a) {
+    constexpr auto S = sqr_n<uint32_t, mul32_lazy>;
+    const uint32_t x2 = mul32_lazy(S(a, 1), a), x4 = mul32_lazy(S(x2, 2), x2), x8 = mul32_lazy(S(x4, 4), x4);
+    const uint32_t x16 = mul32_lazy(S(x8, 8), x8), x24 = mul32_lazy(S(x16, 8), x8), x28 = mul32_lazy(S(x24, 4), x4);
+    const uint32_t x29 = mul32_lazy(S(x28, 1), a);
+    return canon32(mul32_lazy(S(x29, 3), a));
+}
+static uint64_t inv64_chain(uint64_t a) {
+    constexpr auto S = sqr_n<uint64_t, mul64_lazy>;
+    const uint64_t x2 = mul64_lazy(S(a, 1), a), x4 = mul64_lazy(S(x2, 2), x2), x8 = mul64_lazy(S(x4, 4), x4);
+    const uint64_t x16 = mul64_lazy(S(x8, 8), x8), x32 = mul64_lazy(S(x16, 16), x16);
+    const uint64_t x48 = mul64_lazy(S(x32, 16), x16), x56 = mul64_lazy(S(x48, 8), x8), x58 = mul64_lazy(S(x56, 2), x2);
+    return canon64(mul64_lazy(S(x58, 6), x2));
+}
+
+// splitting arity per field (a divisor of p - 1; p32 - 1 = 2 5 19 ...,
+// p64 - 1 = 4 11 137 ...).  With the power-of-two cuts first (Splitter),
+// d = 32 on one Xeon core (tools/prof_roots.cpp): u32
+// 10 / 19 / 38 / 190-way 67 / 76 / 56 / 144 us, u64 4 / 11 / 22 / 44 /
+// 548-way 274 / 184 / 112 / 113 / 208 us (44 ahead at d = 64)
 #ifndef SPLIT32
-#define SPLIT32 19
+#define SPLIT32 38
 #endif
 #ifndef SPLIT64
-#define SPLIT64 22
+#define SPLIT64 44
 #endif
 
 // Field policies: canonical elements T, lazy accumulator A (sums of folded
@@ -410,12 +541,14 @@ struct F32 {
     static constexpr uint64_t C = C32;
     static constexpr uint64_t PM1 = P32 - 1;       // = 2 * 5 * 19 * 22605091
     static constexpr uint32_t L = SPLIT32;         // splitting arity: L | p - 1
+    static constexpr uint32_t E = L & (0u - L);    // its power-of-two part
+    static constexpr uint32_t LO = L / E;          // and its odd part
     static T pow(T a, uint64_t e) { return pow32(a, e); }
     static T add(T a, T b) { return add32(a, b); }
     static T sub(T a, T b) { return sub32(a, b); }
     static T mul(T a, T b) { return mul32(a, b); }
     static T neg(T a) { return neg32(a); }
-    static T inv(T a) { return inv32(a); }
+    static T inv(T a) { return inv32_chain(a); }
     static T canon_any(T a) { return canon32(a); }
     static void mac(A &acc, T a, T b) {
         const uint64_t p = (uint64_t)a * b;
@@ -437,12 +570,14 @@ struct F64 {
     static constexpr uint64_t C = C64;
     static constexpr uint64_t PM1 = P64 - 1;       // = 4 * 11 * 137 * 547 * 5594472617641
     static constexpr uint32_t L = SPLIT64;
+    static constexpr uint32_t E = L & (0u - L);
+    static constexpr uint32_t LO = L / E;
     static T pow(T a, uint64_t e) { return pow64(a, e); }
     static T add(T a, T b) { return add64(a, b); }
     static T sub(T a, T b) { return sub64(a, b); }
     static T mul(T a, T b) { return mul64(a, b); }
     static T neg(T a) { return neg64(a); }
-    static T inv(T a) { return inv64(a); }
+    static T inv(T a) { return inv64_chain(a); }
     static T canon_any(T a) { return canon64(a); }
     static void mac(A &acc, T a, T b) {
         const unsigned __int128 p = (unsigned __int128)a * b;
@@ -454,29 +589,14 @@ struct F64 {
         unsigned __int128 u = (unsigned __int128)(uint64_t)(t >> 64) * C64 + (uint64_t)t;
         return canon64((uint64_t)u + C64 * (uint64_t)(u >> 64));
     }
-    // Tonelli-Shanks: p64 - 1 = 4 Q (Q odd); z = 2 is a non-residue mod p64
-    // (p64 = 5 mod 8), so c = 2^Q has order 4
+    // Atkin (p64 = 5 mod 8, where 2 is a non-residue): v = (2n)^((p-5)/8),
+    // i = 2n v^2 (a square root of -1 when n is a residue), r = n v (i - 1);
+    // one exponentiation, r^2 == n iff n is a residue
     static bool sqrt(T n, T &r) {
-        if (n == 0) {
-            r = 0;
-            return true;
-        }
-        constexpr uint64_t Q = (P64 - 1) / 4;
-        if (pow64(n, (P64 - 1) / 2) != 1) return false;
-        T c = pow64(2, Q), t = pow64(n, Q);
-        r = pow64(n, (Q + 1) / 2);
-        int M = 2;
-        while (t != 1) {
-            int i = 1;
-            for (T t2 = mul64(t, t); t2 != 1; t2 = mul64(t2, t2)) ++i;
-            T b = c;
-            for (int j = 0; j < M - i - 1; ++j) b = mul64(b, b);
-            M = i;
-            c = mul64(b, b);
-            t = mul64(t, c);
-            r = mul64(r, b);
-        }
-        return true;
+        const T n2 = add64(n, n), v = pow64(n2, (P64 - 5) / 8);
+        const T i = mul64(n2, mul64(v, v));
+        r = mul64(mul64(n, v), sub64(i, 1));
+        return mul64(r, r) == n;
     }
 };
 
@@ -518,39 +638,98 @@ template <class F> Poly<F> div_monic(Poly<F> a, const Poly<F> &b) {
     return q;
 }
 
-// a <- a mod b up to a nonzero scalar, fraction-free: each step cancels a's
-// leading term as lead(b) a - lead(a) z^s b (no inversion; a field inverse
-// costs ~60 multiplications, more than the extra row of products here)
-// One pass per step over a's coefficients: a_i <- lb a_i - la b_(i-s) with
-// b zero-extended below (bz: a.size() zeros, then b), so the scaling of the
-// low part and the row operation are one vector row.
-template <class F> void rem_ff(Poly<F> &a, const Poly<F> &b) {
-    const size_t m = b.size() - 1;
-    if (a.size() <= m) return;
-    const typename F::T lb = b.back();
-    const size_t pad = a.size();
-    Poly<F> bz(pad + b.size(), 0);
-    std::copy(b.begin(), b.end(), bz.begin() + pad);
-    while (a.size() > m) {
-        const typename F::T la = a.back();
-        const size_t s = a.size() - 1 - m;
-        axmy<F>(a.data(), bz.data() + pad - s, a.size() - 1, lb, la);   // the top term cancels
-        a.pop_back();
-        trim<F>(a);
+// The same remainder sequence for operands of at most 8 NV coefficients on
+// AVX-512, without a call or a tail mask per step: both operands sit in
+// fixed 64-bit-lane buffers (8 NV zero lanes below each), every step is NV
+// full-vector rows alpha a - beta (z^s b), and lanes above the degree stay 0
+// (the top lane cancels exactly; z^s b is 0 above it).
+QK_AVX512 static inline __m512i row_lanes32(__m512i d, __m512i s, uint64_t alpha, uint64_t beta) {
+    return subc512(mulc512(d, _mm512_set1_epi64((long long)alpha)), mulc512(s, _mm512_set1_epi64((long long)beta)));
+}
+QK_AVX512 static inline __m512i row_lanes64(__m512i d, __m512i s, uint64_t alpha, uint64_t beta) {
+    using namespace simd;
+    return sub64_512(canon64_512(mulmod64_512(d, lo32x8(alpha), hi32x8(alpha))),
+                     canon64_512(mulmod64_512(s, lo32x8(beta), hi32x8(beta))));
+}
+template <class F, int NV>
+QK_AVX512 static size_t gcd_small(const typename F::T *a0, size_t na, const typename F::T *b0, size_t nb,
+                                  typename F::T *out) {
+    alignas(64) uint64_t buf[4 * 8 * NV] = {};
+    uint64_t *pa = buf + 8 * NV, *pb = buf + 3 * 8 * NV;
+    for (size_t i = 0; i < na; ++i) pa[i] = a0[i];
+    for (size_t i = 0; i < nb; ++i) pb[i] = b0[i];
+    while (nb) {
+        const size_t m = nb - 1;
+        const uint64_t lb = pb[m];
+        while (na > m) {
+            const uint64_t la = pa[na - 1];
+            const size_t s = na - 1 - m;
+            const size_t nv = (na + 7) / 8;
+            for (int k = 0; k < NV; ++k) {
+                if ((size_t)k >= nv) break;
+                const __m512i d = _mm512_load_si512(pa + 8 * k), x = _mm512_loadu_si512(pb + 8 * k - s);
+                _mm512_store_si512(pa + 8 * k, F::W == 32 ? row_lanes32(d, x, lb, la) : row_lanes64(d, x, lb, la));
+            }
+            --na;
+            while (na && !pa[na - 1]) --na;
+        }
+        std::swap(pa, pb);
+        std::swap(na, nb);
     }
+    for (size_t i = 0; i < na; ++i) out[i] = (typename F::T)pa[i];
+    return na;
 }
 
-// monic gcd(a, b)
-template <class F> Poly<F> gcd(Poly<F> a, Poly<F> b) {
-    trim<F>(a);
-    trim<F>(b);
-    while (!b.empty()) {
-        rem_ff<F>(a, b);
-        std::swap(a, b);
+// monic gcd(a, b), fraction-free: each step cancels a's leading term as
+// lead(b) a - lead(a) z^s b (no inversion; a field inverse costs ~60
+// multiplications, more than the extra row of products here), one pass per
+// step over a's coefficients: a_i <- lb a_i - la b_(i-s) with b
+// zero-extended below, so the scaling of the low part and the row operation
+// are one vector row.  No vector per step: both operands live in one buffer
+// each behind P zeros (P > either size), so b zero-extended below is b's own
+// buffer read from s slots earlier, and the swap of a step swaps pointers.
+template <class F> Poly<F> gcd_rows(const Poly<F> &a0, const Poly<F> &b0, bool small) {
+    using T = typename F::T;
+    size_t na = a0.size(), nb = b0.size();
+    while (na && !a0[na - 1]) --na;
+    while (nb && !b0[nb - 1]) --nb;
+    const size_t n = std::max(na, nb);
+    if (small && n <= 40 && cpu_has_avx512()) {
+        T g[40];
+        const size_t ng = n <= 8    ? gcd_small<F, 1>(a0.data(), na, b0.data(), nb, g)
+                          : n <= 16 ? gcd_small<F, 2>(a0.data(), na, b0.data(), nb, g)
+                          : n <= 24 ? gcd_small<F, 3>(a0.data(), na, b0.data(), nb, g)
+                          : n <= 32 ? gcd_small<F, 4>(a0.data(), na, b0.data(), nb, g)
+                                    : gcd_small<F, 5>(a0.data(), na, b0.data(), nb, g);
+        if (ng == 1) return Poly<F>{1};   // coprime: no inversion for the monic form
+        Poly<F> r(g, g + ng);
+        if (!r.empty()) make_monic<F>(r);
+        return r;
     }
-    if (!a.empty()) make_monic<F>(a);
-    return a;
+    const size_t P = n + 1;
+    std::vector<T> buf(4 * P, 0);
+    T *pa = buf.data() + P, *pb = buf.data() + 3 * P;
+    std::copy(a0.begin(), a0.begin() + na, pa);
+    std::copy(b0.begin(), b0.begin() + nb, pb);
+    while (nb) {
+        const size_t m = nb - 1;
+        const T lb = pb[m];
+        while (na > m) {
+            const T la = pa[na - 1];
+            const size_t s = na - 1 - m;
+            axmy<F>(pa, pb - s, na - 1, lb, la);   // the top term cancels
+            --na;
+            while (na && !pa[na - 1]) --na;
+        }
+        std::swap(pa, pb);
+        std::swap(na, nb);
+    }
+    if (na == 1) return Poly<F>{1};
+    Poly<F> g(pa, pa + na);
+    if (!g.empty()) make_monic<F>(g);
+    return g;
 }
+template <class F> Poly<F> gcd(const Poly<F> &a, const Poly<F> &b) { return gcd_rows<F>(a, b, true); }
 
 // Arithmetic modulo a fixed monic f of degree m >= 1: residues are vectors of
 // exactly m coefficients.
@@ -596,7 +775,7 @@ template <class F> struct ModRing {
             if constexpr (F::W == 64) {
                 cnt64.assign(2 * m + 16, 0);
                 ifma = cpu_has_ifma();
-                ifma = ifma && m <= 1024;
+                ifma = ifma && m <= IFMA_MAX;
                 if (ifma) {
                     // z^k mod f for k = m .. 2m-2 as limb rows (z^m = -f, then
                     // z^(k+1) = z * z^k: shift, the top coefficient times -f)
@@ -656,13 +835,42 @@ template <class F> struct ModRing {
         }
         reduce_acc(a);
     }
+    // a <- a b (both residues of m coefficients; b may alias a)
+    void mul(std::vector<T> &a, const std::vector<T> &b) {
+        if (&a == &b) return sqr(a);
+        if (vec) {
+            if constexpr (F::W == 32) {
+                uint64_t *c = acc64.data() + ((8 - ((uintptr_t)acc64.data() / 8) % 8) % 8);
+                return mul32_avx512(a.data(), b.data(), m, tl0, a64.data(), c);
+            } else if (ifma) {
+                const size_t cw = 2 * ((m + 7) & ~(size_t)7) + 16;
+                uint64_t *c = cols.data() + ((8 - ((uintptr_t)cols.data() / 8) % 8) % 8);
+                return mul64_ifma((uint64_t *)a.data(), (const uint64_t *)b.data(), m, tl0, tl1, l0.data(), l1.data(),
+                                  c, c + cw, c + 2 * cw);
+            }
+        }
+        std::fill(acc.begin(), acc.end(), A(0));
+        for (size_t i = 0; i < m; ++i) {
+            if (!a[i]) continue;
+            for (size_t j = 0; j < m; ++j) F::mac(acc[i + j], a[i], b[j]);
+        }
+        reduce_acc(a);
+    }
+    // a^e (e >= 1)
+    std::vector<T> pow(const std::vector<T> &a, uint64_t e) {
+        std::vector<T> r = a;
+        for (int b = 62 - __builtin_clzll(e); b >= 0; --b) {
+            sqr(r);
+            if ((e >> b) & 1) mul(r, a);
+        }
+        return r;
+    }
     // a <- a * (z + c)
     void mul_lin(std::vector<T> &a, T c) {
         if constexpr (F::W == 32) {
-            if (vec) {
-                mullin32_avx512(a.data(), m, c, nf.data(), tmp.data());
-                return;
-            }
+            if (vec) return mullin32_avx512(a.data(), m, c, nf.data(), tmp.data());
+        } else {
+            if (ifma) return mullin64_ifma((uint64_t *)a.data(), m, c, (const uint64_t *)nf.data(), (uint64_t *)tmp.data());
         }
         const T top = a[m - 1];                       // coefficient of z^m after the shift
         for (size_t i = m; i-- > 0;) {
@@ -724,12 +932,94 @@ template <class F> typename F::T root_of_unity() {
 // factor.
 // A factor of degree k >= 3 is split L ways at once (Cantor-Zassenhaus with
 // the L-th power character): w = (z + a)^((p-1)/L) mod g takes at a root r
-// the L-th root of unity chi(r + a) (0 for r = -a), so gcd(g, w - zeta^j),
-// j = 0..L-1, sort the roots into L groups — one exponentiation for ~log_L k
-// levels instead of log_2 k (L = 19 for p32, 22 for p64).
+// the L-th root of unity chi(r + a) = zeta^j (0 for r = -a), and the roots
+// of class j are gcd(g, w - zeta^j) — one exponentiation for ~log_L k levels
+// instead of log_2 k (L = 38 for p32, 44 for p64).  The classes are not
+// taken one gcd at a time over all of g: with L = E LO (E the power-of-two
+// part), v = w^LO takes the E-th root of unity zeta^(LO j) at a class-j
+// root, so gcds with v^(E/2) - 1, then v - zeta^(LO c) (E = 4) cut g into E
+// parts by j mod E first (~k/E roots each), and the LO classes of each part
+// run their gcds on that part only.
+template <class F> class Splitter {
+    using T = typename F::T;
+    const T zeta = root_of_unity<F>();
+
+  public:
+    // the roots of g of class j (j mod E == c) for each j, from w mod g;
+    // the factors found (and g's rest) go to parts
+    void classes(const Poly<F> &g, const Poly<F> &w, uint32_t c, std::vector<Poly<F>> &parts) const {
+        if (g.size() <= 1) return;
+        if (g.size() == 2) {
+            parts.push_back(g);
+            return;
+        }
+        Poly<F> rem = g, wg = w;
+        rem_monic<F>(wg, g);
+        const T step = F::pow(zeta, F::E);
+        T zj = F::pow(zeta, c);
+        bool cut = false;
+        for (uint32_t j = c; j < F::L && rem.size() > 2; j += F::E, zj = F::mul(zj, step)) {
+            Poly<F> wr = wg;
+            if (cut) rem_monic<F>(wr, rem);   // w mod rem (rem == g: wg is reduced)
+            if (wr.empty()) wr.push_back(0);
+            wr[0] = F::sub(wr[0], zj);
+            Poly<F> h = gcd<F>(rem, wr);
+            if (h.size() > 1) {
+                rem = div_monic<F>(rem, h);
+                parts.push_back(std::move(h));
+                cut = true;
+            }
+        }
+        if (rem.size() > 1) parts.push_back(std::move(rem));   // the last class, r = -a, or an unsplit rest
+    }
+    // g = gcd(g, u - c) * (g / that): the roots where u == c, and the rest
+    static void cut(const Poly<F> &g, const Poly<F> &u, T c, Poly<F> &in, Poly<F> &out) {
+        Poly<F> ur = u;
+        rem_monic<F>(ur, g);
+        if (ur.empty()) ur.push_back(0);
+        ur[0] = F::sub(ur[0], c);
+        in = gcd<F>(g, ur);
+        out = in.size() > 1 ? div_monic<F>(g, in) : g;
+        if (in.size() <= 1) in.clear();
+    }
+    // every factor one L-way split of g (w = (z + a)^((p-1)/L) mod g) yields
+    void run(ModRing<F> &R, const Poly<F> &g, T a, std::vector<Poly<F>> &parts) const {
+        const std::vector<T> wv = R.pow_lin(a, F::PM1 / F::L);
+        const Poly<F> w = to_poly<F>(wv);
+        if constexpr (F::E == 1) {
+            classes(g, w, 0, parts);
+        } else {
+            const std::vector<T> vv = F::LO > 1 ? R.pow(wv, F::LO) : wv;   // v = w^LO
+            Poly<F> A, B;
+            if constexpr (F::E == 2) {
+                cut(g, to_poly<F>(vv), 1, A, B);   // v = 1: even j; v = -1 (or r = -a): odd j
+                classes(A, w, 0, parts);
+                classes(B, w, 1, parts);
+            } else {
+                static_assert(F::E == 4, "p - 1 has at most 2^2");
+                std::vector<T> qv = vv;
+                R.sqr(qv);                        // v^2 = +-1: j even / odd
+                cut(g, to_poly<F>(qv), 1, A, B);
+                const Poly<F> v = to_poly<F>(vv);
+                const T i4 = F::pow(zeta, F::LO);   // zeta^LO: a primitive 4th root of unity
+                Poly<F> A0, A2, B1, B3;
+                if (A.size() > 2) cut(A, v, 1, A0, A2);   // j = 0 / 2 mod 4
+                else A2 = A;
+                if (B.size() > 2) cut(B, v, i4, B1, B3);  // j = 1 / 3 mod 4
+                else B3 = B;
+                classes(A0, w, 0, parts);
+                classes(A2, w, 2, parts);
+                classes(B1, w, 1, parts);
+                classes(B3, w, 3, parts);
+            }
+        }
+    }
+};
+
 template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out, bool exact) {
     using T = typename F::T;
-    const T inv2 = F::inv(2), zeta = root_of_unity<F>();
+    const T inv2 = F::inv(2);
+    const Splitter<F> S{};
     std::vector<Poly<F>> todo{g0};
     uint64_t s = 0x243F6A8885A308D3ull;   // fixed seed: a deterministic sequence of a's
     while (!todo.empty()) {
@@ -758,23 +1048,8 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
         for (int fails = 0;; ++fails) {
             if (!exact && fails >= 24) return false;
             s += GAMMA;
-            const T a = F::canon_any((T)splitmix_mix(s));
-            const Poly<F> w = to_poly<F>(R.pow_lin(a, F::PM1 / F::L));
-            Poly<F> rem = g;
             std::vector<Poly<F>> parts;
-            T zj = 1;
-            for (uint32_t j = 0; j < F::L && rem.size() > 2; ++j, zj = F::mul(zj, zeta)) {
-                Poly<F> wr = w;
-                if (parts.size()) rem_monic<F>(wr, rem);      // w mod rem (rem == g: w is reduced)
-                if (wr.empty()) wr.push_back(0);
-                wr[0] = F::sub(wr[0], zj);
-                Poly<F> h = gcd<F>(rem, std::move(wr));
-                if (h.size() > 1) {
-                    rem = div_monic<F>(rem, h);
-                    parts.push_back(std::move(h));
-                }
-            }
-            if (rem.size() > 1) parts.push_back(std::move(rem));   // the last group, r = -a, or an unsplit rest
+            S.run(R, g, F::canon_any((T)splitmix_mix(s)), parts);
             if (parts.size() < 2) continue;
             for (auto &p : parts) todo.push_back(std::move(p));
             break;

@@ -120,3 +120,28 @@ def test_roots_large_degree_u32():
     rng = np.random.default_rng(5)
     ids = rng.integers(0, 1 << 32, size=300, dtype=np.uint64).tolist()
     assert roots(coeffs_of(ids, 32), 32) == sorted({x % P[32] for x in ids})
+
+
+@pytest.mark.parametrize("k", [300, 700])
+def test_roots_large_degree_u64(k):
+    """Degrees past the IFMA products' limit (roots.cpp IFMA_MAX = 640) take
+    the other vector path; both must find every root."""
+    rng = np.random.default_rng(k)
+    ids = [int(v) for v in rng.integers(0, 1 << 63, size=k, dtype=np.uint64)]
+    ids += [P[64] - 1 - i for i in range(8)]   # coefficients near p: the largest column sums
+    assert roots(coeffs_of(ids, 64), 64) == sorted({x % P[64] for x in ids})
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+def test_roots_repeated_and_clustered_classes(bits):
+    """Multiplicities up to 5 and many roots sharing a splitting class (roots
+    r, r * zeta^L' ... fall in related classes): still exactly the distinct
+    roots."""
+    p = P[bits]
+    rng = random.Random(7 + bits)
+    base = [rng.randrange(1, p) for _ in range(12)]
+    ids = []
+    for i, r in enumerate(base):
+        ids += [r] * (1 + i % 5)
+    ids += [(base[0] + j) % p for j in range(1, 20)]   # a run of consecutive residues
+    assert roots(coeffs_of(ids, bits), bits) == sorted({x % p for x in ids})
