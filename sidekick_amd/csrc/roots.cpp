@@ -750,56 +750,40 @@ template <class F> struct ModRing {
     explicit ModRing(const Poly<F> &f) : m(f.size() - 1), nf(m), acc(2 * m) {
         for (size_t i = 0; i < m; ++i) nf[i] = F::neg(f[i]);
         vec = m >= 8 && m <= 1024 && cpu_has_avx512();
-        if (vec) {
-            const size_t mb = (m + 7) & ~(size_t)7;
-            nf64.assign(mb + 8, 0);
-            for (size_t i = 0; i < m; ++i) nf64[i] = nf[i];
-            a64.assign(mb + 8, 0);
-            acc64.assign(2 * m + 16, 0);
-            if constexpr (F::W == 32) {
-                // z^k mod f for k = m .. 2m-2 (z^m = -f; z^(k+1) = z z^k: shift,
-                // the top coefficient times -f), one zero-padded row of mb per k
-                tab.assign((m - 1) * mb + 8, 0);
-                uint64_t *t0 = tab.data() + ((8 - ((uintptr_t)tab.data() / 8) % 8) % 8);
-                std::vector<T> row(nf);
-                for (size_t r = 0; r + 1 < m; ++r) {
-                    for (size_t i = 0; i < m; ++i) t0[r * mb + i] = row[i];
-                    const T top = row[m - 1];
-                    for (size_t i = m; i-- > 1;) row[i] = F::add(row[i - 1], F::mul(top, nf[i]));
-                    row[0] = F::mul(top, nf[0]);
-                }
-                tl0 = t0;
-                a64.assign(IPAD32 + mb + 16, 0);
-                acc64.assign(2 * mb + 16 + 8, 0);
-            }
-            if constexpr (F::W == 64) {
-                cnt64.assign(2 * m + 16, 0);
-                ifma = cpu_has_ifma();
-                ifma = ifma && m <= IFMA_MAX;
-                if (ifma) {
-                    // z^k mod f for k = m .. 2m-2 as limb rows (z^m = -f, then
-                    // z^(k+1) = z * z^k: shift, the top coefficient times -f)
-                    tab.assign(2 * (m - 1) * mb + 8, 0);
-                    uint64_t *t0 = tab.data() + ((8 - ((uintptr_t)tab.data() / 8) % 8) % 8), *t1 = t0 + (m - 1) * mb;
-                    std::vector<T> row(nf);
-                    for (size_t r = 0; r + 1 < m; ++r) {
-                        for (size_t i = 0; i < m; ++i) {
-                            t0[r * mb + i] = (uint64_t)row[i] & M52;
-                            t1[r * mb + i] = (uint64_t)row[i] >> 52;
-                        }
-                        const T top = row[m - 1];
-                        for (size_t i = m; i-- > 1;) row[i] = F::add(row[i - 1], F::mul(top, nf[i]));
-                        row[0] = F::mul(top, nf[0]);
-                    }
-                    tl0 = t0;
-                    tl1 = t1;
-                    l0.assign(IPAD + mb + 16, 0);
-                    l1.assign(IPAD + mb + 16, 0);
-                    cols.assign(3 * (2 * mb + 16) + 8, 0);   // + 8: room to align to 64 bytes
-                }
-            }
-            tmp.assign(m, 0);
+        if (!vec) return;
+        const size_t mb = (m + 7) & ~(size_t)7;
+        nf64.assign(mb + 8, 0);
+        for (size_t i = 0; i < m; ++i) nf64[i] = nf[i];
+        a64.assign(mb + 8, 0);
+        acc64.assign(2 * m + 16, 0);
+        tmp.assign(m, 0);
+        if constexpr (F::W == 32) {
+            a64.assign(IPAD32 + mb + 16, 0);
+            acc64.assign(2 * mb + 16 + 8, 0);
+        } else {
+            cnt64.assign(2 * m + 16, 0);
+            ifma = cpu_has_ifma() && m <= IFMA_MAX;
+            if (!ifma) return;
+            l0.assign(IPAD + mb + 16, 0);
+            l1.assign(IPAD + mb + 16, 0);
+            cols.assign(3 * (2 * mb + 16) + 8, 0);   // + 8: room to align to 64 bytes
         }
+        // the reduction table: z^k mod f for k = m .. 2m-2, one zero-padded
+        // row of mb per k (u64: as 52-bit limb rows), from z^m = -f by
+        // z^(k+1) = z z^k (mul_lin with c = 0, vectorised)
+        const size_t rows = (m - 1) * mb;
+        tab.assign((F::W == 32 ? 1 : 2) * rows + 8, 0);
+        uint64_t *t0 = tab.data() + ((8 - ((uintptr_t)tab.data() / 8) % 8) % 8), *t1 = t0 + rows;
+        std::vector<T> row(nf);
+        for (size_t r = 0; r + 1 < m; ++r) {
+            for (size_t i = 0; i < m; ++i) {
+                if constexpr (F::W == 32) t0[r * mb + i] = row[i];
+                else t0[r * mb + i] = (uint64_t)row[i] & M52, t1[r * mb + i] = (uint64_t)row[i] >> 52;
+            }
+            if (r + 2 < m) mul_lin(row, 0);
+        }
+        tl0 = t0;
+        if constexpr (F::W == 64) tl1 = t1;
     }
     // acc[0 .. 2m-1) (degree <= 2m-2) -> r (m coefficients): top-down, each
     // top coefficient q adds q * (-f_i) below it

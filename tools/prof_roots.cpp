@@ -4,7 +4,8 @@
 // top-level exponentiation (z + a)^((p-1)/L), and one gcd of the product
 // with w - 1.
 // Min over reps (a shared host); one JSON line per field.
-//   g++ -O3 -std=c++17 -march=native -I../include prof_roots.cpp -o prof_roots
+//   make -C tools prof_roots   (the product library's flags: baseline x86-64,
+//   the vector paths behind target attributes and a CPU check)
 //   ./prof_roots [d] [reps]
 #include <chrono>
 #include <cstdio>
