@@ -99,12 +99,14 @@ __device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
 // ---- baby-step / giant-step encode for 9 <= t <= 32 (bsgs.h)
 // waves per SIMD the register budget is sized for (tools/tune_bsgs.hip: 5 for
 // (8,4) beat 4 by 2-3 %; its three spilled VGPRs live outside the loop)
-template <int NB, int NA, int SG>
+// PRIO: s_setprio around each id's MAC phase (bsgs.h; knob bsgs_prio)
+template <int NB, int NA, int SG, int PRIO = 1>
 __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB * NA > 40 ? 3 : 4)) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids,
                                                                                   uint64_t n, uint32_t head,
                                                                                   uint32_t T,
                                                                                   uint64_t *__restrict__ partials) {
-    bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD>>(ids, n, head, T, partials);
+    bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD, false, false, 0, false, PRIO>>(ids, n, head, T,
+                                                                                                partials);
 }
 
 
@@ -974,9 +976,12 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
     auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
-#define QK_BSGS(NB_, NA_, G_)                                                                        \
-    run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
+    const int prio = ctx->knobs.bsgs_prio;
+#define QK_BSGS_P(NB_, NA_, G_, P_)                                                                          \
+    run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_, P_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
                          (n + 3) / 4, BLOCK, out, acc, s)
+#define QK_BSGS(NB_, NA_, G_)                                                                                 \
+    (prio ? QK_BSGS_P(NB_, NA_, G_, 1) : QK_BSGS_P(NB_, NA_, G_, 0))
     if (T >= 5 && T <= 8 && sg(1)) return QK_BSGS(4, 2, 1);
     if (T >= 9 && T <= 12) return sg(3) ? QK_BSGS(4, 3, 3) : QK_BSGS(4, 3, 0);
     if (T >= 13 && T <= 16) return sg(4) ? QK_BSGS(4, 4, 4) : QK_BSGS(4, 4, 0);
@@ -1019,6 +1024,7 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const int passes_env = ctx->knobs.u32_passes;
     if (T > 80 && sg(16) && passes_env) return enc32_passes(ctx, ids, n, head, T, out, acc, s);
 #undef QK_BSGS
+#undef QK_BSGS_P
     int G, K;
     choose_gk(T, 32, K32_G1, 10, K32_GN, 4, G, K);
     switch (G) {

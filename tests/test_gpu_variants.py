@@ -18,7 +18,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "bsgs64_tmin": 14, "bsgs64_shapes": 1, "u32_xcache": 1, "u64_xcache": 1,
-            "bsgs_shapes": 1}
+            "bsgs_shapes": 1, "bsgs_prio": 1}
 
 
 @contextlib.contextmanager
@@ -104,6 +104,17 @@ def test_u32_bsgs_shapes(shapes):
     assert all(res.values()), res
 
 
+@pytest.mark.parametrize("prio", [1, 0])
+def test_u32_bsgs_prio(prio):
+    """Every single-pass u32 BSGS shape with and without s_setprio around its
+    MAC phase (knob bsgs_prio; the default raises it), against the oracle,
+    ragged and misaligned."""
+    cases = [(f"t{t}", 100_003 + t, t, t % 4) for t in (8, 12, 16, 20, 24, 28, 30, 32, 36, 40, 42, 48, 56, 64, 72, 80)]
+    with knob("bsgs_prio", prio):
+        res = _run(32, cases)
+    assert all(res.values()), res
+
+
 @pytest.mark.parametrize("xcache", [1, 0])
 def test_u32_passes_xbase_cache(xcache):
     """u32 thresholds > 128 run two or more offset passes; with the per-id
@@ -169,6 +180,6 @@ def test_knob_validation():
     from sidekick_amd._lib import QuackError
     ctx = sk.get_context(0)
     for name, bad in (("flow_load", 0), ("flow_load", 65), ("root_test", 3), ("no_such_knob", 1),
-                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1)):
+                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2)):
         with pytest.raises(QuackError):
             ctx.set_knob(name, bad)
