@@ -540,6 +540,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"bsgs_prio", &qk_knobs::bsgs_prio, 0, 1},
         {"bsgs64_sg", &qk_knobs::bsgs64_sg, -1, 64},   {"bsgs64_off", &qk_knobs::bsgs64_off, 0, 1},
         {"bsgs64_tmin", &qk_knobs::bsgs64_tmin, 9, 81}, {"bsgs64_shapes", &qk_knobs::bsgs64_shapes, 0, 1},
+        {"bsgs64_prio", &qk_knobs::bsgs64_prio, 0, 1},
         {"u64_passes", &qk_knobs::u64_passes, 0, 1},
         {"u64_xcache", &qk_knobs::u64_xcache, 0, 1},   {"u64_kmax", &qk_knobs::u64_kmax, 4, 40},
         {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},

@@ -310,8 +310,10 @@ struct Smem<NG, true, NBB> {
 //   NBT     babies per id: 8 (two per wave), or 4 (one per wave: thresholds
 //           t <= 40 waste fewer powers in 4-wide rows, and the babies and
 //           giants of an id cost 3 + NA - 2 products instead of 7 + NA - 2)
+//   PRIO    s_setprio 1 for a wave in its MAC step (1), or in its babies /
+//           giants step (2); 0: no priority changes
 template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0,
-          int XC = 0, int NBT = NB>
+          int XC = 0, int NBT = NB, int PRIO = 0>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
                                      uint64_t *__restrict__ partials, uint32_t base = 0,
                                      const uint64_t *xin = nullptr, uint64_t *xout = nullptr) {
@@ -350,6 +352,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     }
     for (; tile < ntiles; tile += gridDim.x) {
         // ---- step 1: this thread's id -> babies (+ B * 2^32), giants -> LDS
+        if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
         {
             const uint64_t x = nxt;
             const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
@@ -396,7 +399,9 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 if (tile * BLOCK + tid < n) xout[tile * BLOCK + tid] = V;
             }
         }
+        if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
         // next tile's id in flight during step 3
         const uint64_t tn = tile + gridDim.x;
         nxt = 0;
@@ -492,6 +497,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 }
             }
         }
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
     }
 

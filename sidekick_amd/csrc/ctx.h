@@ -19,6 +19,7 @@ struct qk_knobs {
     int bsgs64_sg = -1;    // u64 BSGS MAC mode override (-1: default)
     int bsgs64_off = 0;    // 1: u64 on the power chain instead of BSGS
     int bsgs64_shapes = 1; // 0: u64 t = 14..20, 25..28, 33..36 with 8 babies per id instead of 4
+    int bsgs64_prio = 1;   // 0: u64 BSGS without s_setprio in the MAC step and without paired MACs (round 3)
     int bsgs64_tmin = 14;  // lowest u64 threshold on BSGS (below: the power chain; round 2: 21)
     int u64_passes = 1;    // 0: u64 t > 80 on the power chain instead of BSGS passes
     int u64_xcache = 1;    // 0: u64 offset passes raise x^8 to base/8 themselves (no per-id x^base cache)

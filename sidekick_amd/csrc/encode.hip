@@ -112,25 +112,25 @@ __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB *
 
 // Pass 0 of a multi-pass encode (powers 1..80) that also writes x^80 per id
 // for pass 1 (the x^base cache, enc32_passes)
-template <int SG>
+template <int SG, int PRIO = 1>
 __global__ __launch_bounds__(BLOCK, 2) void k_encode_u32_bsgs_x80(const uint32_t *__restrict__ ids, uint64_t n,
                                                                  uint32_t head, uint32_t T,
                                                                  uint64_t *__restrict__ partials,
                                                                  const uint32_t *xin,
                                                                  uint32_t *xout) {
     (void)xin;
-    bsgs::body<bsgs::Cfg<8, 10, SG, 1, 1, false, false, 2>>(ids, n, head, T, partials, 0, nullptr, xout);
+    bsgs::body<bsgs::Cfg<8, 10, SG, 1, 1, false, false, 2, false, PRIO>>(ids, n, head, T, partials, 0, nullptr, xout);
 }
 
 // Offset pass for thresholds > 80 (several passes over the ids): powers
 // base+1 .. base+8*NA with giants x^(base + 8a), a = 0..NA-1 (bsgs.h OFF).
 // XC: x^base from the previous pass's per-id cache (bit 0) / x^(base + 8 NA)
 // to the next pass's (bit 1) instead of square-and-multiply per pass.
-template <int NA, int SG, int XC = 0>
+template <int NA, int SG, int XC = 0, int PRIO = 1>
 __global__ __launch_bounds__(BLOCK, (NA > 6 ? 2 : NA > 5 ? 3 : 4)) void k_encode_u32_bsgs_off(
     const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T, uint32_t base,
     uint64_t *__restrict__ partials, const uint32_t *xin, uint32_t *xout) {
-    bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true, XC>>(ids, n, head, T, partials, base, xin, xout);
+    bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true, XC, false, PRIO>>(ids, n, head, T, partials, base, xin, xout);
 }
 
 // lane j of a G-group: start = x^(j+1), step = x^G (square-and-multiply).
@@ -553,37 +553,41 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restri
 // is read from baby 8: 32 KB of LDS per workgroup at t = 80, 4 per CU
 // (tools/tune_u64.hip: 24.1 vs 25.6 ms per 1e9 ids with 50 KB at 3 per CU).
 // The first SG MACs of a wave's tile count their carries on the scalar unit.
-template <int NA, int SG>
+// F (knob bsgs64_prio): 1 — s_setprio in the MAC step and, with two babies
+// per wave, the two MACs of a giant row issued as one interleaved block
+// (MODE 3); 0 — the round-3 form (MODE 0, no priority changes)
+template <int NA, int SG, int F = 1>
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs(const uint64_t *__restrict__ ids, uint64_t n,
                                                                       uint32_t head, uint32_t T,
                                                                       uint64_t *__restrict__ partials) {
     (void)head;
-    bsgs64::body<NA, 0, SG, 0, 0, false, true, 1>(ids, n, T, partials);
+    bsgs64::body<NA, F ? 3 : 0, SG, 0, 0, false, true, 1, 0, bsgs64::NB, F>(ids, n, T, partials);
 }
 
 // the same with four babies per id (one per wave) and NA giant rows of 4
 // powers: t <= 40 (bsgs64.h NBT)
-template <int NA>
+template <int NA, int F = 1>
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs4(const uint64_t *__restrict__ ids, uint64_t n,
                                                                        uint32_t head, uint32_t T,
                                                                        uint64_t *__restrict__ partials) {
     (void)head;
-    bsgs64::body<NA, 0, 16, 0, 0, false, true, 1, 0, 4>(ids, n, T, partials);
+    bsgs64::body<NA, 0, 16, 0, 0, false, true, 1, 0, 4, F>(ids, n, T, partials);
 }
 
 // Pass 0 of a u64 multi-pass encode that also writes x^80 per id for pass 1
+template <int F = 1>
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_x80(const uint64_t *__restrict__ ids,
                                                                           uint64_t n, uint32_t head, uint32_t T,
                                                                           uint64_t *__restrict__ partials,
                                                                           uint64_t *xout) {
     (void)head;
-    bsgs64::body<10, 0, 16, 0, 0, false, true, 1, 2>(ids, n, T, partials, 0, nullptr, xout);
+    bsgs64::body<10, F ? 3 : 0, 16, 0, 0, false, true, 1, 2, bsgs64::NB, F>(ids, n, T, partials, 0, nullptr, xout);
 }
 
 // Offset pass for u64 thresholds > 80: powers base+1 .. base+8NA with giants
 // x^(base + 8a) (bsgs64.h OFF); the ids are read once per pass.
 // XC: the per-id x^base cache between passes (bsgs64.h)
-template <int NA, int XC = 0>
+template <int NA, int XC = 0, int F = 1>
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_off(const uint64_t *__restrict__ ids,
                                                                           uint64_t n, uint32_t head, uint32_t T,
                                                                           uint32_t base,
@@ -591,7 +595,7 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_off(const 
                                                                           const uint64_t *xin,
                                                                           uint64_t *xout) {
     (void)head;
-    bsgs64::body<NA, 0, 16, 0, 0, true, true, 1, XC>(ids, n, T, partials, base, xin, xout);
+    bsgs64::body<NA, F ? 3 : 0, 16, 0, 0, true, true, 1, XC, bsgs64::NB, F>(ids, n, T, partials, base, xin, xout);
 }
 
 // ------------------------------------------------------------- dispatch
@@ -696,6 +700,7 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
             xc = (uint32_t *)((char *)ctx->d_scratch + poff + ((uintptr_t)ids & 15));
         // else: no room for the cache, each pass raises x^8 itself
     }
+    const bool prio = ctx->knobs.bsgs_prio;   // s_setprio around the MAC phase (knob bsgs_prio)
     uint32_t pass = 0;
     for (uint32_t base = 0; base < T; ++pass) {
         const uint32_t Tp = std::min<uint32_t>(base == 0 ? 80 : 48, T - base);
@@ -704,14 +709,17 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
         const int xcm = !xc ? 0 : (pass > 0 ? 1 : 0) | (pass < npass ? 2 : 0);
         int rc;
         if (base == 0 && xc)
-            rc = run_pass<2>(ctx, k_encode_u32_bsgs_x80<16>, 80, ids, n, head, Tp, 0, out, meta, acc, s, nullptr, xc);
+            rc = run_pass<2>(ctx, prio ? k_encode_u32_bsgs_x80<16, 1> : k_encode_u32_bsgs_x80<16, 0>, 80, ids, n, head,
+                             Tp, 0, out, meta, acc, s, nullptr, xc);
         else if (base == 0)
-            rc = run_pass<0>(ctx, k_encode_u32_bsgs<8, 10, 16>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
+            rc = run_pass<0>(ctx, prio ? k_encode_u32_bsgs<8, 10, 16, 1> : k_encode_u32_bsgs<8, 10, 16, 0>, 80, ids, n,
+                             head, Tp, 0, out, meta, acc, s);
         else if (Tp <= 40) {   // the last pass (npass >= 1): NA = ceil(Tp / 8) giant rows
+#define QK_OFF32(NA_, XC_) (prio ? k_encode_u32_bsgs_off<NA_, 2 * NA_, XC_, 1> : k_encode_u32_bsgs_off<NA_, 2 * NA_, XC_, 0>)
 #define QK_LAST32(NA_)                                                                                       \
-    (xcm & 1 ? run_pass<1>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 1>, 8 * NA_, ids, n, head, Tp, base,      \
+    (xcm & 1 ? run_pass<1>(ctx, QK_OFF32(NA_, 1), 8 * NA_, ids, n, head, Tp, base,                            \
                               out + base, meta, acc, s, xc, nullptr)                                          \
-             : run_pass<1>(ctx, k_encode_u32_bsgs_off<NA_, 2 * NA_, 0>, 8 * NA_, ids, n, head, Tp, base,      \
+             : run_pass<1>(ctx, QK_OFF32(NA_, 0), 8 * NA_, ids, n, head, Tp, base,                            \
                               out + base, meta, acc, s))
             switch ((Tp + 7) / 8) {
             case 1: rc = QK_LAST32(1); break;   // <= 8 powers: one giant row (x^base)
@@ -723,15 +731,16 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
 #undef QK_LAST32
         } else {
             switch (xcm) {
-            case 1: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 1>, 48, ids, n, head, Tp, base, out + base,
+            case 1: rc = run_pass<1>(ctx, QK_OFF32(6, 1), 48, ids, n, head, Tp, base, out + base,
                                         meta, acc, s, xc, nullptr); break;
-            case 2: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 2>, 48, ids, n, head, Tp, base, out + base,
+            case 2: rc = run_pass<1>(ctx, QK_OFF32(6, 2), 48, ids, n, head, Tp, base, out + base,
                                         meta, acc, s, nullptr, xc); break;
-            case 3: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 3>, 48, ids, n, head, Tp, base, out + base,
+            case 3: rc = run_pass<1>(ctx, QK_OFF32(6, 3), 48, ids, n, head, Tp, base, out + base,
                                         meta, acc, s, xc, xc); break;
-            default: rc = run_pass<1>(ctx, k_encode_u32_bsgs_off<6, 12, 0>, 48, ids, n, head, Tp, base, out + base,
+            default: rc = run_pass<1>(ctx, QK_OFF32(6, 0), 48, ids, n, head, Tp, base, out + base,
                                          meta, acc, s); break;
             }
+#undef QK_OFF32
         }
         if (rc) return rc;
         base += Tp;
@@ -762,7 +771,7 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
 template <int NA, int XC = 0>
 static int run_pass64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t Tp, uint32_t base,
                       uint64_t *out, uint64_t *meta, int acc, hipStream_t s, uint64_t *xc = nullptr) {
-    auto kern = k_encode_u64_bsgs_off<NA, XC>;
+    auto kern = ctx->knobs.bsgs64_prio ? k_encode_u64_bsgs_off<NA, XC, 1> : k_encode_u64_bsgs_off<NA, XC, 0>;
     const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
     if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 8 * NA * sizeof(uint64_t), s)) return rc;
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
@@ -790,21 +799,22 @@ static int enc64_passes_chunk(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32
     if (npass >= 1 && ctx->knobs.u64_xcache) {
         const uint64_t tiles = (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK;
         const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u64_bsgs<10, 16>, tiles, 1),
-                                         grid_for(ctx, k_encode_u64_bsgs_x80, tiles, 1),
+                                         grid_for(ctx, k_encode_u64_bsgs_x80<1>, tiles, 1),
                                          grid_for(ctx, k_encode_u64_bsgs_off<10, 3>, tiles, 1)});
         const size_t poff = ((size_t)nbmax * 2 * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
         if (ensure_scratch(ctx, poff + (size_t)n * 8, s) == QK_OK) xc = (uint64_t *)((char *)ctx->d_scratch + poff);
     }
     {   // pass 0: powers 1..80 (+ x^80 per id for pass 1 when the cache is on)
-        auto kern = k_encode_u64_bsgs<10, 16>;
+        const bool f1 = ctx->knobs.bsgs64_prio;
+        auto kern = f1 ? k_encode_u64_bsgs<10, 16, 1> : k_encode_u64_bsgs<10, 16, 0>;
+        auto kx80 = f1 ? k_encode_u64_bsgs_x80<1> : k_encode_u64_bsgs_x80<0>;
         const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
         if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 80 * sizeof(uint64_t), s)) return rc;
         uint64_t *partials = (uint64_t *)ctx->d_scratch;
         if (int rc = scratch_acquire(ctx, s)) return rc;
         hipEvent_t e0 = prof_begin(ctx, s);
         if (xc)
-            hipLaunchKernelGGL(k_encode_u64_bsgs_x80, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, 80u,
-                               partials, xc);
+            hipLaunchKernelGGL(kx80, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, 80u, partials, xc);
         else
             hipLaunchKernelGGL(kern, dim3(nb), dim3(BLOCK), 0, s, ids, (uint64_t)n, head, 80u, partials);
         prof_end(ctx, s, e0);
@@ -1053,14 +1063,16 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     // power chain.
     const int sg64 = ctx->knobs.bsgs64_sg;
     const int no64 = ctx->knobs.bsgs64_off;
+    const bool f64 = ctx->knobs.bsgs64_prio;   // s_setprio + paired MACs (knob bsgs64_prio)
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     if (T >= (uint32_t)ctx->knobs.bsgs64_tmin && T <= 80 && !no64 && n / min_grid64 < (1ull << 30)) {
 #define QK_BSGS64(NA_, SG_)                                                                           \
-    run_encode<uint64_t>(ctx, k_encode_u64_bsgs<NA_, SG_>, k_finalize_u64, 8 * NA_, 2, ids, n, head, T,     \
+    run_encode<uint64_t>(ctx, f64 ? k_encode_u64_bsgs<NA_, SG_, 1> : k_encode_u64_bsgs<NA_, SG_, 0>,         \
+                         k_finalize_u64, 8 * NA_, 2, ids, n, head, T,                                          \
                          (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
 #define QK_BSGS64_4(NA_)                                                                              \
-    run_encode<uint64_t>(ctx, k_encode_u64_bsgs4<NA_>, k_finalize_u64, 4 * NA_, 2, ids, n, head, T,         \
-                         (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
+    run_encode<uint64_t>(ctx, f64 ? k_encode_u64_bsgs4<NA_, 1> : k_encode_u64_bsgs4<NA_, 0>, k_finalize_u64,  \
+                         4 * NA_, 2, ids, n, head, T, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
         // four babies per id and ceil(T/4) giant rows (knob bsgs64_shapes)
         // where 8 babies would compute 4+ powers more: t = 14..20, 25..28,
         // 33..36 (+8..17 %, profiles/r03/shapes/sweep64_four_babies_ab.jsonl;

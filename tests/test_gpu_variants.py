@@ -18,7 +18,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "bsgs64_tmin": 14, "bsgs64_shapes": 1, "u32_xcache": 1, "u64_xcache": 1,
-            "bsgs_shapes": 1, "bsgs_prio": 1}
+            "bsgs_shapes": 1, "bsgs_prio": 1, "bsgs64_prio": 1}
 
 
 @contextlib.contextmanager
@@ -106,12 +106,26 @@ def test_u32_bsgs_shapes(shapes):
 
 @pytest.mark.parametrize("prio", [1, 0])
 def test_u32_bsgs_prio(prio):
-    """Every single-pass u32 BSGS shape with and without s_setprio around its
-    MAC phase (knob bsgs_prio; the default raises it), against the oracle,
-    ragged and misaligned."""
-    cases = [(f"t{t}", 100_003 + t, t, t % 4) for t in (8, 12, 16, 20, 24, 28, 30, 32, 36, 40, 42, 48, 56, 64, 72, 80)]
+    """Every single-pass u32 BSGS shape and the multi-pass kernels (pass 0 with
+    x^80 out, offset passes with and without the x^base cache, a one-row last
+    pass) with and without s_setprio around the MAC phase (knob bsgs_prio;
+    the default raises it), against the oracle, ragged and misaligned."""
+    cases = [(f"t{t}", 100_003 + t, t, t % 4)
+             for t in (8, 12, 16, 20, 24, 28, 30, 32, 36, 40, 42, 48, 56, 64, 72, 80, 88, 129, 300)]
     with knob("bsgs_prio", prio):
         res = _run(32, cases)
+    assert all(res.values()), res
+
+
+@pytest.mark.parametrize("prio", [1, 0])
+def test_u64_bsgs_prio(prio):
+    """u64 baby-step/giant-step with s_setprio in the MAC step and paired
+    MACs (knob bsgs64_prio, the default) and in the round-3 form, against the
+    oracle: eight- and four-baby shapes, pass 0 with x^80 out, offset passes,
+    a one-row last pass."""
+    cases = [(f"t{t}", 40_009 + t, t, t % 2) for t in (14, 16, 20, 24, 32, 40, 56, 72, 80, 88, 169, 250)]
+    with knob("bsgs64_prio", prio):
+        res = _run(64, cases)
     assert all(res.values()), res
 
 
@@ -180,6 +194,6 @@ def test_knob_validation():
     from sidekick_amd._lib import QuackError
     ctx = sk.get_context(0)
     for name, bad in (("flow_load", 0), ("flow_load", 65), ("root_test", 3), ("no_such_knob", 1),
-                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2)):
+                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2), ("bsgs64_prio", 2)):
         with pytest.raises(QuackError):
             ctx.set_knob(name, bad)

@@ -44,6 +44,7 @@ for s in $STEPS; do
     dist4full) step dist4full 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29536 bench.py --gpus 4 --steps 3 --warmup 1 --cpu-sample 0 || exit 3 ;;
     roots) step roots 300 python3 -u tools/bench_roots.py ${ROOTS_ARGS:-} || exit 3
            step profroots 120 ./tools/prof_roots 32 300 || exit 3 ;;
+    abenc) step abenc 600 python3 -u tools/ab_encode.py ${ABENC_ARGS:-} || exit 3 ;;
     abflows) step abflows 600 python3 -u tools/ab_flows.py ${ABFLOWS_ARGS:-} || exit 3 ;;
     profabflows)
       export TMPDIR=/tmp

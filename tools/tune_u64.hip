@@ -28,12 +28,12 @@ __global__ void k_fill(uint64_t *out, uint64_t n, uint64_t seed) {
         out[i] = splitmix_mix(seed + (i + 1) * GAMMA);
 }
 
-template <int NA, int MODE, int SG, int ABL, int OCC, int PF = 0, bool BSH = false, int LD = 0>
+template <int NA, int MODE, int SG, int ABL, int OCC, int PF = 0, bool BSH = false, int LD = 0, int PRIO = 0>
 __global__ __launch_bounds__(256, OCC) void k_var(const uint64_t *ids, uint64_t n, uint32_t T, uint64_t *partials,
                                                   uint64_t *clk) {
     uint64_t t0 = 0, r0 = 0;
     if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
-    bsgs64::body<NA, MODE, SG, ABL, PF, false, BSH, LD>(ids, n, T, partials);
+    bsgs64::body<NA, MODE, SG, ABL, PF, false, BSH, LD, 0, bsgs64::NB, PRIO>(ids, n, T, partials);
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
         clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
@@ -56,22 +56,18 @@ int main() {
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, ids, n, 0x5EED0003ull);
     int cus = 0;
     CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    // (the round-3/4 layout and carry-mode variants are in the git history and
+    // profiles/r03/tune_u64*.json, profiles/r04/u64/)
     std::vector<Var> vars = {
         {"product: mode0 sg16, B*2^32 recomputed, occ4, row-ahead giants", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
-        {"mode3 (paired interleaved MACs) sg16 bsh occ4 ld", k_var<10, 3, 16, 0, 4, 0, true, 1>, 4},
-        {"mode3 (paired interleaved MACs) sg18 bsh occ4 ld", k_var<10, 3, 18, 0, 4, 0, true, 1>, 4},
-        {"mode3 (paired interleaved MACs) sg14 bsh occ4 ld", k_var<10, 3, 14, 0, 4, 0, true, 1>, 4},
-        {"mode0 sg16 bsh occ4 (all giant rows loaded at once)", k_var<10, 0, 16, 0, 4, 0, true, 0>, 4},
-        {"mode0 sg12 bsh occ4 ld", k_var<10, 0, 12, 0, 4, 0, true, 1>, 4},
-        {"mode0 sg15 bsh occ4 ld", k_var<10, 0, 15, 0, 4, 0, true, 1>, 4},
-        {"mode0 sg18 bsh occ4 ld", k_var<10, 0, 18, 0, 4, 0, true, 1>, 4},
-        {"mode0 sg16 bsh occ3 ld", k_var<10, 0, 16, 0, 3, 0, true, 1>, 3},
-        {"mode1 bsh occ3", k_var<10, 1, 0, 0, 3, 0, true>, 3},
-        {"round 2: mode1, B*2^32 in LDS (50 KB), occ3", k_var<10, 1, 0, 0, 3>, 3},
-        {"round 2 layout: mode0 sg8 occ3", k_var<10, 0, 8, 0, 3>, 3},
-        {"round 2 layout: mode0 sg12 prefetch occ3", k_var<10, 0, 12, 0, 3, 1>, 3},
-        {"ablate: no MACs (product)", k_var<10, 0, 16, 1, 4, 0, true, 1>, 4, 1},
-        {"ablate: no modmuls (product)", k_var<10, 0, 16, 2, 4, 0, true, 1>, 4, 2},
+        {"mode0 sg16 + s_setprio in the MAC step", k_var<10, 0, 16, 0, 4, 0, true, 1, 1>, 4},
+        {"mode3 sg16 + s_setprio in the MAC step", k_var<10, 3, 16, 0, 4, 0, true, 1, 1>, 4},
+        {"mode3 sg14 + s_setprio in the MAC step", k_var<10, 3, 14, 0, 4, 0, true, 1, 1>, 4},
+        {"mode3 sg18 + s_setprio in the MAC step", k_var<10, 3, 18, 0, 4, 0, true, 1, 1>, 4},
+        {"mode3 sg16 + s_setprio, all giant rows at once", k_var<10, 3, 16, 0, 4, 0, true, 0, 1>, 4},
+        {"mode3 sg16, no s_setprio", k_var<10, 3, 16, 0, 4, 0, true, 1>, 4},
+        {"mode3 sg16 + s_setprio in the MAC step (again)", k_var<10, 3, 16, 0, 4, 0, true, 1, 1>, 4},
+        {"product again", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
     };
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
