@@ -544,7 +544,8 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"u64_passes", &qk_knobs::u64_passes, 0, 1},
         {"u64_xcache", &qk_knobs::u64_xcache, 0, 1},   {"u64_kmax", &qk_knobs::u64_kmax, 4, 40},
         {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
-        {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 0, 9},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
+        {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 0, 9},
+        {"flow_prio", &qk_knobs::flow_prio, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
         {"root_test", &qk_knobs::root_test, 0, 2},      {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
     };
     for (const K &k : table)

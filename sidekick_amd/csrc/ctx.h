@@ -31,6 +31,8 @@ struct qk_knobs {
                            // throughout; 2: pair arrays between the first and last pass; 3 / 4: 512 / 1024
                            // threads; 5 / 6: 11-bit digits, 512 / 1024 threads; 7-9: as 2, 5, 6 without LDS
                            // staging (direct scatter); 0: hipCUB's onesweep
+    int flow_prio = 0;     // 1: per-flow encode kernels with s_setprio around the MACs (1e6 flows: 7.57 vs
+                           // 6.80 ms, 16 / 1e4 flows even; profiles/r04/prio/ab_flows_prio.jsonl)
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)

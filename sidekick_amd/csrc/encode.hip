@@ -1095,11 +1095,15 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
         case 8: return QK_BSGS64(8, 16);
         case 9: return QK_BSGS64(9, 16);
         default:
-            switch (sg64) {   // knob bsgs64_sg (measurements): scalar-counted MACs of the 18
+            // knob bsgs64_sg (measurements): scalar-counted MACs of the 18; the
+            // default 14 with the paired-MAC form (22.65 vs 23.19 ms at 16,
+            // twice, profiles/r04/prio/tune_u64_prio.json), 16 without it
+            switch (sg64 >= 0 ? sg64 : f64 ? 14 : 16) {
             case 8: return QK_BSGS64(10, 8);
             case 12: return QK_BSGS64(10, 12);
+            case 14: return QK_BSGS64(10, 14);
             case 18: return QK_BSGS64(10, 18);
-            default: return QK_BSGS64(10, 16);   // sg64 = -1, the default
+            default: return QK_BSGS64(10, 16);
             }
         }
 #undef QK_BSGS64

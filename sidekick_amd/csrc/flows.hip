@@ -129,7 +129,7 @@ __global__ __launch_bounds__(SG_BLOCK) void k_seg_encode(const uint32_t *__restr
 // headline kernel's baby-step/giant-step body (bsgs.h).  All lanes of the
 // workgroup belong to one flow, so the wave-level scalar wrap counts stay
 // valid; the workgroup's sums go to the flow's accumulator row by atomicAdd.
-template <int NB, int NA, int SG>
+template <int NB, int NA, int SG, int PRIO>
 __global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB * NA > 40 ? 3 : 4)) void k_seg_bsgs(
     const uint32_t *__restrict__ ids, const SegItem *__restrict__ items, uint32_t T,
     unsigned long long *__restrict__ acc_out) {
@@ -137,7 +137,8 @@ __global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 
     const uint32_t *p = ids + it.lo;
     const uint32_t head = (uint32_t)(((16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u) >> 2);   // ids to 16-B alignment
     unsigned long long *row = acc_out + (size_t)it.seg * T;
-    bsgs::body_gen<bsgs::Cfg<NB, NA, SG>>(p, it.hi - it.lo, head, T, threadIdx.x, (uint64_t)bsgs::BLOCK,
+    bsgs::body_gen<bsgs::Cfg<NB, NA, SG, 1, 1, false, false, 0, false, PRIO>>(p, it.hi - it.lo, head, T, threadIdx.x,
+                                                                             (uint64_t)bsgs::BLOCK,
                                           [=](uint32_t m, uint64_t s) {
                                               atomicAdd(&row[m], (unsigned long long)fold64_32(s));
                                           });
@@ -203,15 +204,25 @@ __global__ __launch_bounds__(SG_BLOCK, 4) void k_seg_small(const uint32_t *__res
     }
 }
 
-// per-lane (VALU) wrap counters: SG = 0
-static int seg_small_launch(uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
-                            unsigned long long *acc, hipStream_t s) {
+// per-lane (VALU) wrap counters: SG = 0; P: s_setprio around the MACs
+template <int P>
+static void seg_small_launch_p(uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
+                               unsigned long long *acc, hipStream_t s) {
     const dim3 grid((nseg + SG_BLOCK - 1) / SG_BLOCK), block(SG_BLOCK);
-    if (T <= 8) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<4, 2, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
-    else if (T <= 12) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<4, 3, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
-    else if (T <= 16) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<4, 4, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
-    else if (T <= 24) hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<6, 4, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
-    else hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<8, 4, 0>>), grid, block, 0, s, ids, d_offs, nseg, T, acc);
+#define QK_SMALL(NB_, NA_)                                                                                         \
+    hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<NB_, NA_, 0, 1, 1, false, false, 0, false, P>>), grid, block, 0, s, ids, \
+                       d_offs, nseg, T, acc)
+    if (T <= 8) QK_SMALL(4, 2);
+    else if (T <= 12) QK_SMALL(4, 3);
+    else if (T <= 16) QK_SMALL(4, 4);
+    else if (T <= 24) QK_SMALL(6, 4);
+    else QK_SMALL(8, 4);
+#undef QK_SMALL
+}
+static int seg_small_launch(int prio, uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
+                            unsigned long long *acc, hipStream_t s) {
+    if (prio) seg_small_launch_p<1>(T, ids, d_offs, nseg, acc, s);
+    else seg_small_launch_p<0>(T, ids, d_offs, nseg, acc, s);
     return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
 }
 
@@ -716,7 +727,7 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
     QK_HIP_TRY(hipMemsetAsync(d_acc, 0, nseg * T * sizeof(uint64_t), s));
     if (small_ok(T) && nseg) {
         hipEvent_t e0 = prof_begin(ctx, s);
-        const int rs = seg_small_launch(T, d_ids, d_offs, (uint32_t)nseg, d_acc, s);
+        const int rs = seg_small_launch(ctx->knobs.flow_prio, T, d_ids, d_offs, (uint32_t)nseg, d_acc, s);
         prof_end(ctx, s, e0);
         if (rs) return rs;
     }
@@ -732,16 +743,21 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
         hipEvent_t e0 = prof_begin(ctx, s);
         const dim3 grid(ni), block(bsgs::BLOCK);
         if (T >= 5 && T <= 80) {   // same configurations as the headline encode
-            if (T <= 8) hipLaunchKernelGGL((k_seg_bsgs<4, 2, 1>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 12) hipLaunchKernelGGL((k_seg_bsgs<4, 3, 3>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 16) hipLaunchKernelGGL((k_seg_bsgs<4, 4, 4>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 24) hipLaunchKernelGGL((k_seg_bsgs<6, 4, 4>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 32) hipLaunchKernelGGL((k_seg_bsgs<8, 4, 8>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 40) hipLaunchKernelGGL((k_seg_bsgs<8, 5, 10>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 48) hipLaunchKernelGGL((k_seg_bsgs<8, 6, 12>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 56) hipLaunchKernelGGL((k_seg_bsgs<8, 7, 14>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else if (T <= 64) hipLaunchKernelGGL((k_seg_bsgs<8, 8, 16>), grid, block, 0, s, d_ids, d_items, T, d_acc);
-            else hipLaunchKernelGGL((k_seg_bsgs<8, 10, 16>), grid, block, 0, s, d_ids, d_items, T, d_acc);
+            const bool fp = ctx->knobs.flow_prio;   // s_setprio around the MACs (knob flow_prio)
+#define QK_SEGB(NB_, NA_, SG_)                                                                                     \
+    hipLaunchKernelGGL((fp ? k_seg_bsgs<NB_, NA_, SG_, 1> : k_seg_bsgs<NB_, NA_, SG_, 0>), grid, block, 0, s, d_ids, \
+                       d_items, T, d_acc)
+            if (T <= 8) QK_SEGB(4, 2, 1);
+            else if (T <= 12) QK_SEGB(4, 3, 3);
+            else if (T <= 16) QK_SEGB(4, 4, 4);
+            else if (T <= 24) QK_SEGB(6, 4, 4);
+            else if (T <= 32) QK_SEGB(8, 4, 8);
+            else if (T <= 40) QK_SEGB(8, 5, 10);
+            else if (T <= 48) QK_SEGB(8, 6, 12);
+            else if (T <= 56) QK_SEGB(8, 7, 14);
+            else if (T <= 64) QK_SEGB(8, 8, 16);
+            else QK_SEGB(8, 10, 16);
+#undef QK_SEGB
             rc = hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
             G = 0;
         }

@@ -81,7 +81,7 @@ def test_u64_lane_split(kmax):
     assert all(res.values()), res
 
 
-@pytest.mark.parametrize("sg", [-1, 8, 12, 18])
+@pytest.mark.parametrize("sg", [-1, 8, 12, 14, 16, 18])
 def test_u64_bsgs_scalar_carry_macs(sg):
     """The u64 baby-step/giant-step kernel (bsgs64.h) with the first sg MACs
     of each wave's tile counting carries on the scalar unit, the rest per

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--t", type=int, default=32)
+    ap.add_argument("--default", type=int, default=None, help="knob value restored afterwards (default: the first mode)")
     a = ap.parse_args()
     import torch
     import sidekick_amd as sk
@@ -74,7 +75,7 @@ def main():
                     ref = out
                 elif out != ref:
                     same[m] = False
-        ctx.set_knob(a.knob, 1 if a.knob == "flow_sort" else 0)
+        ctx.set_knob(a.knob, modes[0] if a.default is None else a.default)
         print(json.dumps({"flows": nflows, "n_packets": n, "t": t, "knob": a.knob,
                           "median_ms": {str(m): float(np.median(times[m])) * 1e3 for m in modes},
                           "min_ms": {str(m): float(np.min(times[m])) * 1e3 for m in modes},

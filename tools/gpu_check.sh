@@ -45,6 +45,8 @@ for s in $STEPS; do
     roots) step roots 300 python3 -u tools/bench_roots.py ${ROOTS_ARGS:-} || exit 3
            step profroots 120 ./tools/prof_roots 32 300 || exit 3 ;;
     abenc) step abenc 600 python3 -u tools/ab_encode.py ${ABENC_ARGS:-} || exit 3 ;;
+    abenc2) step abenc2 600 python3 -u tools/ab_encode.py ${ABENC2_ARGS:-} || exit 3 ;;
+    abenc3) step abenc3 600 python3 -u tools/ab_encode.py ${ABENC3_ARGS:-} || exit 3 ;;
     abflows) step abflows 600 python3 -u tools/ab_flows.py ${ABFLOWS_ARGS:-} || exit 3 ;;
     profabflows)
       export TMPDIR=/tmp
