@@ -270,7 +270,7 @@ template <typename T> static bool rt_use_scan(const qk_ctx *ctx, uint32_t d, siz
     const double nn = (double)n, dd = (double)d;
     const bool w32 = sizeof(T) == 4;
     const double horner = nn * dd * (w32 ? 1.43e-7 : 3.8e-7);
-    const double scan = nn * (w32 ? 0.7e-6 : 1.4e-6) + dd * dd * (w32 ? 0.06 : 0.18);
+    const double scan = nn * (w32 ? 0.7e-6 : 1.4e-6) + dd * dd * (w32 ? 0.025 : 0.055);
     return scan < horner;
 }
 
