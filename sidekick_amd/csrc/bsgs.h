@@ -440,8 +440,10 @@ __device__ __forceinline__ void two(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id0,
         if (w0) powers_exact<C>(B0, A0);
         if (w1) powers_exact<C>(B1, A1);
     }
+    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(1);
     accumulate<C>(S, B0, A0);
     accumulate<C>(S, B1, A1);
+    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(0);
 }
 
 template <class C>

@@ -175,12 +175,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void k_sg(const uint32_t *ids, uint64_
 }
 
 // s_setprio around the MAC phase (bsgs.h Cfg PRIO)
-template <int PRIO, int SG = 8, int MINW = 5, bool TREE = false>
+template <int PRIO, int SG = 8, int MINW = 5, bool TREE = false, bool PAIR = false>
 __global__ __launch_bounds__(BLOCK, MINW) void k_prio(const uint32_t *ids, uint64_t n, uint64_t *partials,
                                                       uint64_t *clk) {
     uint64_t c0, r0;
     clk_begin(c0, r0);
-    bsgs::body<bsgs::Cfg<8, 4, SG, 1, 1, false, false, 0, TREE, PRIO>>(ids, n, 0, T, partials);
+    bsgs::body<bsgs::Cfg<8, 4, SG, 1, 1, PAIR, false, 0, TREE, PRIO>>(ids, n, 0, T, partials);
     clk_end(clk, c0, r0);
 }
 
@@ -238,12 +238,12 @@ int main(int argc, char **argv) {
     // 2.68; with priority (profiles/r04/prio/tune_bsgs_prio_sweep.json): 4
     // waves/SIMD 2.73 vs 2.63-2.66, 7 / 6 scalar-counted groups 3.42 / 4.05,
     // product-tree babies 2.57; again (tune_bsgs_prio_tree.json) tree 2.559 /
-    // 2.569 vs product 2.559 / 2.587: even, not adopted.  This set: the same
-    std::vector<Var> vars = {{"prio_mac_tree_w5", k_prio<1, 8, 5, true>},
-                             {"prio_mac_w5 (product)", k_prio<1>},
-                             {"tree_w5 (no priority)", k_prio<0, 8, 5, true>},
-                             {"prio_mac_tree_w4", k_prio<1, 8, 4, true>},
-                             {"prio_mac_tree_w5_again", k_prio<1, 8, 5, true>},
+    // 2.569 vs product 2.559 / 2.587: even, not adopted.  This set: two ids'
+    // powers interleaved (PAIR) under priority
+    std::vector<Var> vars = {{"prio_mac_w5 (product)", k_prio<1>},
+                             {"prio_pair_w4", k_prio<1, 8, 4, false, true>},
+                             {"prio_pair_w3", k_prio<1, 8, 3, false, true>},
+                             {"pair_w4 (no priority)", k_prio<0, 8, 4, false, true>},
                              {"prio_mac_w5_again", k_prio<1>}};
     uint32_t ref[T], got[T];
     std::vector<std::vector<float>> times(vars.size());
