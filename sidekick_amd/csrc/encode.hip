@@ -13,12 +13,13 @@
 //     (NB, NA) = (8, 4): 9 lazy modmuls + 24 MACs + 8 row-0 mads per id =
 //     4.47 SIMD-cycles of VALU issue per id (the algorithmic anchor,
 //     tools/issue_model.py); the kernel issues 1.19 VALU + 0.76 SALU
-//     wave-instructions per id and runs at ~0.76 of the anchor at the
+//     wave-instructions per id, each id's MAC phase at raised wave priority
+//     (s_setprio, knob bsgs_prio), and runs at ~0.80 of the anchor at the
 //     bench run's own shader clock (bench.py roofline.valu)
-//     and ~0.18 of the HBM read roofline (4 B/id).
-//   * 14 <= t <= 80 (u64) — k_encode_u64_bsgs<NA,MODE,SG> (bsgs64.h): the
+//     and ~0.19 of the HBM read roofline (4 B/id).
+//   * 14 <= t <= 80 (u64) — k_encode_u64_bsgs<NA,SG,F> (bsgs64.h): the
 //     same split with the babies/giants of a 256-id tile shared through LDS,
-//     each wave owning two babies' MAC rows.
+//     each wave owning two babies' MAC rows (paired, at raised priority).
 //   * t > 80 — passes of the BSGS kernels (offset giants x^(base + 8a)).
 //   * small t (u32 t <= 4, u64 t <= 13) — power chains: a lane group of G
 //     lanes owns one id, lane j computes powers j+1, j+1+G, ... with step
