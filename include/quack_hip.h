@@ -158,9 +158,10 @@ int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
 /* Measurement knobs of this context (the defaults are the
  * product's measured choices — tools/ and the variant tests set them):
  * "bsgs_sg", "bsgs_shapes", "bsgs_prio", "u32_passes", "u32_xcache", "bsgs64_sg", "bsgs64_off", "bsgs64_tmin", "bsgs64_shapes", "bsgs64_prio", "u64_passes",
- * "u64_xcache", "u64_kmax", "flow_load" (2..64), "flow_wgpc", "flow_hist",
+ * "u64_xcache", "u64_kmax", "flow_load" (2..64), "flow_wgpc", "flow_hist", "flow_sort", "flow_prio",
  * "pkt_fused", "rt64_horner",
- * "root_test" (0 automatic, 1 Horner, 2 root-set scan), "comm_fault" (tests:
+ * "root_test" (0 automatic, 1 Horner, 2 root-set scan), "rt_direct" (0: the
+ * root-set scan's results by copies, not its pinned host slots), "comm_fault" (tests:
  * the k-th collective's payload staging of this context's rank fails once).
  * Unknown name or out-of-range value -> QK_E_INVAL. */
 int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value);

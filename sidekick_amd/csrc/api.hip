@@ -252,8 +252,10 @@ static int encode_host_impl(qk_ctx *ctx, const IdT *h_ids, size_t n, uint32_t t,
 
 // Root test in two phases, so that several devices (a multi-GPU
 // communicator, comm.hip) can have theirs in flight at once.
-// root_test_begin enqueues on s: coefficients H2D, counter reset, the kernel,
-// counters D2H.  root_test_finish waits for s, reruns once with a larger hit
+// root_test_begin enqueues on s: counters + coefficients (or root set) H2D,
+// the kernel, and for Horner the counters and first hits D2H (the scan
+// writes its hits and stops into pinned host memory itself, so no copy
+// trails the kernel).  root_test_finish waits for s, reruns once with a larger hit
 // buffer if the kernel ran out of room, and returns the hit positions sorted
 // ascending (every hit of the log, not cut at the stop) and the first stop
 // position (n if none or !use_stop).
@@ -283,7 +285,8 @@ template <typename T> int root_test_plan(const qk_ctx *ctx, const T *coeffs, uin
     if constexpr (sizeof(T) == 4) rc = qk_u32_roots(coeffs, d, r.data(), d, &k);
     else rc = qk_u64_roots(coeffs, d, r.data(), d, &k);
     if (rc) return rc;
-    plan.scan = rt_scan_table<T>(r.data(), k, plan.set, plan.tab) && plan.set.words * sizeof(T) <= SMALL_NHITS * 8;
+    plan.scan = rt_scan_table<T>(r.data(), k, plan.set, plan.tab) &&
+                plan.set.words * sizeof(T) <= (SMALL_NHITS - RT_C) * 8;
     if (!plan.scan) plan.tab.clear();
     return QK_OK;
 }
@@ -291,41 +294,54 @@ template <typename T> int root_test_plan(const qk_ctx *ctx, const T *coeffs, uin
 template <typename T>
 int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_t d, const T *d_log, size_t n,
                     int use_stop, T stop_value, hipStream_t s) {
-    // layout of d_small: [0, SMALL_NHITS) coefficients (or the root set), [SMALL_NHITS] hit count,
-    // [SMALL_STOP] stop index
-    uint64_t *d_counters = ctx->d_small + SMALL_NHITS;
-    T *d_c = (T *)ctx->d_small;
-    const bool scan = n && plan.scan;
+    // d_small: [0] hit count, [1] stop index, [2] finished workgroups, from
+    // [RT_C] the coefficients or the root set (ctx.h)
+    uint64_t *d_counters = ctx->d_small;
+    T *d_c = (T *)(ctx->d_small + RT_C);
+    uint64_t *h_c = ctx->h_small + RT_C;
+    const bool scan = n && plan.scan, direct = scan && ctx->knobs.rt_direct;
     size_t cbytes = (size_t)d * sizeof(T);
     if (scan) {
         cbytes = (size_t)plan.set.words * sizeof(T);
-        memcpy(ctx->h_small, plan.tab.data(), cbytes);
+        memcpy(h_c, plan.tab.data(), cbytes);
     } else if constexpr (sizeof(T) == 8) {
-        if (rt64_use_bsgs(ctx, d)) cbytes = rt64_bsgs_table(coeffs, d, ctx->h_small) * 8;   // limb-shifted table
-        else memcpy(ctx->h_small, coeffs, cbytes);
+        if (rt64_use_bsgs(ctx, d)) cbytes = rt64_bsgs_table(coeffs, d, h_c) * 8;   // limb-shifted table
+        else memcpy(h_c, coeffs, cbytes);
     } else {
-        memcpy(ctx->h_small, coeffs, cbytes);
+        memcpy(h_c, coeffs, cbytes);
     }
-    // one copy carries the table (or coefficients) and the zeroed hit
-    // counter / stop index (no counter-initialising launch)
-    ctx->h_small[SMALL_NHITS] = 0;
-    ctx->h_small[SMALL_STOP] = ~0ull;
-    QK_HIP_TRY(hipMemcpyAsync(d_c, ctx->h_small, (SMALL_STOP + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    (void)cbytes;
+    // one copy carries the zeroed counters and the table (or coefficients):
+    // no counter-initialising launch
+    ctx->h_small[0] = 0;
+    ctx->h_small[1] = ~0ull;
+    ctx->h_small[2] = 0;
+    ctx->h_small[3] = 0;
+    if (direct) {   // the direct form's slots (decode.hip rt_record): empty, no overflow
+        std::fill(ctx->h_small + SMALL_HITPF, ctx->h_small + SMALL_WORDS, ~0ull);
+        ctx->h_small[SMALL_OVF] = 0;
+    }
+    QK_HIP_TRY(hipMemcpyAsync(ctx->d_small, ctx->h_small, (RT_C + (cbytes + 7) / 8) * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, s));
     if (int rc = ensure_hits(ctx, 4096, s)) return rc;
     if (n) {
         int rc;
+        if (direct) {
+            // the scan writes its hits and stops into h_small's slots itself
+            // (rt_record); root_test_finish derives count and stop from them
+            return launch_root_scan<T>(ctx, d_c, plan.set, d_log, n, use_stop, stop_value, ctx->d_hits,
+                                       (uint64_t)ctx->hits_cap, d_counters, ctx->h_small_dev + SMALL_NHITS, s);
+        }
         if (scan) {
             rc = launch_root_scan<T>(ctx, d_c, plan.set, d_log, n, use_stop, stop_value, ctx->d_hits,
-                                     (uint64_t)ctx->hits_cap, d_counters, s);
-        } else {
-            int (*launch)(qk_ctx *, const T *, uint32_t, const T *, size_t, int, T, uint64_t *, uint64_t, uint64_t *,
-                          hipStream_t);
-            if constexpr (sizeof(T) == 4) launch = launch_root_test_u32;
-            else launch = launch_root_test_u64;
-            rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap,
-                        d_counters, s);
+                                     (uint64_t)ctx->hits_cap, d_counters, nullptr, s);
+            if (rc) return rc;
         }
+        int (*launch)(qk_ctx *, const T *, uint32_t, const T *, size_t, int, T, uint64_t *, uint64_t, uint64_t *,
+                      hipStream_t);
+        if constexpr (sizeof(T) == 4) launch = launch_root_test_u32;
+        else launch = launch_root_test_u64;
+        if (!scan) rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap,
+                               d_counters, s);
         if (rc) return rc;
     }
     QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_NHITS, d_counters, 16, hipMemcpyDeviceToHost, s));
@@ -339,12 +355,32 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
 template <typename T>
 int root_test_finish(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_t d, const T *d_log, size_t n,
                      int use_stop, T stop_value, hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index) {
-    QK_HIP_TRY(hipStreamSynchronize(s));
+    // count and stop into h_small[SMALL_NHITS], [SMALL_STOP]: the Horner
+    // form copied them; the direct form (the scan) has its slots, or on
+    // overflow the device counters are copied now
+    auto counts = [&]() -> int {
+        QK_HIP_TRY(hipStreamSynchronize(s));
+        if (!(n && plan.scan && ctx->knobs.rt_direct)) return QK_OK;
+        uint64_t *h = ctx->h_small;
+        if (h[SMALL_OVF]) {
+            QK_HIP_TRY(hipMemcpyAsync(h + SMALL_NHITS, ctx->d_small, 16, hipMemcpyDeviceToHost, s));
+            QK_HIP_TRY(hipStreamSynchronize(s));
+            return QK_OK;
+        }
+        uint64_t c = 0;
+        while (c < SMALL_HITPF_N && h[SMALL_HITPF + c] != ~0ull) ++c;
+        uint64_t st = ~0ull;
+        for (uint32_t k = 0; k < RT_NSTOP; ++k) st = std::min(st, h[SMALL_STOPS + k]);
+        h[SMALL_NHITS] = c;
+        h[SMALL_STOP] = st;
+        return QK_OK;
+    };
+    if (int rc = counts()) return rc;
     uint64_t cnt = ctx->h_small[SMALL_NHITS];
     if (cnt > ctx->hits_cap) {   // grow and rerun once (the kernel counts every hit)
         if (int rc = ensure_hits(ctx, (size_t)cnt, s)) return rc;
         if (int rc = root_test_begin<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
-        QK_HIP_TRY(hipStreamSynchronize(s));
+        if (int rc = counts()) return rc;
         cnt = ctx->h_small[SMALL_NHITS];
         if (cnt > ctx->hits_cap) return QK_E_HIP;
     }
@@ -439,6 +475,7 @@ int qk_ctx_create(int device, qk_ctx **out) {
         hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ctx->d_small, SMALL_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&ctx->h_small, SMALL_WORDS * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&ctx->h_small_dev, ctx->h_small, 0) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->stage_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->stage_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess ||
@@ -546,7 +583,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
         {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 0, 9},
         {"flow_prio", &qk_knobs::flow_prio, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
-        {"root_test", &qk_knobs::root_test, 0, 2},      {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
+        {"root_test", &qk_knobs::root_test, 0, 2},      {"rt_direct", &qk_knobs::rt_direct, 0, 1},      {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
     };
     for (const K &k : table)
         if (strcmp(k.name, name) == 0) {

@@ -36,6 +36,7 @@ struct qk_knobs {
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)
+    int rt_direct = 1;     // 0: the root-set scan's results by D2H copies instead of its host slots
     int comm_fault = 0;    // k > 0 (tests): this rank's payload staging for the k-th collective of its
                            // next sharded operation fails, once (comm.hip fault_now)
 };
@@ -54,6 +55,7 @@ struct qk_ctx {
     size_t scratch_bytes = 0;
     uint64_t *d_small = nullptr;       // partial output / hit counters (small, fixed)
     uint64_t *h_small = nullptr;       // pinned mirror of d_small
+    uint64_t *h_small_dev = nullptr;   // h_small as the device addresses it
     uint64_t *d_hits = nullptr;
     size_t hits_cap = 0;
 
@@ -99,12 +101,25 @@ struct qk_ctx {
 
 namespace qk {
 
-// Small-buffer layout (u64 words) inside ctx->d_small.
+// Small-buffer layout (u64 words).  Root tests: d_small[0] hit count, [1]
+// first stop, [3] stops recorded (root-set scan), [RT_C ..) the
+// coefficients or the root set — one H2D copy of h_small[0 .. RT_C + words)
+// sets all of it.  Results in h_small from SMALL_NHITS: count, stop, the
+// overflow flag of the direct form, then from SMALL_HITPF the first hits and
+// at the end RT_NSTOP stop slots.  Horner's arrive by D2H copies; the
+// root-set scan writes its hits and stops there itself (decode.hip
+// rt_record) and the host derives count and stop from the slots.
 constexpr size_t SMALL_WORDS = 4096;   // >= max partial words (2*1024+2) plus counters
-constexpr size_t SMALL_NHITS = 3072;   // hit counter
-constexpr size_t SMALL_STOP = 3073;    // first stop index
-constexpr size_t SMALL_HITPF = 3076;   // h_small only: the first hits, copied with the counters
-constexpr size_t SMALL_HITPF_N = SMALL_WORDS - SMALL_HITPF;
+constexpr size_t RT_C = 4;             // root tests: coefficients / root set from d_small[RT_C]
+constexpr size_t SMALL_NHITS = 3072;   // h_small: hit count
+constexpr size_t SMALL_STOP = 3073;    // h_small: first stop index
+constexpr size_t SMALL_OVF = 3074;     // h_small: a hit or stop slot past the direct form's room
+constexpr size_t SMALL_HITPF = 3076;   // h_small: the first hits
+constexpr uint32_t RT_NSTOP = 16;      // stop slots of the direct form
+constexpr size_t SMALL_STOPS = SMALL_WORDS - RT_NSTOP;
+constexpr size_t SMALL_HITPF_N = SMALL_STOPS - SMALL_HITPF;
+// the same slots relative to SMALL_NHITS (the kernel's hout)
+constexpr size_t RT_STOP0 = SMALL_STOPS - SMALL_NHITS;
 
 hipStream_t pick_stream(qk_ctx *ctx, void *stream);
 // order stream s after the previous user of the context's scratch buffers
@@ -157,7 +172,8 @@ struct RtScanSet {
 template <typename T> bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &out);
 template <typename T>
 int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
-                     T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, hipStream_t s);
+                     T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,
+                     hipStream_t s);
 
 // root test in two phases (api.hip): root_test_plan picks Horner or the
 // root-set scan for (d, n) and, for the scan, finds the roots on the host and

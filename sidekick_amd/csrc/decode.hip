@@ -25,13 +25,25 @@ namespace qk {
 
 constexpr int RT_BLOCK = 256;
 
+// hout (optional, k_root_scan): the hit / stop also into pinned host memory
 __device__ __forceinline__ void rt_record(uint64_t pos, bool hit, bool stop, uint64_t *hits, uint64_t cap,
-                                          uint64_t *counters) {
+                                          uint64_t *counters, uint64_t *hout = nullptr, uint32_t nhpf = 0) {
     if (hit) {
         const uint64_t slot = atomicAdd((unsigned long long *)&counters[0], 1ull);
         if (slot < cap) hits[slot] = pos;
+        if (hout) {
+            if (slot < nhpf) hout[4 + slot] = pos;
+            else hout[2] = 1;
+        }
     }
-    if (stop) atomicMin((unsigned long long *)&counters[1], (unsigned long long)pos);
+    if (stop) {
+        atomicMin((unsigned long long *)&counters[1], (unsigned long long)pos);
+        if (hout) {
+            const uint64_t k = atomicAdd((unsigned long long *)&counters[3], 1ull);
+            if (k < RT_NSTOP) hout[RT_STOP0 + k] = pos;
+            else hout[2] = 1;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ u32
@@ -187,7 +199,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_test_u64(const uint64_t *__re
 // p_(8a+b) * 2^(22j) mod p (u64), blocks a = 0 .. nblk - 1 (the last one the
 // top block when d % 8 != 0).
 constexpr uint32_t RT64_BSGS_MIND = 16;
-constexpr uint32_t RT64_BSGS_MAXD = 1000;   // (ceil((d+1)/8) * 24 words <= SMALL_NHITS)
+constexpr uint32_t RT64_BSGS_MAXD = 1000;   // (ceil((d+1)/8) * 24 words <= SMALL_NHITS - RT_C)
 
 __device__ __forceinline__ uint64_t rt_limb_sum(uint64_t lo, uint64_t hi, uint64_t c) {
     // lo + hi * 2^32 + c  (lo, hi < 2^59) reduced below 2^64 (not canonical)
@@ -402,12 +414,19 @@ __device__ __forceinline__ bool rs_member(T x, const T *__restrict__ set, uint32
     return hit;
 }
 
+// hout (pinned host memory, the context's h_small from SMALL_NHITS): every
+// recorded hit also goes straight to the host — hit slot k < nhpf to
+// hout[4 + k], a stop to one of the RT_NSTOP stop slots (device counter
+// counters[3]) — and a slot past either sets the overflow flag hout[2], so
+// the host reads the result after the kernel with no copy behind it (the
+// slots are pre-filled with ~0 by the host; a decode finds ~d hits).
 template <typename T, int S>
 __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ log, uint64_t n, uint32_t head,
                                                         const T *__restrict__ tab, uint32_t words, uint32_t m1,
                                                         uint32_t m2, uint32_t shift, int use_stop, T stop_value,
                                                         uint64_t *__restrict__ hits, uint64_t cap,
-                                                        uint64_t *__restrict__ counters) {
+                                                        uint64_t *__restrict__ counters, uint64_t *hout,
+                                                        uint32_t nhpf) {
     extern __shared__ __align__(16) unsigned char rs_lds[];
     T *set = reinterpret_cast<T *>(rs_lds);
     for (uint32_t i = threadIdx.x; i < words; i += RT_BLOCK) set[i] = tab[i];
@@ -436,8 +455,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ lo
         if (any) {
 #pragma unroll
             for (int j = 0; j < V; ++j) {
-                rt_record(h + (uint64_t)V * i + j, hit[0][j], st[0][j], hits, cap, counters);
-                rt_record(h + (uint64_t)V * (i + nthr) + j, hit[1][j], st[1][j], hits, cap, counters);
+                rt_record(h + (uint64_t)V * i + j, hit[0][j], st[0][j], hits, cap, counters, hout, nhpf);
+                rt_record(h + (uint64_t)V * (i + nthr) + j, hit[1][j], st[1][j], hits, cap, counters, hout, nhpf);
             }
         }
     }
@@ -448,18 +467,20 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ lo
         for (int j = 0; j < V; ++j) {
             const bool hit = rs_member<T, S>(e0[j], set, m1, m2, shift);
             const bool st = use_stop && e0[j] == stop_value;
-            if (hit | st) rt_record(h + (uint64_t)V * i + j, hit, st, hits, cap, counters);
+            if (hit | st) rt_record(h + (uint64_t)V * i + j, hit, st, hits, cap, counters, hout, nhpf);
         }
     }
     const uint64_t tail0 = h + body * V;
     if (gtid < h) {
         const T x = log[gtid];
-        rt_record(gtid, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters);
+        rt_record(gtid, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters,
+                  hout, nhpf);
     }
     if (gtid < n - tail0) {
         const uint64_t pos = tail0 + gtid;
         const T x = log[pos];
-        rt_record(pos, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters);
+        rt_record(pos, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters,
+                  hout, nhpf);
     }
 }
 
@@ -503,7 +524,8 @@ template bool rt_scan_table<uint64_t>(const uint64_t *, uint32_t, RtScanSet &, s
 
 template <typename T>
 int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
-                     T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, hipStream_t s) {
+                     T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,
+                     hipStream_t s) {
     const uintptr_t a = (uintptr_t)log;
     if (a & (sizeof(T) - 1)) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / sizeof(T));
@@ -513,7 +535,7 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
 #define QK_RS(SS)                                                                                             \
     hipLaunchKernelGGL((k_root_scan<T, SS>), dim3(rs_grid(ctx, k_root_scan<T, SS>, units, lds)), dim3(RT_BLOCK), \
                        lds, s, log, (uint64_t)n, head, d_tab, set.words, set.m1, set.m2, set.shift, use_stop,     \
-                       stop_value, hits, cap, counters)
+                       stop_value, hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N)
     if (set.S == 1) QK_RS(1);
     else QK_RS(4);
 #undef QK_RS
@@ -586,8 +608,8 @@ int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uin
 }
 
 template int launch_root_scan<uint32_t>(qk_ctx *, const uint32_t *, const RtScanSet &, const uint32_t *, size_t, int,
-                                        uint32_t, uint64_t *, uint64_t, uint64_t *, hipStream_t);
+                                        uint32_t, uint64_t *, uint64_t, uint64_t *, uint64_t *, hipStream_t);
 template int launch_root_scan<uint64_t>(qk_ctx *, const uint64_t *, const RtScanSet &, const uint64_t *, size_t, int,
-                                        uint64_t, uint64_t *, uint64_t, uint64_t *, hipStream_t);
+                                        uint64_t, uint64_t *, uint64_t, uint64_t *, uint64_t *, hipStream_t);
 
 } // namespace qk

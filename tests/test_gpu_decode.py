@@ -223,6 +223,37 @@ def test_many_hits_capacity_growth():
     assert got == want.tolist() and len(got) > 16000
 
 
+@pytest.mark.parametrize("nhit", [1003, 1004, 1005, 1100])
+def test_hit_and_stop_slot_boundaries(nhit):
+    """The root-set scan writes its hits and stops straight into pinned host
+    slots (1004 hit slots, 16 stop slots; a slot past either falls back to
+    the device counters): hit counts around the hit slots' end, and a stop
+    value occurring 40 times (its first occurrence must win), against the
+    oracle."""
+    rng = np.random.default_rng(nhit)
+    roots = [0x1234567, 0x7654321]
+    log = rng.integers(0, 1 << 32, size=200_000, dtype=np.uint64).astype(np.uint32)
+    log[np.isin(log, roots)] = 5
+    pos = np.sort(rng.choice(len(log), size=nhit, replace=False))
+    log[pos] = np.array(roots, dtype=np.uint32)[np.arange(nhit) % 2]
+    q = sk.PowerSumQuackU32(4)
+    for r in roots:
+        q.insert(r)
+    c = q.to_coeffs()
+    d = dev(log)
+    got = q.root_test(c, d)
+    assert got == pos.tolist()
+    stop_value = 0xABCDEF
+    log2 = log.copy()
+    log2[log2 == stop_value] = 6
+    spos = np.sort(rng.choice(np.setdiff1d(np.arange(len(log)), pos), size=40, replace=False))
+    log2[spos] = stop_value
+    want = qo.root_test_indices(list(c), log2.tolist(), qo.P32, stop_value=stop_value)
+    assert want == [p for p in pos.tolist() if p < spos[0]]
+    assert q.root_test(c, dev(log2), stop_value=stop_value) == want
+    assert q.root_test_shard(c, dev(log2), stop_value=stop_value) == (want, int(spos[0]))
+
+
 def test_undecodable_and_empty():
     q = sk.PowerSumQuackU32(4)
     assert q.decode_with_log(dev(np.arange(10, dtype=np.uint32))) == []

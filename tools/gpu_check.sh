@@ -31,6 +31,12 @@ for s in $STEPS; do
       for g in ${SG_LIST:-0 2 4 6 8}; do
         step sg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
       done ;;
+    configsab)  # the same configs with knob settings alternated: CONFIGS_AB="k=v1 k=v2", CONFIGS_ROUNDS rounds
+      for r in $(seq ${CONFIGS_ROUNDS:-2}); do
+        for kv in ${CONFIGS_AB}; do
+          step "configsab_${kv}_r$r" 600 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-decode} --knob $kv || exit 3
+        done
+      done ;;
     configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
     pktab)  # packet batch: fused extract+encode vs the two-pass path
       step pkt_fused 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 || exit 3
@@ -67,6 +73,9 @@ for s in $STEPS; do
         step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
         step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
       done ;;
+    proftrace)  # kernel + memory-copy + HIP runtime trace (no counters) of one command, for the gaps between them
+      export TMPDIR=/tmp
+      step proftrace 600 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --stats --output-format csv -d "$OUT/proftrace" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFTRACE_ARGS:-decode --rt-modes 2} --steps 10 || exit 3 ;;
     profcfg)  # kernel stats for the secondary configs' kernels (u64 encode, u32/u64 root test)
       export TMPDIR=/tmp
       step profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profcfg" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFCFG_ARGS:-u64 decode decode64} --steps 10 || exit 3 ;;
