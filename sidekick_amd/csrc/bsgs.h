@@ -239,8 +239,10 @@ __device__ __forceinline__ void row2m(uint64_t &a0, uint64_t &a1, uint32_t b0, u
 template <int NB_, int NA_, int SG_, int ROW0_ = 1, int FOLD_ = 1, bool PAIR_ = false, bool OFF_ = false,
           int XC_ = 0, bool TREE_ = false, int PRIO_ = 0>
 struct Cfg {
-    // PRIO  s_setprio around the MAC phase: 1 raises the priority of a wave
-    //       in its MACs (their scalar wrap counts), 2 of a wave in its modmuls
+    // PRIO  wave priority (s_setprio) over the accumulation: 4 (the product)
+    //       row 0 at 1 and the MAC rows with their scalar wrap counts at 2,
+    //       the powers at 0; (measurements) 1 the whole accumulation at 1,
+    //       2 the powers raised instead, 3 the MAC rows only, 5 / 6 other levels
     static constexpr int PRIO = PRIO_;
     static constexpr int NB = NB_, NA = NA_, SG = SG_, ROW0 = ROW0_, FOLD = FOLD_, XC = XC_;
     static constexpr bool TREE = TREE_;
@@ -386,8 +388,16 @@ __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA, C::ROWS> &S, const 
         if constexpr (C::ROW0 == 1) row2m(S.r0[NB - 2], S.r0[NB - 1], B[NB - 2], B[NB - 1]);
         else add2v(S.lo0[NB - 2], S.lo0[NB - 1], S.c0[NB - 2], S.c0[NB - 1], B[NB - 2], B[NB - 1]);
     }
+    if constexpr (C::PRIO == 3) __builtin_amdgcn_s_setprio(1);   // (measurements: the MAC rows only)
+    if constexpr (C::PRIO == 4) __builtin_amdgcn_s_setprio(2);   // row 0 at 1, the MAC rows at 2
+    if constexpr (C::PRIO == 6) __builtin_amdgcn_s_setprio(2);   // (measurements: row 0 at 3, the rows at 2)
 #pragma unroll
     for (int a = 0; a < C::ROWS; ++a) {
+        // (measurements) 5: row 0 at 1, MAC row a at min(3, 2 + a)
+        if constexpr (C::PRIO == 5) {
+            if (a == 0) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(3);
+        }
 #pragma unroll
         for (int b = 0; b + 4 <= NB; b += 4) {
             const int g = (a + C::ROW1) * (NB / 4) + b / 4;   // group index: parity picks the SGPR set
@@ -412,6 +422,18 @@ __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA, C::ROWS> &S, const 
     }
 }
 
+// wave priority around an id's accumulation (Cfg PRIO; accumulate raises it
+// further before the MAC rows for PRIO 3-6)
+template <class C> __device__ __forceinline__ void prio_enter() {
+    if constexpr (C::PRIO == 1 || C::PRIO == 4 || C::PRIO == 5) __builtin_amdgcn_s_setprio(1);
+    if constexpr (C::PRIO == 6) __builtin_amdgcn_s_setprio(3);
+    if constexpr (C::PRIO == 2) __builtin_amdgcn_s_setprio(0);
+}
+template <class C> __device__ __forceinline__ void prio_exit() {
+    if constexpr (C::PRIO == 1 || C::PRIO >= 3) __builtin_amdgcn_s_setprio(0);
+    if constexpr (C::PRIO == 2) __builtin_amdgcn_s_setprio(1);
+}
+
 // xb / xnext: an offset pass's cached x^base and the next pass's (Cfg XC)
 template <class C>
 __device__ __forceinline__ void one(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id, uint32_t base = 0, uint32_t xb = 0,
@@ -421,11 +443,9 @@ __device__ __forceinline__ void one(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id, 
     if (__builtin_expect(__any(w), 0)) {
         if (w) powers_exact<C>(B, A, base, xb, xnext);
     }
-    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(1);
-    if constexpr (C::PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    prio_enter<C>();
     accumulate<C>(S, B, A);
-    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(0);
-    if constexpr (C::PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    prio_exit<C>();
 }
 
 // two ids at once: their power chains are independent straight-line code, so
@@ -440,10 +460,10 @@ __device__ __forceinline__ void two(Acc<C::NB, C::NA, C::ROWS> &S, uint32_t id0,
         if (w0) powers_exact<C>(B0, A0);
         if (w1) powers_exact<C>(B1, A1);
     }
-    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    prio_enter<C>();
     accumulate<C>(S, B0, A0);
     accumulate<C>(S, B1, A1);
-    if constexpr (C::PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    prio_exit<C>();
 }
 
 template <class C>

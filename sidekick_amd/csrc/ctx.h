@@ -14,7 +14,7 @@ struct qk_knobs {
     int bsgs_sg = -1;      // u32 BSGS: scalar-counted wrap groups (-1: the per-shape default)
     int u32_passes = 1;    // 0: u32 t > 80 on the power chain instead of BSGS passes
     int bsgs_shapes = 1;   // 0: the round-2 u32 BSGS shapes (t 17..36, 41..42, 65..72)
-    int bsgs_prio = 1;     // 0: u32 BSGS t <= 80 without s_setprio around the MAC phase (bsgs.h Cfg PRIO)
+    int bsgs_prio = 1;     // 0: u32 BSGS without wave priority over the accumulation (bsgs.h Cfg PRIO 4)
     int u32_xcache = 1;    // 0: u32 offset passes raise x^8 to base/8 themselves (no per-id x^base cache)
     int bsgs64_sg = -1;    // u64 BSGS MAC mode override (-1: default)
     int bsgs64_off = 0;    // 1: u64 on the power chain instead of BSGS

@@ -100,14 +100,17 @@ __device__ __forceinline__ void chain32x4(uint64_t (&acc)[K], uint4 w) {
 // ---- baby-step / giant-step encode for 9 <= t <= 32 (bsgs.h)
 // waves per SIMD the register budget is sized for (tools/tune_bsgs.hip: 5 for
 // (8,4) beat 4 by 2-3 %; its three spilled VGPRs live outside the loop)
-// PRIO: s_setprio around each id's MAC phase (bsgs.h; knob bsgs_prio)
+// PRIO (knob bsgs_prio): wave priority over each id's accumulation — row 0
+// at 1, the MAC rows at 2, the powers at 0 (bsgs.h Cfg PRIO 4; t = 32: 2.60 /
+// 2.67 vs 2.66 / 2.73 ms for the MAC phase at 1, vs 2.77 ms for none,
+// profiles/r04/prio/tune_bsgs_prio_levels*.json)
 template <int NB, int NA, int SG, int PRIO = 1>
 __global__ __launch_bounds__(BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB * NA > 40 ? 3 : 4)) void k_encode_u32_bsgs(const uint32_t *__restrict__ ids,
                                                                                   uint64_t n, uint32_t head,
                                                                                   uint32_t T,
                                                                                   uint64_t *__restrict__ partials) {
-    bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD, false, false, 0, false, PRIO>>(ids, n, head, T,
-                                                                                                partials);
+    bsgs::body<bsgs::Cfg<NB, NA, SG, QK_BSGS_ROW0, QK_BSGS_FOLD, false, false, 0, false, PRIO ? 4 : 0>>(ids, n, head,
+                                                                                                        T, partials);
 }
 
 
@@ -120,7 +123,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_encode_u32_bsgs_x80(const uint32_t
                                                                  const uint32_t *xin,
                                                                  uint32_t *xout) {
     (void)xin;
-    bsgs::body<bsgs::Cfg<8, 10, SG, 1, 1, false, false, 2, false, PRIO>>(ids, n, head, T, partials, 0, nullptr, xout);
+    bsgs::body<bsgs::Cfg<8, 10, SG, 1, 1, false, false, 2, false, PRIO ? 4 : 0>>(ids, n, head, T, partials, 0, nullptr,
+                                                                                 xout);
 }
 
 // Offset pass for thresholds > 80 (several passes over the ids): powers
@@ -131,7 +135,8 @@ template <int NA, int SG, int XC = 0, int PRIO = 1>
 __global__ __launch_bounds__(BLOCK, (NA > 6 ? 2 : NA > 5 ? 3 : 4)) void k_encode_u32_bsgs_off(
     const uint32_t *__restrict__ ids, uint64_t n, uint32_t head, uint32_t T, uint32_t base,
     uint64_t *__restrict__ partials, const uint32_t *xin, uint32_t *xout) {
-    bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true, XC, false, PRIO>>(ids, n, head, T, partials, base, xin, xout);
+    bsgs::body<bsgs::Cfg<8, NA, SG, 1, 1, false, true, XC, false, PRIO ? 4 : 0>>(ids, n, head, T, partials, base, xin,
+                                                                                 xout);
 }
 
 // lane j of a G-group: start = x^(j+1), step = x^G (square-and-multiply).

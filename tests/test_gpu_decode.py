@@ -24,15 +24,19 @@ def QT(bits):
     return sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
 
 
-@pytest.fixture(autouse=True, params=["horner", "scan"])
+@pytest.fixture(autouse=True, params=["horner", "scan", "scan_copies"])
 def root_test_mode(request):
-    """Every test of this module runs twice: the root test by Horner per
-    candidate (k_root_test_*) and by host root finding + the root-set scan
-    (roots.cpp, k_root_scan; forced for 2 <= d <= 256): the same hit lists."""
+    """Every test of this module runs three times: the root test by Horner
+    per candidate (k_root_test_*), by host root finding + the root-set scan
+    (roots.cpp, k_root_scan; forced for 2 <= d <= 256) handing its results
+    over through pinned host slots (the default), and the same scan with its
+    results copied back (knob rt_direct = 0): the same hit lists."""
     ctx = sk.get_context(0)
     ctx.set_knob("root_test", 1 if request.param == "horner" else 2)
+    ctx.set_knob("rt_direct", 0 if request.param == "scan_copies" else 1)
     yield request.param
     ctx.set_knob("root_test", 0)
+    ctx.set_knob("rt_direct", 1)
 
 
 def _poly_mul(a, b, p):

@@ -238,13 +238,19 @@ int main(int argc, char **argv) {
     // 2.68; with priority (profiles/r04/prio/tune_bsgs_prio_sweep.json): 4
     // waves/SIMD 2.73 vs 2.63-2.66, 7 / 6 scalar-counted groups 3.42 / 4.05,
     // product-tree babies 2.57; again (tune_bsgs_prio_tree.json) tree 2.559 /
-    // 2.569 vs product 2.559 / 2.587: even, not adopted.  This set: two ids'
-    // powers interleaved (PAIR) under priority
+    // 2.569 vs product 2.559 / 2.587: even, not adopted; two ids interleaved
+    // (PAIR) under priority 2.72 (w4) vs 2.64-2.71 (tune_bsgs_prio_pair.json).
+    // The priority window without row 0 2.67 / 2.67, row 0 at 1 and the MAC
+    // rows at 2 2.652 / 2.654 vs 2.720 / 2.733 (tune_bsgs_prio_levels.json).
+    // This set: more level schemes
     std::vector<Var> vars = {{"prio_mac_w5 (product)", k_prio<1>},
-                             {"prio_pair_w4", k_prio<1, 8, 4, false, true>},
-                             {"prio_pair_w3", k_prio<1, 8, 3, false, true>},
-                             {"pair_w4 (no priority)", k_prio<0, 8, 4, false, true>},
-                             {"prio_mac_w5_again", k_prio<1>}};
+                             {"prio_row0_1_macrows_2_w5", k_prio<4>},
+                             {"prio_row0_1_rows_2_3_3_w5", k_prio<5>},
+                             {"prio_row0_3_macrows_2_w5", k_prio<6>},
+                             {"prio_row0_1_macrows_2_w4", k_prio<4, 8, 4>},
+                             {"prio_mac_w5_again", k_prio<1>},
+                             {"prio_row0_1_macrows_2_w5_again", k_prio<4>},
+                             {"prio_row0_1_rows_2_3_3_w5_again", k_prio<5>}};
     uint32_t ref[T], got[T];
     std::vector<std::vector<float>> times(vars.size());
     std::vector<double> mhz(vars.size(), 0.0);
