@@ -311,7 +311,8 @@ struct Smem<NG, true, NBB> {
 //           t <= 40 waste fewer powers in 4-wide rows, and the babies and
 //           giants of an id cost 3 + NA - 2 products instead of 7 + NA - 2)
 //   PRIO    s_setprio 1 for a wave in its MAC step (1), or in its babies /
-//           giants step (2); 0: no priority changes
+//           giants step (2); 3: the row-0 sums at 1 and the MACs at 2 (per
+//           64-id chunk); 0: no priority changes
 template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0,
           int XC = 0, int NBT = NB, int PRIO = 0>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
@@ -401,7 +402,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
         }
         if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
-        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+        if constexpr (PRIO == 1 || PRIO == 3) __builtin_amdgcn_s_setprio(1);
         // next tile's id in flight during step 3
         const uint64_t tn = tile + gridDim.x;
         nxt = 0;
@@ -456,6 +457,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
             }
             if constexpr (!OFF && CW == 2) row2<1>(r0lo, r0hi, bv);
             if constexpr (!OFF && CW == 1) row1(r0lo[0], r0hi[0], bv[0]);
+            if constexpr (PRIO == 3) __builtin_amdgcn_s_setprio(2);   // the MACs above the row-0 sums
             // LD: one giant row's operands in flight while the previous row's
             // MACs run (2 rows live instead of NR: fewer VGPRs)
             uint2 gn;
@@ -497,7 +499,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
                 }
             }
         }
-        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+        if constexpr (PRIO == 1 || PRIO == 3) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
     }
 

@@ -559,15 +559,16 @@ __global__ __launch_bounds__(BLOCK) void k_finalize_u64(const uint64_t *__restri
 // is read from baby 8: 32 KB of LDS per workgroup at t = 80, 4 per CU
 // (tools/tune_u64.hip: 24.1 vs 25.6 ms per 1e9 ids with 50 KB at 3 per CU).
 // The first SG MACs of a wave's tile count their carries on the scalar unit.
-// F (knob bsgs64_prio): 1 — s_setprio in the MAC step and, with two babies
-// per wave, the two MACs of a giant row issued as one interleaved block
-// (MODE 3); 0 — the round-3 form (MODE 0, no priority changes)
+// F (knob bsgs64_prio): 1 — wave priority in the MAC step (the row-0 sums
+// at 1, the MACs at 2: bsgs64.h PRIO 3, ~1 % over one level) and, with two
+// babies per wave, the two MACs of a giant row issued as one interleaved
+// block (MODE 3); 0 — the round-3 form (MODE 0, no priority changes)
 template <int NA, int SG, int F = 1>
 __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs(const uint64_t *__restrict__ ids, uint64_t n,
                                                                       uint32_t head, uint32_t T,
                                                                       uint64_t *__restrict__ partials) {
     (void)head;
-    bsgs64::body<NA, F ? 3 : 0, SG, 0, 0, false, true, 1, 0, bsgs64::NB, F>(ids, n, T, partials);
+    bsgs64::body<NA, F ? 3 : 0, SG, 0, 0, false, true, 1, 0, bsgs64::NB, F ? 3 : 0>(ids, n, T, partials);
 }
 
 // the same with four babies per id (one per wave) and NA giant rows of 4
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs4(const uin
                                                                        uint32_t head, uint32_t T,
                                                                        uint64_t *__restrict__ partials) {
     (void)head;
-    bsgs64::body<NA, 0, 16, 0, 0, false, true, 1, 0, 4, F>(ids, n, T, partials);
+    bsgs64::body<NA, 0, 16, 0, 0, false, true, 1, 0, 4, F ? 3 : 0>(ids, n, T, partials);
 }
 
 // Pass 0 of a u64 multi-pass encode that also writes x^80 per id for pass 1
@@ -587,7 +588,8 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_x80(const 
                                                                           uint64_t *__restrict__ partials,
                                                                           uint64_t *xout) {
     (void)head;
-    bsgs64::body<10, F ? 3 : 0, 16, 0, 0, false, true, 1, 2, bsgs64::NB, F>(ids, n, T, partials, 0, nullptr, xout);
+    bsgs64::body<10, F ? 3 : 0, 16, 0, 0, false, true, 1, 2, bsgs64::NB, F ? 3 : 0>(ids, n, T, partials, 0, nullptr,
+                                                                                 xout);
 }
 
 // Offset pass for u64 thresholds > 80: powers base+1 .. base+8NA with giants
@@ -601,7 +603,8 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_off(const 
                                                                           const uint64_t *xin,
                                                                           uint64_t *xout) {
     (void)head;
-    bsgs64::body<NA, F ? 3 : 0, 16, 0, 0, true, true, 1, XC, bsgs64::NB, F>(ids, n, T, partials, base, xin, xout);
+    bsgs64::body<NA, F ? 3 : 0, 16, 0, 0, true, true, 1, XC, bsgs64::NB, F ? 3 : 0>(ids, n, T, partials, base, xin,
+                                                                                     xout);
 }
 
 // ------------------------------------------------------------- dispatch

@@ -59,15 +59,11 @@ int main() {
     // (the round-3/4 layout and carry-mode variants are in the git history and
     // profiles/r03/tune_u64*.json, profiles/r04/u64/)
     std::vector<Var> vars = {
-        {"product: mode0 sg16, B*2^32 recomputed, occ4, row-ahead giants", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
-        {"mode0 sg16 + s_setprio in the MAC step", k_var<10, 0, 16, 0, 4, 0, true, 1, 1>, 4},
-        {"mode3 sg16 + s_setprio in the MAC step", k_var<10, 3, 16, 0, 4, 0, true, 1, 1>, 4},
-        {"mode3 sg14 + s_setprio in the MAC step", k_var<10, 3, 14, 0, 4, 0, true, 1, 1>, 4},
-        {"mode3 sg18 + s_setprio in the MAC step", k_var<10, 3, 18, 0, 4, 0, true, 1, 1>, 4},
-        {"mode3 sg16 + s_setprio, all giant rows at once", k_var<10, 3, 16, 0, 4, 0, true, 0, 1>, 4},
-        {"mode3 sg16, no s_setprio", k_var<10, 3, 16, 0, 4, 0, true, 1>, 4},
-        {"mode3 sg16 + s_setprio in the MAC step (again)", k_var<10, 3, 16, 0, 4, 0, true, 1, 1>, 4},
-        {"product again", k_var<10, 0, 16, 0, 4, 0, true, 1>, 4},
+        {"product: mode3 sg14 + s_setprio in the MAC step", k_var<10, 3, 14, 0, 4, 0, true, 1, 1>, 4},
+        {"mode3 sg14, row-0 sums at 1 and the MACs at 2", k_var<10, 3, 14, 0, 4, 0, true, 1, 3>, 4},
+        {"mode3 sg16, row-0 sums at 1 and the MACs at 2", k_var<10, 3, 16, 0, 4, 0, true, 1, 3>, 4},
+        {"product again", k_var<10, 3, 14, 0, 4, 0, true, 1, 1>, 4},
+        {"mode3 sg14, row-0 sums at 1 and the MACs at 2 (again)", k_var<10, 3, 14, 0, 4, 0, true, 1, 3>, 4},
     };
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
