@@ -36,6 +36,8 @@ struct qk_knobs {
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)
+    int rt_scan_u = 1;     // root-set scan: 16-byte loads per lane per iteration (1, 2, 4; 3 runs as 2; 1: u32
+                           // kernel 70 vs 84 / 78 us at 2 / 4, profiles/r04/decode_scan_u/)
     int rt_direct = 1;     // 0: the root-set scan's results by D2H copies instead of its host slots
     int comm_fault = 0;    // k > 0 (tests): this rank's payload staging for the k-th collective of its
                            // next sharded operation fails, once (comm.hip fault_now)

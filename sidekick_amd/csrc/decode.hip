@@ -420,7 +420,9 @@ __device__ __forceinline__ bool rs_member(T x, const T *__restrict__ set, uint32
 // counters[3]) — and a slot past either sets the overflow flag hout[2], so
 // the host reads the result after the kernel with no copy behind it (the
 // slots are pre-filled with ~0 by the host; a decode finds ~d hits).
-template <typename T, int S>
+// U: 16-byte loads per lane per iteration (knob rt_scan_u; 1 is the fastest
+// measured)
+template <typename T, int S, int U = 1>
 __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ log, uint64_t n, uint32_t head,
                                                         const T *__restrict__ tab, uint32_t words, uint32_t m1,
                                                         uint32_t m2, uint32_t shift, int use_stop, T stop_value,
@@ -438,29 +440,33 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ lo
     const uint64_t h = head < n ? head : n;
     const uint64_t body = (n - h) / V;
     const Vec *__restrict__ v = reinterpret_cast<const Vec *>(log + h);
-    // two loads in flight per lane
+    // U loads in flight per lane
     uint64_t i = gtid;
-    for (; i + nthr < body; i += 2 * nthr) {
-        const Vec w0 = v[i], w1 = v[i + nthr];
-        const T *e0 = reinterpret_cast<const T *>(&w0), *e1 = reinterpret_cast<const T *>(&w1);
-        bool any = false, hit[2][V], st[2][V];
+    for (; i + (U - 1) * nthr < body; i += U * nthr) {
+        Vec w[U];
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            hit[0][j] = rs_member<T, S>(e0[j], set, m1, m2, shift);
-            hit[1][j] = rs_member<T, S>(e1[j], set, m1, m2, shift);
-            st[0][j] = use_stop && e0[j] == stop_value;
-            st[1][j] = use_stop && e1[j] == stop_value;
-            any |= hit[0][j] | hit[1][j] | st[0][j] | st[1][j];
+        for (int u = 0; u < U; ++u) w[u] = v[i + u * nthr];
+        bool any = false, hit[U][V], st[U][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const T *e = reinterpret_cast<const T *>(&w[u]);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                hit[u][j] = rs_member<T, S>(e[j], set, m1, m2, shift);
+                st[u][j] = use_stop && e[j] == stop_value;
+                any |= hit[u][j] | st[u][j];
+            }
         }
         if (any) {
 #pragma unroll
-            for (int j = 0; j < V; ++j) {
-                rt_record(h + (uint64_t)V * i + j, hit[0][j], st[0][j], hits, cap, counters, hout, nhpf);
-                rt_record(h + (uint64_t)V * (i + nthr) + j, hit[1][j], st[1][j], hits, cap, counters, hout, nhpf);
-            }
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < V; ++j)
+                    rt_record(h + (uint64_t)V * (i + u * nthr) + j, hit[u][j], st[u][j], hits, cap, counters, hout,
+                              nhpf);
         }
     }
-    if (i < body) {
+    for (; i < body; i += nthr) {   // the last < U loads of this lane
         const Vec w0 = v[i];
         const T *e0 = reinterpret_cast<const T *>(&w0);
 #pragma unroll
@@ -530,14 +536,20 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
     if (a & (sizeof(T) - 1)) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / sizeof(T));
     const size_t lds = (size_t)set.words * sizeof(T);
-    const uint64_t units = (n + 2 * (16 / sizeof(T)) - 1) / (2 * (16 / sizeof(T)));
+    const int U = ctx->knobs.rt_scan_u;
+    const uint64_t units = (n + U * (16 / sizeof(T)) - 1) / (U * (16 / sizeof(T)));
     hipEvent_t e0 = prof_begin(ctx, s);
-#define QK_RS(SS)                                                                                             \
-    hipLaunchKernelGGL((k_root_scan<T, SS>), dim3(rs_grid(ctx, k_root_scan<T, SS>, units, lds)), dim3(RT_BLOCK), \
-                       lds, s, log, (uint64_t)n, head, d_tab, set.words, set.m1, set.m2, set.shift, use_stop,     \
-                       stop_value, hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N)
-    if (set.S == 1) QK_RS(1);
-    else QK_RS(4);
+#define QK_RS(SS, UU)                                                                                         \
+    hipLaunchKernelGGL((k_root_scan<T, SS, UU>), dim3(rs_grid(ctx, k_root_scan<T, SS, UU>, units, lds)),         \
+                       dim3(RT_BLOCK), lds, s, log, (uint64_t)n, head, d_tab, set.words, set.m1, set.m2, set.shift, \
+                       use_stop, stop_value, hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N)
+    if (set.S == 1) {
+        if (U == 4) QK_RS(1, 4);
+        else if (U == 1) QK_RS(1, 1);
+        else QK_RS(1, 2);
+    } else {
+        QK_RS(4, 1);
+    }
 #undef QK_RS
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());

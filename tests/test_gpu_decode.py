@@ -258,6 +258,28 @@ def test_hit_and_stop_slot_boundaries(nhit):
     assert q.root_test_shard(c, dev(log2), stop_value=stop_value) == (want, int(spos[0]))
 
 
+@pytest.mark.parametrize("u", [2, 4])
+def test_scan_loads_per_iteration(u, root_test_mode):
+    """The root-set scan with 2 / 4 loads per lane per iteration (knob
+    rt_scan_u, measurements; the product takes 1): ragged length, a
+    misaligned start, both widths, against the oracle."""
+    import sidekick_amd as skm
+    ctx = skm.get_context(0)
+    ctx.set_knob("rt_scan_u", u)
+    try:
+        for bits in (32, 64):
+            log = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(90 + u + bits, 100_007)
+            q = QT(bits)(16)
+            for i in (0, 1, 777, 23_456, 100_006):
+                q.insert(int(log[i]))
+            c = q.to_coeffs()
+            d = dev(log, bits)[1:]
+            want = qo.root_test_indices(list(c), log[1:].tolist(), qo.P32 if bits == 32 else qo.P64)
+            assert q.root_test(c, d) == want
+    finally:
+        ctx.set_knob("rt_scan_u", 1)
+
+
 def test_undecodable_and_empty():
     q = sk.PowerSumQuackU32(4)
     assert q.decode_with_log(dev(np.arange(10, dtype=np.uint32))) == []
