@@ -33,6 +33,7 @@ struct qk_knobs {
                            // staging (direct scatter); 0: hipCUB's onesweep
     int flow_prio = 0;     // 1: per-flow encode kernels with s_setprio around the MACs (1e6 flows: 7.57 vs
                            // 6.80 ms, 16 / 1e4 flows even; profiles/r04/prio/ab_flows_prio.jsonl)
+    int pkt_wgpc = 4;      // packet batches: workgroups per CU
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)

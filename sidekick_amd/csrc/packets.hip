@@ -186,9 +186,11 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     QK_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = pick_stream(ctx, stream);
 
-    // chunking: >= 4 tiles per workgroup, enough workgroups to cover the chip
+    // chunking: >= 4 tiles per workgroup, pkt_wgpc workgroups per CU (each
+    // keeps one staged tile of loads in flight)
     const uint64_t tiles = (n + PK_BLOCK - 1) / PK_BLOCK;
-    uint64_t tiles_per_chunk = std::max<uint64_t>(4, (tiles + (uint64_t)ctx->num_cus * 4 - 1) / ((uint64_t)ctx->num_cus * 4));
+    const uint64_t wgs = (uint64_t)ctx->num_cus * (uint64_t)ctx->knobs.pkt_wgpc;
+    uint64_t tiles_per_chunk = std::max<uint64_t>(4, (tiles + wgs - 1) / wgs);
     const uint64_t chunk = tiles_per_chunk * PK_BLOCK;
     const uint32_t nchunks = (uint32_t)((n + chunk - 1) / chunk);
 
