@@ -361,33 +361,36 @@ template <class C>
 __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA, C::ROWS> &S, const uint32_t (&B)[C::NB],
                                            const uint32_t (&A)[C::ROWS]) {
     constexpr int NB = C::NB;
-#pragma unroll
-    for (int b = 0; b + 4 <= NB; b += 4) {
-        if constexpr (C::OFF) break;   // no sum row in an offset pass
-        const bool s0 = (b / 4) % 2 == 0;
-        if constexpr (C::ROW0 == 1) {
-            if (s0) row4m<0>(S.r0[b], S.r0[b + 1], S.r0[b + 2], S.r0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
-            else row4m<1>(S.r0[b], S.r0[b + 1], S.r0[b + 2], S.r0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
-        } else if (scalar_group<C>(0, b)) {
-            if (s0)
-                add4s<0>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
-                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
-            else
-                add4s<1>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
-                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
-        } else {
-            if (s0)
-                add4v<0>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
-                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
-            else
-                add4v<1>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
-                         S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+    auto row0 = [&]() {
+    #pragma unroll
+        for (int b = 0; b + 4 <= NB; b += 4) {
+            if constexpr (C::OFF) break;   // no sum row in an offset pass
+            const bool s0 = (b / 4) % 2 == 0;
+            if constexpr (C::ROW0 == 1) {
+                if (s0) row4m<0>(S.r0[b], S.r0[b + 1], S.r0[b + 2], S.r0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+                else row4m<1>(S.r0[b], S.r0[b + 1], S.r0[b + 2], S.r0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            } else if (scalar_group<C>(0, b)) {
+                if (s0)
+                    add4s<0>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                             S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+                else
+                    add4s<1>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                             S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            } else {
+                if (s0)
+                    add4v<0>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                             S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+                else
+                    add4v<1>(S.lo0[b], S.lo0[b + 1], S.lo0[b + 2], S.lo0[b + 3], S.c0[b], S.c0[b + 1], S.c0[b + 2],
+                             S.c0[b + 3], B[b], B[b + 1], B[b + 2], B[b + 3]);
+            }
         }
-    }
-    if constexpr (NB % 4 == 2 && !C::OFF) {
-        if constexpr (C::ROW0 == 1) row2m(S.r0[NB - 2], S.r0[NB - 1], B[NB - 2], B[NB - 1]);
-        else add2v(S.lo0[NB - 2], S.lo0[NB - 1], S.c0[NB - 2], S.c0[NB - 1], B[NB - 2], B[NB - 1]);
-    }
+        if constexpr (NB % 4 == 2 && !C::OFF) {
+            if constexpr (C::ROW0 == 1) row2m(S.r0[NB - 2], S.r0[NB - 1], B[NB - 2], B[NB - 1]);
+            else add2v(S.lo0[NB - 2], S.lo0[NB - 1], S.c0[NB - 2], S.c0[NB - 1], B[NB - 2], B[NB - 1]);
+        }
+    };
+    if constexpr (C::PRIO != 7) row0();
     if constexpr (C::PRIO == 3) __builtin_amdgcn_s_setprio(1);   // (measurements: the MAC rows only)
     if constexpr (C::PRIO == 4) __builtin_amdgcn_s_setprio(2);   // row 0 at 1, the MAC rows at 2
     if constexpr (C::PRIO == 6) __builtin_amdgcn_s_setprio(2);   // (measurements: row 0 at 3, the rows at 2)
@@ -420,6 +423,10 @@ __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA, C::ROWS> &S, const 
         if constexpr (NB % 4 == 2)
             mac2v(S.m[a][NB - 2], S.m[a][NB - 1], S.c[a][NB - 2], S.c[a][NB - 1], A[a], B[NB - 2], B[NB - 1]);
     }
+    if constexpr (C::PRIO == 7) {   // (measurements: the MAC rows first at 2, then row 0 at 1)
+        __builtin_amdgcn_s_setprio(1);
+        row0();
+    }
 }
 
 // wave priority around an id's accumulation (Cfg PRIO; accumulate raises it
@@ -427,6 +434,7 @@ __device__ __forceinline__ void accumulate(Acc<C::NB, C::NA, C::ROWS> &S, const 
 template <class C> __device__ __forceinline__ void prio_enter() {
     if constexpr (C::PRIO == 1 || C::PRIO == 4 || C::PRIO == 5) __builtin_amdgcn_s_setprio(1);
     if constexpr (C::PRIO == 6) __builtin_amdgcn_s_setprio(3);
+    if constexpr (C::PRIO == 7) __builtin_amdgcn_s_setprio(2);
     if constexpr (C::PRIO == 2) __builtin_amdgcn_s_setprio(0);
 }
 template <class C> __device__ __forceinline__ void prio_exit() {

@@ -149,3 +149,28 @@ def test_gpu_packets_fused_thresholds(golden, t):
         assert st["filtered"] == n - len(ids) - st["discarded"] - st["resets"]
         if len(ids):
             assert q.last_value() == int(ids[-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wgpc", [1, 12])
+def test_gpu_packets_workgroups_per_cu(wgpc):
+    """The chunking by knob pkt_wgpc (measurements; 4 is the product's):
+    fewer or more chunks give the same sums, counts and reset bookkeeping,
+    fused (t = 12) and two-pass (t = 32), with resets."""
+    import torch
+    import sidekick_amd as sk
+    from sidekick_amd.quack import encode_packets
+    ctx = sk.get_context(0)
+    ctx.set_knob("pkt_wgpc", wgpc)
+    try:
+        for t, resets in ((12, ()), (32, (77_777,)), (32, ())):
+            n = 300_007
+            bufs, meta = make_batch(n, seed=wgpc * 100 + t, reset_at=resets, p_filter=0.05)
+            q = sk.PowerSumQuackU32(t)
+            st = encode_packets(q, torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
+                                meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_ipv4=MY_IP)
+            ids, last = vector_sniff(bufs, meta)
+            assert q.power_sums() == coracle.encode_u32(ids, t), (wgpc, t, resets)
+            assert st["inserted"] == len(ids) and st["last_reset_index"] == last
+    finally:
+        ctx.set_knob("pkt_wgpc", 4)

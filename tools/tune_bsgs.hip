@@ -242,15 +242,14 @@ int main(int argc, char **argv) {
     // (PAIR) under priority 2.72 (w4) vs 2.64-2.71 (tune_bsgs_prio_pair.json).
     // The priority window without row 0 2.67 / 2.67, row 0 at 1 and the MAC
     // rows at 2 2.652 / 2.654 vs 2.720 / 2.733 (tune_bsgs_prio_levels.json).
-    // This set: more level schemes
-    std::vector<Var> vars = {{"prio_mac_w5 (product)", k_prio<1>},
-                             {"prio_row0_1_macrows_2_w5", k_prio<4>},
-                             {"prio_row0_1_rows_2_3_3_w5", k_prio<5>},
-                             {"prio_row0_3_macrows_2_w5", k_prio<6>},
-                             {"prio_row0_1_macrows_2_w4", k_prio<4, 8, 4>},
-                             {"prio_mac_w5_again", k_prio<1>},
+    // More schemes (tune_bsgs_prio_levels2.json): rows rising 2 -> 3 2.68,
+    // row 0 above the rows 2.70, 4 waves 2.75.  This set: row 0 after the MAC
+    // rows
+    std::vector<Var> vars = {{"prio_row0_1_macrows_2_w5 (product)", k_prio<4>},
+                             {"prio_macrows_2_then_row0_1_w5", k_prio<7>},
+                             {"prio_mac_w5 (one level)", k_prio<1>},
                              {"prio_row0_1_macrows_2_w5_again", k_prio<4>},
-                             {"prio_row0_1_rows_2_3_3_w5_again", k_prio<5>}};
+                             {"prio_macrows_2_then_row0_1_w5_again", k_prio<7>}};
     uint32_t ref[T], got[T];
     std::vector<std::vector<float>> times(vars.size());
     std::vector<double> mhz(vars.size(), 0.0);
