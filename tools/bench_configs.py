@@ -355,13 +355,17 @@ def main():
     ap.add_argument("--cpu-sample64", type=float, default=5e6)
     ap.add_argument("--cpu-sample-dec", type=float, default=2e7)
     ap.add_argument("--rt-modes", default="1,2", help="decode: root-test modes to time (0 auto, 1 Horner, 2 scan)")
-    ap.add_argument("--knob", action="append", default=[], help="NAME=VALUE measurement knob (qk_ctx_set_knob)")
+    ap.add_argument("--knob", action="append", default=[],
+                    help="NAME=VALUE measurement knob (qk_ctx_set_knob; grid=N: qk_ctx_set_grid)")
     args = ap.parse_args()
     args.rt_modes = [int(x) for x in args.rt_modes.split(",")]
     ctx = sk.get_context(0)
     for kv in args.knob:
         k, v = kv.split("=")
-        ctx.set_knob(k, int(v))
+        if k == "grid":   # workgroups per launch for every kernel (qk_ctx_set_grid), measurements
+            ctx.set_grid(int(v))
+        else:
+            ctx.set_knob(k, int(v))
     for w in args.what:
         {"u64": run_u64, "decode": run_decode, "decode64": run_decode64, "host": run_host, "sweep": run_sweep, "sweep64": run_sweep64,
          "packets": run_packets, "flows": run_flows, "micro": run_micro}[w](args, ctx)
