@@ -681,7 +681,7 @@ QK_AVX512 static size_t gcd_small(const typename F::T *a0, size_t na, const type
 }
 
 // monic gcd(a, b), fraction-free: each step cancels a's leading term as
-// lead(b) a - lead(a) z^s b (no inversion; a field inverse costs ~60
+// lead(b) a - lead(a) z^s b (no inversion; a field inverse costs ~70
 // multiplications, more than the extra row of products here), one pass per
 // step over a's coefficients: a_i <- lb a_i - la b_(i-s) with b
 // zero-extended below, so the scaling of the low part and the row operation
