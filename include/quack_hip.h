@@ -157,8 +157,7 @@ int qk_ctx_trim(qk_ctx *ctx);
 int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
 /* Measurement knobs of this context (the defaults are the
  * product's measured choices — tools/ and the variant tests set them):
- * "bsgs_sg", "bsgs_shapes", "bsgs_prio", "u32_mfma" (0: u32 t <= 32 on the VALU kernels, not the
- * i8 matrix cores), "u32_mfma_tmin" (1..33), "mfma_wgpc" (1..32), "u32_passes", "u32_xcache", "bsgs64_sg", "bsgs64_off", "bsgs64_tmin", "bsgs64_shapes", "bsgs64_prio", "u64_passes",
+ * "bsgs_sg", "bsgs_shapes", "bsgs_prio", "u32_passes", "u32_xcache", "bsgs64_sg", "bsgs64_off", "bsgs64_tmin", "bsgs64_shapes", "bsgs64_prio", "u64_passes",
  * "u64_xcache", "u64_kmax", "flow_load" (2..64), "flow_wgpc", "flow_hist", "flow_sort", "flow_prio",
  * "pkt_fused", "rt64_horner",
  * "root_test" (0 automatic, 1 Horner, 2 root-set scan), "rt_direct" (0: the

@@ -15,9 +15,6 @@ struct qk_knobs {
     int u32_passes = 1;    // 0: u32 t > 80 on the power chain instead of BSGS passes
     int bsgs_shapes = 1;   // 0: the round-2 u32 BSGS shapes (t 17..36, 41..42, 65..72)
     int bsgs_prio = 1;     // 0: u32 BSGS without wave priority over the accumulation (bsgs.h Cfg PRIO 4)
-    int u32_mfma = 1;      // 0: u32 t <= 32 on the VALU baby-step/giant-step kernels instead of the i8 matrix cores
-    int u32_mfma_tmin = 25; // lowest u32 threshold on the matrix cores (mfma32.h)
-    int mfma_wgpc = 12;    // matrix-core encode: workgroups per CU
     int u32_xcache = 1;    // 0: u32 offset passes raise x^8 to base/8 themselves (no per-id x^base cache)
     int bsgs64_sg = -1;    // u64 BSGS MAC mode override (-1: default)
     int bsgs64_off = 0;    // 1: u64 on the power chain instead of BSGS

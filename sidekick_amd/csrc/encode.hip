@@ -35,7 +35,6 @@
 #include "field.h"
 #include "bsgs.h"
 #include "bsgs64.h"
-#include "mfma32.h"
 
 // scalar-counted wrap groups of the t = 25..32 BSGS kernel (tools/tune_bsgs.hip)
 #ifndef QK_BSGS_SG_T32
@@ -642,33 +641,6 @@ static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t
     return scratch_release(ctx, s);
 }
 
-// t <= 32 on the i8 matrix cores (mfma32.h): ids cut into one contiguous
-// run per workgroup (a multiple of 1024 ids; knob mfma_wgpc workgroups per
-// CU), each workgroup's 32 partial sums in the bsgs partial layout, then
-// k_finalize_u32 as for every other u32 kernel.
-static int enc32_mfma(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out, int acc,
-                      hipStream_t s) {
-    const uint32_t h = (uint32_t)std::min<uint64_t>(head, n);
-    const uint64_t na = n - h;
-    uint64_t nb = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus * (uint64_t)ctx->knobs.mfma_wgpc;
-    nb = std::max<uint64_t>(1, std::min<uint64_t>(nb, (na + 1023) / 1024));
-    const uint64_t per_wg = ((na + nb - 1) / nb + 1023) / 1024 * 1024;
-    int rc = ensure_scratch(ctx, (size_t)nb * T * sizeof(uint64_t), s);
-    if (rc) return rc;
-    uint64_t *partials = (uint64_t *)ctx->d_scratch;
-    rc = scratch_acquire(ctx, s);
-    if (rc) return rc;
-    hipEvent_t e0 = prof_begin(ctx, s);
-    hipLaunchKernelGGL(mfma32::k_encode_u32_mfma, dim3((uint32_t)nb), dim3(mfma32::BLK), 0, s, ids, (uint64_t)n, h, T,
-                       per_wg, partials);
-    prof_end(ctx, s, e0);
-    QK_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_finalize_u32, dim3(T), dim3(BLOCK), 0, s, partials, (uint32_t)nb, T, ids, (uint64_t)n, out,
-                       acc);
-    QK_HIP_TRY(hipGetLastError());
-    return scratch_release(ctx, s);
-}
-
 // sums of per-block partials [power][block] -> canonical S_1..S_T in out[0..T)
 int launch_finalize_powers_u32(const uint64_t *partials, uint32_t nblocks, uint32_t T, uint64_t *out,
                                hipStream_t s) {
@@ -1047,10 +1019,6 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     if (r3 && T >= 41 && T <= 42 && sg(7)) return QK_BSGS(6, 7, 7);
     if (r3 && T >= 65 && T <= 72 && sg(14)) return QK_BSGS(8, 9, 14);
     if (T >= 17 && T <= 24) return sg(4) ? QK_BSGS(6, 4, 4) : QK_BSGS(6, 4, 0);
-    // the i8 matrix cores (knob u32_mfma; u32_mfma_tmin: the lowest threshold
-    // sent there — below it the VALU shapes compute fewer powers for less)
-    if (ctx->knobs.u32_mfma && T >= (uint32_t)ctx->knobs.u32_mfma_tmin && T <= 32)
-        return enc32_mfma(ctx, ids, n, head, T, out, acc, s);
     if (T >= 25 && T <= 32) {
         switch (sg(QK_BSGS_SG_T32)) {
         case 0: return QK_BSGS(8, 4, 0);

@@ -18,26 +18,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "bsgs64_tmin": 14, "bsgs64_shapes": 1, "u32_xcache": 1, "u64_xcache": 1,
-            "bsgs_shapes": 1, "bsgs_prio": 1, "bsgs64_prio": 1, "u32_mfma": 1, "u32_mfma_tmin": 25, "mfma_wgpc": 12}
+            "bsgs_shapes": 1, "bsgs_prio": 1, "bsgs64_prio": 1}
 
 
 @contextlib.contextmanager
-def knob(name, value, grid=0, **more):
-    """Set knob `name` (and `more`) plus an override grid; restore the
-    defaults afterwards.  The VALU-kernel variants run with u32_mfma = 0, or
-    their t 25..32 cases would go to the matrix-core kernel."""
+def knob(name, value, grid=0):
     import sidekick_amd as sk
     ctx = sk.get_context(0)
     ctx.set_knob(name, value)
-    for k, v in more.items():
-        ctx.set_knob(k, v)
     ctx.set_grid(grid)
     try:
         yield
     finally:
         ctx.set_knob(name, DEFAULTS[name])
-        for k in more:
-            ctx.set_knob(k, DEFAULTS[k])
         ctx.set_grid(0)
 
 
@@ -67,14 +60,14 @@ U32_CASES = [("t32_ragged", 1_000_003, 32, 1), ("t32_small", 77, 32, 3), ("t24",
 
 @pytest.mark.parametrize("sg", [0, 1, 2, 3, 5, 8])
 def test_bsgs_scalar_carry_groups(sg):
-    with knob("bsgs_sg", sg, u32_mfma=0):
+    with knob("bsgs_sg", sg):
         res = _run(32, U32_CASES)
     assert all(res.values()), res
 
 
 def test_bsgs_scalar_carry_small_grid():
     """Override grid of one workgroup: long per-wave trip counts."""
-    with knob("bsgs_sg", 8, grid=1, u32_mfma=0):
+    with knob("bsgs_sg", 8, grid=1):
         res = _run(32, [("g1", 3_000_001, 32, 1)])
     assert all(res.values()), res
 
@@ -106,7 +99,7 @@ def test_u32_bsgs_shapes(shapes):
     replaced (knob bsgs_shapes = 0), against the oracle at both ends of each
     range, ragged and misaligned."""
     cases = [(f"t{t}", 100_003 + t, t, t % 4) for t in (17, 20, 21, 24, 25, 28, 29, 30, 33, 36, 41, 42, 65, 72)]
-    with knob("bsgs_shapes", shapes, u32_mfma=0):
+    with knob("bsgs_shapes", shapes):
         res = _run(32, cases)
     assert all(res.values()), res
 
@@ -119,7 +112,7 @@ def test_u32_bsgs_prio(prio):
     the default raises it), against the oracle, ragged and misaligned."""
     cases = [(f"t{t}", 100_003 + t, t, t % 4)
              for t in (8, 12, 16, 20, 24, 28, 30, 32, 36, 40, 42, 48, 56, 64, 72, 80, 88, 129, 300)]
-    with knob("bsgs_prio", prio, u32_mfma=0):
+    with knob("bsgs_prio", prio):
         res = _run(32, cases)
     assert all(res.values()), res
 
@@ -201,47 +194,6 @@ def test_knob_validation():
     from sidekick_amd._lib import QuackError
     ctx = sk.get_context(0)
     for name, bad in (("flow_load", 0), ("flow_load", 65), ("root_test", 3), ("no_such_knob", 1),
-                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2), ("bsgs64_prio", 2),
-                      ("u32_mfma", 2), ("u32_mfma_tmin", 0), ("mfma_wgpc", 0)):
+                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2), ("bsgs64_prio", 2)):
         with pytest.raises(QuackError):
             ctx.set_knob(name, bad)
-
-
-@pytest.mark.parametrize("wgpc,grid", [(12, 0), (4, 0), (32, 0), (12, 1), (12, 3)])
-def test_u32_mfma(wgpc, grid):
-    """The i8 matrix-core encode (mfma32.h) for every t <= 32 (u32_mfma_tmin
-    = 1 sends them all there), against the oracle: ragged tails, an unaligned
-    head (1..3 ids before the first 16-byte boundary, also with fewer ids than
-    that), tiny batches, one or three workgroups (per-wave runs of 2^20 ids:
-    the i32 accumulators are flushed every 65536 ids) and the default grid."""
-    cases = [(f"t{t}_{n}_{off}", n, t, off)
-             for t, n, off in ((32, 1_000_003, 1), (32, 77, 3), (32, 2, 3), (32, 1, 1), (31, 100_003, 2),
-                               (30, 65_537, 0), (28, 4096, 1), (25, 300_007, 3), (24, 100_001, 0), (17, 1025, 2),
-                               (16, 50_003, 1), (8, 1023, 0), (5, 3, 2), (1, 10_007, 1))]
-    if grid:
-        cases.append((f"g{grid}_long", 4_200_007, 32, 1))
-    with knob("u32_mfma_tmin", 1, grid=grid, mfma_wgpc=wgpc):
-        res = _run(32, cases)
-    assert all(res.values()), res
-
-
-def test_u32_mfma_lazy_wrap_ids():
-    """Ids whose lazy products come out below 25 (0, 1, 2, p - 1, p, p + 1,
-    2^32 - 1, small powers...) take the exact-product branch of their wave;
-    the sums equal the oracle's and the VALU kernel's."""
-    import torch
-    import sidekick_amd as sk
-    from oracle import coracle
-    P = (1 << 32) - 5
-    special = np.array([0, 1, 2, 3, 4, 5, P - 1, P - 2, P, P + 1, P + 4, (1 << 32) - 1, 65536, 65537, 1 << 31],
-                       dtype=np.uint64).astype(np.uint32)
-    rnd = coracle.splitmix_u32(0xBEEF, 20_000)
-    ids = np.concatenate([np.tile(special, 40), rnd, special])
-    want = list(coracle.encode_u32(ids, 32))
-    got = {}
-    for m in (1, 0):
-        with knob("u32_mfma", m):
-            q = sk.PowerSumQuackU32(32)
-            q.insert_batch(torch.from_numpy(ids.view(np.int32)).cuda())
-            got[m] = q.power_sums()
-    assert got[1] == want and got[0] == want
