@@ -157,7 +157,8 @@ int qk_ctx_trim(qk_ctx *ctx);
 int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
 /* Measurement knobs of this context (the defaults are the
  * product's measured choices — tools/ and the variant tests set them):
- * "bsgs_sg", "bsgs_shapes", "bsgs_prio", "u32_passes", "u32_xcache", "bsgs64_sg", "bsgs64_off", "bsgs64_tmin", "bsgs64_shapes", "bsgs64_prio", "u64_passes",
+ * "bsgs_sg", "bsgs_shapes", "bsgs_prio", "grid_mult" (1..8: encode grids of that many rounds of
+ * resident workgroups), "u32_passes", "u32_xcache", "bsgs64_sg", "bsgs64_off", "bsgs64_tmin", "bsgs64_shapes", "bsgs64_prio", "u64_passes",
  * "u64_xcache", "u64_kmax", "flow_load" (2..64), "flow_wgpc", "flow_hist", "flow_sort", "flow_prio",
  * "pkt_fused", "rt64_horner",
  * "root_test" (0 automatic, 1 Horner, 2 root-set scan), "rt_direct" (0: the

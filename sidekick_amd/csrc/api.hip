@@ -574,7 +574,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
     static const K table[] = {
         {"bsgs_sg", &qk_knobs::bsgs_sg, -1, 64},       {"u32_passes", &qk_knobs::u32_passes, 0, 1},
         {"u32_xcache", &qk_knobs::u32_xcache, 0, 1},     {"bsgs_shapes", &qk_knobs::bsgs_shapes, 0, 1},
-        {"bsgs_prio", &qk_knobs::bsgs_prio, 0, 1},
+        {"bsgs_prio", &qk_knobs::bsgs_prio, 0, 1},      {"grid_mult", &qk_knobs::grid_mult, 1, 8},
         {"bsgs64_sg", &qk_knobs::bsgs64_sg, -1, 64},   {"bsgs64_off", &qk_knobs::bsgs64_off, 0, 1},
         {"bsgs64_tmin", &qk_knobs::bsgs64_tmin, 9, 81}, {"bsgs64_shapes", &qk_knobs::bsgs64_shapes, 0, 1},
         {"bsgs64_prio", &qk_knobs::bsgs64_prio, 0, 1},

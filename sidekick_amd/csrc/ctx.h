@@ -15,6 +15,7 @@ struct qk_knobs {
     int u32_passes = 1;    // 0: u32 t > 80 on the power chain instead of BSGS passes
     int bsgs_shapes = 1;   // 0: the round-2 u32 BSGS shapes (t 17..36, 41..42, 65..72)
     int bsgs_prio = 1;     // 0: u32 BSGS without wave priority over the accumulation (bsgs.h Cfg PRIO 4)
+    int grid_mult = 3;     // encode launches: resident workgroups x this (1: one round; grid_for, encode.hip)
     int u32_xcache = 1;    // 0: u32 offset passes raise x^8 to base/8 themselves (no per-id x^base cache)
     int bsgs64_sg = -1;    // u64 BSGS MAC mode override (-1: default)
     int bsgs64_off = 0;    // 1: u64 on the power chain instead of BSGS

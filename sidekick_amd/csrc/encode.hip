@@ -609,11 +609,17 @@ __global__ __launch_bounds__(bsgs64::BLOCK, 4) void k_encode_u64_bsgs_off(const 
 
 // ------------------------------------------------------------- dispatch
 template <typename KernelT>
-static uint32_t grid_for(qk_ctx *ctx, KernelT kern, uint64_t units, uint32_t per_block) {
+static uint32_t grid_for(qk_ctx *ctx, KernelT kern, uint64_t units, uint32_t per_block, int mult = 0) {
     if (ctx->grid_override) return ctx->grid_override;
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BLOCK, 0) != hipSuccess || occ < 1) occ = 1;
-    const uint64_t full = (uint64_t)ctx->num_cus * (uint64_t)occ;
+    // knob grid_mult: resident workgroups x this.  The encode kernels take
+    // one contiguous run per workgroup; with one round of workgroups the
+    // launch ends with the slowest CU's run, with three the runs are a third
+    // as long and the CUs that finish early take the later ones
+    // (mult > 0: fixed by the caller — u32 t > 48 and the u32 passes measured
+    // 0.4-2.3 % slower at three rounds, profiles/r04/grid_mult/)
+    const uint64_t full = (uint64_t)ctx->num_cus * (uint64_t)occ * (uint64_t)(mult > 0 ? mult : ctx->knobs.grid_mult);
     uint64_t need = (units + per_block - 1) / per_block;
     if (need < 1) need = 1;
     return (uint32_t)(need < full ? need : full);
@@ -623,8 +629,8 @@ static uint32_t grid_for(qk_ctx *ctx, KernelT kern, uint64_t units, uint32_t per
 template <typename IdT, typename KernelT, typename FinT>
 static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t words_per_power,
                       const IdT *d_ids, size_t n, uint32_t head, uint32_t T, uint64_t units,
-                      uint32_t per_block, uint64_t *d_partial, int accumulate, hipStream_t s) {
-    const uint32_t nb = grid_for(ctx, kern, units, per_block);
+                      uint32_t per_block, uint64_t *d_partial, int accumulate, hipStream_t s, int mult = 0) {
+    const uint32_t nb = grid_for(ctx, kern, units, per_block, mult);
     const size_t need = (size_t)nb * words_per_power * GK * sizeof(uint64_t);
     int rc = ensure_scratch(ctx, need, s);
     if (rc) return rc;
@@ -662,7 +668,7 @@ template <int KIND, class KernelT>
 static int run_pass(qk_ctx *ctx, KernelT kern, uint32_t GK, const uint32_t *d_ids, size_t n,
                     uint32_t head, uint32_t Tp, uint32_t base, uint64_t *out, uint64_t *meta, int acc,
                     hipStream_t s, const uint32_t *xin = nullptr, uint32_t *xout = nullptr) {
-    const uint32_t nb = grid_for(ctx, kern, (n + 3) / 4, BLOCK);
+    const uint32_t nb = grid_for(ctx, kern, (n + 3) / 4, BLOCK, 1);
     if (int rc = ensure_scratch(ctx, (size_t)nb * GK * sizeof(uint64_t), s)) return rc;
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
     if (int rc = scratch_acquire(ctx, s)) return rc;
@@ -701,9 +707,9 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
     const uint32_t npass = T <= 80 ? 0 : (T - 80 + 47) / 48;   // offset passes
     uint32_t *xc = nullptr;
     if (npass >= 1 && ctx->knobs.u32_xcache) {
-        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u32_bsgs_x80<16>, (n + 3) / 4, BLOCK),
-                                         grid_for(ctx, k_encode_u32_bsgs_off<6, 12, 3>, (n + 3) / 4, BLOCK),
-                                         grid_for(ctx, k_encode_u32_bsgs_off<5, 10, 1>, (n + 3) / 4, BLOCK)});
+        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u32_bsgs_x80<16>, (n + 3) / 4, BLOCK, 1),
+                                         grid_for(ctx, k_encode_u32_bsgs_off<6, 12, 3>, (n + 3) / 4, BLOCK, 1),
+                                         grid_for(ctx, k_encode_u32_bsgs_off<5, 10, 1>, (n + 3) / 4, BLOCK, 1)});
         const size_t poff = ((size_t)nbmax * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
         if (ensure_scratch(ctx, poff + 16 + (size_t)n * 4, s) == QK_OK)
             xc = (uint32_t *)((char *)ctx->d_scratch + poff + ((uintptr_t)ids & 15));
@@ -998,7 +1004,7 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     const int prio = ctx->knobs.bsgs_prio;
 #define QK_BSGS_P(NB_, NA_, G_, P_)                                                                          \
     run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_, P_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
-                         (n + 3) / 4, BLOCK, out, acc, s)
+                         (n + 3) / 4, BLOCK, out, acc, s, NB_ * NA_ > 48 ? 1 : 0)
 #define QK_BSGS(NB_, NA_, G_)                                                                                 \
     (prio ? QK_BSGS_P(NB_, NA_, G_, 1) : QK_BSGS_P(NB_, NA_, G_, 0))
     if (T >= 5 && T <= 8 && sg(1)) return QK_BSGS(4, 2, 1);

@@ -18,7 +18,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 DEFAULTS = {"bsgs_sg": -1, "u64_kmax": 40, "bsgs64_sg": -1, "bsgs64_off": 0, "bsgs64_tmin": 14, "bsgs64_shapes": 1, "u32_xcache": 1, "u64_xcache": 1,
-            "bsgs_shapes": 1, "bsgs_prio": 1, "bsgs64_prio": 1}
+            "bsgs_shapes": 1, "bsgs_prio": 1, "bsgs64_prio": 1, "grid_mult": 3}
 
 
 @contextlib.contextmanager
@@ -194,6 +194,20 @@ def test_knob_validation():
     from sidekick_amd._lib import QuackError
     ctx = sk.get_context(0)
     for name, bad in (("flow_load", 0), ("flow_load", 65), ("root_test", 3), ("no_such_knob", 1),
-                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2), ("bsgs64_prio", 2)):
+                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2), ("bsgs64_prio", 2),
+                      ("grid_mult", 0), ("grid_mult", 9)):
         with pytest.raises(QuackError):
             ctx.set_knob(name, bad)
+
+
+@pytest.mark.parametrize("mult", [1, 3, 8])
+def test_encode_grid_mult(mult):
+    """Encode grids of 1, 3 (the default) and 8 rounds of resident workgroups
+    (knob grid_mult): shorter contiguous runs per workgroup, more partials —
+    u32 and u64, single-pass and passes, against the oracle."""
+    c32 = [(f"t{t}", 1_000_003 + t, t, t % 4) for t in (8, 16, 28, 32, 48, 80, 129)]
+    c64 = [(f"t{t}", 200_003 + t, t, t % 2) for t in (8, 16, 32, 80, 100)]
+    with knob("grid_mult", mult):
+        res = _run(32, c32)
+        res.update({f"u64_{k}": v for k, v in _run(64, c64).items()})
+    assert all(res.values()), res
