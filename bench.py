@@ -34,10 +34,15 @@ Rank 0 prints ONE JSON line.  Alongside the metric it reports
                 against rank 0's single-GPU encode and the recorded N = 1
                 digest; `rccl` / `ranks`: what RCCL reports on every rank
                 (ncclCommCount, ncclCommCuDevice, ncclCommUserRank);
+  decode_parity N > 1: configs[4]'s decode through the same communicator
+                (two sharded encodes, the difference, decode_sharded's
+                broadcast and all-gathers) against rank 0's single-GPU root
+                test: equal hit lists, every drop recovered;
   cpu_baseline  the oracle's scalar C restatement of the reference insert
                 loop on ONE host core over a bounded prefix of the same
-                stream (rank 0, N = 1 only), with a GPU/CPU parity check on
-                that prefix.
+                stream (rank 0, N = 1 only), timed in the crate's own unit
+                (rdtsc around the loop) and in ns, with a GPU/CPU parity
+                check on that prefix.
 """
 from __future__ import annotations
 
@@ -84,28 +89,41 @@ def measure_clock(ctx, step, dev_index, kern_avg_ms, steps=10):
     """The shader clock the chip holds under this kernel, in this run: after
     the timed region, qk_clock_probe's one wave spins on a side stream for
     ~90 % of `steps` further (untimed) steps and reads s_memtime against
-    s_memrealtime (100 MHz).  Returns GHz or None."""
+    s_memrealtime (100 MHz).  Returns GHz or None.  For N > 1 every step is a
+    collective, so every rank runs all of them whatever happens to its probe
+    (a probe failure only nulls the clock); a failing step raises."""
     import torch
+    out = torch.zeros(2, dtype=torch.int64, device=f"cuda:{dev_index}")
+    side = torch.cuda.Stream(device=dev_index)
+    for _ in range(2):
+        step()                                       # the chip busy before the probe lands
+    probe_ok = True
     try:
-        out = torch.zeros(2, dtype=torch.int64, device=f"cuda:{dev_index}")
-        side = torch.cuda.Stream(device=dev_index)
-        for _ in range(2):
-            step()                                   # the chip busy before the probe lands
         us = max(1000, int(kern_avg_ms * steps * 0.9 * 1e3))
         ctx.clock_probe_async(us, out, side.cuda_stream)
-        for _ in range(steps):
-            step()
-        torch.cuda.synchronize()
-        c, r = (int(v) for v in out.cpu().tolist())
-        return c / r * 0.1 if r > 0 else None
     except Exception as e:  # noqa: BLE001 — a measurement aid, never fatal
         log(f"clock probe failed: {e!r}")
+        probe_ok = False
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if not probe_ok:
         return None
+    c, r = (int(v) for v in out.cpu().tolist())
+    return c / r * 0.1 if r > 0 else None
 
 
-# Digest of the folded power sums of the N = 1 stream (configs[1]: 1e9 u32
-# ids, t = 32, seed 0x5EED0002): unchanged since round 1 (BENCH_r01..r03).
-RECORDED_DIGESTS = {(32, 32, 1_000_000_000, 0x5EED0002): "523499db79543cdf"}
+# Digests of the folded power sums of the global stream (u32 ids, t = 32,
+# seed 0x5EED0002): N = 1 (configs[1], 1e9 ids) unchanged since round 1
+# (BENCH_r01..r04); N = 2, 4, 8 (2e9 / 4e9 / 8e9 ids, configs[3] at N = 8)
+# recorded by tests/test_gpu_comm.py::test_configs3_full_size_world8_host_channel
+# (whole-stream single-GPU encodes, equal to the world-8 sharded encode;
+# profiles/r05/check1/pytest.txt), so the driver's scaling runs check their
+# result too.
+RECORDED_DIGESTS = {(32, 32, 1_000_000_000, 0x5EED0002): "523499db79543cdf",
+                    (32, 32, 2_000_000_000, 0x5EED0002): "bb61bb32e92b9799",
+                    (32, 32, 4_000_000_000, 0x5EED0002): "37d66ecb59b3a758",
+                    (32, 32, 8_000_000_000, 0x5EED0002): "032bc2155ec17f4a"}
 
 
 def digest_of(S, count) -> str:
@@ -146,26 +164,87 @@ def strong_scaling_check(args, comm, ctx, ids, rank, world, dev_index, bits, t):
             "last_value_equal": q.last_value() == q1.last_value()}
 
 
+# configs[4]: decode-missing over a 1e8-id candidate log with 32 drops
+DECODE_SEED, DECODE_N, DECODE_DROPS, DECODE_T = 0x5EED0005, 100_000_000, 32, 32
+
+
+def decode_check(comm, ctx, ids, n_per_gpu, rank, world, bits):
+    """N > 1, untimed: configs[4]'s decode through the same communicator.  The
+    1e8-id log (seed 0x5EED0005) is cut into `world` contiguous shards, one
+    per rank, filled on its own GPU; 32 seeded drops (the same on every rank)
+    are removed from the receiver's copy of each shard.  quack_A = the sharded
+    encode of the log, quack_B = the sharded encode of the log without the
+    drops (one reduce each), diff = A - B on the root, then decode_sharded
+    (ncclBroadcast of the coefficients, every rank root-tests its shard, two
+    all-gathers).  Rank 0 then fills the whole log on its own GPU and runs
+    the single-GPU root test with the same difference; the two hit lists
+    must be equal and contain every drop.  Returns the record on rank 0."""
+    import numpy as np
+    import torch
+    import sidekick_amd as sk
+    from sidekick_amd import dist as skd
+    from sidekick_amd.quack import fill_splitmix
+    Q = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+    n_log = min(DECODE_N, n_per_gpu)           # alike on every rank; rank 0's id buffer then holds the whole log
+    drops = np.sort(np.random.default_rng(DECODE_SEED).choice(n_log, DECODE_DROPS, replace=False))
+    s, c = skd.shard(n_log, rank, world)
+    log_view = ids[:c]
+    fill_splitmix(ctx, log_view, DECODE_SEED, s, bits=bits)
+    keep = torch.ones(c, dtype=torch.bool, device=ids.device)
+    mine = drops[(drops >= s) & (drops < s + c)] - s
+    if len(mine):
+        keep[torch.from_numpy(mine).to(ids.device)] = False
+    recv_view = log_view[keep]
+    torch.cuda.synchronize()
+    A, B = Q(DECODE_T), Q(DECODE_T)
+    comm.encode_sharded([log_view], A)
+    comm.encode_sharded([recv_view], B)
+    diff = None
+    if rank == 0:
+        diff = A.clone()
+        diff.sub_assign(B)
+    t0 = time.perf_counter()
+    hits = comm.decode_sharded(diff, [log_view], bits=bits, stop_at_last=True)
+    dec_ms = (time.perf_counter() - t0) * 1e3
+    del recv_view, keep
+    if rank != 0:
+        return None
+    fill_splitmix(ctx, ids[:n_log], DECODE_SEED, 0, bits=bits)
+    want = diff.root_test(diff.to_coeffs(), ids[:n_log], stop_value=diff.last_value())
+    torch.cuda.synchronize()
+    return {"workload": f"configs[4], untimed: decode-missing over a {n_log:.0e}-id u{bits} log (seed "
+                        f"{hex(DECODE_SEED)}) in {world} contiguous shards with {DECODE_DROPS} seeded drops: two "
+                        f"sharded encodes (A = log, B = log without the drops), diff = A - B on rank 0, "
+                        f"decode_sharded (broadcast + all-gathers) against rank 0's single-GPU root test",
+            "d": diff.count(), "hits": len(hits), "equals_single_gpu": hits == want,
+            "drops_recovered": bool(set(drops.tolist()) <= set(hits)), "decode_sharded_ms": dec_ms}
+
+
 # The published crate at the metric's threshold: benchmark_construct on one
-# core of a Xeon E5 (rdtsc ~2.256 GHz), t = 32 interpolated between the t = 30
-# and t = 40 rows (zip:nsdi24/quack/threshold_vs_encode_time/32.txt:9,12;
-# BASELINE.md).
-PUBLISHED_NS_PER_ID = {(32, 32): 125.8, (32, 16): 58.6, (64, 80): 461.0}
+# core of a Xeon E5, `-e 1000 --trials 100`, in its own units — avg_cycles
+# (rdtsc around the insert loop) / 1000 ids and avg_us / 1000 ids; t = 32 and
+# t = 16 interpolated between the neighbouring rows
+# (zip:nsdi24/quack/threshold_vs_encode_time/32.txt:3,6,9,12, 64.txt:24;
+# profiles/published/quack_logs.json; BASELINE.md, SURVEY.md §6).
+PUBLISHED = {  # (bits, t): (ns per id, TSC cycles per id)
+    (32, 32): (117.159 + 0.2 * (161.618 - 117.159), (268165 + 0.2 * (370345 - 268165)) / 1000),
+    (32, 16): (34.676 + 0.6 * (75.334 - 34.676), (78220 + 0.6 * (171639 - 78220)) / 1000),
+    (64, 80): (461.745, 1060.493),
+}
 
 
 def host_cpu():
-    """(model name, current MHz of cpu0, logical CPUs) of this host."""
-    model, mhz = "unknown", None
+    """(model name, logical CPUs) of this host."""
+    model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
-                if line.startswith("model name") and model == "unknown":
+                if line.startswith("model name"):
                     model = line.split(":", 1)[1].strip()
-                elif line.startswith("cpu MHz") and mhz is None:
-                    mhz = float(line.split(":", 1)[1])
+                    break
     except OSError:
         pass
-    return model, mhz, os.cpu_count() or 1
+    return model, os.cpu_count() or 1
 
 
 def usable_cpus():
@@ -196,33 +275,37 @@ def cpu_baselines(args, bits, t, start, cnt, ids):
     from oracle import coracle
     m = int(min(args.cpu_sample, cnt))
     host_ids = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(args.seed, m, start)
-    tc = time.perf_counter()
-    cpu_S = (coracle.encode_u32 if bits == 32 else coracle.encode_u64)(host_ids, t)
-    cpu_s = time.perf_counter() - tc
+    # the insert loop timed in the crate's own unit (rdtsc, as its
+    # benchmark_construct's avg_cycles) and by the monotonic clock over the
+    # same region: the TSC rate comes from this run, not from /proc/cpuinfo
+    cpu_S, tsc, ns = coracle.encode_timed(host_ids, t)
+    cpu_s = ns * 1e-9
     q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
     q.insert_batch(ids[:m])                    # GPU on the same prefix: bit-exact parity check
     parity = q.power_sums() == cpu_S
     if not parity:
         log("PARITY FAILURE: GPU power sums differ from the CPU oracle on the sample prefix")
-    model, mhz, ncpu = host_cpu()
-    pub = PUBLISHED_NS_PER_ID.get((bits, t))
-    host = f"host {model}, {ncpu} logical CPUs" + (f", cpu0 at {mhz:.0f} MHz" if mhz else "")
+    model, ncpu = host_cpu()
+    pub_ns, pub_cyc = PUBLISHED.get((bits, t), (None, None))
+    host = f"host {model}, {ncpu} logical CPUs"
     ns_id = cpu_s / m * 1e9
-    cpp = ns_id * mhz * 1e-3 / t if mhz else None          # cycles per power at cpu0's reported clock
-    pub_cpp = pub * 2.256 / t if pub else None              # the crate: rdtsc ~2.256 GHz
+    tsc_id = tsc / m if tsc else None
+    tsc_ghz = tsc / ns if tsc else None
     one = {
         "value": m / cpu_s, "unit": "identifiers/s", "cores": 1, "kind": "port",
-        "ns_per_id": ns_id, "cycles_per_power": cpp,
+        "ns_per_id": ns_id, "tsc_cycles_per_id": tsc_id, "tsc_cycles_per_power": tsc_id / t if tsc_id else None,
+        "tsc_ghz": tsc_ghz,
         "sample": f"first {m} ids of the same stream (seed {hex(args.seed)}), pre-generated, inserted by the "
-                  f"scalar C restatement of the reference insert loop (oracle/quack_oracle.c qo_encode_u{bits}), "
+                  f"scalar C restatement of the reference insert loop (oracle/quack_oracle.c qo_encode_timed), "
                   f"1 core, {cpu_s:.1f} s = {ns_id:.1f} ns/id"
-                  + (f" = {cpp:.1f} cycles per power at cpu0's {mhz:.0f} MHz" if cpp else "") + f"; {host}"
-                  + (f"; the published crate: {pub} ns/id at u{bits} t={t} on one Xeon E5 core at ~2.26 GHz "
-                     f"= {pub_cpp:.1f} cycles per power (BASELINE.md), so per clock this port is "
-                     f"{cpp / pub_cpp:.1f}x slower than the crate and GPU/CPU ratios against it overstate the "
-                     f"gap to the crate by that factor" if pub and cpp else ""),
-        "published_crate_ns_per_id": pub,
-        "published_crate_cycles_per_power": pub_cpp,
+                  + (f" = {tsc_id:.1f} TSC cycles/id (rdtsc around the loop, TSC at {tsc_ghz:.3f} GHz from the "
+                     f"same region)" if tsc_id else "") + f"; {host}"
+                  + (f"; the published crate in the same units: {pub_cyc:.1f} TSC cycles/id = {pub_ns:.1f} ns/id "
+                     f"at u{bits} t={t} on one Xeon E5 core (benchmark_construct avg_cycles / 1000 ids; "
+                     f"BASELINE.md), so this port takes {tsc_id / pub_cyc:.2f}x the crate's TSC cycles per id"
+                     if pub_cyc and tsc_id else ""),
+        "published_crate_ns_per_id": pub_ns,
+        "published_crate_tsc_cycles_per_id": pub_cyc,
         "parity_with_gpu": parity,
     }
     thr, how = usable_cpus()
@@ -371,10 +454,11 @@ def main():
     clock_ghz = measure_clock(ctx, step, dev_index, kern_avg_ms)
     if comm is not None:   # drain the probe's steps (the root merges into a throwaway sketch)
         comm.encode_sharded_wait((sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t))
-    strong = None
+    strong = dec = None
     ranks = None
     if world > 1:
         strong = strong_scaling_check(args, comm, ctx, ids, rank, world, dev_index, bits, t)
+        dec = decode_check(comm, ctx, ids, n, rank, world, bits)
         info = comm.rccl_info()
         props = torch.cuda.get_device_properties(dev_index)
         mine = {"rank": rank, "local_rank": local, "device": dev_index,
@@ -445,6 +529,7 @@ def main():
         out["result"]["equals_recorded"] = digest == rec
     if world > 1:
         out["parity"] = strong
+        out["decode_parity"] = dec
         out["ranks"] = ranks
         if data_path == "rccl":
             out["rccl"] = {"ranks_reported": sorted({r["rccl_count"] for r in ranks}),

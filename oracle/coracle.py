@@ -47,6 +47,7 @@ def lib():
             "qo_root_test_u64": (C.c_uint64, [u64p, C.c_uint32, u64p, C.c_uint64, i64p, C.c_uint64]),
             "qo_bench_construct": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, u64p]),
             "qo_bench_decode": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, u64p]),
+            "qo_encode_timed": (None, [C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, u64p, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -93,6 +94,18 @@ def encode_seed_mt(bits, seed, n, t, threads, start=0):
     if rc:
         raise RuntimeError(f"qo_encode_seed_mt rc={rc}")
     return [int(v) for v in S]
+
+
+def encode_timed(ids, t):
+    """The scalar insert loop over pre-generated ids timed as the crate's
+    benchmark_construct does (rdtsc) and by CLOCK_MONOTONIC over the same
+    region: (power sums, TSC ticks, nanoseconds)."""
+    bits = 32 if ids.dtype == np.uint32 else 64
+    ids = np.ascontiguousarray(ids)
+    S = np.zeros(t, dtype=np.uint32 if bits == 32 else np.uint64)
+    tsc, ns = C.c_uint64(), C.c_uint64()
+    lib().qo_encode_timed(bits, ids.ctypes.data, len(ids), t, S.ctypes.data, C.byref(tsc), C.byref(ns))
+    return [int(v) for v in S], tsc.value, ns.value
 
 
 def encode_mt(ids, t, threads):

@@ -261,6 +261,32 @@ uint64_t qo_bench_construct(uint32_t bits, uint64_t seed, uint64_t n, uint32_t t
     return total;
 }
 
+/* The crate's own unit: benchmark_construct reports avg_cycles, rdtsc
+ * around its insert loop (zip:nsdi24/quack/threshold_vs_encode_time/32.txt:
+ * 1-3; parsed by figures/fig2_microbenchmarks.py:48-69).  This times the
+ * restatement's insert loop over pre-generated ids with the TSC and with
+ * CLOCK_MONOTONIC around the same region, so the TSC rate comes from the
+ * same run.  *tsc = 0 where there is no TSC (not x86-64). */
+#if defined(__x86_64__)
+#include <x86intrin.h>
+static inline uint64_t qo_tsc(void) {
+    _mm_lfence();
+    const uint64_t v = __rdtsc();
+    _mm_lfence();
+    return v;
+}
+#else
+static inline uint64_t qo_tsc(void) { return 0; }
+#endif
+void qo_encode_timed(uint32_t bits, const void *ids, uint64_t n, uint32_t t, void *S, uint64_t *tsc, uint64_t *ns) {
+    const uint64_t n0 = qo_now_ns(), c0 = qo_tsc();
+    if (bits == 32) qo_encode_u32((const uint32_t *)ids, n, t, (uint32_t *)S);
+    else qo_encode_u64((const uint64_t *)ids, n, t, (uint64_t *)S);
+    const uint64_t c1 = qo_tsc(), n1 = qo_now_ns();
+    *tsc = c1 - c0;
+    *ns = n1 - n0;
+}
+
 /* CPU port of quack's benchmark_decode (figures/fig2_microbenchmarks.py:
  * 134-141,175-183; timed region [RECALL]): sender sketch of n ids, receiver
  * missing d of them (evenly spread), threshold t = d; each trial times

@@ -288,6 +288,9 @@ template <typename T> int root_test_plan(const qk_ctx *ctx, const T *coeffs, uin
     plan.scan = rt_scan_table<T>(r.data(), k, plan.set, plan.tab) &&
                 plan.set.words * sizeof(T) <= (SMALL_NHITS - RT_C) * 8;
     if (!plan.scan) plan.tab.clear();
+    // begin and finish must agree on the form even if the knob changes in
+    // between (comm.hip releases ctx->mu between the two)
+    plan.direct = plan.scan && ctx->knobs.rt_direct;
     return QK_OK;
 }
 
@@ -299,7 +302,7 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
     uint64_t *d_counters = ctx->d_small;
     T *d_c = (T *)(ctx->d_small + RT_C);
     uint64_t *h_c = ctx->h_small + RT_C;
-    const bool scan = n && plan.scan, direct = scan && ctx->knobs.rt_direct;
+    const bool scan = n && plan.scan, direct = scan && plan.direct;
     size_t cbytes = (size_t)d * sizeof(T);
     if (scan) {
         cbytes = (size_t)plan.set.words * sizeof(T);
@@ -360,7 +363,7 @@ int root_test_finish(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32
     // overflow the device counters are copied now
     auto counts = [&]() -> int {
         QK_HIP_TRY(hipStreamSynchronize(s));
-        if (!(n && plan.scan && ctx->knobs.rt_direct)) return QK_OK;
+        if (!(n && plan.scan && plan.direct)) return QK_OK;
         uint64_t *h = ctx->h_small;
         if (h[SMALL_OVF]) {
             QK_HIP_TRY(hipMemcpyAsync(h + SMALL_NHITS, ctx->d_small, 16, hipMemcpyDeviceToHost, s));

@@ -84,6 +84,8 @@ struct qk_comm {
         uint64_t *d_coll = nullptr;   // collective payload (device), coll_cap(world) words
         uint64_t *h_coll = nullptr;   // pinned host mirror
         hipEvent_t ev_in = nullptr, ev_out = nullptr;
+        hipEvent_t ev_pre = nullptr;  // the local work before the RCCL collective in flight
+        bool pre = false;             // ev_pre recorded and not yet waited on
         hipStream_t user = nullptr;   // caller stream of the operation in flight
     };
     int world = 1;
@@ -144,6 +146,7 @@ static int init_local(Local &L, int device, int world) {
     QK_HIP_TRY(hipSetDevice(device));
     QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_in, hipEventDisableTiming));
     QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_out, hipEventDisableTiming));
+    QK_HIP_TRY(hipEventCreateWithFlags(&L.ev_pre, hipEventDisableTiming));
     const size_t w = coll_cap(world);
     if (hipMalloc(&L.d_coll, w * 8) != hipSuccess) return QK_E_NOMEM;
     if (hipHostMalloc(&L.h_coll, w * 8, hipHostMallocDefault) != hipSuccess) return QK_E_NOMEM;
@@ -182,14 +185,28 @@ static int abort_comm(qk_comm *c) {
     return QK_E_COMM;
 }
 
+// Mark the end of a local rank's own work (its encode, the caller's work
+// ordered in by enter, the payload staging) just before an RCCL collective.
+static void mark_pre(Local &L) {
+    (void)hipSetDevice(L.device);
+    L.pre = hipEventRecord(L.ev_pre, L.ctx->stream) == hipSuccess;
+}
+
 // Drain the local rank's stream.  With RCCL work in it, the wait polls the
 // communicator's asynchronous error and gives up after the timeout (a peer
 // that never reaches the collective): the communicator is aborted, QK_E_COMM.
+// The timeout covers the collective only: the local work recorded before it
+// (mark_pre) is waited for first, without a limit — slow local work is not a
+// missing peer.
 static int wait_local(qk_comm *c, Local &L) {
     QK_HIP_TRY(hipSetDevice(L.device));
     if (c->host || !L.nc) {
         QK_HIP_TRY(hipStreamSynchronize(L.ctx->stream));
         return QK_OK;
+    }
+    if (L.pre) {
+        L.pre = false;
+        QK_HIP_TRY(hipEventSynchronize(L.ev_pre));
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned spin = 0;; ++spin) {
@@ -253,6 +270,7 @@ static int reduce_payload(qk_comm *c, size_t w, int root, std::vector<int> &lerr
             if (!lerr[i]) lerr[i] = QK_E_HIP;
         }
     }
+    for (auto &L : c->local) mark_pre(L);
     bool ok = ncclGroupStart() == ncclSuccess;
     for (auto &L : c->local) {
         if (!ok) break;
@@ -299,6 +317,7 @@ static int exchange(qk_comm *c, Op op, size_t w, int root, size_t sidx, std::vec
             if (!ls[i]) ls[i] = QK_E_HIP;
         }
     }
+    for (auto &L : c->local) mark_pre(L);
     bool ok = ncclGroupStart() == ncclSuccess;
     for (auto &L : c->local) {
         if (!ok) break;
@@ -604,6 +623,7 @@ static void destroy_local(Local &L) {
     if (L.h_coll) hipHostFree(L.h_coll);
     if (L.ev_in) hipEventDestroy(L.ev_in);
     if (L.ev_out) hipEventDestroy(L.ev_out);
+    if (L.ev_pre) hipEventDestroy(L.ev_pre);
     if (L.ctx) qk_ctx_destroy(L.ctx);
     L = Local{};
 }

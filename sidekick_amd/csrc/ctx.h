@@ -186,6 +186,7 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
 // sorted hit positions (all of them) and the first stop position
 template <typename T> struct RtPlan {
     bool scan = false;
+    bool direct = false;  // the scan writes its hits into pinned host slots (knob rt_direct, read once at plan time)
     RtScanSet set;
     std::vector<T> tab;   // the root set (scan)
 };

@@ -625,6 +625,18 @@ static uint32_t grid_for(qk_ctx *ctx, KernelT kern, uint64_t units, uint32_t per
     return (uint32_t)(need < full ? need : full);
 }
 
+// An upper bound on grid_for over every kernel a multi-pass encode may
+// launch, whatever its occupancy (which depends on the knob-selected
+// instantiation): at most 8 workgroups of 256 threads per CU (32 waves).
+// The x^base cache is placed after the largest partials this allows.
+static uint32_t grid_cap(const qk_ctx *ctx, uint64_t units, uint32_t per_block, int mult = 0) {
+    if (ctx->grid_override) return ctx->grid_override;
+    const uint64_t full = (uint64_t)ctx->num_cus * 8u * (uint64_t)(mult > 0 ? mult : ctx->knobs.grid_mult);
+    uint64_t need = (units + per_block - 1) / per_block;
+    if (need < 1) need = 1;
+    return (uint32_t)(need < full ? need : full);
+}
+
 // Launch main kernel (+profiling events) then finalize.
 template <typename IdT, typename KernelT, typename FinT>
 static int run_encode(qk_ctx *ctx, KernelT kern, FinT fin, uint32_t GK, uint32_t words_per_power,
@@ -707,9 +719,7 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
     const uint32_t npass = T <= 80 ? 0 : (T - 80 + 47) / 48;   // offset passes
     uint32_t *xc = nullptr;
     if (npass >= 1 && ctx->knobs.u32_xcache) {
-        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u32_bsgs_x80<16>, (n + 3) / 4, BLOCK, 1),
-                                         grid_for(ctx, k_encode_u32_bsgs_off<6, 12, 3>, (n + 3) / 4, BLOCK, 1),
-                                         grid_for(ctx, k_encode_u32_bsgs_off<5, 10, 1>, (n + 3) / 4, BLOCK, 1)});
+        const uint32_t nbmax = grid_cap(ctx, (n + 3) / 4, BLOCK, 1);   // run_pass: one round
         const size_t poff = ((size_t)nbmax * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
         if (ensure_scratch(ctx, poff + 16 + (size_t)n * 4, s) == QK_OK)
             xc = (uint32_t *)((char *)ctx->d_scratch + poff + ((uintptr_t)ids & 15));
@@ -813,9 +823,7 @@ static int enc64_passes_chunk(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32
     uint64_t *xc = nullptr;
     if (npass >= 1 && ctx->knobs.u64_xcache) {
         const uint64_t tiles = (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK;
-        const uint32_t nbmax = std::max({grid_for(ctx, k_encode_u64_bsgs<10, 16>, tiles, 1),
-                                         grid_for(ctx, k_encode_u64_bsgs_x80<1>, tiles, 1),
-                                         grid_for(ctx, k_encode_u64_bsgs_off<10, 3>, tiles, 1)});
+        const uint32_t nbmax = grid_cap(ctx, tiles, 1);
         const size_t poff = ((size_t)nbmax * 2 * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
         if (ensure_scratch(ctx, poff + (size_t)n * 8, s) == QK_OK) xc = (uint64_t *)((char *)ctx->d_scratch + poff);
     }

@@ -470,10 +470,11 @@ def encode_segments(ids, offsets, threshold: int, ctx: Context | None = None) ->
     check(lib().qk_u32_encode_segments_device(ctx.handle, ptr, offs.ctypes.data_as(C.POINTER(C.c_uint64)), nseg,
                                                threshold, out, stream), "encode_segments")
     res = []
+    raw = out.raw                     # one copy (ctypes .raw copies the whole buffer per access)
     for i in range(nseg):
         q = PowerSumQuackU32.__new__(PowerSumQuackU32)
         q._t = threshold
-        q._buf = C.create_string_buffer(out.raw[i * rec:(i + 1) * rec], rec)
+        q._buf = C.create_string_buffer(raw[i * rec:(i + 1) * rec], rec)
         res.append(q)
     return res
 
@@ -523,11 +524,12 @@ def encode_flows(bufs, threshold: int, stride: int = 67, meta=None, my_addr=None
     if device_out:
         return keys[:m], sk[:m], stats
     out_k, out_q = [], []
+    raw = sk.raw                      # one copy of the records (ctypes .raw copies the whole buffer per access)
     for i in range(m):
         out_k.append(bytes(keys[i].addr))
         q = PowerSumQuackU32.__new__(PowerSumQuackU32)
         q._t = threshold
-        q._buf = C.create_string_buffer(sk.raw[i * rec:(i + 1) * rec], rec)
+        q._buf = C.create_string_buffer(raw[i * rec:(i + 1) * rec], rec)
         out_q.append(q)
     return out_k, out_q, stats
 

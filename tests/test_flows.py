@@ -350,3 +350,42 @@ def test_gpu_flows_device_resident_output(nflows):
                                           d_meta.data_ptr(), (C.c_uint8 * 6)(*MY_ADDR), 32, keys.data_ptr(), host_sk,
                                           len(hk), C.byref(nf), None, None)
     assert rc == -1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nflows,skew,p_reset,hist", [(80_000, False, 0.002, 1), (120_000, True, 0.0, 1),
+                                                       (80_000, False, 0.0, 0)])
+def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
+    """More than 65 536 flows over 1e6 records: the flow table has > 2^16
+    slots, so the default grouping sort (radix.h, knob flow_sort = 2) runs
+    three digit passes — key/value arrays in, the pair array in and out in
+    the middle pass, arrays out (sidekick_multi.rs:65-90's per-flow map for a
+    batch).  Against the literal sniff loop's tables: every flow's sums,
+    count and last_value, in ascending key order; the records must equal the
+    two-array sort's (flow_sort = 1) and the direct-scatter sort's (7) byte
+    for byte; flow_hist on and off (the table is above its few-flow size, so
+    both take the sort)."""
+    import torch
+    from sidekick_amd.quack import Context, encode_flows
+    bufs, meta = make_flows(1_000_000, nflows, seed=nflows + int(skew), p_reset=p_reset, skew=skew,
+                            reset_until=0.2)
+    want, nres, _ = vector_flows(bufs, meta)
+    assert len(want) > (1 << 16) or skew
+    d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
+    d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
+    recs = {}
+    for mode in (2, 1, 7):
+        ctx = Context(0)
+        ctx.set_knob("flow_hist", hist)
+        ctx.set_knob("flow_sort", mode)
+        keys, qs, st = encode_flows(d_bufs, 32, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
+        assert st["resets"] == nres and st["inserted"] == sum(len(v) for v in want.values())
+        assert keys == sorted(want)
+        recs[mode] = [bytes(q._buf.raw) for q in qs]
+        if mode == 2:
+            for k, q in zip(keys, qs):
+                ids = want[k]
+                assert q.count() == len(ids) and q.last_value() == ids[-1], k.hex()
+                assert q.power_sums() == coracle.encode_u32(np.array(ids, dtype=np.uint32), 32), k.hex()
+        ctx.close()
+    assert recs[1] == recs[2] and recs[7] == recs[2]

@@ -443,3 +443,68 @@ def test_host_channel_staging_fault_at_every_step_same_status_everywhere():
     finally:
         for c in comms:
             c.close()
+
+
+def test_configs3_full_size_world8_host_channel():
+    """configs[3] at full size on one GPU: 8e9 u32 ids (32 GB, the bench's
+    global stream at N = 8: seed 0x5EED0002) at t = 32, one contiguous shard
+    per rank of a world-8 communicator — the native protocol (per-rank encode,
+    k_comm_pack, one sum-reduce, the root's fold) with its collectives over
+    the host channel, since RCCL takes one rank per GPU.  The root's sketch
+    must equal the single-GPU encode of the whole stream (> 2^32 ids, count
+    wrapping as the crate's u32) and the merge of uneven pieces; the same
+    with uneven shards (two ranks empty); a 2e6 prefix against the oracle.
+    The digests of the N = 2, 4, 8 global streams are checked against the
+    ones bench.py records for the driver's scaling runs."""
+    import torch
+    import bench
+    import sidekick_amd as sk
+    from sidekick_amd.quack import fill_splitmix
+    n, t, world, seed = 8_000_000_000, 32, 8, 0x5EED0002
+    ctx = sk.get_context(0)
+    d = torch.empty(n, dtype=torch.int32, device="cuda")
+    try:
+        fill_splitmix(ctx, d, seed)
+        whole = sk.PowerSumQuackU32(t)
+        whole.insert_batch(d)
+        assert whole.count() == n & 0xFFFFFFFF
+        assert whole.last_value() == int(coracle.splitmix_u32(seed, 1, start=n - 1)[0])
+        pieces = sk.PowerSumQuackU32(t)
+        for a, b in ((0, 3_000_000_007), (3_000_000_007, 4_294_967_301), (4_294_967_301, n - 1), (n - 1, n)):
+            pieces.insert_batch(d[a:b])
+        assert pieces == whole
+        assert pieces.power_sums() != sk.PowerSumQuackU32(t).power_sums()
+
+        for bounds in (_shards(n, world),
+                       [(0, 1_000_000_000), (1_000_000_000, 0), (1_000_000_000, 2_500_000_001),
+                        (3_500_000_001, 1), (3_500_000_002, 0), (3_500_000_002, 3_000_000_000),
+                        (6_500_000_002, 1_499_999_997), (7_999_999_999, 1)]):
+            assert sum(c for _, c in bounds) == n
+            views = [d[s:s + c] if c else d[:0] for s, c in bounds]
+
+            def rank_fn(r, comm):
+                q = sk.PowerSumQuackU32(t)
+                comm.encode_sharded([views[r]], q)
+                return q
+
+            res = _run_ranks(world, rank_fn, timeout=600)
+            assert all(ok for ok, _ in res), res
+            assert res[0][1] == whole
+            assert all(res[r][1].count() == 0 for r in range(1, world))
+
+        head = sk.PowerSumQuackU32(t)
+        head.insert_batch(d[:2_000_000])
+        assert head.power_sums() == coracle.encode_u32_seed(seed, 2_000_000, t)
+
+        got = {n: bench.digest_of(whole.power_sums(), whole.count())}
+        for m in (2_000_000_000, 4_000_000_000):
+            q = sk.PowerSumQuackU32(t)
+            q.insert_batch(d[:m])
+            got[m] = bench.digest_of(q.power_sums(), q.count())
+        print("configs[3] digests:", {f"{m:.0e}": v for m, v in got.items()})
+        for m, v in got.items():
+            rec = bench.RECORDED_DIGESTS.get((32, t, m, seed))
+            assert rec is None or rec == v, (m, rec, v)
+    finally:
+        del d
+        torch.cuda.empty_cache()

@@ -200,6 +200,61 @@ def test_knob_validation():
             ctx.set_knob(name, bad)
 
 
+P32, P64 = 4294967291, 18446744073709551557
+
+
+def _run_tiled(bits, cases):
+    """Streams long enough to saturate the grid cap: one oracle-encoded block
+    of m ids tiled R times on the device, so the expected sums are R * S_block
+    mod p exactly (the oracle stays cheap at millions of ids)."""
+    import sidekick_amd as sk
+    import torch
+    from oracle import coracle
+    out = {}
+    for name, m, R, t in cases:
+        if bits == 32:
+            blk = coracle.splitmix_u32(0xB1 + m + t, m)
+            want = coracle.encode_u32(blk, t)
+            big = torch.from_numpy(blk.view(np.int32)).cuda().repeat(R)
+            q, p = sk.PowerSumQuackU32(t), P32
+        else:
+            blk = coracle.splitmix_u64(0xB2 + m + t, m)
+            want = coracle.encode_u64(blk, t)
+            big = torch.from_numpy(blk.view(np.int64)).cuda().repeat(R)
+            q, p = sk.PowerSumQuackU64(t), P64
+        q.insert_batch(big)
+        out[name] = q.power_sums() == [(R * int(s)) % p for s in want] and q.count() == m * R \
+            and q.last_value() == int(blk[-1])
+        del big
+    return out
+
+
+@pytest.mark.parametrize("prio", [1, 0])
+def test_passes_prio_saturated_grid(prio):
+    """Multi-pass encodes (t > 80) with the x^base cache, on streams long
+    enough that every pass launches the capped grid (u32: > 256 CUs x 8 x 256
+    threads x 4 ids; u64: > 256 CUs x 8 x 3 rounds of 256-id tiles), for both
+    wave-priority instantiations: the cache placed after the partials must
+    not overlap the partials of whichever kernel the knobs select."""
+    with knob("bsgs_prio", prio):
+        res = _run_tiled(32, [("u32_t100", 100_003, 42, 100), ("u32_t200", 100_003, 42, 200)])
+    with knob("bsgs64_prio", prio):
+        res.update(_run_tiled(64, [("u64_t100", 50_021, 70, 100), ("u64_t200", 50_021, 70, 200)]))
+    assert all(res.values()), res
+
+
+@pytest.mark.parametrize("mult", [1, 3, 8])
+def test_encode_grid_mult_saturated(mult):
+    """Grid rounds 1 / 3 / 8 on streams above the resident-workgroup count at
+    every multiplier (u32 t = 32: 1280 x 8 workgroups of 1024 ids; u64 t = 80
+    and 100: 1024 x 8 tiles of 256 ids), so each multiplier really changes
+    the grid — against the tiled oracle blocks."""
+    with knob("grid_mult", mult):
+        res = _run_tiled(32, [("u32_t32", 1_000_003, 12, 32), ("u32_t129", 1_000_003, 12, 129)])
+        res.update(_run_tiled(64, [("u64_t80", 300_007, 10, 80), ("u64_t100", 300_007, 10, 100)]))
+    assert all(res.values()), res
+
+
 @pytest.mark.parametrize("mult", [1, 3, 8])
 def test_encode_grid_mult(mult):
     """Encode grids of 1, 3 (the default) and 8 rounds of resident workgroups
