@@ -584,7 +584,8 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"u64_passes", &qk_knobs::u64_passes, 0, 1},
         {"u64_xcache", &qk_knobs::u64_xcache, 0, 1},   {"u64_kmax", &qk_knobs::u64_kmax, 4, 40},
         {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
-        {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 0, 9},
+        {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 1, 9},
+        {"flow_fuse0", &qk_knobs::flow_fuse0, 0, 1},    {"flow_pipe", &qk_knobs::flow_pipe, 0, 1},
         {"flow_prio", &qk_knobs::flow_prio, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},
         {"pkt_wgpc", &qk_knobs::pkt_wgpc, 1, 16},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
         {"root_test", &qk_knobs::root_test, 0, 2},      {"rt_direct", &qk_knobs::rt_direct, 0, 1},

@@ -31,7 +31,9 @@ struct qk_knobs {
     int flow_sort = 2;     // grouping sort (radix.h, flows.hip rs_sort): 1: 8-bit digits, 256 threads, two arrays
                            // throughout; 2: pair arrays between the first and last pass; 3 / 4: 512 / 1024
                            // threads; 5 / 6: 11-bit digits, 512 / 1024 threads; 7-9: as 2, 5, 6 without LDS
-                           // staging (direct scatter); 0: hipCUB's onesweep
+                           // staging (direct scatter)
+    int flow_pipe = 1;     // 0: the flow extract probes its table in its own tile (no read one tile ahead)
+    int flow_fuse0 = 1;    // 0: the grouping sort's first-digit counts by its own pass, not fused into the extract
     int flow_prio = 0;     // 1: per-flow encode kernels with s_setprio around the MACs (1e6 flows: 7.57 vs
                            // 6.80 ms, 16 / 1e4 flows even; profiles/r04/prio/ab_flows_prio.jsonl)
     int pkt_wgpc = 4;      // packet batches: workgroups per CU

@@ -23,24 +23,30 @@
 //                       reset reruns the pass over the packets after it with
 //                       an empty table (resets are rare: one per receiver
 //                       request, media_client.rs:272).
-//   2. the occupied slots (DeviceSelect) sorted by AddrKey (two stable 48-bit
-//      radix sorts of the flows only) -> rank of each flow = output order.
-//   3. per packet slot -> rank; one stable radix sort of (rank, id) pairs over
-//      bit_width(flows) bits (1 pass for <= 256 flows) groups the ids by flow
-//      with packet order preserved (last_value = last id); offsets from the
-//      rank changes.  Flows of > SMALL_SEG ids (or any flow when T > 32) ->
-//      work items of <= 64 Ki ids per workgroup.
+//   2. the occupied slots listed in slot order (k_used_count / k_used_write)
+//      and sorted by AddrKey (radix.h over the three 32-bit words of the
+//      96-bit key, or one workgroup's rank sort for few flows) -> rank of each
+//      flow = output order.
+//   3. one stable radix sort of (key, id) pairs (radix.h) groups the ids by
+//      flow with packet order preserved (last_value = last id): keyed by the
+//      table slot when its bits need no more 8-bit passes than the flow
+//      count's (the first pass's chunk histograms come fused from step 1),
+//      else by flow rank (a per-packet slot -> rank remap first); few flows
+//      (a table of <= 8192 slots) are grouped by per-chunk slot histograms
+//      instead.  Offsets from the key changes.  Flows of > SMALL_SEG ids (or
+//      any flow when T > 32) -> work items of <= 64 Ki ids per workgroup.
 //   4. k_seg_small<Cfg>   one lane per small flow: baby-step/giant-step per id
-//      (bsgs.h) with the whole flow in that lane's registers, one plain store
-//      per (flow, power); k_seg_encode<G,K> for the work items: power chains
-//      per id, block reduction, one integer atomicAdd per (flow, power) per
-//      work item (order-independent, exact).
+//      (bsgs.h) with the whole flow in that lane's registers, writing the
+//      flow's finished qk_u32 record at its output rank; k_seg_bsgs /
+//      k_seg_encode<G,K> for the work items (one workgroup per item, one
+//      integer atomicAdd per (flow, power) per item: order-independent,
+//      exact), then k_flow_finalize_big writes those flows' records.  The
+//      key bytes come from step 2.
 // The CSR primitive qk_u32_encode_segments_device runs step 4 directly on
 // caller-grouped ids.
 #include <string.h>
 
 #include <algorithm>
-#include <hipcub/hipcub.hpp>
 #include <vector>
 
 #include "bsgs.h"
@@ -52,7 +58,7 @@
 namespace qk {
 
 static_assert(sizeof(qk_flow_key) == 12, "qk_flow_key is 12 packed bytes");
-static_assert(sizeof(qk_u32) == 16, "qk_u32 header is 4 words (k_flow_finalize writes it)");
+static_assert(sizeof(qk_u32) == 16, "qk_u32 header is 4 words (k_seg_small / k_flow_finalize_big write it)");
 
 constexpr int SG_BLOCK = 256;
 constexpr int SG_WAVES = SG_BLOCK / 64;
@@ -154,10 +160,18 @@ __global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 
 // the work-item kernel above (a long flow in one lane would stall its wave).
 constexpr uint64_t SMALL_SEG = 4096;
 
+// Output: acc_out rows [nseg][T] of folded sums (the CSR primitive), or —
+// rec != null, the per-flow batch — each flow's finished qk_u32 record
+// (header + T canonical sums) at its output rank (rseg[g], or g itself): no
+// accumulator round trip and no finalize pass for the small flows.  The last
+// id is the segment's last (packet order kept by the grouping sort) or, after
+// the histogram grouping (any order inside a flow), lastid[g].
 template <class C>
 __global__ __launch_bounds__(SG_BLOCK, 4) void k_seg_small(const uint32_t *__restrict__ ids,
                                                         const uint64_t *__restrict__ offs, uint32_t nseg,
-                                                        uint32_t T, unsigned long long *__restrict__ acc_out) {
+                                                        uint32_t T, unsigned long long *__restrict__ acc_out,
+                                                        uint32_t *__restrict__ rec, const uint32_t *__restrict__ rseg,
+                                                        const uint32_t *__restrict__ lastid) {
     const uint32_t g = blockIdx.x * SG_BLOCK + threadIdx.x;
     if (g >= nseg) return;
     const uint64_t b = offs[g], e = offs[g + 1];
@@ -189,6 +203,14 @@ __global__ __launch_bounds__(SG_BLOCK, 4) void k_seg_small(const uint32_t *__res
     }
     // power a*NB + j + 1: a = 0 row is a 64-bit sum; a >= 1 is m + c * 2^64,
     // 2^64 == 25 (mod p)
+    uint32_t *o = nullptr;
+    if (rec) {
+        o = rec + (size_t)(rseg ? rseg[g] : g) * (4 + T);
+        o[0] = T;
+        o[1] = (uint32_t)(e - b);   // count
+        o[2] = 1u;                  // has_last (a flow has >= 1 id)
+        o[3] = lastid ? lastid[g] : ids[e - 1];
+    }
 #pragma unroll
     for (int a = 0; a < C::NA; ++a) {
 #pragma unroll
@@ -198,20 +220,26 @@ __global__ __launch_bounds__(SG_BLOCK, 4) void k_seg_small(const uint32_t *__res
                 const uint64_t v = a == 0 ? (uint64_t)fold64_32(S.r0[j])
                                           : (uint64_t)fold64_32(S.m[a - 1][j]) +
                                                 fold64_32((uint64_t)S.c[a - 1][j] * 25u);
-                acc_out[(size_t)g * T + m] = fold64_32(v);
+                if (o) o[4 + m] = canon32(fold64_32(v));
+                else acc_out[(size_t)g * T + m] = fold64_32(v);
             }
         }
     }
 }
 
 // per-lane (VALU) wrap counters: SG = 0; P: s_setprio around the MACs
+// where k_seg_small writes (SmallOut: acc rows, or records by rank)
+struct SmallOut {
+    uint32_t *rec = nullptr;
+    const uint32_t *rseg = nullptr, *lastid = nullptr;
+};
 template <int P>
 static void seg_small_launch_p(uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
-                               unsigned long long *acc, hipStream_t s) {
+                               unsigned long long *acc, const SmallOut &so, hipStream_t s) {
     const dim3 grid((nseg + SG_BLOCK - 1) / SG_BLOCK), block(SG_BLOCK);
 #define QK_SMALL(NB_, NA_)                                                                                         \
     hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<NB_, NA_, 0, 1, 1, false, false, 0, false, P>>), grid, block, 0, s, ids, \
-                       d_offs, nseg, T, acc)
+                       d_offs, nseg, T, acc, so.rec, so.rseg, so.lastid)
     if (T <= 8) QK_SMALL(4, 2);
     else if (T <= 12) QK_SMALL(4, 3);
     else if (T <= 16) QK_SMALL(4, 4);
@@ -220,9 +248,9 @@ static void seg_small_launch_p(uint32_t T, const uint32_t *ids, const uint64_t *
 #undef QK_SMALL
 }
 static int seg_small_launch(int prio, uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
-                            unsigned long long *acc, hipStream_t s) {
-    if (prio) seg_small_launch_p<1>(T, ids, d_offs, nseg, acc, s);
-    else seg_small_launch_p<0>(T, ids, d_offs, nseg, acc, s);
+                            unsigned long long *acc, const SmallOut &so, hipStream_t s) {
+    if (prio) seg_small_launch_p<1>(T, ids, d_offs, nseg, acc, so, s);
+    else seg_small_launch_p<0>(T, ids, d_offs, nseg, acc, so, s);
     return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
 }
 
@@ -261,17 +289,27 @@ __device__ __forceinline__ uint64_t ft_settle(uint64_t *w, uint64_t want) {
     return o == 0 ? want : o;
 }
 
+// home slot of (src, dst): slot `mask` (all ones) is never used, so
+// SLOT_NONE then sorts after every slot on the low log2(C) bits (the by-slot
+// grouping sort)
+__device__ __forceinline__ uint32_t ft_home(uint64_t src, uint64_t dst, uint32_t mask) {
+    const uint32_t slot = ft_hash(src, dst) & mask;
+    return slot == mask ? 0 : slot;
+}
+
 // slot of (src, dst), inserting it if absent (++created when this call made
-// the flow); SLOT_NONE (and a flag) when the probe limit is reached
+// the flow); SLOT_NONE (and a flag) when the probe limit is reached.
+// first: the home slot's entry read earlier (k_flow_extract_pipe issues that
+// read one tile ahead) or null to read it here.  Any earlier read is as good
+// as a fresh one: a nonzero word is final, and a zero word is resolved by
+// the CAS below whatever was written since.
 __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t probe_limit, uint64_t src,
-                                      uint64_t dst, unsigned long long *counters, uint32_t &created) {
+                                      uint64_t dst, unsigned long long *counters, uint32_t &created,
+                                      const FlowSlot *first = nullptr) {
     const uint64_t a0 = ft_w0(src, dst), a1 = ft_w1(dst);
-    // slot `mask` (all ones) is never used: SLOT_NONE then sorts after every
-    // slot on the low log2(C) bits (the by-slot grouping sort)
-    uint32_t slot = ft_hash(src, dst) & mask;
-    if (slot == mask) slot = 0;
+    uint32_t slot = ft_home(src, dst, mask);
     for (uint32_t probe = 0; probe < probe_limit; ++probe, slot = slot + 1 == mask ? 0 : slot + 1) {
-        const FlowSlot e = tab[slot];                  // one 16-byte read: the common cases
+        const FlowSlot e = probe == 0 && first ? *first : tab[slot];   // one 16-byte read: the common cases
         if (e.w0 == a0 && e.w1 == a1) return slot;
         if (e.w0 != 0 && (e.w0 != a0 || e.w1 != 0)) continue;
         if (ft_settle(&tab[slot].w0, a0) != a0) continue;
@@ -295,21 +333,30 @@ __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t pro
 // lines are not hammered by every packet).  Writes slot (SLOT_NONE if not an
 // Insert) and id per packet; counters: [0] inserts, [1] resets, [2] distinct
 // flows, [3] flags, [4] 1 + the position of the last reset (0: none).
+// hcnt != null: also the chunk's histogram of the grouping sort's first
+// digit (slot & hmask, SLOT_NONE included), digit-major as k_rs_count writes
+// it (hcnt[d * gridDim.x + chunk]): the sort's first pass then reads no keys.
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
                                                            uint32_t stride, const qk_pkt_meta *__restrict__ meta,
                                                            uint64_t my_key_lo, uint64_t chunk,
                                                            FlowSlot *__restrict__ tab, uint32_t mask,
                                                            uint32_t probe_limit, uint32_t *__restrict__ slots,
                                                            uint32_t *__restrict__ ids,
-                                                           unsigned long long *__restrict__ counters) {
+                                                           unsigned long long *__restrict__ counters,
+                                                           uint32_t hmask, uint32_t *__restrict__ hcnt) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    __shared__ uint32_t l_hist[rsort::R];
+    if (hcnt)
+        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) l_hist[j] = 0;
     constexpr uint32_t LH = 2 * REC_TILE;                // LDS election table
     __shared__ uint64_t l_src[REC_TILE], l_dst[REC_TILE];
     __shared__ uint32_t l_lead[LH];
     __shared__ uint32_t l_slot[REC_TILE];
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
-    uint64_t n_ins = 0, n_rst = 0;   // thread 0's running totals
+    uint32_t n_ins = 0, n_rst = 0;   // this thread's inserts and resets (< 2^32 packets)
+    __shared__ unsigned long long l_ins, l_rsts;
+    if (threadIdx.x == 0) l_ins = l_rsts = 0;
     uint64_t my_rst = 0;             // 1 + this thread's last reset position (0: none)
     __shared__ unsigned long long l_rst;
     if (threadIdx.x == 0) l_rst = 0;
@@ -369,30 +416,253 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
         }
         __syncthreads();
         if (valid) {
-            slots[i] = cls == 1 ? l_slot[lead] : SLOT_NONE;
+            const uint32_t sl = cls == 1 ? l_slot[lead] : SLOT_NONE;
+            slots[i] = sl;
             ids[i] = id;
+            if (hcnt) atomicAdd(&l_hist[sl & hmask], 1u);
         }
-        const int ins = __syncthreads_count(cls == 1), rst = __syncthreads_count(cls == 2);
-        n_ins += (uint64_t)ins;
-        n_rst += (uint64_t)rst;
+        n_ins += cls == 1;   // summed once per workgroup below (no per-tile barrier count)
+        n_rst += cls == 2;
     }
     if (n_new) atomicAdd(&l_new, n_new);
     if (my_rst) atomicMax(&l_rst, (unsigned long long)my_rst);
+    if (n_ins) atomicAdd(&l_ins, (unsigned long long)n_ins);
+    if (n_rst) atomicAdd(&l_rsts, (unsigned long long)n_rst);
     __syncthreads();
+    if (hcnt)
+        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) hcnt[(size_t)j * gridDim.x + blockIdx.x] = l_hist[j];
     // one atomic per workgroup (a per-packet atomic on one address
     // serialises: 1.2 s per 1e8 packets)
     if (threadIdx.x == 0) {
-        if (n_ins) atomicAdd(&counters[0], (unsigned long long)n_ins);
-        if (n_rst) atomicAdd(&counters[1], (unsigned long long)n_rst);
+        if (l_ins) atomicAdd(&counters[0], l_ins);
+        if (l_rsts) atomicAdd(&counters[1], l_rsts);
         if (l_new) atomicAdd(&counters[2], (unsigned long long)l_new);
         if (l_rst) atomicMax(&counters[4], l_rst);
     }
 }
 
-struct SlotUsed {
-    const FlowSlot *tab;
-    __device__ bool operator()(uint32_t s) const { return tab[s].w0 != 0; }
-};
+// k_flow_extract with the table probes one tile behind (knob flow_pipe): a
+// leader issues its home slot's read right after its tile's election and
+// resolves it (hit, or the probe / CAS loop) during the NEXT tile's
+// iteration, after that tile's records are classified and elected, so the
+// read's latency (a random line of a table far larger than L2 at 1e6 flows)
+// overlaps a tile of other work instead of stalling its own.  Outputs (slot,
+// id, the fused histogram) are written one iteration late; l_slot is double
+// buffered.  Same arguments and results as k_flow_extract.
+__global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *__restrict__ bufs, uint64_t n,
+                                                                uint32_t stride, const qk_pkt_meta *__restrict__ meta,
+                                                                uint64_t my_key_lo, uint64_t chunk,
+                                                                FlowSlot *__restrict__ tab, uint32_t mask,
+                                                                uint32_t probe_limit, uint32_t *__restrict__ slots,
+                                                                uint32_t *__restrict__ ids,
+                                                                unsigned long long *__restrict__ counters,
+                                                                uint32_t hmask, uint32_t *__restrict__ hcnt) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    __shared__ uint32_t l_hist[rsort::R];
+    if (hcnt)
+        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) l_hist[j] = 0;
+    constexpr uint32_t LH = 2 * REC_TILE;                // LDS election table
+    __shared__ uint64_t l_src[REC_TILE], l_dst[REC_TILE];
+    __shared__ uint32_t l_lead[LH];
+    __shared__ uint32_t l_slot[2][REC_TILE];
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
+    uint32_t n_ins = 0, n_rst = 0;
+    __shared__ unsigned long long l_ins, l_rsts, l_rst;
+    __shared__ uint32_t l_new;
+    if (threadIdx.x == 0) { l_ins = l_rsts = l_rst = 0; l_new = 0; }
+    uint64_t my_rst = 0;
+    uint32_t n_new = 0;
+    const bool pipe = stage_pipelined(stride, REC_TILE);
+    TileStage st;
+    if (pipe && c0 < c1) stage_issue(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
+    // the previous tile's state: its packet, and for its leaders the key and
+    // the home slot's entry in flight
+    bool pv_valid = false, pv_leader = false;
+    uint64_t pv_i = 0, pv_src = 0, pv_dst = 0;
+    uint32_t pv_id = 0, pv_lead = SLOT_NONE;
+    FlowSlot pv_e{0, 0};
+    uint32_t buf = 0;   // l_slot buffer of the current tile
+    for (uint64_t p0 = c0;; p0 += REC_TILE) {
+        const bool have = p0 < c1;   // a tile this iteration (else: drain the previous one)
+        const uint64_t np = have ? (c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE) : 0;
+        __syncthreads();   // the previous election's LDS reads are done
+        uint32_t r0 = 0;
+        if (have) {
+            r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records(bufs, n, stride, p0, np, tile);
+            for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
+        }
+        __syncthreads();
+        bool valid = false, leader = false;
+        uint64_t i = p0 + threadIdx.x, src = 0, dst = 0;
+        uint32_t id = 0, lead = SLOT_NONE;
+        FlowSlot e{0, 0};
+        if (have) {
+            if (pipe && p0 + REC_TILE < c1)
+                stage_issue(bufs, n, stride, p0 + REC_TILE,
+                            c1 - p0 - REC_TILE < (uint64_t)REC_TILE ? c1 - p0 - REC_TILE : REC_TILE, st);
+            valid = threadIdx.x < np;
+            const uint8_t *rec = tile + r0 + threadIdx.x * stride;
+            int cls = 0;
+            const qk_pkt_meta m = valid ? record_meta(meta, i) : qk_pkt_meta{};
+            if (valid && record_is_incoming_udp(m, rec)) {
+                src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
+                      ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];
+                dst = ((uint64_t)rec[30] << 40) | ((uint64_t)rec[31] << 32) | ((uint64_t)rec[32] << 24) |
+                      ((uint64_t)rec[33] << 16) | ((uint64_t)rec[36] << 8) | (uint64_t)rec[37];
+                if (dst == my_key_lo) {
+                    cls = 2;
+                    my_rst = i + 1;
+                } else if (m.len == QK_BUFFER_SIZE) {
+                    cls = 1;
+                    id = record_identifier(rec);
+                }
+            }
+            n_ins += cls == 1;
+            n_rst += cls == 2;
+            l_src[threadIdx.x] = src;
+            l_dst[threadIdx.x] = dst;
+            __syncthreads();
+            if (cls == 1) {
+                uint32_t h = ft_hash(src, dst) & (LH - 1);
+                for (;;) {   // at most REC_TILE claims in LH slots: terminates
+                    const uint32_t o = atomicCAS(&l_lead[h], SLOT_NONE, threadIdx.x);
+                    if (o == SLOT_NONE) { lead = threadIdx.x; break; }
+                    if (l_src[o] == src && l_dst[o] == dst) { lead = o; break; }
+                    h = (h + 1) & (LH - 1);
+                }
+                leader = lead == threadIdx.x;
+                if (leader) e = tab[ft_home(src, dst, mask)];   // resolved next iteration
+            }
+        }
+        // the previous tile's leaders resolve their slots (its read has landed)
+        if (pv_leader)
+            l_slot[buf ^ 1][threadIdx.x] = ft_find_or_insert(tab, mask, probe_limit, pv_src, pv_dst, counters, n_new,
+                                                              &pv_e);
+        __syncthreads();
+        if (pv_valid) {
+            const uint32_t sl = pv_lead != SLOT_NONE ? l_slot[buf ^ 1][pv_lead] : SLOT_NONE;
+            slots[pv_i] = sl;
+            ids[pv_i] = pv_id;
+            if (hcnt) atomicAdd(&l_hist[sl & hmask], 1u);
+        }
+        if (!have) break;
+        pv_valid = valid;
+        pv_leader = leader;
+        pv_i = i;
+        pv_src = src;
+        pv_dst = dst;
+        pv_id = id;
+        pv_lead = lead;
+        pv_e = e;
+        buf ^= 1;
+    }
+    if (n_new) atomicAdd(&l_new, n_new);
+    if (my_rst) atomicMax(&l_rst, (unsigned long long)my_rst);
+    if (n_ins) atomicAdd(&l_ins, (unsigned long long)n_ins);
+    if (n_rst) atomicAdd(&l_rsts, (unsigned long long)n_rst);
+    __syncthreads();
+    if (hcnt)
+        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) hcnt[(size_t)j * gridDim.x + blockIdx.x] = l_hist[j];
+    if (threadIdx.x == 0) {
+        if (l_ins) atomicAdd(&counters[0], l_ins);
+        if (l_rsts) atomicAdd(&counters[1], l_rsts);
+        if (l_new) atomicAdd(&counters[2], (unsigned long long)l_new);
+        if (l_rst) atomicMax(&counters[4], l_rst);
+    }
+}
+
+// ---- the occupied slots in slot order (an ordered compaction) -------------
+// nb workgroups, workgroup w takes slots [w chunk, (w + 1) chunk) (chunk a
+// multiple of 256): k_used_count counts its occupied slots, k_used_write
+// finds its place (the counts of the workgroups before it) and writes them in
+// order, one 256-slot round at a time (ballot ranks within a wave, the wave
+// offsets in LDS); the last workgroup writes the total to *nsel.
+__global__ __launch_bounds__(256) void k_used_count(const FlowSlot *__restrict__ tab, uint64_t C, uint64_t chunk,
+                                                    uint32_t *__restrict__ wcnt) {
+    __shared__ uint32_t ws[4];
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < C ? c0 + chunk : C;
+    uint32_t k = 0;
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += 256) k += tab[i].w0 != 0;
+    uint32_t all;
+    (void)rsort::block_excl<4>(k, ws, &all);
+    if (threadIdx.x == 0) wcnt[blockIdx.x] = all;
+}
+
+__global__ __launch_bounds__(256) void k_used_write(const FlowSlot *__restrict__ tab, uint64_t C, uint64_t chunk,
+                                                    const uint32_t *__restrict__ wcnt, uint32_t *__restrict__ used,
+                                                    uint32_t *__restrict__ nsel) {
+    __shared__ uint32_t ws[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // this workgroup's place: the counts of the workgroups before it
+    uint32_t before = 0;
+    for (uint32_t w = threadIdx.x; w < blockIdx.x; w += 256) before += wcnt[w];
+    uint32_t pos;
+    (void)rsort::block_excl<4>(before, ws, &pos);
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < C ? c0 + chunk : C;
+    for (uint64_t b = c0; b < c1; b += 256) {
+        const uint64_t i = b + threadIdx.x;
+        const bool u = i < c1 && tab[i].w0 != 0;
+        const uint64_t m = __ballot(u);
+        if (lane == 0) ws[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t off = 0, round = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            off += w < wave ? ws[w] : 0u;
+            round += ws[w];
+        }
+        if (u) used[pos + off + rsort::lanes_below(m)] = (uint32_t)i;
+        pos += round;
+        __syncthreads();
+    }
+    if (blockIdx.x + 1 == gridDim.x && threadIdx.x == 0) *nsel = pos;
+}
+
+// ---- flows in ascending AddrKey order ---------------------------------------
+// The 96-bit key src48 2^48 + dst48 as three 32-bit words, least significant
+// first (an LSD sort takes them in that order)
+__device__ __forceinline__ uint32_t ft_word(const FlowSlot &e, int q) {
+    const uint64_t src = ft_src(e), dst = ft_dst(e);
+    return q == 0 ? (uint32_t)dst : q == 1 ? (uint32_t)(dst >> 32) | (uint32_t)(src & 0xFFFF) << 16
+                                           : (uint32_t)(src >> 16);
+}
+
+// key[i] = word q of slot val[i]'s key (val == slots: also copied to vals)
+__global__ void k_slot_word(const FlowSlot *__restrict__ tab, const uint32_t *__restrict__ slots, uint32_t nf, int q,
+                            uint32_t *__restrict__ key, uint32_t *__restrict__ vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nf) return;
+    const uint32_t sl = slots[i];
+    key[i] = ft_word(tab[sl], q);
+    if (vals) vals[i] = sl;
+}
+
+// few flows (nf <= KR_MAX): one workgroup ranks every key against all the
+// others in LDS (keys are distinct: one flow per occupied slot)
+constexpr uint32_t KR_MAX = 2048;
+__global__ __launch_bounds__(1024) void k_key_rank_small(const FlowSlot *__restrict__ tab,
+                                                         const uint32_t *__restrict__ used, uint32_t nf,
+                                                         uint32_t *__restrict__ sorted) {
+    __shared__ uint32_t kw[3][KR_MAX];
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) {
+        const FlowSlot e = tab[used[i]];
+        kw[0][i] = ft_word(e, 0);
+        kw[1][i] = ft_word(e, 1);
+        kw[2][i] = ft_word(e, 2);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) {
+        const uint32_t a2 = kw[2][i], a1 = kw[1][i], a0 = kw[0][i];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < nf; ++j) {
+            const uint32_t b2 = kw[2][j], b1 = kw[1][j], b0 = kw[0][j];
+            rank += b2 < a2 || (b2 == a2 && (b1 < a1 || (b1 == a1 && b0 < a0)));
+        }
+        sorted[rank] = used[i];
+    }
+}
 
 // the AddrKey halves of listed slots (either output may be null)
 __global__ void k_slot_keys(const FlowSlot *__restrict__ tab, const uint32_t *__restrict__ slot, uint32_t nf,
@@ -404,16 +674,30 @@ __global__ void k_slot_keys(const FlowSlot *__restrict__ tab, const uint32_t *__
     if (src_key) src_key[r] = ft_src(e);
 }
 
-// flows in ascending AddrKey order: rank r <-> slot; info[4r] = src, [4r+1] = dst
+// the 12 AddrKey bytes of output rank r: src48 then dst48, big-endian
+// (3 words when the array is 4-byte aligned)
+__device__ __forceinline__ void put_key(uint8_t *__restrict__ keys, uint32_t r, uint64_t a, uint64_t b) {
+    auto byte = [&](uint32_t bi) { return (uint8_t)((bi < 6 ? a : b) >> (40 - 8 * (bi % 6))); };
+    if (((uintptr_t)keys & 3) == 0) {
+        uint32_t *kw = reinterpret_cast<uint32_t *>(keys) + 3 * (size_t)r;
+#pragma unroll
+        for (uint32_t q = 0; q < 3; ++q)
+            kw[q] = (uint32_t)byte(4 * q) | (uint32_t)byte(4 * q + 1) << 8 | (uint32_t)byte(4 * q + 2) << 16 |
+                    (uint32_t)byte(4 * q + 3) << 24;
+    } else {
+        for (uint32_t bi = 0; bi < 12; ++bi) keys[12 * (size_t)r + bi] = byte(bi);
+    }
+}
+
+// flows in ascending AddrKey order: rank r <-> slot; the key bytes of rank r
 __global__ void k_slot_rank(const FlowSlot *__restrict__ tab, const uint32_t *__restrict__ slot_of_rank, uint32_t nf,
-                            uint32_t *__restrict__ rank_of_slot, uint64_t *__restrict__ info) {
+                            uint32_t *__restrict__ rank_of_slot, uint8_t *__restrict__ keys) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nf) return;
     const uint32_t s = slot_of_rank[r];
     const FlowSlot e = tab[s];
     rank_of_slot[s] = r;
-    info[4 * (uint64_t)r + 0] = ft_src(e);
-    info[4 * (uint64_t)r + 1] = ft_dst(e);
+    put_key(keys, r, ft_src(e), ft_dst(e));
 }
 
 // by-slot grouping: pos_of_slot[used[p]] = p (segments are in slot order)
@@ -422,17 +706,17 @@ __global__ void k_slot_pos(const uint32_t *__restrict__ used, uint32_t nf, uint3
     if (p < nf) pos_of_slot[used[p]] = p;
 }
 
-// by-slot grouping: output rank r -> segment perm[r]; info[4r] = src, [4r+1] = dst
+// by-slot grouping: segment (occupied-slot position) -> output rank; the key
+// bytes of rank r
 __global__ void k_rank_perm(const FlowSlot *__restrict__ tab, const uint32_t *__restrict__ slot_of_rank, uint32_t nf,
-                            const uint32_t *__restrict__ pos_of_slot, uint32_t *__restrict__ perm,
-                            uint64_t *__restrict__ info) {
+                            const uint32_t *__restrict__ pos_of_slot, uint32_t *__restrict__ rseg,
+                            uint8_t *__restrict__ keys) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nf) return;
     const uint32_t s = slot_of_rank[r];
     const FlowSlot e = tab[s];
-    perm[r] = pos_of_slot[s];
-    info[4 * (uint64_t)r + 0] = ft_src(e);
-    info[4 * (uint64_t)r + 1] = ft_dst(e);
+    rseg[pos_of_slot[s]] = r;
+    put_key(keys, r, ft_src(e), ft_dst(e));
 }
 
 // ---- histogram grouping (few flows: a table of <= HIST_MAX slots) ----------
@@ -482,6 +766,7 @@ __global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__
 __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict__ slots,
                                                       const uint32_t *__restrict__ ids, uint64_t n, uint64_t chunk,
                                                       uint32_t C, uint32_t nwg, const uint32_t *__restrict__ base,
+                                                      const uint32_t *__restrict__ spre,
                                                       uint32_t *__restrict__ grouped) {
     extern __shared__ uint32_t lc[];   // C running counts
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) lc[j] = 0;
@@ -490,7 +775,7 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
     auto one = [&](uint32_t sl, uint32_t id) {
         if (sl != SLOT_NONE) {
             const uint32_t r = atomicAdd(&lc[sl], 1u);
-            grouped[base[(size_t)sl * nwg + blockIdx.x] + r] = id;
+            grouped[spre[sl] + base[(size_t)sl * nwg + blockIdx.x] + r] = id;   // k_row_scan's two levels
         }
     };
     const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
@@ -503,23 +788,20 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
 }
 
 // histogram grouping: segment p = the p-th occupied slot (ascending), its
-// start = the place of (slot, workgroup 0)
-__global__ void k_hist_offsets(const uint32_t *__restrict__ used, uint32_t nf, const uint32_t *__restrict__ base,
-                               uint32_t nwg, uint64_t inserted, uint64_t *__restrict__ offs) {
+// start = the place of (slot, workgroup 0): the slot's prefix
+__global__ void k_hist_offsets(const uint32_t *__restrict__ used, uint32_t nf, const uint32_t *__restrict__ spre,
+                               uint64_t inserted, uint64_t *__restrict__ offs) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < nf) offs[p] = base[(size_t)used[p] * nwg];
+    if (p < nf) offs[p] = spre[used[p]];
     if (p == 0) offs[nf] = inserted;
 }
 
-// histogram grouping: info[4r+2] = count, [4r+3] = the id of the flow's last packet
-__global__ void k_hist_info(const uint32_t *__restrict__ perm, const uint64_t *__restrict__ offs, uint32_t nf,
-                            const uint32_t *__restrict__ used, const uint32_t *__restrict__ last,
-                            const uint32_t *__restrict__ ids, uint64_t *__restrict__ info) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nf) return;
-    const uint32_t g = perm[r];   // rank -> segment (slot order)
-    info[4 * (uint64_t)r + 2] = offs[g + 1] - offs[g];
-    info[4 * (uint64_t)r + 3] = ids[last[used[g]] - 1];
+// histogram grouping: lastid[p] = the id of segment p's last packet (the
+// order inside a segment is arbitrary; last[] holds the slot's last index + 1)
+__global__ void k_hist_last(const uint32_t *__restrict__ used, uint32_t nf, const uint32_t *__restrict__ last,
+                            const uint32_t *__restrict__ ids, uint32_t *__restrict__ lastid) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < nf) lastid[p] = ids[last[used[p]] - 1];
 }
 
 // by-slot grouping: segment starts of the slot-sorted packets
@@ -565,16 +847,6 @@ __global__ void k_rank_offsets(const uint32_t *__restrict__ key, uint64_t ninser
     segment_starts(key, ninserted, nf, offs, [](uint32_t k) { return k; });
 }
 
-// info[4r+2] = count, [4r+3] = last id of flow r (segment perm[r], or r)
-__global__ void k_flow_counts(const uint64_t *__restrict__ offs, const uint32_t *__restrict__ ids, uint32_t nf,
-                              const uint32_t *__restrict__ perm, uint64_t *__restrict__ info) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nf) return;
-    const uint32_t g = perm ? perm[r] : r;
-    info[4 * (uint64_t)r + 2] = offs[g + 1] - offs[g];
-    info[4 * (uint64_t)r + 3] = ids[offs[g + 1] - 1];
-}
-
 // the flows the lane-per-flow kernel does not take (all of them when !small,
 // else those of more than SMALL_SEG ids), as (segment, [lo, hi)) work-item
 // seeds in any order: the host cuts them into SEG_CHUNK items.  With many
@@ -589,61 +861,39 @@ __global__ void k_list_big(const uint64_t *__restrict__ offs, uint32_t nseg, int
     big[k] = SegItem{g, 0u, lo, hi};
 }
 
+// The records (header + T canonical sums) of the flows that went through work
+// items — big[j] = (segment g, its ids [lo, hi)), accumulator row j — at
+// their output ranks; k_seg_small wrote every other flow's record itself.
+// (32-bit index arithmetic whenever the words fit: a 64-bit division per word
+// made the all-flows form of this kernel 4x slower than its stores)
 template <typename Idx>
-__device__ __forceinline__ void flow_finalize_body(const unsigned long long *__restrict__ acc,
-                                                   const uint64_t *__restrict__ info, const uint32_t *__restrict__ perm,
-                                                   Idx nseg, uint32_t T, uint32_t *__restrict__ rec,
-                                                   uint8_t *__restrict__ keys) {
+__device__ __forceinline__ void finalize_big_body(const unsigned long long *__restrict__ acc,
+                                                  const SegItem *__restrict__ big, Idx nbig,
+                                                  const uint32_t *__restrict__ rseg,
+                                                  const uint32_t *__restrict__ lastid,
+                                                  const uint32_t *__restrict__ ids, uint32_t T,
+                                                  uint32_t *__restrict__ rec) {
     const Idx words = (Idx)4 + T, stride = (Idx)gridDim.x * blockDim.x, tid = (Idx)blockIdx.x * blockDim.x + threadIdx.x;
-    for (Idx j = tid; j < nseg * words; j += stride) {
-        const Idx i = j / words;
-        const uint32_t w = (uint32_t)(j - i * words);
+    for (Idx i = tid; i < nbig * words; i += stride) {
+        const Idx j = i / words;
+        const uint32_t w = (uint32_t)(i - j * words);
+        const SegItem it = big[j];
         uint32_t v;
         if (w == 0) v = T;
-        else if (w == 1) v = (uint32_t)info[4 * (uint64_t)i + 2];  // count
-        else if (w == 2) v = 1u;                                    // has_last
-        else if (w == 3) v = (uint32_t)info[4 * (uint64_t)i + 3];  // last_value
-        else v = canon32(fold64_32(acc[(perm ? (uint64_t)perm[i] : (uint64_t)i) * T + (w - 4)]));
-        rec[j] = v;
-    }
-    if (((uintptr_t)keys & 3) == 0) {
-        // 12 key bytes = 3 words per flow: the two 48-bit halves, big-endian
-        uint32_t *kw = reinterpret_cast<uint32_t *>(keys);
-        for (Idx j = tid; j < nseg * 3; j += stride) {
-            const Idx i = j / 3;
-            const uint32_t q = (uint32_t)(j - i * 3);
-            const uint64_t a = info[4 * (uint64_t)i], b = info[4 * (uint64_t)i + 1];
-            // byte 4q + r of the key is byte 4q + r of (a[47..0], b[47..0]) in big-endian order
-            uint32_t v = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t bi = 4 * q + r;
-                const uint64_t k = bi < 6 ? a : b;
-                v |= (uint32_t)(uint8_t)(k >> (40 - 8 * (bi % 6))) << (8 * r);
-            }
-            kw[j] = v;
-        }
-    } else {
-        for (Idx j = tid; j < nseg * 12; j += stride) {
-            const Idx i = j / 12;
-            const uint32_t bi = (uint32_t)(j - i * 12);
-            const uint64_t k = bi < 6 ? info[4 * (uint64_t)i] : info[4 * (uint64_t)i + 1];
-            keys[j] = (uint8_t)(k >> (40 - 8 * (bi % 6)));
-        }
+        else if (w == 1) v = (uint32_t)(it.hi - it.lo);                   // count
+        else if (w == 2) v = 1u;                                          // has_last
+        else if (w == 3) v = lastid ? lastid[it.seg] : ids[it.hi - 1];    // last_value
+        else v = canon32(fold64_32(acc[(uint64_t)j * T + (w - 4)]));
+        rec[(uint64_t)(rseg ? rseg[it.seg] : it.seg) * words + w] = v;
     }
 }
 
-// qk_u32 records (header + T canonical sums) and AddrKey bytes of every flow,
-// written on the device so the host receives exactly its output in two copies
-// (32-bit index arithmetic whenever the record words fit: a 64-bit division
-// per word made this kernel 4x slower than its stores)
-__global__ void k_flow_finalize(const unsigned long long *__restrict__ acc, const uint64_t *__restrict__ info,
-                                const uint32_t *__restrict__ perm, uint64_t nseg, uint32_t T,
-                                uint32_t *__restrict__ rec, uint8_t *__restrict__ keys) {
-    if (nseg * (4ull + T) < (1ull << 31) && nseg * 12 < (1ull << 31))
-        flow_finalize_body<uint32_t>(acc, info, perm, (uint32_t)nseg, T, rec, keys);
-    else
-        flow_finalize_body<uint64_t>(acc, info, perm, nseg, T, rec, keys);
+__global__ void k_flow_finalize_big(const unsigned long long *__restrict__ acc, const SegItem *__restrict__ big,
+                                    uint64_t nbig, const uint32_t *__restrict__ rseg,
+                                    const uint32_t *__restrict__ lastid, const uint32_t *__restrict__ ids, uint32_t T,
+                                    uint32_t *__restrict__ rec) {
+    if (nbig * (4ull + T) < (1ull << 31)) finalize_big_body<uint32_t>(acc, big, (uint32_t)nbig, rseg, lastid, ids, T, rec);
+    else finalize_big_body<uint64_t>(acc, big, nbig, rseg, lastid, ids, T, rec);
 }
 
 // (G, K) for a threshold: smallest G with ceil(T/G) <= 32, K = ceil(T/G) rounded to a supported size
@@ -700,11 +950,12 @@ __global__ void k_seg_last(const uint32_t *__restrict__ ids, const uint64_t *__r
 // work items of the flows k_seg_small does not take: every flow when T > 32,
 // else the flows of more than SMALL_SEG ids
 static bool small_ok(uint32_t T) { return T <= 32; }
+// (the work items of flow j of the list accumulate into row j)
 static std::vector<SegItem> seg_items_from_big(const std::vector<SegItem> &big) {
     std::vector<SegItem> items;
-    for (const SegItem &b : big)
-        for (uint64_t lo = b.lo; lo < b.hi; lo += SEG_CHUNK)
-            items.push_back({b.seg, 0u, lo, std::min<uint64_t>(lo + SEG_CHUNK, b.hi)});
+    for (size_t j = 0; j < big.size(); ++j)
+        for (uint64_t lo = big[j].lo; lo < big[j].hi; lo += SEG_CHUNK)
+            items.push_back({(uint32_t)j, 0u, lo, std::min<uint64_t>(lo + SEG_CHUNK, big[j].hi)});
     return items;
 }
 static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs, uint32_t T) {
@@ -717,17 +968,18 @@ static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs, uint32_
     return items;
 }
 
-// Segmented encode of a grouped id array into a device accumulator [nseg][T]
-// (u64, zeroed here): the small flows by k_seg_small (d_offs: the nseg + 1
-// offsets on the device), the rest by the work items from seg_items (d_items
-// holds items.size() entries).
+// Segmented encode of a grouped id array: the small flows by k_seg_small
+// (d_offs: the nseg + 1 offsets on the device) into accumulator rows or
+// records (so), the rest by the work items from seg_items (d_items holds
+// items.size() entries) into the accumulator rows item.seg of d_acc (u64,
+// acc_rows rows, zeroed here).
 static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs,
                       const std::vector<SegItem> &items, size_t nseg, uint32_t T, unsigned long long *d_acc,
-                      SegItem *d_items, hipStream_t s) {
-    QK_HIP_TRY(hipMemsetAsync(d_acc, 0, nseg * T * sizeof(uint64_t), s));
+                      size_t acc_rows, SegItem *d_items, const SmallOut &so, hipStream_t s) {
+    if (acc_rows) QK_HIP_TRY(hipMemsetAsync(d_acc, 0, acc_rows * T * sizeof(uint64_t), s));
     if (small_ok(T) && nseg) {
         hipEvent_t e0 = prof_begin(ctx, s);
-        const int rs = seg_small_launch(ctx->knobs.flow_prio, T, d_ids, d_offs, (uint32_t)nseg, d_acc, s);
+        const int rs = seg_small_launch(ctx->knobs.flow_prio, T, d_ids, d_offs, (uint32_t)nseg, d_acc, so, s);
         prof_end(ctx, s, e0);
         if (rs) return rs;
     }
@@ -817,7 +1069,7 @@ extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids,
     uint64_t *d_offs = cv.take<uint64_t>(nseg + 1);
     int rc = QK_OK;
     if (hipMemcpyAsync(d_offs, offs.data(), (nseg + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = QK_E_HIP;
-    if (!rc) rc = seg_encode(ctx, d_ids, d_offs, items, nseg, T, d_acc, d_items, s);
+    if (!rc) rc = seg_encode(ctx, d_ids, d_offs, items, nseg, T, d_acc, nseg, d_items, SmallOut{}, s);
     std::vector<uint64_t> acc(nseg * T);
     std::vector<uint32_t> last(nseg, 0);
     if (!rc && hipMemcpyAsync(acc.data(), d_acc, acc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -853,6 +1105,18 @@ static RsPlan rs_plan(const qk_ctx *ctx, uint64_t n, uint32_t wgpc) {
     return {nwg, (((n + nwg - 1) / nwg) + 3) & ~(uint64_t)3};
 }
 constexpr uint32_t RS_WGPC_MAX = 4;
+// per-digit chunk counts and their scan (k_row_scan) for one sort at a time
+struct RsScratch {
+    uint32_t *cnt, *base, *tot, *dpre;
+    unsigned int *ticket;   // zero between launches (k_row_scan resets it)
+    template <class Carver> void take(Carver &c, uint32_t nwg) {
+        cnt = c.template take<uint32_t>((size_t)rsort::RMAX * nwg);
+        base = c.template take<uint32_t>((size_t)rsort::RMAX * nwg);
+        tot = c.template take<uint32_t>(rsort::RMAX);
+        dpre = c.template take<uint32_t>(rsort::RMAX);
+        ticket = c.template take<unsigned int>(1);
+    }
+};
 // Stable sort of (key, val) by the low `bits` bits of key, 8 bits per pass,
 // ping-ponging between region X = (k0, v0) and region Y = (k1, v1); each
 // region must also hold n (key, value) pairs from k0 / k1 (arena layout: the
@@ -860,13 +1124,16 @@ constexpr uint32_t RS_WGPC_MAX = 4;
 // last writes two, the passes between use pair arrays (knob flow_sort 2, 3;
 // 1: two arrays throughout).  Returns in `where` the region holding the
 // result: 1 = Y, 0 = X (an even number of passes).
+// plan: the chunking to use instead of rs_plan's (pre0: sc.cnt already holds
+// the first pass's counts for it — k_flow_extract's fused histogram; the
+// scratch must hold RMAX x plan->nwg counts)
 template <int D, int BLK, int K, bool PAIRS, uint32_t WGPC, bool DIRECT = false>
 static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, uint64_t n, int bits,
-                     uint32_t *cnt, uint32_t *base, void *temp, size_t temp_bytes, hipStream_t s, int &where) {
+                     const RsScratch &sc, hipStream_t s, int &where, const RsPlan *plan = nullptr, bool pre0 = false) {
     static_assert(WGPC <= RS_WGPC_MAX, "scratch is sized for RS_WGPC_MAX");
     where = 0;
     if (n == 0 || bits <= 0) return QK_OK;
-    const RsPlan pl = rs_plan(ctx, n, WGPC);
+    const RsPlan pl = plan ? *plan : rs_plan(ctx, n, WGPC);
     const int passes = (bits + D - 1) / D;
     const int dd = (bits + passes - 1) / passes;   // the digit width actually used (<= D): balanced passes
     uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
@@ -876,16 +1143,19 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
         const uint32_t mask = left >= dd ? (1u << dd) - 1 : (1u << left) - 1;
         const bool ip = PAIRS && q > 0, op = PAIRS && q + 1 < passes;
         auto count = ip ? rsort::k_rs_count<D, true> : rsort::k_rs_count<D, false>;
-        hipLaunchKernelGGL(count, dim3(pl.nwg), dim3(256), 0, s, ki, n, pl.chunk, shift, mask, pl.nwg, cnt);
+        if (!(pre0 && q == 0))
+            hipLaunchKernelGGL(count, dim3(pl.nwg), dim3(256), 0, s, ki, n, pl.chunk, shift, mask, pl.nwg, sc.cnt);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
-        size_t tb = temp_bytes;
-        if (hipcub::DeviceScan::ExclusiveSum(temp, tb, cnt, base, (int)((1u << D) * pl.nwg), s) != hipSuccess)
-            return QK_E_HIP;
+        // digit-major counts -> each digit's chunk prefixes + the digits' prefix
+        hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3(1u << D), dim3(256), 0, s, sc.cnt, 1u << D, pl.nwg, sc.base,
+                           sc.tot, sc.dpre, sc.ticket);
+        if (hipGetLastError() != hipSuccess) return QK_E_HIP;
         auto kern = ip ? (op ? rsort::k_rs_scatter<D, BLK, K, true, true, DIRECT>
                              : rsort::k_rs_scatter<D, BLK, K, true, false, DIRECT>)
                        : (op ? rsort::k_rs_scatter<D, BLK, K, false, true, DIRECT>
                              : rsort::k_rs_scatter<D, BLK, K, false, false, DIRECT>);
-        hipLaunchKernelGGL(kern, dim3(pl.nwg), dim3(BLK), 0, s, ki, vi, n, pl.chunk, shift, mask, pl.nwg, base, ko, vo);
+        hipLaunchKernelGGL(kern, dim3(pl.nwg), dim3(BLK), 0, s, ki, vi, n, pl.chunk, shift, mask, pl.nwg, sc.base,
+                           sc.dpre, ko, vo);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
         std::swap(ki, ko);
         std::swap(vi, vo);
@@ -893,11 +1163,16 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
     where = passes % 2;
     return QK_OK;
 }
+// the digit width of the knob-selected variant (flow_sort 5, 6, 8, 9: 11 bits)
+static int rs_digit_bits(const qk_ctx *ctx) {
+    const int m = ctx->knobs.flow_sort;
+    return m == 5 || m == 6 || m == 8 || m == 9 ? 11 : 8;
+}
 static int rs_sort(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, uint64_t n, int bits,
-                   uint32_t *cnt, uint32_t *base, void *temp, size_t temp_bytes, hipStream_t s, int &where) {
+                   const RsScratch &sc, hipStream_t s, int &where, const RsPlan *plan = nullptr, bool pre0 = false) {
 #define QK_RS(D, BLK, K, PAIRS, WGPC, ...)                                                              \
-    return rs_sort_k<D, BLK, K, PAIRS, WGPC, ##__VA_ARGS__>(ctx, k0, v0, k1, v1, n, bits, cnt, base, temp,         \
-                                                           temp_bytes, s, where)
+    return rs_sort_k<D, BLK, K, PAIRS, WGPC, ##__VA_ARGS__>(ctx, k0, v0, k1, v1, n, bits, sc, s, where, plan, \
+                                                           pre0 && D == 8)
     switch (ctx->knobs.flow_sort) {
     case 1: QK_RS(8, 256, 16, false, 4);
     case 2: QK_RS(8, 256, 16, true, 4);
@@ -910,6 +1185,17 @@ static int rs_sort(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
     default: QK_RS(11, 1024, 8, true, 1, true);
     }
 #undef QK_RS
+}
+
+// k_flow_extract's chunking of pn packets: >= 4 tiles per workgroup, enough
+// workgroups to cover the chip (knob flow_wgpc: workgroups per CU; 4, 6, 8,
+// 12 measured, 12 best at 1e4 and 1e6 flows).  With the fused first-digit
+// histogram the grouping sort keeps this chunking (RsPlan).
+static RsPlan extract_plan(const qk_ctx *ctx, uint64_t pn) {
+    const uint64_t ntiles = (pn + REC_TILE - 1) / REC_TILE;
+    const uint64_t wg = (uint64_t)ctx->num_cus * (uint64_t)ctx->knobs.flow_wgpc;
+    const uint64_t chunk = std::max<uint64_t>(4, (ntiles + wg - 1) / wg) * REC_TILE;
+    return {(uint32_t)std::max<uint64_t>(1, (pn + chunk - 1) / chunk), chunk};
 }
 
 extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, size_t n, size_t stride,
@@ -937,43 +1223,22 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     const uint32_t T = threshold;
 
     // device scratch.  Arena 0, per packet: slot/rank key, id, their sorted
-    // copies (16 B per packet), counters, hipCUB temp storage.  Arena 2: the
-    // flow table (C slots) and slot -> rank.  Arena 1, per flow: see below.
+    // copies (16 B per packet), counters, the grouping sort's scan scratch.
+    // Arena 2: the flow table (C slots) and slot -> rank.  Arena 1, per flow:
+    // see below.
     const uint64_t cmax = std::min<uint64_t>(next_pow2(2 * (uint64_t)n + 2), 1ull << 31);
     // table slots per expected flow (knob flow_load, [2, 64], for measurements)
     const uint64_t spf = (uint64_t)ctx->knobs.flow_load;
     uint64_t C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(4096, spf * (uint64_t)ctx->flow_hint)));
-    size_t tb = 0;
-    {
-        uint32_t *u = nullptr;
-        uint64_t *k = nullptr;
-        size_t b = 0;
-        for (int bits = 1; bits <= 32; ++bits) {   // the per-packet sort runs over bit_width(flows) bits
-            if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, u, u, u, u, (uint32_t)n, 0, bits, s) != hipSuccess)
-                return QK_E_HIP;
-            tb = std::max(tb, b);
-        }
-        if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, k, u, u, (uint32_t)n, 0, 48, s) != hipSuccess)
-            return QK_E_HIP;
-        tb = std::max(tb, b);
-        if (hipcub::DeviceSelect::If(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), u, u, (int64_t)cmax,
-                                     SlotUsed{nullptr}, s) != hipSuccess)
-            return QK_E_HIP;
-        tb = std::max(tb, b);
-        if (hipcub::DeviceScan::ExclusiveSum(nullptr, b, u, u, (int)(rsort::RMAX * rs_plan(ctx, n, RS_WGPC_MAX).nwg), s) != hipSuccess)
-            return QK_E_HIP;
-        tb = std::max(tb, b);
-    }
-    const uint32_t rs_nwg = rs_plan(ctx, n, RS_WGPC_MAX).nwg;
-    uint32_t *slots = nullptr, *ids = nullptr, *key_s = nullptr, *id_s = nullptr, *rs_cnt = nullptr, *rs_base = nullptr;
+    // the grouping sort's chunk counts: its own plan's, or the extract's
+    const uint32_t rs_nwg = std::max(rs_plan(ctx, n, RS_WGPC_MAX).nwg, extract_plan(ctx, n).nwg);
+    uint32_t *slots = nullptr, *ids = nullptr, *key_s = nullptr, *id_s = nullptr;
     unsigned long long *counters = nullptr, *acc = nullptr;
-    void *temp = nullptr;
+    RsScratch rs{};
     auto layout0 = [&](Carve &c) {
         slots = c.take<uint32_t>(n); ids = c.take<uint32_t>(n); key_s = c.take<uint32_t>(n); id_s = c.take<uint32_t>(n);
         counters = c.take<unsigned long long>(5);
-        temp = c.take<char>(tb);
-        rs_cnt = c.take<uint32_t>((size_t)rsort::RMAX * rs_nwg);
-        rs_base = c.take<uint32_t>((size_t)rsort::RMAX * rs_nwg);
+        rs.take(c, rs_nwg);
     };
     {
         Carve probe{nullptr};
@@ -982,6 +1247,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         Carve cv{(char *)ctx->d_flow[0]};
         layout0(cv);
     }
+    if (hipMemsetAsync(rs.ticket, 0, sizeof(unsigned int), s) != hipSuccess) return QK_E_HIP;   // k_row_scan's
     // pass 1: filters + flow table over packets [p_from, n); a table that
     // overflows its probe limit is regrown and the pass rerun (the next batch
     // starts from this size).  When the batch holds a reset, every flow made
@@ -991,18 +1257,13 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     FlowSlot *tab = nullptr;
     uint32_t *rank_of_slot = nullptr;
     uint64_t hc[5] = {0, 0, 0, 0, 0};
+    RsPlan xpl{1, 4};
+    const bool fuse0 = rs_digit_bits(ctx) == 8 && ctx->knobs.flow_fuse0;   // the extract writes the sort's first counts
     auto pass1 = [&](uint64_t p_from) -> int {
         const uint64_t pn = n - p_from;
         const uint8_t *pb = d_bufs + p_from * stride;
         const qk_pkt_meta *pm = d_meta ? d_meta + p_from : nullptr;
-        // >= 4 tiles per workgroup, enough workgroups to cover the chip
-        const uint64_t ntiles = (pn + REC_TILE - 1) / REC_TILE;
-        // knob flow_wgpc: workgroups per CU (measurements; default 12: 4, 6, 8, 12 measured, 12 best at 1e4 and 1e6 flows)
-        const uint64_t wgpc = (uint64_t)ctx->knobs.flow_wgpc;
-        const uint64_t tiles_per_chunk =
-            std::max<uint64_t>(4, (ntiles + (uint64_t)ctx->num_cus * wgpc - 1) / ((uint64_t)ctx->num_cus * wgpc));
-        const uint64_t chunk = tiles_per_chunk * REC_TILE;
-        const uint32_t nchunks = (uint32_t)std::max<uint64_t>(1, (pn + chunk - 1) / chunk);
+        xpl = extract_plan(ctx, pn);
         for (;;) {
             {
                 Carve probe{nullptr};
@@ -1017,10 +1278,14 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipMemsetAsync(counters, 0, 5 * 8, s) != hipSuccess)
                 return QK_E_HIP;
             const uint32_t probe_limit = C == cmax ? (uint32_t)C - 1 : 64u;   // load <= 1/4 when sized from the hint
+            // the by-slot sort's first digit (8-bit variants): its passes and
+            // width as rs_sort_k cuts bits(C - 1)
+            const int cb = bit_width32((uint32_t)(C - 1)), np = (cb + 7) / 8, dd = (cb + np - 1) / np;
             if (pn)
-                hipLaunchKernelGGL(k_flow_extract, dim3(nchunks), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
-                                   pb, pn, (uint32_t)stride, pm, my_key, chunk, tab, (uint32_t)(C - 1), probe_limit,
-                                   slots, ids, counters);
+                hipLaunchKernelGGL(ctx->knobs.flow_pipe ? k_flow_extract_pipe : k_flow_extract, dim3(xpl.nwg),
+                                   dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
+                                   pb, pn, (uint32_t)stride, pm, my_key, xpl.chunk, tab, (uint32_t)(C - 1), probe_limit,
+                                   slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr);
             if (hipGetLastError() != hipSuccess ||
                 hipMemcpyAsync(hc, counters, 40, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)
@@ -1053,60 +1318,57 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     const bool dev_out = keys && sketches && is_device_ptr(keys);
     if (!rc && keys && sketches && dev_out != is_device_ptr(sketches)) rc = QK_E_INVAL;
     if (!rc && nf) {
-        // per-flow arena 1: info, acc, work items (at most one per flow plus
-        // one per SEG_CHUNK ids), output records and keys, offsets, and the
-        // flow-key sort buffers
+        // per-flow arena 1: the work-item accumulator rows and items (at most
+        // one per flow plus one per SEG_CHUNK ids), output records and keys,
+        // offsets, and the flow-key sort buffers
         const size_t items_max = (size_t)nf + inserted / SEG_CHUNK + 1;
         const size_t rec = qk_u32_size(T);
-        uint64_t *info = nullptr, *d_offs = nullptr, *kd = nullptr, *kd2 = nullptr, *ks = nullptr, *ks2 = nullptr;
+        uint64_t *d_offs = nullptr;
         SegItem *d_items = nullptr;
-        uint32_t *d_rec = nullptr, *used = nullptr, *sl2 = nullptr, *sl3 = nullptr, *nsel = nullptr, *perm = nullptr;
+        uint32_t *d_rec = nullptr, *used = nullptr, *sl3 = nullptr, *nsel = nullptr, *rseg = nullptr;
+        uint32_t *kA = nullptr, *vA = nullptr, *kB = nullptr, *vB = nullptr, *wcnt = nullptr, *lastid = nullptr;
         SegItem *big = nullptr;
         uint8_t *d_keys = nullptr;
-        void *temp2 = nullptr;   // hipCUB temp of the flow-key branch (runs beside the packet sort)
-        size_t tb2 = 0;
-        {
-            size_t b = 0;
-            uint64_t *k = nullptr;
-            uint32_t *u = nullptr;
-            if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, k, u, u, nf, 0, 48, s) != hipSuccess) rc = QK_E_HIP;
-            tb2 = std::max(tb2, b);
-            if (hipcub::DeviceSelect::If(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), u, u, (int64_t)C,
-                                         SlotUsed{nullptr}, s) != hipSuccess)
-                rc = QK_E_HIP;
-            tb2 = std::max(tb2, b);
-        }
         // histogram grouping: few flows (a table of <= HIST_MAX slots)
         const bool hist = C <= HIST_MAX && ctx->knobs.flow_hist;
         const uint32_t hnwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->num_cus * 4,
                                                                                   (n_eff + 4095) / 4096));
         const uint64_t hchunk = ((n_eff + hnwg - 1) / hnwg + 3) & ~(uint64_t)3;   // a multiple of 4 (16-byte reads)
-        uint32_t *hcnt = nullptr, *hlast = nullptr, *hbase = nullptr;
-        void *temp3 = nullptr;
-        size_t tb3 = 0;
-        if (hist) {
-            uint32_t *u = nullptr;
-            if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, u, u, (int)(C * hnwg), s) != hipSuccess) rc = QK_E_HIP;
-        }
+        uint32_t *hcnt = nullptr, *hpre = nullptr, *htot = nullptr, *hspre = nullptr, *hlast = nullptr;
+        unsigned int *hticket = nullptr;
+        // the occupied-slot compaction (unb workgroups of uchunk slots) and
+        // the flow-key sort's scan scratch (the side stream's own)
+        const uint32_t unb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (C + 4095) / 4096));
+        const uint64_t uchunk = ((C + unb - 1) / unb + 255) & ~(uint64_t)255;
+        const uint32_t ks_nwg = rs_plan(ctx, nf, RS_WGPC_MAX).nwg;
+        RsScratch krs{};
         auto layout1 = [&](Carve &c) {
             if (hist) {
                 hcnt = c.take<uint32_t>((size_t)C * hnwg);
-                hbase = c.take<uint32_t>((size_t)C * hnwg);
+                hpre = c.take<uint32_t>((size_t)C * hnwg);
+                htot = c.take<uint32_t>(C);
+                hspre = c.take<uint32_t>(C);
                 hlast = c.take<uint32_t>(C);
-                temp3 = c.take<char>(tb3);
+                hticket = c.take<unsigned int>(1);
+                lastid = c.take<uint32_t>(nf);
             }
-            info = c.take<uint64_t>((size_t)nf * 4);
-            acc = c.take<unsigned long long>((size_t)nf * T);
+            // accumulator rows of the work-item flows (< 4096 ids: none of
+            // them for t <= 32; every flow for t > 32), row j = list entry j
+            acc = c.take<unsigned long long>((size_t)(small_ok(T) ? std::min<uint64_t>(nf, inserted / (SMALL_SEG + 1))
+                                                                   : nf) * T);
             d_items = c.take<SegItem>(items_max);
             d_rec = dev_out ? (uint32_t *)sketches : (uint32_t *)c.take<uint8_t>((size_t)nf * rec);
             d_keys = dev_out ? (uint8_t *)keys : c.take<uint8_t>((size_t)nf * 12);
             d_offs = c.take<uint64_t>((size_t)nf + 1);
-            kd = c.take<uint64_t>(nf); kd2 = c.take<uint64_t>(nf); ks = c.take<uint64_t>(nf); ks2 = c.take<uint64_t>(nf);
-            used = c.take<uint32_t>(nf); sl2 = c.take<uint32_t>(nf); sl3 = c.take<uint32_t>(nf);
-            perm = c.take<uint32_t>(nf);
+            // (key word, slot) arrays of the flow-key sort, taken in this order:
+            // each key array followed by its value array holds nf pairs (radix.h)
+            kA = c.take<uint32_t>(nf); vA = c.take<uint32_t>(nf); kB = c.take<uint32_t>(nf); vB = c.take<uint32_t>(nf);
+            used = c.take<uint32_t>(nf); sl3 = c.take<uint32_t>(nf);
+            rseg = c.take<uint32_t>(nf);
             nsel = c.take<uint32_t>(2);   // [0] selected slots, [1] flows needing work items
             big = c.take<SegItem>(nf);
-            temp2 = c.take<char>(tb2);
+            wcnt = c.take<uint32_t>(unb);
+            krs.take(c, ks_nwg);
         };
         {
             Carve probe{nullptr};
@@ -1121,107 +1383,122 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const uint32_t gb = (uint32_t)std::min<uint64_t>((n_eff + 255) / 256, (uint64_t)ctx->num_cus * 8);
         // Two branches (sidekick_multi.rs:265's map iteration order, and the
         // per-packet grouping) that meet at the offsets:
-        //   side stream s2: flows in ascending AddrKey order — stable LSD sort
-        //     of the occupied slots by dst, then by src (48-bit halves) —
-        //     then slot -> segment / rank maps (nf-sized, launch-bound passes);
+        //   side stream s2: the occupied slots in slot order, then in
+        //     ascending AddrKey order (a rank sort in one workgroup for
+        //     <= KR_MAX flows, else LSD radix passes over the 96-bit key's
+        //     three words), then the key bytes of every output rank and the
+        //     segment -> rank map (nf-sized, launch-bound passes);
         //   stream s: one stable radix sort of the packets (key, id), which
         //     groups the ids by flow with packet order kept (last_value = the
         //     flow's last packet).  By slot (no remap: segments come out in
-        //     slot order and perm maps rank -> segment) when the table's
-        //     log2(C) bits need no more 8-bit passes than the flow count's;
-        //     then the sort overlaps the whole s2 branch.  Otherwise by rank
-        //     (slot -> rank remap per packet, bit_width(flows) bits), which
-        //     waits for s2 first.
+        //     slot order and rseg maps a segment to its output rank) when the
+        //     table's log2(C) bits need no more 8-bit passes than the flow
+        //     count's; then the sort is enqueued first and overlaps the whole
+        //     s2 branch (its ~40 launches would otherwise delay the sort's by
+        //     their host launch time).  Otherwise by rank (slot -> rank remap
+        //     per packet, bit_width(flows) bits), which waits for s2 first.
         const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
         const bool by_slot = (cbits + 7) / 8 <= (fbits + 7) / 8;
         const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
         hipStream_t s2 = s == ctx->copy_stream ? ctx->stream : ctx->copy_stream;
         if (!rc && (hipEventRecord(ctx->flow_ev[0], s) != hipSuccess || hipStreamWaitEvent(s2, ctx->flow_ev[0], 0) != hipSuccess))
             rc = QK_E_HIP;
-        if (!rc && hipcub::DeviceSelect::If(temp2, tb2, hipcub::CountingInputIterator<uint32_t>(0), used, nsel,
-                                            (int64_t)C, SlotUsed{tab}, s2) != hipSuccess)
-            rc = QK_E_HIP;
-        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s2, tab, used, nf, kd, (uint64_t *)nullptr);
-        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp2, tb2, kd, kd2, used, sl2, nf, 0, 48, s2) != hipSuccess)
-            rc = QK_E_HIP;
-        if (!rc) hipLaunchKernelGGL(k_slot_keys, dim3(fblocks), dim3(256), 0, s2, tab, sl2, nf, (uint64_t *)nullptr, ks);
-        if (!rc && hipcub::DeviceRadixSort::SortPairs(temp2, tb2, ks, ks2, sl2, sl3, nf, 0, 48, s2) != hipSuccess)
-            rc = QK_E_HIP;
-        if (!rc) {
+        auto side = [&]() -> int {
+            // the occupied slots in slot order
+            hipLaunchKernelGGL(k_used_count, dim3(unb), dim3(256), 0, s2, tab, C, uchunk, wcnt);
+            hipLaunchKernelGGL(k_used_write, dim3(unb), dim3(256), 0, s2, tab, C, uchunk, wcnt, used, nsel);
+            if (hipGetLastError() != hipSuccess) return QK_E_HIP;
+            // ... in AddrKey order: one workgroup's rank sort for few flows,
+            // else an LSD radix sort of (key word, slot) pairs over the key's
+            // three 32-bit words (the next word gathered through the slots)
+            const uint32_t *sorted = sl3;
+            if (nf <= KR_MAX) {
+                hipLaunchKernelGGL(k_key_rank_small, dim3(1), dim3(1024), 0, s2, tab, used, nf, sl3);
+                if (hipGetLastError() != hipSuccess) return QK_E_HIP;
+            } else {
+                if (hipMemsetAsync(krs.ticket, 0, sizeof(unsigned int), s2) != hipSuccess) return QK_E_HIP;
+                for (int q = 0; q < 3; ++q) {
+                    hipLaunchKernelGGL(k_slot_word, dim3(fblocks), dim3(256), 0, s2, tab, q ? vA : used, nf, q, kA,
+                                       q ? (uint32_t *)nullptr : vA);
+                    if (hipGetLastError() != hipSuccess) return QK_E_HIP;
+                    int where = 1;
+                    if (int e = rs_sort_k<8, 256, 16, true, RS_WGPC_MAX>(ctx, kA, vA, kB, vB, nf, 32, krs, s2, where))
+                        return e;
+                    if (where != 0) return QK_E_HIP;   // four passes: the result is back in (kA, vA)
+                }
+                sorted = vA;
+            }
             if (by_slot || hist) {
                 hipLaunchKernelGGL(k_slot_pos, dim3(fblocks), dim3(256), 0, s2, used, nf, rank_of_slot);
-                hipLaunchKernelGGL(k_rank_perm, dim3(fblocks), dim3(256), 0, s2, tab, sl3, nf, rank_of_slot, perm, info);
+                hipLaunchKernelGGL(k_rank_perm, dim3(fblocks), dim3(256), 0, s2, tab, sorted, nf, rank_of_slot, rseg,
+                                   d_keys);
             } else {
-                hipLaunchKernelGGL(k_slot_rank, dim3(fblocks), dim3(256), 0, s2, tab, sl3, nf, rank_of_slot, info);
+                hipLaunchKernelGGL(k_slot_rank, dim3(fblocks), dim3(256), 0, s2, tab, sorted, nf, rank_of_slot, d_keys);
             }
-            if (hipGetLastError() != hipSuccess || hipEventRecord(ctx->flow_ev[1], s2) != hipSuccess) rc = QK_E_HIP;
-        }
+            if (hipGetLastError() != hipSuccess || hipEventRecord(ctx->flow_ev[1], s2) != hipSuccess) return QK_E_HIP;
+            return QK_OK;
+        };
         if (!rc && hist) {
             if (hipMemsetAsync(hcnt, 0, (size_t)C * hnwg * 4, s) != hipSuccess ||
-                hipMemsetAsync(hlast, 0, (size_t)C * 4, s) != hipSuccess)
+                hipMemsetAsync(hlast, 0, (size_t)C * 4, s) != hipSuccess ||
+                hipMemsetAsync(hticket, 0, sizeof(unsigned int), s) != hipSuccess)
                 rc = QK_E_HIP;
             if (!rc) {
                 hipLaunchKernelGGL(k_hist_count, dim3(hnwg), dim3(256), (size_t)C * 8, s, slots, n_eff, hchunk, (uint32_t)C,
                                    hnwg, hcnt, hlast);
-                if (hipGetLastError() != hipSuccess ||
-                    hipcub::DeviceScan::ExclusiveSum(temp3, tb3, hcnt, hbase, (int)(C * hnwg), s) != hipSuccess)
-                    rc = QK_E_HIP;
-            }
-            if (!rc) {
+                // slot-major counts -> each slot's workgroup prefixes + the slots' prefix
+                hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3((uint32_t)C), dim3(256), 0, s, hcnt, (uint32_t)C, hnwg,
+                                   hpre, htot, hspre, hticket);
                 hipLaunchKernelGGL(k_hist_scatter, dim3(hnwg), dim3(256), (size_t)C * 4, s, slots, ids, n_eff, hchunk,
-                                   (uint32_t)C, hnwg, hbase, id_s);
-                if (hipGetLastError() != hipSuccess || hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess)
-                    rc = QK_E_HIP;
+                                   (uint32_t)C, hnwg, hpre, hspre, id_s);
+                if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
+            if (!rc) rc = side();
+            if (!rc && hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess) rc = QK_E_HIP;
             if (!rc) {
-                hipLaunchKernelGGL(k_hist_offsets, dim3(fblocks), dim3(256), 0, s, used, nf, hbase, hnwg, inserted,
-                                   d_offs);
-                hipLaunchKernelGGL(k_hist_info, dim3(fblocks), dim3(256), 0, s, perm, d_offs, nf, used, hlast, ids, info);
+                hipLaunchKernelGGL(k_hist_offsets, dim3(fblocks), dim3(256), 0, s, used, nf, hspre, inserted, d_offs);
+                hipLaunchKernelGGL(k_hist_last, dim3(fblocks), dim3(256), 0, s, used, nf, hlast, ids, lastid);
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
         } else if (!rc && by_slot) {
-            // the grouping sort: radix.h (knob flow_sort = 0: hipCUB's onesweep)
-            if (ctx->knobs.flow_sort) {
-                int where = 0;
-                rc = rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs_cnt, rs_base, temp, tb, s, where);
-                if (!rc && where == 0) {   // even number of passes: the result is in (slots, ids)
-                    std::swap(slots, key_s);
-                    std::swap(ids, id_s);
-                }
-            } else if (hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0, cbits,
-                                                          s) != hipSuccess) {
-                rc = QK_E_HIP;
+            // the grouping sort (radix.h); with the extract's fused histogram
+            // its first pass reads no keys and every pass keeps the extract's
+            // chunking
+            int where = 0;
+            rc = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where, &xpl, true)
+                       : rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where);
+            if (!rc && where == 0) {   // even number of passes: the result is in (slots, ids)
+                std::swap(slots, key_s);
+                std::swap(ids, id_s);
             }
+            if (!rc) rc = side();
             if (!rc && hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess) rc = QK_E_HIP;
             if (!rc) {
                 hipLaunchKernelGGL(k_slot_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted,
                                    rank_of_slot, nf, d_offs);
-                hipLaunchKernelGGL(k_flow_counts, dim3(fblocks), dim3(256), 0, s, d_offs, id_s, nf, perm, info);
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
         } else if (!rc) {
-            if (hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess) rc = QK_E_HIP;
+            rc = side();
+            if (!rc && hipStreamWaitEvent(s, ctx->flow_ev[1], 0) != hipSuccess) rc = QK_E_HIP;
             if (!rc) hipLaunchKernelGGL(k_slot_to_rank, dim3(gb), dim3(256), 0, s, slots, rank_of_slot, n_eff, nf);
             if (!rc && hipGetLastError() != hipSuccess) rc = QK_E_HIP;
-            if (!rc && ctx->knobs.flow_sort) {
+            if (!rc) {
                 int where = 0;
-                rc = rs_sort(ctx, slots, ids, key_s, id_s, n_eff, fbits, rs_cnt, rs_base, temp, tb, s, where);
+                rc = rs_sort(ctx, slots, ids, key_s, id_s, n_eff, fbits, rs, s, where);
                 if (!rc && where == 0) {
                     std::swap(slots, key_s);
                     std::swap(ids, id_s);
                 }
-            } else if (!rc && hipcub::DeviceRadixSort::SortPairs(temp, tb, slots, key_s, ids, id_s, (uint32_t)n_eff, 0,
-                                                                 fbits, s) != hipSuccess) {
-                rc = QK_E_HIP;
             }
             if (!rc) {
                 hipLaunchKernelGGL(k_rank_offsets, dim3(std::max(ob, 1u)), dim3(256), 0, s, key_s, inserted, nf,
                                    d_offs);
-                hipLaunchKernelGGL(k_flow_counts, dim3(fblocks), dim3(256), 0, s, d_offs, id_s, nf,
-                                   (const uint32_t *)nullptr, info);
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
         }
+        // by slot / histogram: segment g is output rank rseg[g]; by rank: g
+        const uint32_t *seg_rank = by_slot || hist ? rseg : nullptr;
         // only the flows that need work items come back to the host (none
         // in the many-small-flows case): 8 bytes of counts, then their seeds
         uint32_t hsel[2] = {0, 0};
@@ -1242,18 +1519,24 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipStreamSynchronize(s) != hipSuccess)
                 rc = QK_E_HIP;
         }
-        if (!rc) rc = seg_encode(ctx, id_s, d_offs, seg_items_from_big(bigs), nf, T, acc, d_items, s);
-        if (!rc) {
-            const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)nf * (4 + T) + 255) / 256,
+        // the small flows' records straight from k_seg_small, the work-item
+        // flows' through their accumulator rows and k_flow_finalize_big
+        SmallOut so;
+        so.rec = d_rec;
+        so.rseg = seg_rank;
+        so.lastid = hist ? lastid : nullptr;
+        if (!rc) rc = seg_encode(ctx, id_s, d_offs, seg_items_from_big(bigs), nf, T, acc, hsel[1], d_items, so, s);
+        if (!rc && hsel[1]) {
+            const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)hsel[1] * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);
-            hipLaunchKernelGGL(k_flow_finalize, dim3(fb), dim3(256), 0, s, acc, info,
-                               by_slot || hist ? (const uint32_t *)perm : nullptr, (uint64_t)nf, T, d_rec, d_keys);
-            if (hipGetLastError() != hipSuccess)
-                rc = QK_E_HIP;
-            else if (!dev_out && (hipMemcpyAsync(sketches, d_rec, (size_t)nf * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                                  hipMemcpyAsync(keys, d_keys, (size_t)nf * 12, hipMemcpyDeviceToHost, s) != hipSuccess))
-                rc = QK_E_HIP;
+            hipLaunchKernelGGL(k_flow_finalize_big, dim3(fb), dim3(256), 0, s, acc, big, (uint64_t)hsel[1], seg_rank,
+                               so.lastid, id_s, T, d_rec);
+            if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
         }
+        if (!rc && !dev_out &&
+            (hipMemcpyAsync(sketches, d_rec, (size_t)nf * rec, hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipMemcpyAsync(keys, d_keys, (size_t)nf * 12, hipMemcpyDeviceToHost, s) != hipSuccess))
+            rc = QK_E_HIP;
     }
     (void)hipStreamSynchronize(s); // the arenas are reused by the next call
     (void)hipStreamSynchronize(s == ctx->copy_stream ? ctx->stream : ctx->copy_stream);   // the flow-key branch

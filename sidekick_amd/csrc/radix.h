@@ -103,6 +103,51 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *ws, uint32_
     return before + x - v;
 }
 
+// Exclusive scan of a row-major rows x cols array of counts (the radix
+// pass's digit-major cnt[d * nwg + w]; the few-flow histogram's
+// hist[slot * nwg + w]) in two levels, one launch: workgroup r scans row r
+// into pre[r * cols + c] (the prefix within the row) and writes the row's
+// total; the last workgroup to finish (a ticket, reset for the next launch)
+// scans the totals into rpre[r].  The full exclusive prefix of (r, c) is
+// rpre[r] + pre[r * cols + c].  cols, rows <= 64 * 256 (IPT below).
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_row_scan(const uint32_t *__restrict__ cnt, uint32_t rows, uint32_t cols,
+                                                  uint32_t *__restrict__ pre, uint32_t *__restrict__ tot,
+                                                  uint32_t *__restrict__ rpre, unsigned int *__restrict__ ticket) {
+    constexpr int NW = BLK / 64;
+    __shared__ uint32_t ws[NW];
+    __shared__ bool last;
+    const uint32_t r = blockIdx.x;
+    // thread t takes the ipt consecutive entries [t ipt, (t + 1) ipt) of the row
+    auto scan_run = [&](const uint32_t *src, uint32_t len, uint32_t *dst, bool coherent) -> uint32_t {
+        const uint32_t ipt = (len + BLK - 1) / BLK;
+        const uint32_t b = threadIdx.x * ipt, e = b + ipt < len ? b + ipt : len;
+        uint32_t s = 0;
+        for (uint32_t i = b; i < e; ++i)
+            s += coherent ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : src[i];
+        uint32_t all;
+        uint32_t run = block_excl<NW>(s, ws, &all);
+        for (uint32_t i = b; i < e; ++i) {
+            const uint32_t v = coherent ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : src[i];
+            dst[i] = run;
+            run += v;
+        }
+        return all;
+    };
+    const uint32_t all = scan_run(cnt + (size_t)r * cols, cols, pre + (size_t)r * cols, false);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(tot + r, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == rows - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    __syncthreads();   // ws reused
+    scan_run(tot, rows, rpre, true);
+    if (threadIdx.x == 0) *ticket = 0;
+}
+
 // D: digit bits; BLK threads; K items per thread and sub-tile.  IP / OP:
 // input / output as one array of (key, value) pairs (keys / keys_out then
 // point at it; vals / vals_out are unused) instead of two arrays — the passes
@@ -115,6 +160,7 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
                                                     const uint32_t *__restrict__ vals, uint64_t n, uint64_t chunk,
                                                     uint32_t shift, uint32_t mask, uint32_t nwg,
                                                     const uint32_t *__restrict__ base,
+                                                    const uint32_t *__restrict__ dpre,
                                                     uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out) {
     constexpr uint32_t RD = 1u << D, TILE = BLK * K;
     constexpr int NW = BLK / 64;
@@ -138,7 +184,7 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
         const uint32_t d = (uint32_t)tid * DPT + j;
-        gp[j] = dth ? base[(size_t)d * nwg + blockIdx.x] : 0u;
+        gp[j] = dth ? base[(size_t)d * nwg + blockIdx.x] + dpre[d] : 0u;   // k_row_scan's two levels
         if (dth)
 #pragma unroll
             for (int w = 0; w < NW; ++w) wc[w][d] = 0;

@@ -680,6 +680,46 @@ QK_AVX512 static size_t gcd_small(const typename F::T *a0, size_t na, const type
     return na;
 }
 
+// The p64 rows on IFMA (52-bit limb column sums, as axmy64_ifma): d' =
+// alpha d - beta s in one pass of seven madd52 per product and one reduction.
+QK_IFMA static inline __m512i row_lanes64_ifma(__m512i d, __m512i s, uint64_t alpha, uint64_t beta) {
+    const uint64_t nb = beta ? P64 - beta : 0;
+    __m512i d0, d1, s0, s1;
+    split52(d, d0, d1);
+    split52(s, s0, s1);
+    __m512i A = _mm512_setzero_si512(), B = A, C = A;
+    prod52(A, B, C, _mm512_set1_epi64((long long)(alpha & M52)), _mm512_set1_epi64((long long)(alpha >> 52)), d0, d1);
+    prod52(A, B, C, _mm512_set1_epi64((long long)(nb & M52)), _mm512_set1_epi64((long long)(nb >> 52)), s0, s1);
+    return red_cols8(A, B, C);
+}
+template <int NV>
+QK_IFMA static size_t gcd_small64_ifma(const uint64_t *a0, size_t na, const uint64_t *b0, size_t nb, uint64_t *out) {
+    alignas(64) uint64_t buf[4 * 8 * NV] = {};
+    uint64_t *pa = buf + 8 * NV, *pb = buf + 3 * 8 * NV;
+    for (size_t i = 0; i < na; ++i) pa[i] = a0[i];
+    for (size_t i = 0; i < nb; ++i) pb[i] = b0[i];
+    while (nb) {
+        const size_t m = nb - 1;
+        const uint64_t lb = pb[m];
+        while (na > m) {
+            const uint64_t la = pa[na - 1];
+            const size_t s = na - 1 - m;
+            const size_t nv = (na + 7) / 8;
+            for (int k = 0; k < NV; ++k) {
+                if ((size_t)k >= nv) break;
+                const __m512i d = _mm512_load_si512(pa + 8 * k), x = _mm512_loadu_si512(pb + 8 * k - s);
+                _mm512_store_si512(pa + 8 * k, row_lanes64_ifma(d, x, lb, la));
+            }
+            --na;
+            while (na && !pa[na - 1]) --na;
+        }
+        std::swap(pa, pb);
+        std::swap(na, nb);
+    }
+    for (size_t i = 0; i < na; ++i) out[i] = pa[i];
+    return na;
+}
+
 // monic gcd(a, b), fraction-free: each step cancels a's leading term as
 // lead(b) a - lead(a) z^s b (no inversion; a field inverse costs ~70
 // multiplications, more than the extra row of products here), one pass per
@@ -688,7 +728,9 @@ QK_AVX512 static size_t gcd_small(const typename F::T *a0, size_t na, const type
 // are one vector row.  No vector per step: both operands live in one buffer
 // each behind P zeros (P > either size), so b zero-extended below is b's own
 // buffer read from s slots earlier, and the swap of a step swaps pointers.
-template <class F> Poly<F> gcd_rows(const Poly<F> &a0, const Poly<F> &b0, bool small) {
+// monic = false: the last nonzero remainder as the rows leave it (a scalar
+// multiple of the gcd, no inversion), {1} when coprime
+template <class F> Poly<F> gcd_rows(const Poly<F> &a0, const Poly<F> &b0, bool small, bool monic = true) {
     using T = typename F::T;
     size_t na = a0.size(), nb = b0.size();
     while (na && !a0[na - 1]) --na;
@@ -696,14 +738,28 @@ template <class F> Poly<F> gcd_rows(const Poly<F> &a0, const Poly<F> &b0, bool s
     const size_t n = std::max(na, nb);
     if (small && n <= 40 && cpu_has_avx512()) {
         T g[40];
-        const size_t ng = n <= 8    ? gcd_small<F, 1>(a0.data(), na, b0.data(), nb, g)
+        size_t ng;
+        if constexpr (F::W == 64) {
+            if (cpu_has_ifma()) {
+                const uint64_t *a = (const uint64_t *)a0.data(), *b = (const uint64_t *)b0.data();
+                uint64_t *o = (uint64_t *)g;
+                ng = n <= 8    ? gcd_small64_ifma<1>(a, na, b, nb, o)
+                     : n <= 16 ? gcd_small64_ifma<2>(a, na, b, nb, o)
+                     : n <= 24 ? gcd_small64_ifma<3>(a, na, b, nb, o)
+                     : n <= 32 ? gcd_small64_ifma<4>(a, na, b, nb, o)
+                               : gcd_small64_ifma<5>(a, na, b, nb, o);
+                goto have;
+            }
+        }
+        ng = n <= 8    ? gcd_small<F, 1>(a0.data(), na, b0.data(), nb, g)
                           : n <= 16 ? gcd_small<F, 2>(a0.data(), na, b0.data(), nb, g)
                           : n <= 24 ? gcd_small<F, 3>(a0.data(), na, b0.data(), nb, g)
                           : n <= 32 ? gcd_small<F, 4>(a0.data(), na, b0.data(), nb, g)
                                     : gcd_small<F, 5>(a0.data(), na, b0.data(), nb, g);
+    have:
         if (ng == 1) return Poly<F>{1};   // coprime: no inversion for the monic form
         Poly<F> r(g, g + ng);
-        if (!r.empty()) make_monic<F>(r);
+        if (!r.empty() && monic) make_monic<F>(r);
         return r;
     }
     const size_t P = n + 1;
@@ -726,7 +782,7 @@ template <class F> Poly<F> gcd_rows(const Poly<F> &a0, const Poly<F> &b0, bool s
     }
     if (na == 1) return Poly<F>{1};
     Poly<F> g(pa, pa + na);
-    if (!g.empty()) make_monic<F>(g);
+    if (!g.empty() && monic) make_monic<F>(g);
     return g;
 }
 template <class F> Poly<F> gcd(const Poly<F> &a, const Poly<F> &b) { return gcd_rows<F>(a, b, true); }
@@ -905,15 +961,6 @@ template <class F> typename F::T root_of_unity() {
     return z;
 }
 
-// Split g into linear factors, appending their roots.  exact: g is monic,
-// squarefree, and all its roots lie in GF(p)*: always succeeds.  !exact
-// (the fast path, any monic g with g(0) != 0): every leaf that is reached is a
-// genuine linear factor of g (split products are exact divisions), so the
-// roots appended are roots of g and, when it returns true, all of them; it
-// returns false when a factor will not split into linear ones (an
-// irreducible factor of degree >= 2, i.e. roots outside GF(p)), after a
-// quadratic with a non-residue discriminant or 24 failed attempts on one
-// factor.
 // A factor of degree k >= 3 is split L ways at once (Cantor-Zassenhaus with
 // the L-th power character): w = (z + a)^((p-1)/L) mod g takes at a root r
 // the L-th root of unity chi(r + a) = zeta^j (0 for r = -a), and the roots
@@ -927,34 +974,92 @@ template <class F> typename F::T root_of_unity() {
 template <class F> class Splitter {
     using T = typename F::T;
     const T zeta = root_of_unity<F>();
+    T zc[4];        // zeta^c, c < E: each part's first class
+    T step;         // zeta^E: the next class of a part
+    T i4;           // zeta^LO: a primitive E-th root of unity (E = 4)
 
   public:
-    // the roots of g of class j (j mod E == c) for each j, from w mod g;
-    // the factors found (and g's rest) go to parts
-    void classes(const Poly<F> &g, const Poly<F> &w, uint32_t c, std::vector<Poly<F>> &parts) const {
+    Splitter() {
+        zc[0] = 1;
+        for (uint32_t c = 1; c < 4; ++c) zc[c] = F::mul(zc[c - 1], zeta);
+        step = F::pow(zeta, F::E);
+        i4 = F::pow(zeta, F::LO);
+    }
+    // the roots of g (monic) of class j (j mod E == c) for each j, from w mod
+    // g.  p64 (E = 4: 11 classes of ~k/4 roots each): the factors found go to
+    // parts as they leave the gcd rows (a scalar multiple of the monic
+    // factor: split() makes the leaves' roots with one batched inversion,
+    // not one 128-bit-product inversion chain per factor).  Every class
+    // against the whole of g (no division of g by the factors found: the
+    // rows of a gcd of <= 8 coefficients are single vector operations, an
+    // inversion and a division per factor cost more than they save), until
+    // the degrees found add up to g's.  A root -a (w = 0 there) is in no
+    // class; whatever else is missing lies outside GF(p) (the fast path's
+    // failure case): then the found factors, made monic, and the rest.
+    void classes(const Poly<F> &g, const Poly<F> &w, uint32_t c, T a, std::vector<Poly<F>> &parts) const {
         if (g.size() <= 1) return;
         if (g.size() == 2) {
             parts.push_back(g);
             return;
         }
-        Poly<F> rem = g, wg = w;
+        const size_t k = g.size() - 1;
+        Poly<F> wg = w;
         rem_monic<F>(wg, g);
-        const T step = F::pow(zeta, F::E);
-        T zj = F::pow(zeta, c);
-        bool cut = false;
-        for (uint32_t j = c; j < F::L && rem.size() > 2; j += F::E, zj = F::mul(zj, step)) {
+        if (wg.empty()) wg.push_back(0);
+        T zj = zc[c];
+        if constexpr (F::W == 32) {
+            // p32 (E = 2, 19 classes of ~k/2 roots each): the rest shrinks
+            // as factors are found — its gcds with the later classes then run
+            // on fewer coefficients, and an inversion costs only ~70 32-bit
+            // products here (measured: +7 % for the unshrunk form at d = 32)
+            Poly<F> rem = g;
+            bool cut = false;
+            for (uint32_t j = c; j < F::L && rem.size() > 2; j += F::E, zj = F::mul(zj, step)) {
+                Poly<F> wr = wg;
+                if (cut) rem_monic<F>(wr, rem);   // w mod rem (rem == g: wg is reduced)
+                if (wr.empty()) wr.push_back(0);
+                wr[0] = F::sub(wr[0], zj);
+                Poly<F> h = gcd<F>(rem, wr);
+                if (h.size() > 1) {
+                    rem = div_monic<F>(rem, h);
+                    parts.push_back(std::move(h));
+                    cut = true;
+                }
+            }
+            if (rem.size() > 1) parts.push_back(std::move(rem));   // the last class, r = -a, or an unsplit rest
+            return;
+        }
+        std::vector<Poly<F>> hs;
+        size_t found = 0;
+        for (uint32_t j = c; j < F::L && found < k; j += F::E, zj = F::mul(zj, step)) {
             Poly<F> wr = wg;
-            if (cut) rem_monic<F>(wr, rem);   // w mod rem (rem == g: wg is reduced)
-            if (wr.empty()) wr.push_back(0);
             wr[0] = F::sub(wr[0], zj);
-            Poly<F> h = gcd<F>(rem, wr);
+            Poly<F> h = gcd_rows<F>(g, wr, true, false);
             if (h.size() > 1) {
-                rem = div_monic<F>(rem, h);
-                parts.push_back(std::move(h));
-                cut = true;
+                found += h.size() - 1;
+                hs.push_back(std::move(h));
             }
         }
-        if (rem.size() > 1) parts.push_back(std::move(rem));   // the last class, r = -a, or an unsplit rest
+        if (found < k) {   // the root -a?
+            const T x = F::neg(a);
+            T v = 1;
+            for (size_t i = k; i-- > 0;) v = F::add(F::mul(v, x), g[i]);   // g monic: Horner from z^k
+            if (v == 0) {
+                hs.push_back(Poly<F>{a, 1});
+                ++found;
+            }
+        }
+        if (found == k) {
+            for (auto &h : hs) parts.push_back(std::move(h));
+            return;
+        }
+        Poly<F> rem = g;
+        for (auto &h : hs) {
+            make_monic<F>(h);
+            rem = div_monic<F>(rem, h);
+            parts.push_back(std::move(h));
+        }
+        if (rem.size() > 1) parts.push_back(std::move(rem));
     }
     // g = gcd(g, u - c) * (g / that): the roots where u == c, and the rest
     static void cut(const Poly<F> &g, const Poly<F> &u, T c, Poly<F> &in, Poly<F> &out) {
@@ -971,39 +1076,50 @@ template <class F> class Splitter {
         const std::vector<T> wv = R.pow_lin(a, F::PM1 / F::L);
         const Poly<F> w = to_poly<F>(wv);
         if constexpr (F::E == 1) {
-            classes(g, w, 0, parts);
+            classes(g, w, 0, a, parts);
         } else {
             const std::vector<T> vv = F::LO > 1 ? R.pow(wv, F::LO) : wv;   // v = w^LO
             Poly<F> A, B;
             if constexpr (F::E == 2) {
                 cut(g, to_poly<F>(vv), 1, A, B);   // v = 1: even j; v = -1 (or r = -a): odd j
-                classes(A, w, 0, parts);
-                classes(B, w, 1, parts);
+                classes(A, w, 0, a, parts);
+                classes(B, w, 1, a, parts);
             } else {
                 static_assert(F::E == 4, "p - 1 has at most 2^2");
                 std::vector<T> qv = vv;
                 R.sqr(qv);                        // v^2 = +-1: j even / odd
                 cut(g, to_poly<F>(qv), 1, A, B);
                 const Poly<F> v = to_poly<F>(vv);
-                const T i4 = F::pow(zeta, F::LO);   // zeta^LO: a primitive 4th root of unity
                 Poly<F> A0, A2, B1, B3;
                 if (A.size() > 2) cut(A, v, 1, A0, A2);   // j = 0 / 2 mod 4
                 else A2 = A;
                 if (B.size() > 2) cut(B, v, i4, B1, B3);  // j = 1 / 3 mod 4
                 else B3 = B;
-                classes(A0, w, 0, parts);
-                classes(A2, w, 2, parts);
-                classes(B1, w, 1, parts);
-                classes(B3, w, 3, parts);
+                classes(A0, w, 0, a, parts);
+                classes(A2, w, 2, a, parts);
+                classes(B1, w, 1, a, parts);
+                classes(B3, w, 3, a, parts);
             }
         }
     }
 };
 
+// Split g into linear factors, appending their roots.  exact: g is monic,
+// squarefree, and all its roots lie in GF(p)*: always succeeds.  !exact
+// (the fast path, any monic g with g(0) != 0): every leaf that is reached is a
+// genuine linear factor of g (split products are exact divisions), so the
+// roots appended are roots of g and, when it returns true, all of them; it
+// returns false when a factor will not split into linear ones (an
+// irreducible factor of degree >= 2, i.e. roots outside GF(p)), after a
+// quadratic with a non-residue discriminant or 24 failed attempts on one
+// factor.  The factors come out of the splitting as scalar multiples of
+// their monic forms; a leaf's roots are fractions num / den whose
+// denominators are inverted together at the end (Montgomery's trick: one
+// inversion and 3 products per root instead of one inversion per factor).
 template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out, bool exact) {
     using T = typename F::T;
-    const T inv2 = F::inv(2);
     const Splitter<F> S{};
+    std::vector<T> num, den;
     std::vector<Poly<F>> todo{g0};
     uint64_t s = 0x243F6A8885A308D3ull;   // fixed seed: a deterministic sequence of a's
     while (!todo.empty()) {
@@ -1011,23 +1127,27 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
         todo.pop_back();
         const size_t k = g.size() - 1;
         if (k == 0) continue;
-        if (k == 1) {
-            out.push_back(F::neg(g[0]));
+        if (k == 1) {   // g1 z + g0
+            num.push_back(F::neg(g[0]));
+            den.push_back(g[1]);
             continue;
         }
-        if (k == 2) {   // z^2 + b z + c: (-b +- sqrt(b^2 - 4c)) / 2
-            const T b = g[1], c = g[0];
-            const T disc = F::sub(F::mul(b, b), F::mul(4, c));
+        if (k == 2) {   // g2 z^2 + g1 z + g0: (-g1 +- sqrt(g1^2 - 4 g2 g0)) / (2 g2)
+            const T a2 = g[2], b = g[1], c = g[0];
+            const T disc = F::sub(F::mul(b, b), F::mul(F::mul(4, a2), c));
             T sq;
             if (!F::sqrt(disc, sq)) {
                 if (!exact) return false;
                 continue;   // (cannot happen for an exact-mode factor)
             }
-            const T nb = F::neg(b);
-            out.push_back(F::mul(F::add(nb, sq), inv2));
-            out.push_back(F::mul(F::sub(nb, sq), inv2));
+            const T nb = F::neg(b), d2 = F::add(a2, a2);
+            num.push_back(F::add(nb, sq));
+            den.push_back(d2);
+            num.push_back(F::sub(nb, sq));
+            den.push_back(d2);
             continue;
         }
+        if (g.back() != 1) make_monic<F>(g);
         ModRing<F> R(g);
         for (int fails = 0;; ++fails) {
             if (!exact && fails >= 24) return false;
@@ -1037,6 +1157,19 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
             if (parts.size() < 2) continue;
             for (auto &p : parts) todo.push_back(std::move(p));
             break;
+        }
+    }
+    // num_i / den_i: prefix products, one inversion, back substitution
+    const size_t n = den.size();
+    if (n) {
+        std::vector<T> pre(n);
+        pre[0] = den[0];
+        for (size_t i = 1; i < n; ++i) pre[i] = F::mul(pre[i - 1], den[i]);
+        T inv = F::inv(pre[n - 1]);
+        for (size_t i = n; i-- > 0;) {
+            const T di = i ? F::mul(inv, pre[i - 1]) : inv;   // 1 / den_i
+            if (i) inv = F::mul(inv, den[i]);
+            out.push_back(F::mul(num[i], di));
         }
     }
     return true;

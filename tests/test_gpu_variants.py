@@ -194,7 +194,7 @@ def test_knob_validation():
     from sidekick_amd._lib import QuackError
     ctx = sk.get_context(0)
     for name, bad in (("flow_load", 0), ("flow_load", 65), ("root_test", 3), ("no_such_knob", 1),
-                      ("matrix_cores", 1), ("flow_sort", 10), ("comm_fault", -1), ("bsgs_prio", 2), ("bsgs64_prio", 2),
+                      ("matrix_cores", 1), ("flow_sort", 10), ("flow_sort", 0), ("comm_fault", -1), ("bsgs_prio", 2), ("bsgs64_prio", 2),
                       ("grid_mult", 0), ("grid_mult", 9)):
         with pytest.raises(QuackError):
             ctx.set_knob(name, bad)

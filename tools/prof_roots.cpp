@@ -77,8 +77,8 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
     std::vector<Poly<F>> parts;
     const double t_classes = best_us(reps, [&] {
         parts.clear();
-        S.classes(A, wp, 0, parts);
-        S.classes(B, wp, 1, parts);
+        S.classes(A, wp, 0, F::canon_any((T)777), parts);
+        S.classes(B, wp, 1, F::canon_any((T)777), parts);
     });
     const double t_inv = best_us(reps, [&] {
         T x = 3;

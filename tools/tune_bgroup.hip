@@ -157,6 +157,9 @@ int main(int argc, char **argv) {
     const uint64_t chunk = (((n + nwg - 1) / nwg) + 3) & ~(uint64_t)3;
     CK(hipMalloc(&cnt, (size_t)256 * nwg * 4));
     CK(hipMalloc(&base, (size_t)256 * nwg * 4));
+    uint32_t *zdp = nullptr;   // k_rs_scatter digit prefixes: 0 (base holds the full scan)
+    CK(hipMalloc(&zdp, rsort::RMAX * 4));
+    CK(hipMemset(zdp, 0, rsort::RMAX * 4));
     CK(hipMalloc(&st0, (size_t)C * 4));
     CK(hipMalloc(&la0, (size_t)C * 4));
     CK(hipMalloc(&st1, (size_t)C * 4));
@@ -175,7 +178,7 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, 0, cnt, base, 256 * nwg);
         auto kern = ip ? (op ? rsort::k_rs_scatter<8, 256, 16, true, true> : rsort::k_rs_scatter<8, 256, 16, true, false>)
                        : (op ? rsort::k_rs_scatter<8, 256, 16, false, true> : rsort::k_rs_scatter<8, 256, 16, false, false>);
-        hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), 0, 0, ki, vi, n, chunk, shift, 0xFFu, nwg, base, ko, vo);
+        hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), 0, 0, ki, vi, n, chunk, shift, 0xFFu, nwg, base, zdp, ko, vo);
     };
     float best[3] = {1e30f, 1e30f, 1e30f};   // radix3 + starts, bucket pass + group, bucket pass alone
     for (int r = 0; r < rounds; ++r) {

@@ -87,6 +87,9 @@ int main(int argc, char **argv) {
     const uint32_t nwg4 = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 4, (n + 4095) / 4096);
     CK(hipMalloc(&cnt, (size_t)rsort::R * nwg4 * 4));
     CK(hipMalloc(&base, (size_t)rsort::R * nwg4 * 4));
+    uint32_t *zdp = nullptr;   // k_rs_scatter digit prefixes: 0 (base holds the full scan)
+    CK(hipMalloc(&zdp, rsort::RMAX * 4));
+    CK(hipMemset(zdp, 0, rsort::RMAX * 4));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -123,13 +126,13 @@ int main(int argc, char **argv) {
             default:
                 if (v.kind == 4)
                     hipLaunchKernelGGL((rsort::k_rs_scatter<8, 256, 16, false, true, true>), dim3(nwg), dim3(256), 0, 0,
-                                       k0, v0, n, chunk, 0u, 0xFFu, nwg, base, k1, v1);
+                                       k0, v0, n, chunk, 0u, 0xFFu, nwg, base, zdp, k1, v1);
                 else if (v.blk == 1024)
                     hipLaunchKernelGGL((rsort::k_rs_scatter<8, 1024, 16, false, true>), dim3(nwg), dim3(1024), 0, 0, k0, v0,
-                                       n, chunk, 0u, 0xFFu, nwg, base, k1, v1);
+                                       n, chunk, 0u, 0xFFu, nwg, base, zdp, k1, v1);
                 else
                     hipLaunchKernelGGL((rsort::k_rs_scatter<8, 256, 16, false, true>), dim3(nwg), dim3(256), 0, 0, k0, v0,
-                                       n, chunk, 0u, 0xFFu, nwg, base, k1, v1);
+                                       n, chunk, 0u, 0xFFu, nwg, base, zdp, k1, v1);
             }
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
