@@ -32,8 +32,10 @@ struct qk_knobs {
                            // throughout; 2: pair arrays between the first and last pass; 3 / 4: 512 / 1024
                            // threads; 5 / 6: 11-bit digits, 512 / 1024 threads; 7-9: as 2, 5, 6 without LDS
                            // staging (direct scatter)
-    int flow_pipe = 1;     // 0: the flow extract probes its table in its own tile (no read one tile ahead)
+    int flow_pipe = 0;     // 1: the flow extract reads its table one tile ahead (k_flow_extract_pipe: slower,
+                           // 1e6 flows 7.14 vs 6.25 ms, 1e4 4.42 vs 4.11; profiles/r05/check4/ab_pipe.log)
     int flow_fuse0 = 1;    // 0: the grouping sort's first-digit counts by its own pass, not fused into the extract
+                           // (1e6 flows 6.71 vs 6.61 ms, 1e4 4.46 vs 4.42; profiles/r05/check4/ab_fuse0.log)
     int flow_prio = 0;     // 1: per-flow encode kernels with s_setprio around the MACs (1e6 flows: 7.57 vs
                            // 6.80 ms, 16 / 1e4 flows even; profiles/r04/prio/ab_flows_prio.jsonl)
     int pkt_wgpc = 4;      // packet batches: workgroups per CU
