@@ -457,8 +457,25 @@ def main():
     strong = dec = None
     ranks = None
     if world > 1:
-        strong = strong_scaling_check(args, comm, ctx, ids, rank, world, dev_index, bits, t)
-        dec = decode_check(comm, ctx, ids, n, rank, world, bits)
+        # untimed checks after the measurement: a failure is reported in the
+        # line, not raised (the measured value stands).  The native
+        # communicator makes a collective's failure the same status on every
+        # rank; the ranks also agree over gloo before the next check starts,
+        # so none enters a collective its peers have left.
+        def agreed(fn, *a):
+            err = None
+            try:
+                res = fn(*a)
+            except Exception as e:  # noqa: BLE001
+                res, err = None, f"{type(e).__name__}: {e}"
+                log(f"rank {rank}: {fn.__name__} failed: {err}")
+            bad = torch.tensor([1 if err else 0], dtype=torch.int64)
+            dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+            if int(bad.item()):
+                return {"error": err or f"failed on {int(bad.item())} other rank(s)"}, False
+            return res, True
+        strong, ok = agreed(strong_scaling_check, args, comm, ctx, ids, rank, world, dev_index, bits, t)
+        dec = agreed(decode_check, comm, ctx, ids, n, rank, world, bits)[0] if ok else {"error": "skipped"}
         info = comm.rccl_info()
         props = torch.cuda.get_device_properties(dev_index)
         mine = {"rank": rank, "local_rank": local, "device": dev_index,

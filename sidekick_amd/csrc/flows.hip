@@ -335,7 +335,8 @@ __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t pro
 // flows, [3] flags, [4] 1 + the position of the last reset (0: none).
 // hcnt != null: also the chunk's histogram of the grouping sort's first
 // digit (slot & hmask, SLOT_NONE included), digit-major as k_rs_count writes
-// it (hcnt[d * gridDim.x + chunk]): the sort's first pass then reads no keys.
+// it, added into the sort's chunk (hgroup consecutive extract chunks; hcnt
+// zeroed first): the sort's first pass then reads no keys.
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
                                                            uint32_t stride, const qk_pkt_meta *__restrict__ meta,
                                                            uint64_t my_key_lo, uint64_t chunk,
@@ -343,7 +344,8 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
                                                            uint32_t probe_limit, uint32_t *__restrict__ slots,
                                                            uint32_t *__restrict__ ids,
                                                            unsigned long long *__restrict__ counters,
-                                                           uint32_t hmask, uint32_t *__restrict__ hcnt) {
+                                                           uint32_t hmask, uint32_t *__restrict__ hcnt,
+                                                           uint32_t hgroup) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
     __shared__ uint32_t l_hist[rsort::R];
     if (hcnt)
@@ -430,7 +432,8 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     if (n_rst) atomicAdd(&l_rsts, (unsigned long long)n_rst);
     __syncthreads();
     if (hcnt)
-        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) hcnt[(size_t)j * gridDim.x + blockIdx.x] = l_hist[j];
+        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE)
+            if (l_hist[j]) atomicAdd(&hcnt[(size_t)j * ((gridDim.x + hgroup - 1) / hgroup) + blockIdx.x / hgroup], l_hist[j]);
     // one atomic per workgroup (a per-packet atomic on one address
     // serialises: 1.2 s per 1e8 packets)
     if (threadIdx.x == 0) {
@@ -456,7 +459,8 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
                                                                 uint32_t probe_limit, uint32_t *__restrict__ slots,
                                                                 uint32_t *__restrict__ ids,
                                                                 unsigned long long *__restrict__ counters,
-                                                                uint32_t hmask, uint32_t *__restrict__ hcnt) {
+                                                                uint32_t hmask, uint32_t *__restrict__ hcnt,
+                                                           uint32_t hgroup) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
     __shared__ uint32_t l_hist[rsort::R];
     if (hcnt)
@@ -563,7 +567,8 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
     if (n_rst) atomicAdd(&l_rsts, (unsigned long long)n_rst);
     __syncthreads();
     if (hcnt)
-        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) hcnt[(size_t)j * gridDim.x + blockIdx.x] = l_hist[j];
+        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE)
+            if (l_hist[j]) atomicAdd(&hcnt[(size_t)j * ((gridDim.x + hgroup - 1) / hgroup) + blockIdx.x / hgroup], l_hist[j]);
     if (threadIdx.x == 0) {
         if (l_ins) atomicAdd(&counters[0], l_ins);
         if (l_rsts) atomicAdd(&counters[1], l_rsts);
@@ -1105,16 +1110,17 @@ static RsPlan rs_plan(const qk_ctx *ctx, uint64_t n, uint32_t wgpc) {
     return {nwg, (((n + nwg - 1) / nwg) + 3) & ~(uint64_t)3};
 }
 constexpr uint32_t RS_WGPC_MAX = 4;
-// per-digit chunk counts and their scan (k_row_scan) for one sort at a time
+// per-digit chunk counts, their prefixes within each digit and the digit
+// totals (k_row_scan) for one sort at a time; dig: one byte per item, the
+// next pass's 8-bit digit written by the scatter
 struct RsScratch {
-    uint32_t *cnt, *base, *tot, *dpre;
-    unsigned int *ticket;   // zero between launches (k_row_scan resets it)
-    template <class Carver> void take(Carver &c, uint32_t nwg) {
+    uint32_t *cnt, *base, *tot;
+    uint8_t *dig;
+    template <class Carver> void take(Carver &c, uint32_t nwg, uint64_t n) {
         cnt = c.template take<uint32_t>((size_t)rsort::RMAX * nwg);
         base = c.template take<uint32_t>((size_t)rsort::RMAX * nwg);
         tot = c.template take<uint32_t>(rsort::RMAX);
-        dpre = c.template take<uint32_t>(rsort::RMAX);
-        ticket = c.template take<unsigned int>(1);
+        dig = c.template take<uint8_t>(n + 16);
     }
 };
 // Stable sort of (key, val) by the low `bits` bits of key, 8 bits per pass,
@@ -1133,7 +1139,9 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
     static_assert(WGPC <= RS_WGPC_MAX, "scratch is sized for RS_WGPC_MAX");
     where = 0;
     if (n == 0 || bits <= 0) return QK_OK;
-    const RsPlan pl = plan ? *plan : rs_plan(ctx, n, WGPC);
+    const RsPlan pl0 = plan ? *plan : rs_plan(ctx, n, WGPC);
+    // the digit byte stream needs 16-item chunks (k_rs_count8's loads)
+    const RsPlan pl = D == 8 ? RsPlan{pl0.nwg, (pl0.chunk + 15) & ~(uint64_t)15} : pl0;
     const int passes = (bits + D - 1) / D;
     const int dd = (bits + passes - 1) / passes;   // the digit width actually used (<= D): balanced passes
     uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
@@ -1143,19 +1151,26 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
         const uint32_t mask = left >= dd ? (1u << dd) - 1 : (1u << left) - 1;
         const bool ip = PAIRS && q > 0, op = PAIRS && q + 1 < passes;
         auto count = ip ? rsort::k_rs_count<D, true> : rsort::k_rs_count<D, false>;
-        if (!(pre0 && q == 0))
+        if (D == 8 && q > 0)   // the previous scatter wrote this pass's digits as bytes
+            hipLaunchKernelGGL(rsort::k_rs_count8, dim3(pl.nwg), dim3(256), 0, s, sc.dig, n, pl.chunk, pl.nwg, sc.cnt);
+        else if (!(pre0 && q == 0))
             hipLaunchKernelGGL(count, dim3(pl.nwg), dim3(256), 0, s, ki, n, pl.chunk, shift, mask, pl.nwg, sc.cnt);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
-        // digit-major counts -> each digit's chunk prefixes + the digits' prefix
-        hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3(1u << D), dim3(256), 0, s, sc.cnt, 1u << D, pl.nwg, sc.base,
-                           sc.tot, sc.dpre, sc.ticket);
+        // digit-major counts -> each digit's chunk prefixes + the digit totals
+        // (the scatter scans the totals itself)
+        hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3(1u << D), dim3(256), 0, s, sc.cnt, pl.nwg, sc.base, sc.tot);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
         auto kern = ip ? (op ? rsort::k_rs_scatter<D, BLK, K, true, true, DIRECT>
                              : rsort::k_rs_scatter<D, BLK, K, true, false, DIRECT>)
                        : (op ? rsort::k_rs_scatter<D, BLK, K, false, true, DIRECT>
                              : rsort::k_rs_scatter<D, BLK, K, false, false, DIRECT>);
+        // the next pass's digit as a byte beside each item (8-bit digits)
+        const bool nd = D == 8 && q + 1 < passes;
+        const uint32_t nshift = (uint32_t)((q + 1) * dd);
+        const int nleft = bits - (q + 1) * dd;
+        const uint32_t nmask = nleft >= dd ? (1u << dd) - 1 : (1u << (nleft > 0 ? nleft : 0)) - 1;
         hipLaunchKernelGGL(kern, dim3(pl.nwg), dim3(BLK), 0, s, ki, vi, n, pl.chunk, shift, mask, pl.nwg, sc.base,
-                           sc.dpre, ko, vo);
+                           sc.tot, ko, vo, nd ? sc.dig : (uint8_t *)nullptr, nshift, nmask);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
         std::swap(ki, ko);
         std::swap(vi, vo);
@@ -1238,7 +1253,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     auto layout0 = [&](Carve &c) {
         slots = c.take<uint32_t>(n); ids = c.take<uint32_t>(n); key_s = c.take<uint32_t>(n); id_s = c.take<uint32_t>(n);
         counters = c.take<unsigned long long>(5);
-        rs.take(c, rs_nwg);
+        rs.take(c, rs_nwg, n);
     };
     {
         Carve probe{nullptr};
@@ -1247,7 +1262,6 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         Carve cv{(char *)ctx->d_flow[0]};
         layout0(cv);
     }
-    if (hipMemsetAsync(rs.ticket, 0, sizeof(unsigned int), s) != hipSuccess) return QK_E_HIP;   // k_row_scan's
     // pass 1: filters + flow table over packets [p_from, n); a table that
     // overflows its probe limit is regrown and the pass rerun (the next batch
     // starts from this size).  When the batch holds a reset, every flow made
@@ -1257,7 +1271,12 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     FlowSlot *tab = nullptr;
     uint32_t *rank_of_slot = nullptr;
     uint64_t hc[5] = {0, 0, 0, 0, 0};
-    RsPlan xpl{1, 4};
+    RsPlan xpl{1, 4};   // the extract's chunking of the last pass 1
+    // the grouping sort's chunks when the extract counts its first digit: hg
+    // consecutive extract chunks each (~RS_WGPC_MAX workgroups per CU: the
+    // scatter's LDS allows 4; the extract's 12 per CU measured slower)
+    const uint32_t hg = std::max<uint32_t>(1, ((uint32_t)ctx->knobs.flow_wgpc + RS_WGPC_MAX - 1) / RS_WGPC_MAX);
+    auto sort_plan = [&]() { return RsPlan{(xpl.nwg + hg - 1) / hg, xpl.chunk * hg}; };
     const bool fuse0 = rs_digit_bits(ctx) == 8 && ctx->knobs.flow_fuse0;   // the extract writes the sort's first counts
     auto pass1 = [&](uint64_t p_from) -> int {
         const uint64_t pn = n - p_from;
@@ -1275,7 +1294,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 rank_of_slot = cv.take<uint32_t>(C);
             }
             if (hipMemsetAsync(tab, 0, C * sizeof(FlowSlot), s) != hipSuccess ||
-                hipMemsetAsync(counters, 0, 5 * 8, s) != hipSuccess)
+                hipMemsetAsync(counters, 0, 5 * 8, s) != hipSuccess ||
+                (fuse0 && hipMemsetAsync(rs.cnt, 0, (size_t)rsort::R * sort_plan().nwg * 4, s) != hipSuccess))
                 return QK_E_HIP;
             const uint32_t probe_limit = C == cmax ? (uint32_t)C - 1 : 64u;   // load <= 1/4 when sized from the hint
             // the by-slot sort's first digit (8-bit variants): its passes and
@@ -1285,7 +1305,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipLaunchKernelGGL(ctx->knobs.flow_pipe ? k_flow_extract_pipe : k_flow_extract, dim3(xpl.nwg),
                                    dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
                                    pb, pn, (uint32_t)stride, pm, my_key, xpl.chunk, tab, (uint32_t)(C - 1), probe_limit,
-                                   slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr);
+                                   slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr, hg);
             if (hipGetLastError() != hipSuccess ||
                 hipMemcpyAsync(hc, counters, 40, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)
@@ -1335,7 +1355,6 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                                                                                   (n_eff + 4095) / 4096));
         const uint64_t hchunk = ((n_eff + hnwg - 1) / hnwg + 3) & ~(uint64_t)3;   // a multiple of 4 (16-byte reads)
         uint32_t *hcnt = nullptr, *hpre = nullptr, *htot = nullptr, *hspre = nullptr, *hlast = nullptr;
-        unsigned int *hticket = nullptr;
         // the occupied-slot compaction (unb workgroups of uchunk slots) and
         // the flow-key sort's scan scratch (the side stream's own)
         const uint32_t unb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (C + 4095) / 4096));
@@ -1349,7 +1368,6 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 htot = c.take<uint32_t>(C);
                 hspre = c.take<uint32_t>(C);
                 hlast = c.take<uint32_t>(C);
-                hticket = c.take<unsigned int>(1);
                 lastid = c.take<uint32_t>(nf);
             }
             // accumulator rows of the work-item flows (< 4096 ids: none of
@@ -1368,7 +1386,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             nsel = c.take<uint32_t>(2);   // [0] selected slots, [1] flows needing work items
             big = c.take<SegItem>(nf);
             wcnt = c.take<uint32_t>(unb);
-            krs.take(c, ks_nwg);
+            krs.take(c, ks_nwg, nf);
         };
         {
             Carve probe{nullptr};
@@ -1416,7 +1434,6 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipLaunchKernelGGL(k_key_rank_small, dim3(1), dim3(1024), 0, s2, tab, used, nf, sl3);
                 if (hipGetLastError() != hipSuccess) return QK_E_HIP;
             } else {
-                if (hipMemsetAsync(krs.ticket, 0, sizeof(unsigned int), s2) != hipSuccess) return QK_E_HIP;
                 for (int q = 0; q < 3; ++q) {
                     hipLaunchKernelGGL(k_slot_word, dim3(fblocks), dim3(256), 0, s2, tab, q ? vA : used, nf, q, kA,
                                        q ? (uint32_t *)nullptr : vA);
@@ -1440,15 +1457,14 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         };
         if (!rc && hist) {
             if (hipMemsetAsync(hcnt, 0, (size_t)C * hnwg * 4, s) != hipSuccess ||
-                hipMemsetAsync(hlast, 0, (size_t)C * 4, s) != hipSuccess ||
-                hipMemsetAsync(hticket, 0, sizeof(unsigned int), s) != hipSuccess)
+                hipMemsetAsync(hlast, 0, (size_t)C * 4, s) != hipSuccess)
                 rc = QK_E_HIP;
             if (!rc) {
                 hipLaunchKernelGGL(k_hist_count, dim3(hnwg), dim3(256), (size_t)C * 8, s, slots, n_eff, hchunk, (uint32_t)C,
                                    hnwg, hcnt, hlast);
-                // slot-major counts -> each slot's workgroup prefixes + the slots' prefix
-                hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3((uint32_t)C), dim3(256), 0, s, hcnt, (uint32_t)C, hnwg,
-                                   hpre, htot, hspre, hticket);
+                // slot-major counts -> each slot's workgroup prefixes, then the slots' prefix
+                hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3((uint32_t)C), dim3(256), 0, s, hcnt, hnwg, hpre, htot);
+                hipLaunchKernelGGL(rsort::k_tot_scan<1024>, dim3(1), dim3(1024), 0, s, htot, (uint32_t)C, hspre);
                 hipLaunchKernelGGL(k_hist_scatter, dim3(hnwg), dim3(256), (size_t)C * 4, s, slots, ids, n_eff, hchunk,
                                    (uint32_t)C, hnwg, hpre, hspre, id_s);
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
@@ -1465,7 +1481,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             // its first pass reads no keys and every pass keeps the extract's
             // chunking
             int where = 0;
-            rc = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where, &xpl, true)
+            const RsPlan spl = sort_plan();
+            rc = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where, &spl, true)
                        : rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where);
             if (!rc && where == 0) {   // even number of passes: the result is in (slots, ids)
                 std::swap(slots, key_s);

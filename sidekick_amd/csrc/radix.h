@@ -75,6 +75,30 @@ __global__ __launch_bounds__(256) void k_rs_count(const uint32_t *__restrict__ k
     for (uint32_t j = threadIdx.x; j < RD; j += blockDim.x) cnt[(size_t)j * nwg + blockIdx.x] = h[j];
 }
 
+// the same histogram from a byte per item: the digit the previous pass's
+// scatter wrote beside each item (k_rs_scatter nd_out), 16 per load — the
+// pass reads 1 byte per item instead of the 8 of a (key, value) pair
+__global__ __launch_bounds__(256) void k_rs_count8(const uint8_t *__restrict__ dig, uint64_t n, uint64_t chunk,
+                                                   uint32_t nwg, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t h[R];
+    for (uint32_t j = threadIdx.x; j < R; j += blockDim.x) h[j] = 0;
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+    // chunk is a multiple of 16 here (rs_sort_k), dig 16-byte aligned
+    const uint64_t v1 = c0 < c1 ? c0 + ((c1 - c0) & ~(uint64_t)15) : c0;
+    for (uint64_t i = c0 + 16 * threadIdx.x; i < v1; i += 16 * blockDim.x) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(dig + i);
+        const uint32_t q[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) atomicAdd(&h[(q[k] >> (8 * b)) & 0xFFu], 1u);
+    }
+    for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) atomicAdd(&h[dig[i]], 1u);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < R; j += blockDim.x) cnt[(size_t)j * nwg + blockIdx.x] = h[j];
+}
+
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -105,47 +129,54 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *ws, uint32_
 
 // Exclusive scan of a row-major rows x cols array of counts (the radix
 // pass's digit-major cnt[d * nwg + w]; the few-flow histogram's
-// hist[slot * nwg + w]) in two levels, one launch: workgroup r scans row r
-// into pre[r * cols + c] (the prefix within the row) and writes the row's
-// total; the last workgroup to finish (a ticket, reset for the next launch)
-// scans the totals into rpre[r].  The full exclusive prefix of (r, c) is
-// rpre[r] + pre[r * cols + c].  cols, rows <= 64 * 256 (IPT below).
+// hist[slot * nwg + w]) in two levels: k_row_scan (workgroup r) scans row r
+// into pre[r * cols + c], the prefix within the row, and writes the row's
+// total; the prefix of the row totals comes from k_tot_scan (one workgroup)
+// or, for the radix pass's 2^D digits, from the scatter kernel itself.  The
+// full exclusive prefix of (r, c) is rpre[r] + pre[r * cols + c].  (A
+// last-workgroup ticket instead of the second step serialised 4096
+// workgroups on one atomic: 0.19 ms for the histogram's 4096 x 1024.)
 template <int BLK>
-__global__ __launch_bounds__(BLK) void k_row_scan(const uint32_t *__restrict__ cnt, uint32_t rows, uint32_t cols,
-                                                  uint32_t *__restrict__ pre, uint32_t *__restrict__ tot,
-                                                  uint32_t *__restrict__ rpre, unsigned int *__restrict__ ticket) {
+__device__ __forceinline__ uint32_t block_scan_run(const uint32_t *__restrict__ src, uint32_t len,
+                                                   uint32_t *__restrict__ dst, uint32_t *ws) {
     constexpr int NW = BLK / 64;
-    __shared__ uint32_t ws[NW];
-    __shared__ bool last;
-    const uint32_t r = blockIdx.x;
-    // thread t takes the ipt consecutive entries [t ipt, (t + 1) ipt) of the row
-    auto scan_run = [&](const uint32_t *src, uint32_t len, uint32_t *dst, bool coherent) -> uint32_t {
-        const uint32_t ipt = (len + BLK - 1) / BLK;
-        const uint32_t b = threadIdx.x * ipt, e = b + ipt < len ? b + ipt : len;
-        uint32_t s = 0;
-        for (uint32_t i = b; i < e; ++i)
-            s += coherent ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : src[i];
-        uint32_t all;
-        uint32_t run = block_excl<NW>(s, ws, &all);
-        for (uint32_t i = b; i < e; ++i) {
-            const uint32_t v = coherent ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : src[i];
-            dst[i] = run;
-            run += v;
-        }
+    // thread t takes the ipt consecutive entries [t ipt, (t + 1) ipt); four
+    // per thread (a row of 4 BLK): one 16-byte load and store
+    uint32_t all;
+    if (len == 4u * BLK && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+        const uint4 v = reinterpret_cast<const uint4 *>(src)[threadIdx.x];
+        const uint32_t run = block_excl<NW>(v.x + v.y + v.z + v.w, ws, &all);
+        reinterpret_cast<uint4 *>(dst)[threadIdx.x] = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
         return all;
-    };
-    const uint32_t all = scan_run(cnt + (size_t)r * cols, cols, pre + (size_t)r * cols, false);
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(tot + r, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence();
-        last = atomicAdd(ticket, 1u) == rows - 1;
     }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    __syncthreads();   // ws reused
-    scan_run(tot, rows, rpre, true);
-    if (threadIdx.x == 0) *ticket = 0;
+    const uint32_t ipt = (len + BLK - 1) / BLK;
+    const uint32_t b = threadIdx.x * ipt, e = b + ipt < len ? b + ipt : len;
+    uint32_t s = 0;
+    for (uint32_t i = b; i < e; ++i) s += src[i];
+    uint32_t run = block_excl<NW>(s, ws, &all);
+    for (uint32_t i = b; i < e; ++i) {
+        const uint32_t v = src[i];
+        dst[i] = run;
+        run += v;
+    }
+    return all;
+}
+
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_row_scan(const uint32_t *__restrict__ cnt, uint32_t cols,
+                                                  uint32_t *__restrict__ pre, uint32_t *__restrict__ tot) {
+    __shared__ uint32_t ws[BLK / 64];
+    const uint32_t r = blockIdx.x;
+    const uint32_t all = block_scan_run<BLK>(cnt + (size_t)r * cols, cols, pre + (size_t)r * cols, ws);
+    if (threadIdx.x == 0) tot[r] = all;
+}
+
+// rpre = exclusive prefix of tot[0 .. rows), one workgroup
+template <int BLK>
+__global__ __launch_bounds__(BLK) void k_tot_scan(const uint32_t *__restrict__ tot, uint32_t rows,
+                                                  uint32_t *__restrict__ rpre) {
+    __shared__ uint32_t ws[BLK / 64];
+    (void)block_scan_run<BLK>(tot, rows, rpre, ws);
 }
 
 // D: digit bits; BLK threads; K items per thread and sub-tile.  IP / OP:
@@ -154,14 +185,18 @@ __global__ __launch_bounds__(BLK) void k_row_scan(const uint32_t *__restrict__ c
 // between the first and the last: one 8-byte store per item.
 // DIRECT: no LDS staging — every item goes straight from its lane to its
 // output position (wc then holds the global position of wave w's first item
-// of each digit)
+// of each digit).  nd_out != null: also the item's next digit
+// ((key >> nshift) & nmask, < 256) as a byte at its output position, for the
+// next pass's k_rs_count8.
 template <int D, int BLK, int K, bool IP, bool OP, bool DIRECT = false>
 __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__ keys,
                                                     const uint32_t *__restrict__ vals, uint64_t n, uint64_t chunk,
                                                     uint32_t shift, uint32_t mask, uint32_t nwg,
                                                     const uint32_t *__restrict__ base,
-                                                    const uint32_t *__restrict__ dpre,
-                                                    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out) {
+                                                    const uint32_t *__restrict__ dtot,
+                                                    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
+                                                    uint8_t *__restrict__ nd_out = nullptr, uint32_t nshift = 0,
+                                                    uint32_t nmask = 0) {
     constexpr uint32_t RD = 1u << D, TILE = BLK * K;
     constexpr int NW = BLK / 64;
     constexpr int DPT = RD >= (uint32_t)BLK ? RD / BLK : 1;   // digits per thread in the per-digit steps
@@ -181,10 +216,18 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
     // this thread's digits: tid * DPT .. + DPT (when RD < BLK: digit tid, threads past RD idle)
     const bool dth = DPT > 1 || (uint32_t)tid < RD;
     uint32_t gp[DPT];   // output position of the chunk's next item of each of this thread's digits
+    // the digits' prefix from their totals (k_row_scan): block scan of this
+    // thread's digits' sum, then a running add
+    uint32_t dsum = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) dsum += dth ? dtot[(uint32_t)tid * DPT + j] : 0u;
+    uint32_t dall;
+    uint32_t drun = block_excl<NW>(dsum, ws, &dall);
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
         const uint32_t d = (uint32_t)tid * DPT + j;
-        gp[j] = dth ? base[(size_t)d * nwg + blockIdx.x] + dpre[d] : 0u;   // k_row_scan's two levels
+        gp[j] = dth ? base[(size_t)d * nwg + blockIdx.x] + drun : 0u;   // the two levels of the scan
+        drun += dth ? dtot[d] : 0u;
         if (dth)
 #pragma unroll
             for (int w = 0; w < NW; ++w) wc[w][d] = 0;
@@ -262,6 +305,7 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
                         keys_out[dst] = it[k].x;
                         vals_out[dst] = it[k].y;
                     }
+                    if (nd_out) nd_out[dst] = (uint8_t)((it[k].x >> nshift) & nmask);
                 }
             nsub = 0;   // (nothing staged)
         } else {
@@ -281,6 +325,7 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
                 keys_out[dst] = v.x;
                 vals_out[dst] = v.y;
             }
+            if (nd_out) nd_out[dst] = (uint8_t)((v.x >> nshift) & nmask);
         }
         __syncthreads();
 #pragma unroll

@@ -38,6 +38,9 @@ def test_bench_contract_and_sharded_parity():
     assert v["anchor"]["ops_per_id"] == {"lazy_modmuls": 9, "macs": 24, "row0_adds": 8}
     cb = one["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["parity_with_gpu"] is True
+    # the crate's own unit: TSC ticks around the insert loop, the TSC rate from the same region
+    assert cb["tsc_cycles_per_id"] > 0 and 0.5 < cb["tsc_ghz"] < 6 and cb["published_crate_tsc_cycles_per_id"] > 0
+    assert abs(cb["tsc_cycles_per_id"] - cb["ns_per_id"] * cb["tsc_ghz"]) < 1e-6 * cb["tsc_cycles_per_id"] + 1e-3
     want = coracle.encode_u32_seed(seed, n_total, t)
     assert one["result"]["power_sums_head"] == want[:4] and one["result"]["count"] == n_total
 
@@ -56,6 +59,10 @@ def test_bench_contract_and_sharded_parity():
     want2 = coracle.encode_u32_seed(seed, n_total // 2, t)
     assert p["digest"] == hashlib.sha256((",".join(map(str, want2)) + f"|{n_total // 2}").encode()).hexdigest()[:16]
     assert len(two["ranks"]) == 2 and [r["rank"] for r in two["ranks"]] == [0, 1]
+    # the untimed sharded decode (configs[4]'s protocol on a log of --ids-per-gpu ids): the broadcast and
+    # all-gathers give rank 0's single-GPU hit list, every drop among the hits
+    dp = two["decode_parity"]
+    assert dp["equals_single_gpu"] is True and dp["drops_recovered"] is True and dp["d"] == 32 and dp["hits"] >= 32
     assert "rccl" not in two                   # host channel: no RCCL communicator to report
 
 

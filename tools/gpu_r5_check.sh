@@ -17,6 +17,7 @@ for s in ${STEPS:-pytest abflows roots u64}; do
     abflows)
       run ab_pipe 600 python3 -u tools/ab_flows.py --knob flow_pipe --modes 1,0 --flows 16,10000,1000000 --rounds 4 || exit 3
       run ab_fuse0 600 python3 -u tools/ab_flows.py --knob flow_fuse0 --modes 1,0 --flows 16,10000,1000000 --rounds 4 || exit 3 ;;
+    abflows1) run ab_flows 600 python3 -u tools/ab_flows.py --knob flow_sort --modes 2,1 --flows 16,10000,1000000 --rounds 4 || exit 3 ;;
     abocc) run ab_occ 600 python3 -u tools/ab_flows.py --knob flow_occ --modes 6,7 --flows 16,10000,1000000 --rounds 4 || exit 3 ;;
     pytestflows) run pytestflows 600 python3 -u -m pytest tests/test_flows.py tests/test_packets.py tests/test_gpu_variants.py -m gpu -q -x -p no:cacheprovider --timeout 300 --timeout-method thread -k "flow or knob or segment or packet" || { [ $? -eq 1 ] || exit 3; } ;;
     profflows) run profflows 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profflows" -o run -- python3 "$ROOT/tools/ab_flows.py" --modes 2 --flows 16,10000,1000000 --rounds 3 || exit 3 ;;

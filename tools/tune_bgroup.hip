@@ -157,7 +157,7 @@ int main(int argc, char **argv) {
     const uint64_t chunk = (((n + nwg - 1) / nwg) + 3) & ~(uint64_t)3;
     CK(hipMalloc(&cnt, (size_t)256 * nwg * 4));
     CK(hipMalloc(&base, (size_t)256 * nwg * 4));
-    uint32_t *zdp = nullptr;   // k_rs_scatter digit prefixes: 0 (base holds the full scan)
+    uint32_t *zdp = nullptr;   // k_rs_scatter digit totals: 0 (base holds the full scan)
     CK(hipMalloc(&zdp, rsort::RMAX * 4));
     CK(hipMemset(zdp, 0, rsort::RMAX * 4));
     CK(hipMalloc(&st0, (size_t)C * 4));

@@ -87,7 +87,7 @@ int main(int argc, char **argv) {
     const uint32_t nwg4 = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 4, (n + 4095) / 4096);
     CK(hipMalloc(&cnt, (size_t)rsort::R * nwg4 * 4));
     CK(hipMalloc(&base, (size_t)rsort::R * nwg4 * 4));
-    uint32_t *zdp = nullptr;   // k_rs_scatter digit prefixes: 0 (base holds the full scan)
+    uint32_t *zdp = nullptr;   // k_rs_scatter digit totals: 0 (base holds the full scan)
     CK(hipMalloc(&zdp, rsort::RMAX * 4));
     CK(hipMemset(zdp, 0, rsort::RMAX * 4));
     hipEvent_t e0, e1;
