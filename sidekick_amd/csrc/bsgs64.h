@@ -44,6 +44,8 @@ constexpr int NB = 8;
 // V <- V * x mod p, V and the result < 2^64 (not necessarily canonical),
 // exact.  V pinned in v[2:3] (the asm addresses its halves):
 //   A = V.lo x0;  B = V.hi x0 + A.hi;  C = V.lo x1 + B (carry cc);
+//   ((A.hi:0) as one v_pk_mov_b32 instead of two moves: 1 % slower at t = 80,
+//   profiles/r05/u64_step1/)
 //   PH = V.hi x1 + C.hi + cc 2^32;  P_L = A.lo + C.lo 2^32          (P = V x)
 //   E = P_L + 59 PH.lo (carry ce);  F = E.hi + ce 2^32 + 59 PH.hi   (t-form)
 //   V' = (F.lo:E.lo) + 59 F.hi; a wrap past 2^64 leaves V' < 59*60, so +59
@@ -77,6 +79,88 @@ __device__ __forceinline__ void mulv(uint64_t &V, uint32_t x0, uint32_t x1) {
                    [tmp] "=&v"(tmp)
                  : [x0] "v"(x0), [x1] "v"(x1)
                  : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11");
+}
+
+// Two independent products V <- V * x, W <- W * y in one block, the two
+// instruction streams interleaved (W in v[12:13], its scratch v14..v21): each
+// stream's carries get their wait states from the other stream's
+// instructions, and the two dependency chains overlap in one wave.
+#define QK_U64_MULV2_ASM                                                                           \
+    "v_mov_b32_e32 v11, 0\n\t"                                                                     \
+    "v_mov_b32_e32 v21, 0\n\t"                                                                     \
+    "v_mad_u64_u32 v[6:7], %[cx], v2, %[x0], 0\n\t"                                                  \
+    "v_mad_u64_u32 v[16:17], %[dx], v12, %[y0], 0\n\t"                                               \
+    "v_mov_b32_e32 v10, v7\n\t"                                                                    \
+    "v_mov_b32_e32 v20, v17\n\t"                                                                   \
+    "v_mad_u64_u32 v[8:9], %[cx], v3, %[x0], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[18:19], %[dx], v13, %[y0], v[20:21]\n\t"                                        \
+    "v_mad_u64_u32 v[8:9], %[cc], v2, %[x1], v[8:9]\n\t"                                             \
+    "v_mad_u64_u32 v[18:19], %[dc], v12, %[y1], v[18:19]\n\t"                                        \
+    "v_mov_b32_e32 v7, v8\n\t"                                                                     \
+    "v_mov_b32_e32 v17, v18\n\t"                                                                   \
+    "v_mov_b32_e32 v10, v9\n\t"                                                                    \
+    "v_mov_b32_e32 v20, v19\n\t"                                                                   \
+    "v_cndmask_b32_e64 v11, 0, 1, %[cc]\n\t"                                                         \
+    "v_cndmask_b32_e64 v21, 0, 1, %[dc]\n\t"                                                         \
+    "v_mad_u64_u32 v[4:5], %[cx], v3, %[x1], v[10:11]\n\t"                                           \
+    "v_mad_u64_u32 v[14:15], %[dx], v13, %[y1], v[20:21]\n\t"                                        \
+    "v_mad_u64_u32 v[2:3], %[ce], v4, 59, v[6:7]\n\t"                                                \
+    "v_mad_u64_u32 v[12:13], %[de], v14, 59, v[16:17]\n\t"                                           \
+    "v_mov_b32_e32 v8, v3\n\t"                                                                     \
+    "v_mov_b32_e32 v18, v13\n\t"                                                                   \
+    "v_cndmask_b32_e64 v9, 0, 1, %[ce]\n\t"                                                          \
+    "v_cndmask_b32_e64 v19, 0, 1, %[de]\n\t"                                                         \
+    "v_mad_u64_u32 v[8:9], %[cx], v5, 59, v[8:9]\n\t"                                                \
+    "v_mad_u64_u32 v[18:19], %[dx], v15, 59, v[18:19]\n\t"                                           \
+    "v_mov_b32_e32 v3, v8\n\t"                                                                     \
+    "v_mov_b32_e32 v13, v18\n\t"                                                                   \
+    "v_mad_u64_u32 v[2:3], %[cw], v9, 59, v[2:3]\n\t"                                                \
+    "v_mad_u64_u32 v[12:13], %[dw], v19, 59, v[12:13]\n\t"                                           \
+    "s_nop 0\n\t"                                                                                  \
+    "v_cndmask_b32_e64 %[tmp], 0, 59, %[cw]\n\t"                                                     \
+    "v_cndmask_b32_e64 %[tmq], 0, 59, %[dw]\n\t"                                                     \
+    "v_add_u32_e32 v2, v2, %[tmp]\n\t"                                                             \
+    "v_add_u32_e32 v12, v12, %[tmq]\n\t"
+
+__device__ __forceinline__ void mulv2(uint64_t &V, uint32_t x0, uint32_t x1, uint64_t &W, uint32_t y0, uint32_t y1) {
+    uint64_t cw, cx, cc, ce, dw, dx, dc, de;
+    uint32_t tmp, tmq;
+    asm volatile(QK_U64_MULV2_ASM
+                 : "+{v[2:3]}"(V), "+{v[12:13]}"(W), [cw] "=&s"(cw), [cx] "=&s"(cx), [cc] "=&s"(cc),
+                   [ce] "=&s"(ce), [dw] "=&s"(dw), [dx] "=&s"(dx), [dc] "=&s"(dc), [de] "=&s"(de),
+                   [tmp] "=&v"(tmp), [tmq] "=&v"(tmq)
+                 : [x0] "v"(x0), [x1] "v"(x1), [y0] "v"(y0), [y1] "v"(y1)
+                 : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v14", "v15", "v16", "v17", "v18", "v19",
+                   "v20", "v21");
+}
+
+// P[1..M] = u^1 .. u^M from P[1] = u in 1 + ceil((M - 2) / 2) dependent
+// steps instead of M - 1: P[2] = P[1]^2, then (P[2j-1], P[2j]) =
+// (P[j] P[j-1], P[j]^2) as one mulv2 block.  store(k, P[k]) after each.
+template <int M, typename St>
+__device__ __forceinline__ void pow_tree(uint64_t (&P)[M + 1], St &&store) {
+    if constexpr (M >= 2) {
+        P[2] = P[1];
+        mulv(P[2], (uint32_t)P[1], (uint32_t)(P[1] >> 32));
+        store(2, P[2]);
+    }
+#pragma unroll
+    for (int j = 2; 2 * j - 1 <= M; ++j) {
+        const uint64_t pj = P[j], pm = P[j - 1];
+        if (2 * j <= M) {
+            uint64_t a = pj, b = pj;
+            mulv2(a, (uint32_t)pm, (uint32_t)(pm >> 32), b, (uint32_t)pj, (uint32_t)(pj >> 32));
+            P[2 * j - 1] = a;
+            P[2 * j] = b;
+            store(2 * j - 1, a);
+            store(2 * j, b);
+        } else {
+            uint64_t a = pj;
+            mulv(a, (uint32_t)pm, (uint32_t)(pm >> 32));
+            P[2 * j - 1] = a;
+            store(2 * j - 1, a);
+        }
+    }
 }
 
 // B * 2^32 mod p for B < 2^64: B.lo 2^32 + 59 B.hi (+59 after a wrap, which
@@ -314,7 +398,7 @@ struct Smem<NG, true, NBB> {
 //           giants step (2); 3: the row-0 sums at 1 and the MACs at 2 (per
 //           64-id chunk); 0: no priority changes
 template <int NA, int MODE, int SG, int ABL = 0, int PF = 0, bool OFF = false, bool BSH = false, int LD = 0,
-          int XC = 0, int NBT = NB, int PRIO = 0>
+          int XC = 0, int NBT = NB, int PRIO = 0, int TR = 0>
 __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t n, uint32_t T,
                                      uint64_t *__restrict__ partials, uint32_t base = 0,
                                      const uint64_t *xin = nullptr, uint64_t *xout = nullptr) {
@@ -322,6 +406,7 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     static_assert((NA >= 2 || (OFF && NA == 1)) && NA <= 10, "giant rows");
     static_assert(!(BSH && PF) && !(LD && PF), "prefetch form: stored B * 2^32, all rows");
     static_assert(NBT == 8 || (NBT == 4 && BSH && !PF && XC == 0), "babies per id: 8, or 4 (plain BSH form)");
+    static_assert(!TR || (BSH && !OFF && ABL == 0), "product-tree step 1: pass-0 BSH form");
     constexpr int CW = NBT / 4;                  // babies per wave
     constexpr int NR = OFF ? NA : NA - 1;        // MAC rows (giants x^8 .. x^(8 NR), or x^base ..)
     constexpr bool G8 = BSH && !OFF;             // giant row 0 (x^8) read from baby 8
@@ -354,7 +439,19 @@ __device__ __forceinline__ void body(const uint64_t *__restrict__ ids, uint64_t 
     for (; tile < ntiles; tile += gridDim.x) {
         // ---- step 1: this thread's id -> babies (+ B * 2^32), giants -> LDS
         if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
-        {
+        if constexpr (TR != 0) {
+            uint64_t Pb[NBT + 1], Pg[NR + 1];
+            Pb[1] = nxt;
+            sm.bb[0][tid] = make_uint2((uint32_t)nxt, (uint32_t)(nxt >> 32));
+            pow_tree<NBT>(Pb, [&](int k, uint64_t v) { sm.bb[k - 1][tid] = make_uint2((uint32_t)v, (uint32_t)(v >> 32)); });
+            Pg[1] = Pb[NBT];   // giant row r = x^(NBT (r + 1)) = Pg[r + 1], rows >= 1 in ga[r - 1]
+            pow_tree<NR>(Pg, [&](int k, uint64_t v) { sm.ga[k - 2][tid] = make_uint2((uint32_t)v, (uint32_t)(v >> 32)); });
+            if constexpr ((XC & 2) != 0) {
+                uint64_t V = Pg[NR];
+                mulv(V, (uint32_t)Pb[NBT], (uint32_t)(Pb[NBT] >> 32));
+                if (tile * BLOCK + tid < n) xout[tile * BLOCK + tid] = V;
+            }
+        } else {
             const uint64_t x = nxt;
             const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
             uint64_t V = x;

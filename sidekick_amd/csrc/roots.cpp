@@ -720,6 +720,78 @@ QK_IFMA static size_t gcd_small64_ifma(const uint64_t *a0, size_t na, const uint
     return na;
 }
 
+// gcd(a, b_j) for cnt <= GB_MAX operands b_j at once (not monic), the same
+// rows as gcd_small: one remainder step of every live gcd per sweep.  A
+// single gcd is a chain of dependent rows (each row's leading coefficient is
+// read back from the row just stored); the rows of different gcds are
+// independent, so the core overlaps them — the class gcds of a part
+// (Splitter::classes) run as one batch.
+constexpr int GB_MAX = 24;
+#define QK_GCD_BATCH_BODY(ROW)                                                                          \
+    constexpr size_t SZ = 4 * 8 * NV;                                                                   \
+    alignas(64) uint64_t buf[GB_MAX][SZ];                                                               \
+    uint64_t *pa[GB_MAX], *pb[GB_MAX];                                                                  \
+    size_t na[GB_MAX], nb[GB_MAX];                                                                      \
+    bool live[GB_MAX];                                                                                  \
+    int nlive = cnt;                                                                                    \
+    for (int j = 0; j < cnt; ++j) {                                                                     \
+        memset(buf[j], 0, sizeof(buf[j]));                                                              \
+        pa[j] = buf[j] + 8 * NV;                                                                        \
+        pb[j] = buf[j] + 3 * 8 * NV;                                                                    \
+        for (size_t i = 0; i < na0; ++i) pa[j][i] = a0[i];                                              \
+        for (size_t i = 0; i < nb0[j]; ++i) pb[j][i] = b0[j][i];                                        \
+        na[j] = na0;                                                                                    \
+        nb[j] = nb0[j];                                                                                 \
+        live[j] = true;                                                                                 \
+    }                                                                                                   \
+    while (nlive) {                                                                                     \
+        for (int j = 0; j < cnt; ++j) {                                                                 \
+            if (!live[j]) continue;                                                                     \
+            if (!nb[j]) {                                                                               \
+                for (size_t i = 0; i < na[j]; ++i) out[j * SO + i] = (T)pa[j][i];                       \
+                nout[j] = na[j];                                                                        \
+                live[j] = false;                                                                        \
+                --nlive;                                                                                \
+                continue;                                                                               \
+            }                                                                                           \
+            const size_t m = nb[j] - 1;                                                                 \
+            if (na[j] <= m) {                                                                           \
+                std::swap(pa[j], pb[j]);                                                                \
+                std::swap(na[j], nb[j]);                                                                \
+                continue;                                                                               \
+            }                                                                                           \
+            const uint64_t lb = pb[j][m], la = pa[j][na[j] - 1];                                        \
+            const size_t s = na[j] - 1 - m, nv = (na[j] + 7) / 8;                                       \
+            for (int k = 0; k < NV; ++k) {                                                              \
+                if ((size_t)k >= nv) break;                                                             \
+                const __m512i d = _mm512_load_si512(pa[j] + 8 * k), x = _mm512_loadu_si512(pb[j] + 8 * k - s); \
+                _mm512_store_si512(pa[j] + 8 * k, ROW(d, x, lb, la));                                   \
+            }                                                                                           \
+            --na[j];                                                                                    \
+            while (na[j] && !pa[j][na[j] - 1]) --na[j];                                                 \
+        }                                                                                               \
+    }
+// out: cnt rows of SO = 8 NV coefficients; nout[j]: the gcd's coefficient count
+template <class F, int NV>
+QK_AVX512 static void gcd_batch(const typename F::T *a0, size_t na0, int cnt, const typename F::T *const *b0,
+                                const size_t *nb0, typename F::T *out, size_t *nout) {
+    using T = typename F::T;
+    constexpr size_t SO = 8 * NV;
+    if constexpr (F::W == 32) {
+        QK_GCD_BATCH_BODY(row_lanes32)
+    } else {
+        QK_GCD_BATCH_BODY(row_lanes64)
+    }
+}
+template <int NV>
+QK_IFMA static void gcd_batch64_ifma(const uint64_t *a0, size_t na0, int cnt, const uint64_t *const *b0,
+                                     const size_t *nb0, uint64_t *out, size_t *nout) {
+    using T = uint64_t;
+    constexpr size_t SO = 8 * NV;
+    QK_GCD_BATCH_BODY(row_lanes64_ifma)
+}
+#undef QK_GCD_BATCH_BODY
+
 // monic gcd(a, b), fraction-free: each step cancels a's leading term as
 // lead(b) a - lead(a) z^s b (no inversion; a field inverse costs ~70
 // multiplications, more than the extra row of products here), one pass per
@@ -787,6 +859,68 @@ template <class F> Poly<F> gcd_rows(const Poly<F> &a0, const Poly<F> &b0, bool s
 }
 template <class F> Poly<F> gcd(const Poly<F> &a, const Poly<F> &b) { return gcd_rows<F>(a, b, true); }
 
+// gcd(a, b_j) for every j, as gcd_rows(a, b_j, true, false) would return
+// them ({1} when coprime), the small cases as one gcd_batch
+template <class F> std::vector<Poly<F>> gcd_many(const Poly<F> &a, const std::vector<Poly<F>> &bs) {
+    using T = typename F::T;
+    const int cnt = (int)bs.size();
+    std::vector<Poly<F>> res(cnt);
+    size_t na = a.size(), n = na;
+    while (na && !a[na - 1]) --na;
+    const T *bp[GB_MAX];
+    size_t nb[GB_MAX];
+    for (int j = 0; j < cnt && j < GB_MAX; ++j) {
+        size_t k = bs[j].size();
+        while (k && !bs[j][k - 1]) --k;
+        bp[j] = bs[j].data();
+        nb[j] = k;
+        n = std::max(n, k);
+    }
+    if (cnt <= GB_MAX && n <= 40 && cpu_has_avx512()) {
+        constexpr size_t SO = 40;
+        alignas(64) T out[GB_MAX * SO];
+        size_t nout[GB_MAX];
+        const int nv = (int)((n + 7) / 8);
+        if constexpr (F::W == 64) {
+            if (cpu_has_ifma()) {
+                uint64_t *o = (uint64_t *)out;
+                const uint64_t *const *b = (const uint64_t *const *)bp;
+                switch (nv) {
+                case 1: gcd_batch64_ifma<1>(a.data(), na, cnt, b, nb, o, nout); break;
+                case 2: gcd_batch64_ifma<2>(a.data(), na, cnt, b, nb, o, nout); break;
+                case 3: gcd_batch64_ifma<3>(a.data(), na, cnt, b, nb, o, nout); break;
+                case 4: gcd_batch64_ifma<4>(a.data(), na, cnt, b, nb, o, nout); break;
+                default: gcd_batch64_ifma<5>(a.data(), na, cnt, b, nb, o, nout); break;
+                }
+                goto have;
+            }
+        }
+        switch (nv) {
+        case 1: gcd_batch<F, 1>(a.data(), na, cnt, bp, nb, out, nout); break;
+        case 2: gcd_batch<F, 2>(a.data(), na, cnt, bp, nb, out, nout); break;
+        case 3: gcd_batch<F, 3>(a.data(), na, cnt, bp, nb, out, nout); break;
+        case 4: gcd_batch<F, 4>(a.data(), na, cnt, bp, nb, out, nout); break;
+        default: gcd_batch<F, 5>(a.data(), na, cnt, bp, nb, out, nout); break;
+        }
+    have:
+        // gcd_batch<NV> writes row j at j * 8 NV
+        const size_t so = 8 * (size_t)nv;
+        for (int j = 0; j < cnt; ++j) {
+            if (nout[j] == 1) res[j] = Poly<F>{1};
+            else res[j].assign(out + j * so, out + j * so + nout[j]);
+        }
+        (void)SO;
+        return res;
+    }
+    for (int j = 0; j < cnt; ++j) res[j] = gcd_rows<F>(a, bs[j], true, false);
+    return res;
+}
+
+// the smallest modulus degree on the vector paths (a variable for
+// tools/prof_roots.cpp's A/B: from degree 3 on, u64 roots at d = 32 took
+// 44.6 against 43.4 us, u32 22.0 against 21.7 — below 8 coefficients the
+// vector forms' fixed costs exceed the scalar loops)
+static size_t ring_vec_min = 8;
 // Arithmetic modulo a fixed monic f of degree m >= 1: residues are vectors of
 // exactly m coefficients.
 template <class F> struct ModRing {
@@ -805,7 +939,7 @@ template <class F> struct ModRing {
 
     explicit ModRing(const Poly<F> &f) : m(f.size() - 1), nf(m), acc(2 * m) {
         for (size_t i = 0; i < m; ++i) nf[i] = F::neg(f[i]);
-        vec = m >= 8 && m <= 1024 && cpu_has_avx512();
+        vec = m >= ring_vec_min && m <= 1024 && cpu_has_avx512();
         if (!vec) return;
         const size_t mb = (m + 7) & ~(size_t)7;
         nf64.assign(mb + 8, 0);
@@ -942,6 +1076,23 @@ template <class F> Poly<F> to_poly(std::vector<typename F::T> r) {
     return p;
 }
 
+// a b (plain product)
+template <class F> Poly<F> mul_poly(const Poly<F> &a, const Poly<F> &b) {
+    if (a.empty() || b.empty()) return {};
+    std::vector<typename F::A> acc(a.size() + b.size() - 1, typename F::A(0));
+    for (size_t i = 0; i < a.size(); ++i)
+        for (size_t j = 0; j < b.size(); ++j) F::mac(acc[i + j], a[i], b[j]);
+    Poly<F> r(acc.size());
+    for (size_t i = 0; i < acc.size(); ++i) r[i] = F::red(acc[i]);
+    return r;
+}
+// split(): the largest product of factors sharing one exponentiation (a
+// variable for tools/prof_roots.cpp's A/B; 0: one exponentiation per factor).
+// EPYC 9575F, d = 32, mean over 8 root sets (profiles/r05/roots/): u64 43.2-
+// 45.0 us alone, 43.4-43.7 at 16, 43.3-43.4 at 24; u32 21.6 alone, 21.9 at
+// 16 and 24 — grouped for u64 only
+static size_t group_deg = 24;
+
 // a primitive L-th root of unity of GF(p) (L | p - 1)
 template <class F> typename F::T root_of_unity() {
     using T = typename F::T;
@@ -986,16 +1137,17 @@ template <class F> class Splitter {
         i4 = F::pow(zeta, F::LO);
     }
     // the roots of g (monic) of class j (j mod E == c) for each j, from w mod
-    // g.  p64 (E = 4: 11 classes of ~k/4 roots each): the factors found go to
-    // parts as they leave the gcd rows (a scalar multiple of the monic
-    // factor: split() makes the leaves' roots with one batched inversion,
-    // not one 128-bit-product inversion chain per factor).  Every class
-    // against the whole of g (no division of g by the factors found: the
-    // rows of a gcd of <= 8 coefficients are single vector operations, an
-    // inversion and a division per factor cost more than they save), until
-    // the degrees found add up to g's.  A root -a (w = 0 there) is in no
-    // class; whatever else is missing lies outside GF(p) (the fast path's
-    // failure case): then the found factors, made monic, and the rest.
+    // g (p64, E = 4: 11 classes of ~k/4 roots each; p32, E = 2: 19 of ~k/2):
+    // every class against the whole of g, the gcds as one gcd_many batch —
+    // each gcd is a chain of dependent rows, the batch overlaps the chains
+    // (EPYC 9575F, d = 32, profiles/r05/roots/: u64 roots 52.4 -> 46.2 us,
+    // u32 24.3 -> 19.4 us against one gcd at a time, the u32 one on the rest
+    // shrinking as factors were found).  The factors go to parts as they
+    // leave the gcd rows (a scalar multiple of the monic factor: split()
+    // makes the leaves' roots with one batched inversion).  A root -a (w = 0
+    // there) is in no class; whatever else is missing lies outside GF(p) (the
+    // fast path's failure case): then the found factors, made monic, and the
+    // rest.
     void classes(const Poly<F> &g, const Poly<F> &w, uint32_t c, T a, std::vector<Poly<F>> &parts) const {
         if (g.size() <= 1) return;
         if (g.size() == 2) {
@@ -1007,39 +1159,17 @@ template <class F> class Splitter {
         rem_monic<F>(wg, g);
         if (wg.empty()) wg.push_back(0);
         T zj = zc[c];
-        if constexpr (F::W == 32) {
-            // p32 (E = 2, 19 classes of ~k/2 roots each): the rest shrinks
-            // as factors are found — its gcds with the later classes then run
-            // on fewer coefficients, and an inversion costs only ~70 32-bit
-            // products here (measured: +7 % for the unshrunk form at d = 32)
-            Poly<F> rem = g;
-            bool cut = false;
-            for (uint32_t j = c; j < F::L && rem.size() > 2; j += F::E, zj = F::mul(zj, step)) {
-                Poly<F> wr = wg;
-                if (cut) rem_monic<F>(wr, rem);   // w mod rem (rem == g: wg is reduced)
-                if (wr.empty()) wr.push_back(0);
-                wr[0] = F::sub(wr[0], zj);
-                Poly<F> h = gcd<F>(rem, wr);
-                if (h.size() > 1) {
-                    rem = div_monic<F>(rem, h);
-                    parts.push_back(std::move(h));
-                    cut = true;
-                }
-            }
-            if (rem.size() > 1) parts.push_back(std::move(rem));   // the last class, r = -a, or an unsplit rest
-            return;
-        }
-        std::vector<Poly<F>> hs;
+        std::vector<Poly<F>> hs, wrs;
         size_t found = 0;
-        for (uint32_t j = c; j < F::L && found < k; j += F::E, zj = F::mul(zj, step)) {
-            Poly<F> wr = wg;
-            wr[0] = F::sub(wr[0], zj);
-            Poly<F> h = gcd_rows<F>(g, wr, true, false);
+        for (uint32_t j = c; j < F::L; j += F::E, zj = F::mul(zj, step)) {
+            wrs.push_back(wg);
+            wrs.back()[0] = F::sub(wrs.back()[0], zj);
+        }
+        for (auto &h : gcd_many<F>(g, wrs))
             if (h.size() > 1) {
                 found += h.size() - 1;
                 hs.push_back(std::move(h));
             }
-        }
         if (found < k) {   // the root -a?
             const T x = F::neg(a);
             T v = 1;
@@ -1071,36 +1201,55 @@ template <class F> class Splitter {
         out = in.size() > 1 ? div_monic<F>(g, in) : g;
         if (in.size() <= 1) in.clear();
     }
-    // every factor one L-way split of g (w = (z + a)^((p-1)/L) mod g) yields
-    void run(ModRing<F> &R, const Poly<F> &g, T a, std::vector<Poly<F>> &parts) const {
+    // The residues one L-way split needs, modulo the ring's f (g itself, or
+    // the product of several parts split with the same a): w = (z + a)^((p -
+    // 1)/L), v = w^LO (E > 1) and q = v^2 (E = 4)
+    struct Pw {
+        Poly<F> w, v, q;
+    };
+    static Pw powers(ModRing<F> &R, T a) {
+        Pw r;
         const std::vector<T> wv = R.pow_lin(a, F::PM1 / F::L);
-        const Poly<F> w = to_poly<F>(wv);
-        if constexpr (F::E == 1) {
-            classes(g, w, 0, a, parts);
-        } else {
-            const std::vector<T> vv = F::LO > 1 ? R.pow(wv, F::LO) : wv;   // v = w^LO
-            Poly<F> A, B;
-            if constexpr (F::E == 2) {
-                cut(g, to_poly<F>(vv), 1, A, B);   // v = 1: even j; v = -1 (or r = -a): odd j
-                classes(A, w, 0, a, parts);
-                classes(B, w, 1, a, parts);
-            } else {
-                static_assert(F::E == 4, "p - 1 has at most 2^2");
-                std::vector<T> qv = vv;
-                R.sqr(qv);                        // v^2 = +-1: j even / odd
-                cut(g, to_poly<F>(qv), 1, A, B);
-                const Poly<F> v = to_poly<F>(vv);
-                Poly<F> A0, A2, B1, B3;
-                if (A.size() > 2) cut(A, v, 1, A0, A2);   // j = 0 / 2 mod 4
-                else A2 = A;
-                if (B.size() > 2) cut(B, v, i4, B1, B3);  // j = 1 / 3 mod 4
-                else B3 = B;
-                classes(A0, w, 0, a, parts);
-                classes(A2, w, 2, a, parts);
-                classes(B1, w, 1, a, parts);
-                classes(B3, w, 3, a, parts);
+        r.w = to_poly<F>(wv);
+        if constexpr (F::E > 1) {
+            std::vector<T> vv = F::LO > 1 ? R.pow(wv, F::LO) : wv;
+            r.v = to_poly<F>(vv);
+            if constexpr (F::E == 4) {
+                R.sqr(vv);
+                r.q = to_poly<F>(std::move(vv));
             }
         }
+        return r;
+    }
+    // every factor the split of g (monic, dividing the ring's f) by these
+    // residues yields
+    void split_with(const Poly<F> &g, const Pw &pw, T a, std::vector<Poly<F>> &parts) const {
+        if constexpr (F::E == 1) {
+            classes(g, pw.w, 0, a, parts);
+        } else {
+            Poly<F> A, B;
+            if constexpr (F::E == 2) {
+                cut(g, pw.v, 1, A, B);   // v = 1: even j; v = -1 (or r = -a): odd j
+                classes(A, pw.w, 0, a, parts);
+                classes(B, pw.w, 1, a, parts);
+            } else {
+                static_assert(F::E == 4, "p - 1 has at most 2^2");
+                cut(g, pw.q, 1, A, B);   // v^2 = +-1: j even / odd
+                Poly<F> A0, A2, B1, B3;
+                if (A.size() > 2) cut(A, pw.v, 1, A0, A2);   // j = 0 / 2 mod 4
+                else A2 = A;
+                if (B.size() > 2) cut(B, pw.v, i4, B1, B3);  // j = 1 / 3 mod 4
+                else B3 = B;
+                classes(A0, pw.w, 0, a, parts);
+                classes(A2, pw.w, 2, a, parts);
+                classes(B1, pw.w, 1, a, parts);
+                classes(B3, pw.w, 3, a, parts);
+            }
+        }
+    }
+    // every factor one L-way split of g (w = (z + a)^((p-1)/L) mod g) yields
+    void run(ModRing<F> &R, const Poly<F> &g, T a, std::vector<Poly<F>> &parts) const {
+        split_with(g, powers(R, a), a, parts);
     }
 };
 
@@ -1121,42 +1270,86 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
     const Splitter<F> S{};
     std::vector<T> num, den;
     std::vector<Poly<F>> todo{g0};
+    std::vector<int> tries{0};
     uint64_t s = 0x243F6A8885A308D3ull;   // fixed seed: a deterministic sequence of a's
     while (!todo.empty()) {
-        Poly<F> g = std::move(todo.back());
-        todo.pop_back();
-        const size_t k = g.size() - 1;
-        if (k == 0) continue;
-        if (k == 1) {   // g1 z + g0
-            num.push_back(F::neg(g[0]));
-            den.push_back(g[1]);
-            continue;
-        }
-        if (k == 2) {   // g2 z^2 + g1 z + g0: (-g1 +- sqrt(g1^2 - 4 g2 g0)) / (2 g2)
-            const T a2 = g[2], b = g[1], c = g[0];
-            const T disc = F::sub(F::mul(b, b), F::mul(F::mul(4, a2), c));
-            T sq;
-            if (!F::sqrt(disc, sq)) {
-                if (!exact) return false;
-                continue;   // (cannot happen for an exact-mode factor)
+        // this generation: the leaves now, the factors of >= 3 roots (big)
+        // split below
+        std::vector<Poly<F>> big;
+        std::vector<int> bt;
+        for (size_t i = 0; i < todo.size(); ++i) {
+            Poly<F> &g = todo[i];
+            const size_t k = g.size() - 1;
+            if (g.empty() || k == 0) continue;
+            if (k == 1) {   // g1 z + g0
+                num.push_back(F::neg(g[0]));
+                den.push_back(g[1]);
+                continue;
             }
-            const T nb = F::neg(b), d2 = F::add(a2, a2);
-            num.push_back(F::add(nb, sq));
-            den.push_back(d2);
-            num.push_back(F::sub(nb, sq));
-            den.push_back(d2);
-            continue;
+            if (k == 2) {   // g2 z^2 + g1 z + g0: (-g1 +- sqrt(g1^2 - 4 g2 g0)) / (2 g2)
+                const T a2 = g[2], b = g[1], c = g[0];
+                const T disc = F::sub(F::mul(b, b), F::mul(F::mul(4, a2), c));
+                T sq;
+                if (!F::sqrt(disc, sq)) {
+                    if (!exact) return false;
+                    continue;   // (cannot happen for an exact-mode factor)
+                }
+                const T nb = F::neg(b), d2 = F::add(a2, a2);
+                num.push_back(F::add(nb, sq));
+                den.push_back(d2);
+                num.push_back(F::sub(nb, sq));
+                den.push_back(d2);
+                continue;
+            }
+            if (!exact && tries[i] >= 24) return false;
+            big.push_back(std::move(g));
+            bt.push_back(tries[i]);
         }
-        if (g.back() != 1) make_monic<F>(g);
-        ModRing<F> R(g);
-        for (int fails = 0;; ++fails) {
-            if (!exact && fails >= 24) return false;
+        todo.clear();
+        tries.clear();
+        if (big.empty()) break;
+        // monic forms: the leading coefficients inverted together
+        {
+            std::vector<T> pre(big.size());
+            T acc = 1;
+            for (size_t i = 0; i < big.size(); ++i) pre[i] = acc = F::mul(acc, big[i].back());
+            T inv = F::inv(acc);
+            for (size_t i = big.size(); i-- > 0;) {
+                const T li = i ? F::mul(inv, pre[i - 1]) : inv;
+                inv = F::mul(inv, big[i].back());
+                if (big[i].back() != 1)
+                    for (auto &v : big[i]) v = F::mul(v, li);
+            }
+        }
+        // groups of consecutive factors of <= group_deg total degree share one
+        // exponentiation, taken mod their product (each factor then reduces
+        // the residues mod itself in its cuts and classes): a small factor's
+        // exponentiation is a chain of latency-bound squarings, so three of
+        // degree 3-4 cost about what one of degree 10 does
+        for (size_t i0 = 0; i0 < big.size();) {
+            size_t i1 = i0 + 1, deg = big[i0].size() - 1;
+            const size_t cap = F::W == 64 ? group_deg : 0;
+            while (i1 < big.size() && deg + big[i1].size() - 1 <= cap) deg += big[i1++].size() - 1;
+            Poly<F> H = big[i0];
+            for (size_t i = i0 + 1; i < i1; ++i) H = mul_poly<F>(H, big[i]);
+            ModRing<F> R(H);
             s += GAMMA;
-            std::vector<Poly<F>> parts;
-            S.run(R, g, F::canon_any((T)splitmix_mix(s)), parts);
-            if (parts.size() < 2) continue;
-            for (auto &p : parts) todo.push_back(std::move(p));
-            break;
+            const T a = F::canon_any((T)splitmix_mix(s));
+            const typename Splitter<F>::Pw pw = Splitter<F>::powers(R, a);
+            for (size_t i = i0; i < i1; ++i) {
+                std::vector<Poly<F>> parts;
+                S.split_with(big[i], pw, a, parts);
+                if (parts.size() < 2) {   // no split with this a: again with the next one
+                    todo.push_back(std::move(big[i]));
+                    tries.push_back(bt[i] + 1);
+                    continue;
+                }
+                for (auto &p : parts) {
+                    todo.push_back(std::move(p));
+                    tries.push_back(0);
+                }
+            }
+            i0 = i1;
         }
     }
     // num_i / den_i: prefix products, one inversion, back substitution

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "../sidekick_amd/csrc/roots.cpp"
 
@@ -43,6 +44,36 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
     for (uint32_t i = 1; i <= d; ++i) c[i - 1] = f[d - i];
     volatile size_t sink = 0;
     const double t_all = best_us(reps, [&] { sink += roots<F>(c.data(), d).size(); });
+    {   // split() settings, alternated, over 8 root sets (the mean of their minima)
+        std::vector<std::vector<T>> cs(8, std::vector<T>(d));
+        for (auto &cv : cs) {
+            Poly<F> h{1};
+            for (uint32_t i = 0; i < d; ++i) {
+                const T r = F::canon_any((T)rnd());
+                Poly<F> g(h.size() + 1, 0);
+                for (size_t k = 0; k < h.size(); ++k) {
+                    g[k + 1] = F::add(g[k + 1], h[k]);
+                    g[k] = F::sub(g[k], F::mul(h[k], r));
+                }
+                h = g;
+            }
+            for (uint32_t i = 1; i <= d; ++i) cv[i - 1] = h[d - i];
+        }
+        const size_t gs[] = {0, 16, 24, 0, 16, 24}, vs[] = {8, 3};
+        printf("{\"field\": \"%s\", \"ab\": [", name);
+        for (int r = 0; r < 6; ++r)
+            for (int v = 0; v < 2; ++v) {
+                group_deg = gs[r];
+                ring_vec_min = vs[v];
+                double t = 0;
+                for (auto &cv : cs) t += best_us(reps, [&] { sink += roots<F>(cv.data(), d).size(); }) / cs.size();
+                printf("%s{\"group_deg\": %zu, \"ring_vec_min\": %zu, \"roots_us\": %.2f}", r + v ? ", " : "",
+                       gs[r], vs[v], t);
+            }
+        printf("]}\n");
+        group_deg = 24;
+        ring_vec_min = 8;
+    }
     const double t_ring = best_us(reps, [&] { ModRing<F> R(f); sink += R.m; });
     ModRing<F> R(f);
     std::vector<T> a(R.m);
@@ -80,6 +111,124 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
         S.classes(A, wp, 0, F::canon_any((T)777), parts);
         S.classes(B, wp, 1, F::canon_any((T)777), parts);
     });
+    // the real top-level split (Splitter::run: exponentiation, v = w^LO, the
+    // E-cuts, the classes of each part) and, for E = 4, the classes of the
+    // four parts alone
+    std::vector<Poly<F>> rp;
+    const double t_run = best_us(reps, [&] {
+        rp.clear();
+        S.run(R, f, F::canon_any((T)777), rp);
+    });
+    if constexpr (F::E == 4) {
+        Poly<F> A0, A2, B1, B3;
+        const Poly<F> v = to_poly<F>(vv);
+        if (A.size() > 2) S.cut(A, v, 1, A0, A2);
+        else A2 = A;
+        if (B.size() > 2) S.cut(B, v, F::pow(root_of_unity<F>(), F::LO), B1, B3);
+        else B3 = B;
+        std::vector<Poly<F>> p4;
+        const double t_parts = best_us(reps, [&] {
+            p4.clear();
+            S.classes(A0, wp, 0, F::canon_any((T)777), p4);
+            S.classes(A2, wp, 2, F::canon_any((T)777), p4);
+            S.classes(B1, wp, 1, F::canon_any((T)777), p4);
+            S.classes(B3, wp, 3, F::canon_any((T)777), p4);
+        });
+        // one class gcd on part B1 against one product mod B1 (scalar)
+        Poly<F> wr = wp;
+        rem_monic<F>(wr, B1);
+        wr[0] = F::sub(wr[0], 5);
+        const double t_g8 = best_us(reps, [&] {
+            for (int i = 0; i < 16; ++i) sink += gcd_rows<F>(B1, wr, true, false).size();
+        }) / 16;
+        const size_t m8 = B1.size() - 1;
+        std::vector<typename F::A> acc(2 * m8);
+        Poly<F> pr = wr;
+        pr.resize(m8, 0);
+        const double t_m8 = best_us(reps, [&] {
+            for (int it = 0; it < 16; ++it) {
+                std::fill(acc.begin(), acc.end(), typename F::A(0));
+                for (size_t i = 0; i < m8; ++i)
+                    for (size_t j = 0; j < m8; ++j) F::mac(acc[i + j], pr[i], wr[j < wr.size() ? j : 0]);
+                for (size_t k = 2 * m8 - 1; k-- > m8;) {
+                    const T q = F::red(acc[k]);
+                    for (size_t i = 0; i < m8; ++i) F::mac(acc[k - m8 + i], q, F::neg(B1[i]));
+                }
+                for (size_t i = 0; i < m8; ++i) pr[i] = F::red(acc[i]);
+            }
+        }) / 16;
+        sink += pr[0];
+        // the 11 class gcds of part B1: one at a time against one batch
+        std::vector<Poly<F>> wrs;
+        for (int j = 0; j < (int)F::LO; ++j) {
+            wrs.push_back(wp);
+            rem_monic<F>(wrs.back(), B1);
+            if (wrs.back().empty()) wrs.back().push_back(0);
+            wrs.back()[0] = F::sub(wrs.back()[0], (T)(1000 + j));
+        }
+        const double t_seq = best_us(reps, [&] {
+            for (auto &b : wrs) sink += gcd_rows<F>(B1, b, true, false).size();
+        });
+        const double t_bat = best_us(reps, [&] { sink += gcd_many<F>(B1, wrs).size(); });
+        const double t_rem = best_us(reps, [&] {
+            Poly<F> wg = wp;
+            rem_monic<F>(wg, B1);
+            sink += wg.size();
+        });
+        std::vector<Poly<F>> p1;
+        const double t_cl1 = best_us(reps, [&] {
+            p1.clear();
+            S.classes(B1, wp, 1, F::canon_any((T)777), p1);
+        });
+        printf("{\"field\": \"%s\", \"class_gcds_seq_us\": %.3f, \"class_gcds_batch_us\": %.3f, \"rem_w_us\": %.3f, "
+               "\"classes_B1_us\": %.3f, \"B1_parts\": %zu}\n",
+               name, t_seq, t_bat, t_rem, t_cl1, p1.size());
+        printf("{\"field\": \"%s\", \"deg\": %zu, \"gcd_part_us\": %.3f, \"mulmod_part_us\": %.3f}\n", name, m8,
+               t_g8, t_m8);
+        printf("{\"field\": \"%s\", \"d\": %u, \"run_us\": %.2f, \"run_parts\": %zu, \"classes4_us\": %.2f, "
+               "\"parts4\": %zu, \"deg\": [%zu, %zu, %zu, %zu]}\n",
+               name, d, t_run, rp.size(), t_parts, p4.size(), A0.size() ? A0.size() - 1 : 0,
+               A2.size() ? A2.size() - 1 : 0, B1.size() ? B1.size() - 1 : 0, B3.size() ? B3.size() - 1 : 0);
+    }
+    // what follows the top-level split in split(): the parts of >= 3 roots
+    // (a ring and a split each), the quadratics (a square root each) — the
+    // parts of the real top-level split above
+    {
+        std::vector<Poly<F>> big, quad;
+        for (auto &p : rp)
+            if (p.size() > 3) big.push_back(p);
+            else if (p.size() == 3) quad.push_back(p);
+        const double t_big = best_us(reps, [&] {
+            for (auto g : big) {
+                make_monic<F>(g);
+                ModRing<F> R2(g);
+                std::vector<Poly<F>> sp;
+                S.run(R2, g, F::canon_any((T)4242), sp);
+                sink += sp.size();
+            }
+        });
+        const double t_quad = best_us(reps, [&] {
+            for (auto &g : quad) {
+                T r;
+                sink += F::sqrt(F::sub(F::mul(g[1], g[1]), F::mul(F::mul(4, g[2]), g[0])), r);
+                sink += r;
+            }
+        });
+        double t_ring2 = 0, t_pow2 = 0;
+        if (!big.empty()) {
+            Poly<F> g = big[0];
+            make_monic<F>(g);
+            t_ring2 = best_us(reps, [&] { ModRing<F> R2(g); sink += R2.m; });
+            ModRing<F> R2(g);
+            t_pow2 = best_us(reps, [&] { sink += R2.pow_lin(F::canon_any((T)4242), F::PM1 / F::L)[0]; });
+        }
+        printf("{\"field\": \"%s\", \"part0_ring_us\": %.2f, \"part0_pow_us\": %.2f}\n", name, t_ring2, t_pow2);
+        std::string degs;
+        for (auto &p : big) degs += std::to_string(p.size() - 1) + " ";
+        printf("{\"field\": \"%s\", \"big_parts_us\": %.2f, \"big_degs\": \"%s\", \"quadratics\": %zu, "
+               "\"quad_us\": %.2f}\n",
+               name, t_big, degs.c_str(), quad.size(), t_quad);
+    }
     const double t_inv = best_us(reps, [&] {
         T x = 3;
         for (int i = 0; i < 16; ++i) x = F::inv(F::add(x, 1));

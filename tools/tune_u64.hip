@@ -28,12 +28,13 @@ __global__ void k_fill(uint64_t *out, uint64_t n, uint64_t seed) {
         out[i] = splitmix_mix(seed + (i + 1) * GAMMA);
 }
 
-template <int NA, int MODE, int SG, int ABL, int OCC, int PF = 0, bool BSH = false, int LD = 0, int PRIO = 0>
+template <int NA, int MODE, int SG, int ABL, int OCC, int PF = 0, bool BSH = false, int LD = 0, int PRIO = 0,
+          int TR = 0>
 __global__ __launch_bounds__(256, OCC) void k_var(const uint64_t *ids, uint64_t n, uint32_t T, uint64_t *partials,
                                                   uint64_t *clk) {
     uint64_t t0 = 0, r0 = 0;
     if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
-    bsgs64::body<NA, MODE, SG, ABL, PF, false, BSH, LD, 0, bsgs64::NB, PRIO>(ids, n, T, partials);
+    bsgs64::body<NA, MODE, SG, ABL, PF, false, BSH, LD, 0, bsgs64::NB, PRIO, TR>(ids, n, T, partials);
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
         clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
@@ -59,11 +60,11 @@ int main() {
     // (the round-3/4 layout and carry-mode variants are in the git history and
     // profiles/r03/tune_u64*.json, profiles/r04/u64/)
     std::vector<Var> vars = {
-        {"product: mode3 sg14 + s_setprio in the MAC step", k_var<10, 3, 14, 0, 4, 0, true, 1, 1>, 4},
-        {"mode3 sg14, row-0 sums at 1 and the MACs at 2", k_var<10, 3, 14, 0, 4, 0, true, 1, 3>, 4},
-        {"mode3 sg16, row-0 sums at 1 and the MACs at 2", k_var<10, 3, 16, 0, 4, 0, true, 1, 3>, 4},
-        {"product again", k_var<10, 3, 14, 0, 4, 0, true, 1, 1>, 4},
-        {"mode3 sg14, row-0 sums at 1 and the MACs at 2 (again)", k_var<10, 3, 14, 0, 4, 0, true, 1, 3>, 4},
+        {"product: mode3 sg14, row-0 sums at prio 1, MACs at 2", k_var<10, 3, 14, 0, 4, 0, true, 1, 3>, 4},
+        {"product-tree step 1 (paired products)", k_var<10, 3, 14, 0, 4, 0, true, 1, 3, 1>, 4},
+        {"product-tree step 1, sg16", k_var<10, 3, 16, 0, 4, 0, true, 1, 3, 1>, 4},
+        {"product again", k_var<10, 3, 14, 0, 4, 0, true, 1, 3>, 4},
+        {"product-tree step 1 (again)", k_var<10, 3, 14, 0, 4, 0, true, 1, 3, 1>, 4},
     };
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
