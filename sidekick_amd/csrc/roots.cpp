@@ -921,6 +921,46 @@ template <class F> std::vector<Poly<F>> gcd_many(const Poly<F> &a, const std::ve
 // 44.6 against 43.4 us, u32 22.0 against 21.7 — below 8 coefficients the
 // vector forms' fixed costs exceed the scalar loops)
 static size_t ring_vec_min = 8;
+// Small moduli (degree 2 .. SMALL_MAX, the factors of a few roots that
+// split() re-splits): the product's top coefficients reduced independently
+// against a table of z^k mod f (k = M .. 2M-2, M coefficients each), fully
+// unrolled per degree — no chain of dependent reductions down the product.
+constexpr size_t SMALL_MAX = 7;
+static bool small_rings = true;   // (tools/prof_roots.cpp's A/B)
+template <class F, int M>
+static void sqr_small(typename F::T *a, const typename F::T *tab) {
+    using T = typename F::T;
+    using A = typename F::A;
+    A acc[2 * M - 1] = {};
+    for (int i = 0; i < M; ++i) {
+        F::mac(acc[2 * i], a[i], a[i]);
+        const T a2 = F::add(a[i], a[i]);
+        for (int j = i + 1; j < M; ++j) F::mac(acc[i + j], a2, a[j]);
+    }
+    T top[M - 1];
+    for (int r = 0; r < M - 1; ++r) top[r] = F::red(acc[M + r]);
+    for (int i = 0; i < M; ++i) {
+        A t = acc[i];
+        for (int r = 0; r < M - 1; ++r) F::mac(t, top[r], tab[r * M + i]);
+        a[i] = F::red(t);
+    }
+}
+template <class F, int M>
+static void mul_small(typename F::T *a, const typename F::T *b, const typename F::T *tab) {
+    using T = typename F::T;
+    using A = typename F::A;
+    A acc[2 * M - 1] = {};
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < M; ++j) F::mac(acc[i + j], a[i], b[j]);
+    T top[M - 1];
+    for (int r = 0; r < M - 1; ++r) top[r] = F::red(acc[M + r]);
+    for (int i = 0; i < M; ++i) {
+        A t = acc[i];
+        for (int r = 0; r < M - 1; ++r) F::mac(t, top[r], tab[r * M + i]);
+        a[i] = F::red(t);
+    }
+}
+
 // Arithmetic modulo a fixed monic f of degree m >= 1: residues are vectors of
 // exactly m coefficients.
 template <class F> struct ModRing {
@@ -937,9 +977,21 @@ template <class F> struct ModRing {
     const uint64_t *tl0 = nullptr, *tl1 = nullptr;
     std::vector<T> tmp;
 
+    std::vector<T> stab;     // the small-modulus table (sqr_small)
+    bool small = false;
+
     explicit ModRing(const Poly<F> &f) : m(f.size() - 1), nf(m), acc(2 * m) {
         for (size_t i = 0; i < m; ++i) nf[i] = F::neg(f[i]);
         vec = m >= ring_vec_min && m <= 1024 && cpu_has_avx512();
+        small = !vec && small_rings && m >= 2 && m <= SMALL_MAX;
+        if (small) {   // rows z^k mod f, k = m .. 2m-2, by z^(k+1) = z z^k
+            stab.resize((m - 1) * m);
+            std::vector<T> row(nf);
+            for (size_t r = 0; r + 1 < m; ++r) {
+                std::copy(row.begin(), row.end(), stab.begin() + r * m);
+                if (r + 2 < m) mul_lin(row, 0);
+            }
+        }
         if (!vec) return;
         const size_t mb = (m + 7) & ~(size_t)7;
         nf64.assign(mb + 8, 0);
@@ -986,6 +1038,16 @@ template <class F> struct ModRing {
         for (size_t i = 0; i < m; ++i) r[i] = F::red(acc[i]);
     }
     void sqr(std::vector<T> &a) {
+        if (small) {
+            switch (m) {
+            case 2: return sqr_small<F, 2>(a.data(), stab.data());
+            case 3: return sqr_small<F, 3>(a.data(), stab.data());
+            case 4: return sqr_small<F, 4>(a.data(), stab.data());
+            case 5: return sqr_small<F, 5>(a.data(), stab.data());
+            case 6: return sqr_small<F, 6>(a.data(), stab.data());
+            default: return sqr_small<F, 7>(a.data(), stab.data());
+            }
+        }
         if (vec) {
             if constexpr (F::W == 32) {
                 uint64_t *c = acc64.data() + ((8 - ((uintptr_t)acc64.data() / 8) % 8) % 8);   // 64-byte aligned
@@ -1012,6 +1074,16 @@ template <class F> struct ModRing {
     // a <- a b (both residues of m coefficients; b may alias a)
     void mul(std::vector<T> &a, const std::vector<T> &b) {
         if (&a == &b) return sqr(a);
+        if (small) {
+            switch (m) {
+            case 2: return mul_small<F, 2>(a.data(), b.data(), stab.data());
+            case 3: return mul_small<F, 3>(a.data(), b.data(), stab.data());
+            case 4: return mul_small<F, 4>(a.data(), b.data(), stab.data());
+            case 5: return mul_small<F, 5>(a.data(), b.data(), stab.data());
+            case 6: return mul_small<F, 6>(a.data(), b.data(), stab.data());
+            default: return mul_small<F, 7>(a.data(), b.data(), stab.data());
+            }
+        }
         if (vec) {
             if constexpr (F::W == 32) {
                 uint64_t *c = acc64.data() + ((8 - ((uintptr_t)acc64.data() / 8) % 8) % 8);

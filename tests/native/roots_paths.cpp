@@ -8,6 +8,7 @@
 //   the u32 squaring and product mod f:   scalar / AVX-512
 //   the multiplication by (z + c) mod f: scalar / AVX-512 (u32) / IFMA (u64)
 //   the u64 row operation d = alpha d - beta s:  scalar / AVX-512 / IFMA
+//   the small-modulus squaring and product (degree 2 .. 7): unrolled / loops
 //   the gcd of operands of <= 40 coefficients: register rows / row calls
 //   the field inverses: addition chains / field.h's binary ladders
 // over degrees 8 .. 70 (vector tails of every length), random and edge
@@ -74,6 +75,40 @@ template <class F> static int check_sqr(const char *name) {
                        got != want ? "sqr" : gotm != wantm ? "mul" : "mul_lin", m, mode, c);
                 return 1;
             }
+        }
+    }
+    return 0;
+}
+
+// the unrolled small-modulus squaring and product (degree 2 .. SMALL_MAX,
+// ModRing::small) against the generic scalar loops
+template <class F> static int check_small(const char *name) {
+    using T = typename F::T;
+    for (int c = 0; c < 6000; ++c) {
+        const size_t m = 2 + c % (SMALL_MAX - 1);
+        const bool worst = c % 7 == 0;
+        Poly<F> f(m + 1);
+        for (size_t i = 0; i < m; ++i) f[i] = worst ? F::neg(1) : pick<F>();
+        f[m] = 1;
+        std::vector<T> a(m), b(m);
+        for (size_t i = 0; i < m; ++i) {
+            a[i] = worst ? F::neg(1) : pick<F>();
+            b[i] = worst ? F::neg(1) : pick<F>();
+        }
+        ModRing<F> R(f);
+        if (!R.small) {
+            printf("%s: degree %zu ring not on the small path\n", name, m);
+            return 1;
+        }
+        std::vector<T> got = a, gotm = a, want = a, wantm = a;
+        R.sqr(got);
+        R.mul(gotm, b);
+        R.small = false;
+        R.sqr(want);
+        R.mul(wantm, b);
+        if (got != want || gotm != wantm) {
+            printf("%s small %s mismatch: m=%zu case=%d\n", name, got != want ? "sqr" : "mul", m, c);
+            return 1;
         }
     }
     return 0;
@@ -158,8 +193,8 @@ static int check_inv() {
 }
 
 int main() {
-    int rc = check_inv() | check_sqr<F64>("u64") | check_sqr<F32>("u32") | check_axmy64() | check_gcd<F32>("u32") |
-             check_gcd<F64>("u64");
+    int rc = check_inv() | check_sqr<F64>("u64") | check_sqr<F32>("u32") | check_small<F64>("u64") |
+             check_small<F32>("u32") | check_axmy64() | check_gcd<F32>("u32") | check_gcd<F64>("u64");
     printf("avx512=%d ifma=%d %s\n", (int)cpu_has_avx512(), (int)cpu_has_ifma(), rc ? "FAIL" : "ok");
     return rc;
 }

@@ -59,20 +59,20 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
             }
             for (uint32_t i = 1; i <= d; ++i) cv[i - 1] = h[d - i];
         }
-        const size_t gs[] = {0, 16, 24, 0, 16, 24}, vs[] = {8, 3};
+        const size_t gs[] = {24, 24, 24, 24, 24, 24}, vs[] = {0, 1};   // vs: small_rings
         printf("{\"field\": \"%s\", \"ab\": [", name);
         for (int r = 0; r < 6; ++r)
             for (int v = 0; v < 2; ++v) {
                 group_deg = gs[r];
-                ring_vec_min = vs[v];
+                small_rings = vs[v];
                 double t = 0;
                 for (auto &cv : cs) t += best_us(reps, [&] { sink += roots<F>(cv.data(), d).size(); }) / cs.size();
-                printf("%s{\"group_deg\": %zu, \"ring_vec_min\": %zu, \"roots_us\": %.2f}", r + v ? ", " : "",
+                printf("%s{\"group_deg\": %zu, \"small_rings\": %zu, \"roots_us\": %.2f}", r + v ? ", " : "",
                        gs[r], vs[v], t);
             }
         printf("]}\n");
         group_deg = 24;
-        ring_vec_min = 8;
+        small_rings = true;
     }
     const double t_ring = best_us(reps, [&] { ModRing<F> R(f); sink += R.m; });
     ModRing<F> R(f);
