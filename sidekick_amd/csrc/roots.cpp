@@ -327,14 +327,17 @@ QK_IFMA static void red64_tab(uint64_t *a, size_t m, const uint64_t *tl0, const 
         _mm512_store_si512(s0 + (k - m), _mm512_and_si512(v, mk52));
         _mm512_store_si512(s1 + (k - m), _mm512_srli_epi64(v, 52));
     }
-    // four output vectors at a time: four independent accumulator chains
-    // per table row instead of one (a row's seven IFMAs chain through B / C)
+    // four output vectors at a time, and each weight's three IFMAs of a row
+    // split over two accumulators (B / B2, C / C2, summed at the end): per
+    // row a chain of at most two dependent IFMAs per accumulator instead of
+    // three, below the unit's issue time for the row's 28
     for (size_t v0 = 0; 8 * v0 < m; v0 += 4) {
         const size_t nv = std::min<size_t>(4, (m - 8 * v0 + 7) / 8);
-        __m512i A[4], B[4], C[4];
+        __m512i A[4], B[4], C[4], B2[4], C2[4];
         for (size_t u = 0; u < 4; ++u) {
             const size_t o = 8 * (v0 + (u < nv ? u : 0));
             A[u] = _mm512_load_si512(c0 + o), B[u] = _mm512_load_si512(c1 + o), C[u] = _mm512_load_si512(c2 + o);
+            B2[u] = C2[u] = _mm512_setzero_si512();
         }
         for (size_t r = 0; r + 1 < m; ++r) {
             const __m512i x0 = _mm512_set1_epi64((long long)s0[r]), x1 = _mm512_set1_epi64((long long)s1[r]);
@@ -345,13 +348,15 @@ QK_IFMA static void red64_tab(uint64_t *a, size_t m, const uint64_t *tl0, const 
                 A[u] = _mm512_madd52lo_epu64(A[u], x0, y0);
                 B[u] = _mm512_madd52hi_epu64(B[u], x0, y0);
                 C[u] = _mm512_madd52hi_epu64(C[u], x0, y1);
-                B[u] = _mm512_madd52lo_epu64(B[u], x0, y1);
-                C[u] = _mm512_madd52hi_epu64(C[u], x1, y0);
+                B2[u] = _mm512_madd52lo_epu64(B2[u], x0, y1);
+                C2[u] = _mm512_madd52hi_epu64(C2[u], x1, y0);
                 B[u] = _mm512_madd52lo_epu64(B[u], x1, y0);
                 C[u] = _mm512_madd52lo_epu64(C[u], x1, y1);
             }
         }
         for (size_t u = 0; u < nv; ++u) {
+            B[u] = _mm512_add_epi64(B[u], B2[u]);
+            C[u] = _mm512_add_epi64(C[u], C2[u]);
             const __m512i r = red_cols8(A[u], B[u], C[u]);
             const size_t v = v0 + u, rem = m - 8 * v;
             if (rem >= 8) _mm512_storeu_si512(a + 8 * v, r);
@@ -401,6 +406,76 @@ QK_IFMA static void sqr64_ifma(uint64_t *a, size_t m, const uint64_t *tl0, const
     red64_tab(a, m, tl0, tl1, c0, c1, c2);
 }
 
+// The same squaring with the product's column sums in registers (NQ = 2 mb /
+// 8 <= 8 column vectors of each weight: 24 zmm at mb = 32): sqr64_ifma's
+// per-(i, q) load-madd-store of the column vectors chains every row of a
+// column through store-to-load forwarding; here the rows of one column are
+// only a chain of register madds, and a column vector leaves (with its
+// diagonal terms added) as soon as the last row reaching it is done, so at
+// most ~5 column vectors are live.  The limbs and the diagonal are vector
+// operations (scalar stores under vector loads do not forward).
+template <int NQ>
+QK_IFMA static void sqr64_ifma_reg(uint64_t *a, size_t m, const uint64_t *tl0, const uint64_t *tl1, uint64_t *l0,
+                                   uint64_t *l1, uint64_t *c0, uint64_t *c1, uint64_t *c2) {
+    const __m512i mk52 = _mm512_set1_epi64((long long)M52);
+    for (size_t k = 0; k < m; k += 8) {   // the limbs, vector by vector
+        const __mmask8 mk = m - k >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << (m - k)) - 1u);
+        const __m512i v = _mm512_maskz_loadu_epi64(mk, a + k);
+        _mm512_mask_storeu_epi64(l0 + IPAD + k, mk, _mm512_and_si512(v, mk52));
+        _mm512_mask_storeu_epi64(l1 + IPAD + k, mk, _mm512_srli_epi64(v, 52));
+    }
+    __m512i A[NQ], B[NQ], C[NQ];
+    for (int q = 0; q < NQ; ++q) A[q] = B[q] = C[q] = _mm512_setzero_si512();
+    // rows i = 4s .. 4s+3 start at column vector s (their first product
+    // a_i a_(i+1) lands in column 2i + 1): that vector takes a fixed lane
+    // mask (j > i: lanes above 2t for i = 4s + t), the later ones full loads
+#pragma GCC unroll 8
+    for (int s = 0; s < NQ; ++s) {
+#pragma GCC unroll 4
+        for (int t = 0; t < 4; ++t) {
+            const size_t i = 4 * (size_t)s + t;
+            if (i + 1 >= m) break;
+            if (!a[i]) continue;
+            const __m512i x0 = _mm512_set1_epi64((long long)(a[i] & M52)),
+                          x1 = _mm512_set1_epi64((long long)(a[i] >> 52));
+            const int qhi = (int)((i + m - 1) / 8);
+            const __mmask8 mk = (__mmask8)(0xFFu << (2 * t + 1));
+            const uint64_t *w0 = l0 + IPAD + 8 * s - i, *w1 = l1 + IPAD + 8 * s - i;
+            __m512i y0 = _mm512_maskz_loadu_epi64(mk, w0), y1 = _mm512_maskz_loadu_epi64(mk, w1);
+#pragma GCC unroll 8
+            for (int q = s; q < NQ; ++q) {
+                if (q > qhi) break;
+                if (q > s) {
+                    y0 = _mm512_loadu_si512(w0 + 8 * (q - s));
+                    y1 = _mm512_loadu_si512(w1 + 8 * (q - s));
+                }
+                A[q] = _mm512_madd52lo_epu64(A[q], x0, y0);
+                B[q] = _mm512_madd52hi_epu64(B[q], x0, y0);
+                C[q] = _mm512_madd52hi_epu64(C[q], x0, y1);
+                B[q] = _mm512_madd52lo_epu64(B[q], x0, y1);
+                C[q] = _mm512_madd52hi_epu64(C[q], x1, y0);
+                B[q] = _mm512_madd52lo_epu64(B[q], x1, y0);
+                C[q] = _mm512_madd52lo_epu64(C[q], x1, y1);
+            }
+        }
+        // column vector s is complete (later rows start above it): its
+        // doubled off-diagonal sums plus the diagonal a_i^2 (i = 4s .. 4s+3,
+        // in the even lanes: u0^2 + 2 u0 u1 2^52 + u1^2 2^104 as lo / hi of
+        // u0 u0, u0 (2 u1) and u1 u1) go out, and its registers are free
+        const __m512i dix = _mm512_set_epi64(3, 3, 2, 2, 1, 1, 0, 0);
+        const __m512i d0 = _mm512_maskz_permutexvar_epi64((__mmask8)0x55, dix, _mm512_loadu_si512(l0 + IPAD + 4 * s)),
+                      d1 = _mm512_maskz_permutexvar_epi64((__mmask8)0x55, dix, _mm512_loadu_si512(l1 + IPAD + 4 * s)),
+                      d1x2 = _mm512_add_epi64(d1, d1);
+        _mm512_store_si512(c0 + 8 * s, _mm512_madd52lo_epu64(_mm512_slli_epi64(A[s], 1), d0, d0));
+        _mm512_store_si512(c1 + 8 * s,
+                           _mm512_madd52lo_epu64(_mm512_madd52hi_epu64(_mm512_slli_epi64(B[s], 1), d0, d0), d0, d1x2));
+        _mm512_store_si512(c2 + 8 * s,
+                           _mm512_madd52lo_epu64(_mm512_madd52hi_epu64(_mm512_slli_epi64(C[s], 1), d0, d1x2), d1, d1));
+    }
+    for (size_t k = 8 * NQ; k < 8 * NQ + 16; ++k) c0[k] = c1[k] = c2[k] = 0;
+    red64_tab(a, m, tl0, tl1, c0, c1, c2);
+}
+
 // a <- a b mod f on IFMA: every a_i against a window of b's limbs (l0 /
 // l1 hold b: IPAD zeros, b, zeros; out-of-range lanes read zeros), then
 // red64_tab
@@ -421,6 +496,54 @@ QK_IFMA static void mul64_ifma(uint64_t *a, const uint64_t *b, size_t m, const u
                     _mm512_loadu_si512(l1 + IPAD + lowest));
         }
     }
+    red64_tab(a, m, tl0, tl1, c0, c1, c2);
+}
+
+// The product in registers, as sqr64_ifma_reg: rows i = 8s .. 8s+7 start
+// at column vector s (windows below b's first limb read IPAD zeros), and a
+// column vector leaves once the last row reaching it is done.
+template <int NQ>
+QK_IFMA static void mul64_ifma_reg(uint64_t *a, const uint64_t *b, size_t m, const uint64_t *tl0,
+                                   const uint64_t *tl1, uint64_t *l0, uint64_t *l1, uint64_t *c0, uint64_t *c1,
+                                   uint64_t *c2) {
+    const __m512i mk52 = _mm512_set1_epi64((long long)M52);
+    for (size_t k = 0; k < m; k += 8) {
+        const __mmask8 mk = m - k >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << (m - k)) - 1u);
+        const __m512i v = _mm512_maskz_loadu_epi64(mk, b + k);
+        _mm512_mask_storeu_epi64(l0 + IPAD + k, mk, _mm512_and_si512(v, mk52));
+        _mm512_mask_storeu_epi64(l1 + IPAD + k, mk, _mm512_srli_epi64(v, 52));
+    }
+    __m512i A[NQ], B[NQ], C[NQ];
+    for (int q = 0; q < NQ; ++q) A[q] = B[q] = C[q] = _mm512_setzero_si512();
+#pragma GCC unroll 8
+    for (int s = 0; s < NQ; ++s) {
+#pragma GCC unroll 8
+        for (int t = 0; t < 8; ++t) {
+            const size_t i = 8 * (size_t)s + t;
+            if (i >= m) break;
+            if (!a[i]) continue;
+            const __m512i x0 = _mm512_set1_epi64((long long)(a[i] & M52)),
+                          x1 = _mm512_set1_epi64((long long)(a[i] >> 52));
+            const int qhi = (int)((i + m - 1) / 8);
+            const uint64_t *w0 = l0 + IPAD + 8 * s - i, *w1 = l1 + IPAD + 8 * s - i;
+#pragma GCC unroll 8
+            for (int q = s; q < NQ; ++q) {
+                if (q > qhi) break;
+                const __m512i y0 = _mm512_loadu_si512(w0 + 8 * (q - s)), y1 = _mm512_loadu_si512(w1 + 8 * (q - s));
+                A[q] = _mm512_madd52lo_epu64(A[q], x0, y0);
+                B[q] = _mm512_madd52hi_epu64(B[q], x0, y0);
+                C[q] = _mm512_madd52hi_epu64(C[q], x0, y1);
+                B[q] = _mm512_madd52lo_epu64(B[q], x0, y1);
+                C[q] = _mm512_madd52hi_epu64(C[q], x1, y0);
+                B[q] = _mm512_madd52lo_epu64(B[q], x1, y0);
+                C[q] = _mm512_madd52lo_epu64(C[q], x1, y1);
+            }
+        }
+        _mm512_store_si512(c0 + 8 * s, A[s]);
+        _mm512_store_si512(c1 + 8 * s, B[s]);
+        _mm512_store_si512(c2 + 8 * s, C[s]);
+    }
+    for (size_t k = 8 * NQ; k < 8 * NQ + 16; ++k) c0[k] = c1[k] = c2[k] = 0;
     red64_tab(a, m, tl0, tl1, c0, c1, c2);
 }
 
@@ -458,22 +581,31 @@ QK_IFMA static void axmy64_ifma(uint64_t *d, const uint64_t *s, size_t m, uint64
 
 // a <- a (z + c) mod f on IFMA: out[i] = a[i-1] + c a[i] + top nf[i] as
 // column sums (a[i-1]'s limbs added to the low two columns)
+// The shifted a (a[i-1]) is an unaligned load one slot down (the first
+// vector: a's lanes moved up one by valignq); the vectors go from the top down, so each reads
+// its window before the store of the vector below it overwrites a slot of
+// it.  c = 0 (the reduction table's z z^k): no c a product.
 QK_IFMA static void mullin64_ifma(uint64_t *a, size_t m, uint64_t c, const uint64_t *nf, uint64_t *tmp) {
+    (void)tmp;
     const uint64_t top = a[m - 1];
-    tmp[0] = 0;
-    for (size_t i = 1; i < m; ++i) tmp[i] = a[i - 1];
     const __m512i c0 = _mm512_set1_epi64((long long)(c & M52)), c1 = _mm512_set1_epi64((long long)(c >> 52)),
                   t0 = _mm512_set1_epi64((long long)(top & M52)), t1 = _mm512_set1_epi64((long long)(top >> 52));
-    for (size_t i = 0; i < m; i += 8) {
+    for (size_t i = (m - 1) & ~(size_t)7;; i -= 8) {
         const size_t r = m - i;
+        const __mmask8 mk = r >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << r) - 1u);
         __m512i a0, a1, n0, n1, A, B;
-        split52(ld8q(a + i, r), a0, a1);
+        const __m512i sh = i ? _mm512_maskz_loadu_epi64(mk, a + i - 1)   // (lane 0 of the first: a[-1] = 0)
+                             : _mm512_alignr_epi64(_mm512_maskz_loadu_epi64(mk, a), _mm512_setzero_si512(), 7);
+        split52(sh, A, B);
         split52(ld8q(nf + i, r), n0, n1);
-        split52(ld8q(tmp + i, r), A, B);
         __m512i C = _mm512_setzero_si512();
-        prod52(A, B, C, c0, c1, a0, a1);
+        if (c) {
+            split52(ld8q(a + i, r), a0, a1);
+            prod52(A, B, C, c0, c1, a0, a1);
+        }
         prod52(A, B, C, t0, t1, n0, n1);
         st8q(a + i, r, red_cols8(A, B, C));
+        if (!i) break;
     }
 }
 
@@ -561,6 +693,13 @@ struct F32 {
         r = pow32(n, (uint64_t)(P32 + 1) / 4);
         return mul32(r, r) == n;
     }
+    // the same in two halves around one exponentiation (sqrt_many)
+    static constexpr uint64_t SQRT_E = (uint64_t)(P32 + 1) / 4;
+    static T sqrt_base(T n) { return n; }
+    static bool sqrt_fin(T n, T v, T &r) {
+        r = v;
+        return mul32(r, r) == n;
+    }
 };
 
 struct F64 {
@@ -598,7 +737,34 @@ struct F64 {
         r = mul64(mul64(n, v), sub64(i, 1));
         return mul64(r, r) == n;
     }
+    // the same in two halves around one exponentiation (sqrt_many)
+    static constexpr uint64_t SQRT_E = (P64 - 5) / 8;
+    static T sqrt_base(T n) { return add64(n, n); }
+    static bool sqrt_fin(T n, T v, T &r) {
+        const T n2 = add64(n, n), i = mul64(n2, mul64(v, v));
+        r = mul64(mul64(n, v), sub64(i, 1));
+        return mul64(r, r) == n;
+    }
 };
+
+// Square roots of several n at once (ok[j]: n_j is a residue): the
+// exponentiations' square-and-multiply steps interleaved across the n_j, so
+// their dependent product chains overlap
+template <class F>
+static void sqrt_many(const std::vector<typename F::T> &n, std::vector<typename F::T> &r, std::vector<char> &ok) {
+    using T = typename F::T;
+    const size_t cnt = n.size();
+    std::vector<T> x(cnt), v(cnt, 1);
+    for (size_t j = 0; j < cnt; ++j) x[j] = F::sqrt_base(n[j]);
+    for (int b = 63 - __builtin_clzll(F::SQRT_E); b >= 0; --b) {
+        for (size_t j = 0; j < cnt; ++j) v[j] = F::mul(v[j], v[j]);
+        if ((F::SQRT_E >> b) & 1)
+            for (size_t j = 0; j < cnt; ++j) v[j] = F::mul(v[j], x[j]);
+    }
+    r.resize(cnt);
+    ok.resize(cnt);
+    for (size_t j = 0; j < cnt; ++j) ok[j] = F::sqrt_fin(n[j], v[j], r[j]);
+}
 
 // Polynomials: coefficient vectors low degree first, canonical, no trailing
 // zeros (the zero polynomial is empty).
@@ -623,6 +789,30 @@ template <class F> void rem_monic(Poly<F> &a, const Poly<F> &b) {
         a[k] = 0;
     }
     trim<F>(a);
+}
+
+// r_j = a mod b_j for several monic b_j at once: the same steps as
+// rem_monic, one step of every remainder per sweep — each remainder is a
+// chain of dependent steps (a step's quotient is the coefficient the
+// previous step just wrote), the sweep lets the core overlap the chains
+template <class F> std::vector<Poly<F>> rem_many(const Poly<F> &a, const std::vector<const Poly<F> *> &bs) {
+    const size_t cnt = bs.size();
+    std::vector<Poly<F>> r(cnt, a);
+    std::vector<size_t> k(cnt, a.size());
+    for (bool any = true; any;) {
+        any = false;
+        for (size_t j = 0; j < cnt; ++j) {
+            const size_t m = bs[j]->size() - 1;
+            if (k[j] <= m) continue;
+            const size_t t = --k[j];
+            const typename F::T q = r[j][t];
+            if (q) axmy<F>(r[j].data() + t - m, bs[j]->data(), m, 1, q);
+            r[j][t] = 0;
+            any = true;
+        }
+    }
+    for (auto &x : r) trim<F>(x);
+    return r;
 }
 
 // a / b (b monic), exact division assumed
@@ -738,9 +928,9 @@ constexpr int GB_MAX = 24;
         memset(buf[j], 0, sizeof(buf[j]));                                                              \
         pa[j] = buf[j] + 8 * NV;                                                                        \
         pb[j] = buf[j] + 3 * 8 * NV;                                                                    \
-        for (size_t i = 0; i < na0; ++i) pa[j][i] = a0[i];                                              \
+        for (size_t i = 0; i < na0[j]; ++i) pa[j][i] = a0[j][i];                                        \
         for (size_t i = 0; i < nb0[j]; ++i) pb[j][i] = b0[j][i];                                        \
-        na[j] = na0;                                                                                    \
+        na[j] = na0[j];                                                                                 \
         nb[j] = nb0[j];                                                                                 \
         live[j] = true;                                                                                 \
     }                                                                                                   \
@@ -773,7 +963,7 @@ constexpr int GB_MAX = 24;
     }
 // out: cnt rows of SO = 8 NV coefficients; nout[j]: the gcd's coefficient count
 template <class F, int NV>
-QK_AVX512 static void gcd_batch(const typename F::T *a0, size_t na0, int cnt, const typename F::T *const *b0,
+QK_AVX512 static void gcd_batch(const typename F::T *const *a0, const size_t *na0, int cnt, const typename F::T *const *b0,
                                 const size_t *nb0, typename F::T *out, size_t *nout) {
     using T = typename F::T;
     constexpr size_t SO = 8 * NV;
@@ -784,7 +974,7 @@ QK_AVX512 static void gcd_batch(const typename F::T *a0, size_t na0, int cnt, co
     }
 }
 template <int NV>
-QK_IFMA static void gcd_batch64_ifma(const uint64_t *a0, size_t na0, int cnt, const uint64_t *const *b0,
+QK_IFMA static void gcd_batch64_ifma(const uint64_t *const *a0, const size_t *na0, int cnt, const uint64_t *const *b0,
                                      const size_t *nb0, uint64_t *out, size_t *nout) {
     using T = uint64_t;
     constexpr size_t SO = 8 * NV;
@@ -859,48 +1049,49 @@ template <class F> Poly<F> gcd_rows(const Poly<F> &a0, const Poly<F> &b0, bool s
 }
 template <class F> Poly<F> gcd(const Poly<F> &a, const Poly<F> &b) { return gcd_rows<F>(a, b, true); }
 
-// gcd(a, b_j) for every j, as gcd_rows(a, b_j, true, false) would return
-// them ({1} when coprime), the small cases as one gcd_batch
-template <class F> std::vector<Poly<F>> gcd_many(const Poly<F> &a, const std::vector<Poly<F>> &bs) {
+// gcd(a_j, b_j) for every j, as gcd_rows(a_j, b_j, true, false) would
+// return them ({1} when coprime), the small cases as one gcd_batch
+template <class F> std::vector<Poly<F>> gcd_pairs(const std::vector<const Poly<F> *> &as, const std::vector<Poly<F>> &bs) {
     using T = typename F::T;
     const int cnt = (int)bs.size();
     std::vector<Poly<F>> res(cnt);
-    size_t na = a.size(), n = na;
-    while (na && !a[na - 1]) --na;
-    const T *bp[GB_MAX];
-    size_t nb[GB_MAX];
+    size_t n = 0;
+    const T *ap[GB_MAX], *bp[GB_MAX];
+    size_t na[GB_MAX], nb[GB_MAX];
     for (int j = 0; j < cnt && j < GB_MAX; ++j) {
-        size_t k = bs[j].size();
-        while (k && !bs[j][k - 1]) --k;
+        size_t ka = as[j]->size(), kb = bs[j].size();
+        while (ka && !(*as[j])[ka - 1]) --ka;
+        while (kb && !bs[j][kb - 1]) --kb;
+        ap[j] = as[j]->data();
+        na[j] = ka;
         bp[j] = bs[j].data();
-        nb[j] = k;
-        n = std::max(n, k);
+        nb[j] = kb;
+        n = std::max(n, std::max(ka, kb));
     }
     if (cnt <= GB_MAX && n <= 40 && cpu_has_avx512()) {
-        constexpr size_t SO = 40;
-        alignas(64) T out[GB_MAX * SO];
+        alignas(64) T out[GB_MAX * 40];
         size_t nout[GB_MAX];
         const int nv = (int)((n + 7) / 8);
         if constexpr (F::W == 64) {
             if (cpu_has_ifma()) {
                 uint64_t *o = (uint64_t *)out;
-                const uint64_t *const *b = (const uint64_t *const *)bp;
+                const uint64_t *const *a = (const uint64_t *const *)ap, *const *b = (const uint64_t *const *)bp;
                 switch (nv) {
-                case 1: gcd_batch64_ifma<1>(a.data(), na, cnt, b, nb, o, nout); break;
-                case 2: gcd_batch64_ifma<2>(a.data(), na, cnt, b, nb, o, nout); break;
-                case 3: gcd_batch64_ifma<3>(a.data(), na, cnt, b, nb, o, nout); break;
-                case 4: gcd_batch64_ifma<4>(a.data(), na, cnt, b, nb, o, nout); break;
-                default: gcd_batch64_ifma<5>(a.data(), na, cnt, b, nb, o, nout); break;
+                case 1: gcd_batch64_ifma<1>(a, na, cnt, b, nb, o, nout); break;
+                case 2: gcd_batch64_ifma<2>(a, na, cnt, b, nb, o, nout); break;
+                case 3: gcd_batch64_ifma<3>(a, na, cnt, b, nb, o, nout); break;
+                case 4: gcd_batch64_ifma<4>(a, na, cnt, b, nb, o, nout); break;
+                default: gcd_batch64_ifma<5>(a, na, cnt, b, nb, o, nout); break;
                 }
                 goto have;
             }
         }
         switch (nv) {
-        case 1: gcd_batch<F, 1>(a.data(), na, cnt, bp, nb, out, nout); break;
-        case 2: gcd_batch<F, 2>(a.data(), na, cnt, bp, nb, out, nout); break;
-        case 3: gcd_batch<F, 3>(a.data(), na, cnt, bp, nb, out, nout); break;
-        case 4: gcd_batch<F, 4>(a.data(), na, cnt, bp, nb, out, nout); break;
-        default: gcd_batch<F, 5>(a.data(), na, cnt, bp, nb, out, nout); break;
+        case 1: gcd_batch<F, 1>(ap, na, cnt, bp, nb, out, nout); break;
+        case 2: gcd_batch<F, 2>(ap, na, cnt, bp, nb, out, nout); break;
+        case 3: gcd_batch<F, 3>(ap, na, cnt, bp, nb, out, nout); break;
+        case 4: gcd_batch<F, 4>(ap, na, cnt, bp, nb, out, nout); break;
+        default: gcd_batch<F, 5>(ap, na, cnt, bp, nb, out, nout); break;
         }
     have:
         // gcd_batch<NV> writes row j at j * 8 NV
@@ -909,11 +1100,14 @@ template <class F> std::vector<Poly<F>> gcd_many(const Poly<F> &a, const std::ve
             if (nout[j] == 1) res[j] = Poly<F>{1};
             else res[j].assign(out + j * so, out + j * so + nout[j]);
         }
-        (void)SO;
         return res;
     }
-    for (int j = 0; j < cnt; ++j) res[j] = gcd_rows<F>(a, bs[j], true, false);
+    for (int j = 0; j < cnt; ++j) res[j] = gcd_rows<F>(*as[j], bs[j], true, false);
     return res;
+}
+// gcd(a, b_j) for every j (one shared first operand)
+template <class F> std::vector<Poly<F>> gcd_many(const Poly<F> &a, const std::vector<Poly<F>> &bs) {
+    return gcd_pairs<F>(std::vector<const Poly<F> *>(bs.size(), &a), bs);
 }
 
 // the smallest modulus degree on the vector paths (a variable for
@@ -921,6 +1115,8 @@ template <class F> std::vector<Poly<F>> gcd_many(const Poly<F> &a, const std::ve
 // 44.6 against 43.4 us, u32 22.0 against 21.7 — below 8 coefficients the
 // vector forms' fixed costs exceed the scalar loops)
 static size_t ring_vec_min = 8;
+static bool reg_sqr = true;   // sqr64_ifma_reg for moduli of <= 32 coefficients (prof_roots A/B)
+static bool pair_cuts = true;  // Splitter::cut2 for the two second-level cuts (prof_roots A/B)
 // Small moduli (degree 2 .. SMALL_MAX, the factors of a few roots that
 // split() re-splits): the product's top coefficients reduced independently
 // against a table of z^k mod f (k = M .. 2M-2, M coefficients each), fully
@@ -1053,9 +1249,17 @@ template <class F> struct ModRing {
                 uint64_t *c = acc64.data() + ((8 - ((uintptr_t)acc64.data() / 8) % 8) % 8);   // 64-byte aligned
                 sqr32_avx512(a.data(), m, tl0, a64.data(), c);
             } else if (ifma) {
-                const size_t cw = 2 * ((m + 7) & ~(size_t)7) + 16;
+                const size_t mb = (m + 7) & ~(size_t)7, cw = 2 * mb + 16;
                 uint64_t *c = cols.data() + ((8 - ((uintptr_t)cols.data() / 8) % 8) % 8);   // 64-byte aligned
-                sqr64_ifma((uint64_t *)a.data(), m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                uint64_t *x = (uint64_t *)a.data();
+                if (reg_sqr) switch (mb) {
+                    case 8: return sqr64_ifma_reg<2>(x, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    case 16: return sqr64_ifma_reg<4>(x, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    case 24: return sqr64_ifma_reg<6>(x, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    case 32: return sqr64_ifma_reg<8>(x, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    default: break;
+                    }
+                sqr64_ifma(x, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
             } else {
                 sqr64_avx512((uint64_t *)a.data(), m, nf64.data(), a64.data(), acc64.data(), cnt64.data());
             }
@@ -1089,10 +1293,18 @@ template <class F> struct ModRing {
                 uint64_t *c = acc64.data() + ((8 - ((uintptr_t)acc64.data() / 8) % 8) % 8);
                 return mul32_avx512(a.data(), b.data(), m, tl0, a64.data(), c);
             } else if (ifma) {
-                const size_t cw = 2 * ((m + 7) & ~(size_t)7) + 16;
+                const size_t mb = (m + 7) & ~(size_t)7, cw = 2 * mb + 16;
                 uint64_t *c = cols.data() + ((8 - ((uintptr_t)cols.data() / 8) % 8) % 8);
-                return mul64_ifma((uint64_t *)a.data(), (const uint64_t *)b.data(), m, tl0, tl1, l0.data(), l1.data(),
-                                  c, c + cw, c + 2 * cw);
+                uint64_t *x = (uint64_t *)a.data();
+                const uint64_t *y = (const uint64_t *)b.data();
+                if (reg_sqr) switch (mb) {
+                    case 8: return mul64_ifma_reg<2>(x, y, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    case 16: return mul64_ifma_reg<4>(x, y, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    case 24: return mul64_ifma_reg<6>(x, y, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    case 32: return mul64_ifma_reg<8>(x, y, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
+                    default: break;
+                    }
+                return mul64_ifma(x, y, m, tl0, tl1, l0.data(), l1.data(), c, c + cw, c + 2 * cw);
             }
         }
         std::fill(acc.begin(), acc.end(), A(0));
@@ -1220,15 +1432,16 @@ template <class F> class Splitter {
     // there) is in no class; whatever else is missing lies outside GF(p) (the
     // fast path's failure case): then the found factors, made monic, and the
     // rest.
-    void classes(const Poly<F> &g, const Poly<F> &w, uint32_t c, T a, std::vector<Poly<F>> &parts) const {
+    void classes(const Poly<F> &g, const Poly<F> &w, uint32_t c, T a, std::vector<Poly<F>> &parts,
+                 bool reduced = false) const {
         if (g.size() <= 1) return;
         if (g.size() == 2) {
             parts.push_back(g);
             return;
         }
         const size_t k = g.size() - 1;
-        Poly<F> wg = w;
-        rem_monic<F>(wg, g);
+        Poly<F> wg = w;   // w mod g (reduced: the caller's rem_many did it)
+        if (!reduced) rem_monic<F>(wg, g);
         if (wg.empty()) wg.push_back(0);
         T zj = zc[c];
         std::vector<Poly<F>> hs, wrs;
@@ -1262,6 +1475,27 @@ template <class F> class Splitter {
             parts.push_back(std::move(h));
         }
         if (rem.size() > 1) parts.push_back(std::move(rem));
+    }
+    // cut(g, u, c, ...) and cut(h, u, e, ...) at once: the two gcds as one
+    // batch, their leading coefficients inverted together
+    static void cut2(const Poly<F> &g, const Poly<F> &h, const Poly<F> &u, T c, T e, Poly<F> &gin, Poly<F> &gout,
+                     Poly<F> &hin, Poly<F> &hout) {
+        std::vector<Poly<F>> ur = rem_many<F>(u, {&g, &h});
+        for (auto &r : ur)
+            if (r.empty()) r.push_back(0);
+        ur[0][0] = F::sub(ur[0][0], c);
+        ur[1][0] = F::sub(ur[1][0], e);
+        std::vector<Poly<F>> d = gcd_pairs<F>({&g, &h}, ur);
+        const T lg = d[0].back(), lh = d[1].back();
+        const T inv = F::inv(F::mul(lg, lh)), ig = F::mul(inv, lh), ih = F::mul(inv, lg);
+        for (auto &v : d[0]) v = F::mul(v, ig);
+        for (auto &v : d[1]) v = F::mul(v, ih);
+        gin = std::move(d[0]);
+        hin = std::move(d[1]);
+        gout = gin.size() > 1 ? div_monic<F>(g, gin) : g;
+        hout = hin.size() > 1 ? div_monic<F>(h, hin) : h;
+        if (gin.size() <= 1) gin.clear();
+        if (hin.size() <= 1) hin.clear();
     }
     // g = gcd(g, u - c) * (g / that): the roots where u == c, and the rest
     static void cut(const Poly<F> &g, const Poly<F> &u, T c, Poly<F> &in, Poly<F> &out) {
@@ -1308,14 +1542,28 @@ template <class F> class Splitter {
                 static_assert(F::E == 4, "p - 1 has at most 2^2");
                 cut(g, pw.q, 1, A, B);   // v^2 = +-1: j even / odd
                 Poly<F> A0, A2, B1, B3;
-                if (A.size() > 2) cut(A, pw.v, 1, A0, A2);   // j = 0 / 2 mod 4
-                else A2 = A;
-                if (B.size() > 2) cut(B, pw.v, i4, B1, B3);  // j = 1 / 3 mod 4
-                else B3 = B;
-                classes(A0, pw.w, 0, a, parts);
-                classes(A2, pw.w, 2, a, parts);
-                classes(B1, pw.w, 1, a, parts);
-                classes(B3, pw.w, 3, a, parts);
+                if (A.size() > 2 && B.size() > 2 && pair_cuts) {
+                    cut2(A, B, pw.v, 1, i4, A0, A2, B1, B3);   // both at once
+                } else {
+                    if (A.size() > 2) cut(A, pw.v, 1, A0, A2);   // j = 0 / 2 mod 4
+                    else A2 = A;
+                    if (B.size() > 2) cut(B, pw.v, i4, B1, B3);  // j = 1 / 3 mod 4
+                    else B3 = B;
+                }
+                if (pair_cuts) {   // w mod the four parts as one rem_many
+                    const Poly<F> one{1};
+                    const Poly<F> *ps[4] = {&A0, &A2, &B1, &B3};
+                    std::vector<const Poly<F> *> bs;
+                    for (auto p : ps) bs.push_back(p->size() > 2 ? p : &one);
+                    const std::vector<Poly<F>> wr = rem_many<F>(pw.w, bs);
+                    const uint32_t cs[4] = {0, 2, 1, 3};
+                    for (int i = 0; i < 4; ++i) classes(*ps[i], wr[i], cs[i], a, parts, true);
+                } else {
+                    classes(A0, pw.w, 0, a, parts);
+                    classes(A2, pw.w, 2, a, parts);
+                    classes(B1, pw.w, 1, a, parts);
+                    classes(B3, pw.w, 3, a, parts);
+                }
             }
         }
     }
@@ -1343,6 +1591,7 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
     std::vector<T> num, den;
     std::vector<Poly<F>> todo{g0};
     std::vector<int> tries{0};
+    std::vector<T> qdisc, qnb, qd2;   // the quadratic leaves, solved together at the end
     uint64_t s = 0x243F6A8885A308D3ull;   // fixed seed: a deterministic sequence of a's
     while (!todo.empty()) {
         // this generation: the leaves now, the factors of >= 3 roots (big)
@@ -1358,19 +1607,11 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
                 den.push_back(g[1]);
                 continue;
             }
-            if (k == 2) {   // g2 z^2 + g1 z + g0: (-g1 +- sqrt(g1^2 - 4 g2 g0)) / (2 g2)
+            if (k == 2) {   // g2 z^2 + g1 z + g0: (-g1 +- sqrt(g1^2 - 4 g2 g0)) / (2 g2), below
                 const T a2 = g[2], b = g[1], c = g[0];
-                const T disc = F::sub(F::mul(b, b), F::mul(F::mul(4, a2), c));
-                T sq;
-                if (!F::sqrt(disc, sq)) {
-                    if (!exact) return false;
-                    continue;   // (cannot happen for an exact-mode factor)
-                }
-                const T nb = F::neg(b), d2 = F::add(a2, a2);
-                num.push_back(F::add(nb, sq));
-                den.push_back(d2);
-                num.push_back(F::sub(nb, sq));
-                den.push_back(d2);
+                qdisc.push_back(F::sub(F::mul(b, b), F::mul(F::mul(4, a2), c)));
+                qnb.push_back(F::neg(b));
+                qd2.push_back(F::add(a2, a2));
                 continue;
             }
             if (!exact && tries[i] >= 24) return false;
@@ -1422,6 +1663,22 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
                 }
             }
             i0 = i1;
+        }
+    }
+    // the quadratics: their square roots as one sqrt_many
+    if (!qdisc.empty()) {
+        std::vector<T> sq;
+        std::vector<char> ok;
+        sqrt_many<F>(qdisc, sq, ok);
+        for (size_t j = 0; j < qdisc.size(); ++j) {
+            if (!ok[j]) {
+                if (!exact) return false;
+                continue;   // (cannot happen for an exact-mode factor)
+            }
+            num.push_back(F::add(qnb[j], sq[j]));
+            den.push_back(qd2[j]);
+            num.push_back(F::sub(qnb[j], sq[j]));
+            den.push_back(qd2[j]);
         }
     }
     // num_i / den_i: prefix products, one inversion, back substitution

@@ -59,20 +59,20 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
             }
             for (uint32_t i = 1; i <= d; ++i) cv[i - 1] = h[d - i];
         }
-        const size_t gs[] = {24, 24, 24, 24, 24, 24}, vs[] = {0, 1};   // vs: small_rings
+        const size_t gs[] = {24, 24, 24, 24, 24, 24}, vs[] = {0, 1};   // vs: pair_cuts
         printf("{\"field\": \"%s\", \"ab\": [", name);
         for (int r = 0; r < 6; ++r)
             for (int v = 0; v < 2; ++v) {
                 group_deg = gs[r];
-                small_rings = vs[v];
+                pair_cuts = vs[v];
                 double t = 0;
                 for (auto &cv : cs) t += best_us(reps, [&] { sink += roots<F>(cv.data(), d).size(); }) / cs.size();
-                printf("%s{\"group_deg\": %zu, \"small_rings\": %zu, \"roots_us\": %.2f}", r + v ? ", " : "",
+                printf("%s{\"group_deg\": %zu, \"pair_cuts\": %zu, \"roots_us\": %.2f}", r + v ? ", " : "",
                        gs[r], vs[v], t);
             }
         printf("]}\n");
         group_deg = 24;
-        small_rings = true;
+        pair_cuts = true;
     }
     const double t_ring = best_us(reps, [&] { ModRing<F> R(f); sink += R.m; });
     ModRing<F> R(f);
@@ -86,6 +86,35 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
     const double t_mul = best_us(reps, [&] {
         for (int i = 0; i < 16; ++i) R.mul(a, b);
     }) / 16;
+    if constexpr (F::W == 64) {   // the IFMA squaring's two stages: the products, the reduction mod f
+        if (R.ifma) {
+            const size_t cw = 2 * ((R.m + 7) & ~(size_t)7) + 16;
+            uint64_t *c0 = R.cols.data() + ((8 - ((uintptr_t)R.cols.data() / 8) % 8) % 8);
+            std::vector<T> x = a;
+            R.sqr(x);   // leaves the last product's columns in c0 / c1 / c2
+            std::vector<uint64_t> keep(c0, c0 + 3 * cw);
+            const double t_red = best_us(reps, [&] {
+                for (int i = 0; i < 16; ++i) {
+                    std::copy(keep.begin(), keep.end(), c0);
+                    red64_tab((uint64_t *)x.data(), R.m, R.tl0, R.tl1, c0, c0 + cw, c0 + 2 * cw);
+                }
+            }) / 16;
+            const double t_cp = best_us(reps, [&] {
+                for (int i = 0; i < 16; ++i) std::copy(keep.begin(), keep.end(), c0);
+            }) / 16;
+            double t_sq[2];
+            for (int v = 0; v < 2; ++v) {
+                reg_sqr = v;
+                t_sq[v] = best_us(reps, [&] {
+                    for (int i = 0; i < 16; ++i) R.sqr(x);
+                }) / 16;
+            }
+            reg_sqr = true;
+            printf("{\"field\": \"%s\", \"m\": %zu, \"sqr_mem_us\": %.3f, \"sqr_reg_us\": %.3f, \"red64_tab_us\": %.3f, "
+                   "\"copy_us\": %.3f}\n",
+                   name, R.m, t_sq[0], t_sq[1], t_red, t_cp);
+        }
+    }
     std::vector<T> w;
     const double t_pow = best_us(reps, [&] { w = R.pow_lin(F::canon_any((T)12345), F::PM1 / F::L); });
     Poly<F> w1 = to_poly<F>(w);
@@ -239,7 +268,35 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
            name, d, t_v, t_cut, t_classes, parts.size(), A.size() ? A.size() - 1 : 0, t_inv);
 }
 
+// IFMA issue rate: 16 independent vpmadd52luq chains (ns per instruction),
+// and one dependent chain (ns of latency); best of 20
+QK_IFMA static void ifma_rate() {
+    __m512i acc[16];
+    for (int i = 0; i < 16; ++i) acc[i] = _mm512_set1_epi64(i);
+    const __m512i x = _mm512_set1_epi64(12345), y = _mm512_set1_epi64(678);
+    const int N = 1 << 16;
+    double t_thr = 1e30, t_lat = 1e30;
+    __m512i c = acc[0];
+    for (int r = 0; r < 20; ++r) {
+        auto t0 = std::chrono::steady_clock::now();
+        for (int it = 0; it < N; ++it)
+            for (int i = 0; i < 16; ++i) acc[i] = _mm512_madd52lo_epu64(acc[i], x, y);
+        for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(acc[i]));
+        auto t1 = std::chrono::steady_clock::now();
+        for (int it = 0; it < N * 4; ++it) c = _mm512_madd52lo_epu64(c, x, y);
+        asm volatile("" : "+v"(c));
+        auto t2 = std::chrono::steady_clock::now();
+        t_thr = std::min(t_thr, std::chrono::duration<double, std::nano>(t1 - t0).count());
+        t_lat = std::min(t_lat, std::chrono::duration<double, std::nano>(t2 - t1).count());
+    }
+    long long sink = _mm512_reduce_add_epi64(c);
+    for (int i = 0; i < 16; ++i) sink += _mm512_reduce_add_epi64(acc[i]);
+    printf("{\"ifma_ns_per_instr_independent\": %.4f, \"ifma_ns_latency\": %.4f, \"sink\": %lld}\n",
+           t_thr / (16.0 * N), t_lat / (4.0 * N), sink & 1);
+}
+
 int main(int argc, char **argv) {
+    if (cpu_has_ifma()) ifma_rate();
     const uint32_t d = argc > 1 ? (uint32_t)atoi(argv[1]) : 32;
     const int reps = argc > 2 ? atoi(argv[2]) : 200;
     prof<F32>("u32", d, reps);
