@@ -586,10 +586,12 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
         {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 1, 9},
         {"flow_fuse0", &qk_knobs::flow_fuse0, 0, 1},    {"flow_pipe", &qk_knobs::flow_pipe, 0, 1},
+        {"flow_nt", &qk_knobs::flow_nt, 0, 1},          {"flow_rs_nt", &qk_knobs::flow_rs_nt, 0, 3},
+        {"pkt_nt", &qk_knobs::pkt_nt, 0, 1},
         {"flow_prio", &qk_knobs::flow_prio, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},
         {"pkt_wgpc", &qk_knobs::pkt_wgpc, 1, 16},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
         {"root_test", &qk_knobs::root_test, 0, 2},      {"rt_direct", &qk_knobs::rt_direct, 0, 1},
-        {"rt_scan_u", &qk_knobs::rt_scan_u, 1, 4},      {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
+        {"rt_scan_u", &qk_knobs::rt_scan_u, 1, 4},      {"rt_scan_nt", &qk_knobs::rt_scan_nt, 0, 1},      {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
     };
     for (const K &k : table)
         if (strcmp(k.name, name) == 0) {

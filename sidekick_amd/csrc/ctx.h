@@ -32,6 +32,13 @@ struct qk_knobs {
                            // throughout; 2: pair arrays between the first and last pass; 3 / 4: 512 / 1024
                            // threads; 5 / 6: 11-bit digits, 512 / 1024 threads; 7-9: as 2, 5, 6 without LDS
                            // staging (direct scatter)
+    int pkt_nt = 1;        // the packet-batch kernels: records read nontemporal (t = 32, 1e8 records:
+                           // 1.83-1.84 -> 1.74-1.76 ms, profiles/r05/packets_nt/)
+    int flow_rs_nt = 1;    // grouping-sort scatters: bit 0 input read, bit 1 output written nontemporal
+                           // (bit 0: 1e6 flows 6.16 -> 6.02 ms, 1e4 4.01 -> 3.89; bit 1: +15 %,
+                           // profiles/r05/flows_nt/ab_rsnt.jsonl)
+    int flow_nt = 1;       // k_flow_extract: records read / (slot, id) written nontemporal (1e6 flows
+                           // 6.04 -> 5.93 ms, 16 flows 2.88 -> 2.81 ms, profiles/r05/flows_nt/)
     int flow_pipe = 0;     // 1: the flow extract reads its table one tile ahead (k_flow_extract_pipe: slower,
                            // 1e6 flows 7.14 vs 6.25 ms, 1e4 4.42 vs 4.11; profiles/r05/check4/ab_pipe.log)
     int flow_fuse0 = 1;    // 0: the grouping sort's first-digit counts by its own pass, not fused into the extract
@@ -42,6 +49,8 @@ struct qk_knobs {
     int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
     int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
     int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)
+    int rt_scan_nt = 1;    // root-set scan: nontemporal 16-byte loads of the log (u32 kernel 72 -> 66 us,
+                           // u64 135 -> 125 us at configs[4], profiles/r05/decode_nt/)
     int rt_scan_u = 1;     // root-set scan: 16-byte loads per lane per iteration (1, 2, 4; 3 runs as 2; 1: u32
                            // kernel 70 vs 84 / 78 us at 2 / 4, profiles/r04/decode_scan_u/)
     int rt_direct = 1;     // 0: the root-set scan's results by D2H copies instead of its host slots

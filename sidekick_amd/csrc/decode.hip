@@ -422,7 +422,8 @@ __device__ __forceinline__ bool rs_member(T x, const T *__restrict__ set, uint32
 // slots are pre-filled with ~0 by the host; a decode finds ~d hits).
 // U: 16-byte loads per lane per iteration (knob rt_scan_u; 1 is the fastest
 // measured)
-template <typename T, int S, int U = 1>
+// NT: the log's 16-byte loads nontemporal (knob rt_scan_nt)
+template <typename T, int S, int U = 1, bool NT = false>
 __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ log, uint64_t n, uint32_t head,
                                                         const T *__restrict__ tab, uint32_t words, uint32_t m1,
                                                         uint32_t m2, uint32_t shift, int use_stop, T stop_value,
@@ -445,7 +446,15 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ lo
     for (; i + (U - 1) * nthr < body; i += U * nthr) {
         Vec w[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = v[i + u * nthr];
+        for (int u = 0; u < U; ++u) {
+            if constexpr (NT) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(&v[i + u * nthr]));
+                __builtin_memcpy(&w[u], &x, 16);
+            } else {
+                w[u] = v[i + u * nthr];
+            }
+        }
         bool any = false, hit[U][V], st[U][V];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -540,7 +549,12 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
     const uint64_t units = (n + U * (16 / sizeof(T)) - 1) / (U * (16 / sizeof(T)));
     hipEvent_t e0 = prof_begin(ctx, s);
 #define QK_RS(SS, UU)                                                                                         \
-    hipLaunchKernelGGL((k_root_scan<T, SS, UU>), dim3(rs_grid(ctx, k_root_scan<T, SS, UU>, units, lds)),         \
+    do {                                                                                                      \
+        if (ctx->knobs.rt_scan_nt) QK_RSN(SS, UU, true);                                                      \
+        else QK_RSN(SS, UU, false);                                                                           \
+    } while (0)
+#define QK_RSN(SS, UU, NT_)                                                                                   \
+    hipLaunchKernelGGL((k_root_scan<T, SS, UU, NT_>), dim3(rs_grid(ctx, k_root_scan<T, SS, UU, NT_>, units, lds)), \
                        dim3(RT_BLOCK), lds, s, log, (uint64_t)n, head, d_tab, set.words, set.m1, set.m2, set.shift, \
                        use_stop, stop_value, hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N)
     if (set.S == 1) {
@@ -551,6 +565,7 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
         QK_RS(4, 1);
     }
 #undef QK_RS
+#undef QK_RSN
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());
     return QK_OK;

@@ -337,6 +337,8 @@ __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t pro
 // digit (slot & hmask, SLOT_NONE included), digit-major as k_rs_count writes
 // it, added into the sort's chunk (hgroup consecutive extract chunks; hcnt
 // zeroed first): the sort's first pass then reads no keys.
+// NT (knob flow_nt): the records read and the (slot, id) written nontemporal
+template <bool NT>
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
                                                            uint32_t stride, const qk_pkt_meta *__restrict__ meta,
                                                            uint64_t my_key_lo, uint64_t chunk,
@@ -369,15 +371,15 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     if (threadIdx.x == 0) l_new = 0;
     const bool pipe = stage_pipelined(stride, REC_TILE);
     TileStage st;
-    if (pipe && c0 < c1) stage_issue(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
+    if (pipe && c0 < c1) stage_issue<NT>(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
     for (uint64_t p0 = c0; p0 < c1; p0 += REC_TILE) {
         const uint64_t np = c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE;
         __syncthreads();   // previous tile fully consumed
-        const uint32_t r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records(bufs, n, stride, p0, np, tile);
+        const uint32_t r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records<NT>(bufs, n, stride, p0, np, tile);
         for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
         __syncthreads();
         if (pipe && p0 + REC_TILE < c1)   // next tile's loads fly while this one is classified
-            stage_issue(bufs, n, stride, p0 + REC_TILE,
+            stage_issue<NT>(bufs, n, stride, p0 + REC_TILE,
                         c1 - p0 - REC_TILE < (uint64_t)REC_TILE ? c1 - p0 - REC_TILE : REC_TILE, st);
         const bool valid = threadIdx.x < np;
         const uint64_t i = p0 + threadIdx.x;
@@ -419,8 +421,13 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
         __syncthreads();
         if (valid) {
             const uint32_t sl = cls == 1 ? l_slot[lead] : SLOT_NONE;
-            slots[i] = sl;
-            ids[i] = id;
+            if constexpr (NT) {
+                __builtin_nontemporal_store(sl, &slots[i]);
+                __builtin_nontemporal_store(id, &ids[i]);
+            } else {
+                slots[i] = sl;
+                ids[i] = id;
+            }
             if (hcnt) atomicAdd(&l_hist[sl & hmask], 1u);
         }
         n_ins += cls == 1;   // summed once per workgroup below (no per-tile barrier count)
@@ -452,6 +459,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
 // overlaps a tile of other work instead of stalling its own.  Outputs (slot,
 // id, the fused histogram) are written one iteration late; l_slot is double
 // buffered.  Same arguments and results as k_flow_extract.
+template <bool NT>
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *__restrict__ bufs, uint64_t n,
                                                                 uint32_t stride, const qk_pkt_meta *__restrict__ meta,
                                                                 uint64_t my_key_lo, uint64_t chunk,
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
     uint32_t n_new = 0;
     const bool pipe = stage_pipelined(stride, REC_TILE);
     TileStage st;
-    if (pipe && c0 < c1) stage_issue(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
+    if (pipe && c0 < c1) stage_issue<NT>(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
     // the previous tile's state: its packet, and for its leaders the key and
     // the home slot's entry in flight
     bool pv_valid = false, pv_leader = false;
@@ -493,7 +501,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
         __syncthreads();   // the previous election's LDS reads are done
         uint32_t r0 = 0;
         if (have) {
-            r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records(bufs, n, stride, p0, np, tile);
+            r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records<NT>(bufs, n, stride, p0, np, tile);
             for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
         }
         __syncthreads();
@@ -503,7 +511,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
         FlowSlot e{0, 0};
         if (have) {
             if (pipe && p0 + REC_TILE < c1)
-                stage_issue(bufs, n, stride, p0 + REC_TILE,
+                stage_issue<NT>(bufs, n, stride, p0 + REC_TILE,
                             c1 - p0 - REC_TILE < (uint64_t)REC_TILE ? c1 - p0 - REC_TILE : REC_TILE, st);
             valid = threadIdx.x < np;
             const uint8_t *rec = tile + r0 + threadIdx.x * stride;
@@ -1170,7 +1178,8 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
         const int nleft = bits - (q + 1) * dd;
         const uint32_t nmask = nleft >= dd ? (1u << dd) - 1 : (1u << (nleft > 0 ? nleft : 0)) - 1;
         hipLaunchKernelGGL(kern, dim3(pl.nwg), dim3(BLK), 0, s, ki, vi, n, pl.chunk, shift, mask, pl.nwg, sc.base,
-                           sc.tot, ko, vo, nd ? sc.dig : (uint8_t *)nullptr, nshift, nmask);
+                           sc.tot, ko, vo, nd ? sc.dig : (uint8_t *)nullptr, nshift, nmask,
+                           (uint32_t)ctx->knobs.flow_rs_nt);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
         std::swap(ki, ko);
         std::swap(vi, vo);
@@ -1302,7 +1311,9 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             // width as rs_sort_k cuts bits(C - 1)
             const int cb = bit_width32((uint32_t)(C - 1)), np = (cb + 7) / 8, dd = (cb + np - 1) / np;
             if (pn)
-                hipLaunchKernelGGL(ctx->knobs.flow_pipe ? k_flow_extract_pipe : k_flow_extract, dim3(xpl.nwg),
+                hipLaunchKernelGGL(ctx->knobs.flow_pipe ? (ctx->knobs.flow_nt ? k_flow_extract_pipe<true> : k_flow_extract_pipe<false>)
+                                                        : (ctx->knobs.flow_nt ? k_flow_extract<true> : k_flow_extract<false>),
+                                   dim3(xpl.nwg),
                                    dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
                                    pb, pn, (uint32_t)stride, pm, my_key, xpl.chunk, tab, (uint32_t)(C - 1), probe_limit,
                                    slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr, hg);

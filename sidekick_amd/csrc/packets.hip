@@ -58,7 +58,8 @@ struct ChunkStat {       // per workgroup chunk, written by lane 0
 struct NoEncode {};
 template <class C> struct AccOf { using type = bsgs::Acc<C::NB, C::NA, C::ROWS>; };
 template <> struct AccOf<NoEncode> { using type = int; };
-template <class C>
+// NT (knob pkt_nt): the records read nontemporal
+template <class C, bool NT = false>
 __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restrict__ bufs, uint64_t n,
                                                          uint32_t stride, const qk_pkt_meta *__restrict__ meta,
                                                          uint32_t my_ip_le, int check_reset, uint64_t chunk,
@@ -83,14 +84,14 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restri
 
     const bool pipe = stage_pipelined(stride, PK_BLOCK);
     TileStage st;
-    if (pipe && c0 < c1) stage_issue(bufs, n, stride, c0, c1 - c0 < PK_BLOCK ? c1 - c0 : PK_BLOCK, st);
+    if (pipe && c0 < c1) stage_issue<NT>(bufs, n, stride, c0, c1 - c0 < PK_BLOCK ? c1 - c0 : PK_BLOCK, st);
     for (uint64_t p0 = c0; p0 < c1; p0 += PK_BLOCK) {
         const uint64_t np = (c1 - p0) < PK_BLOCK ? (c1 - p0) : PK_BLOCK;
         __syncthreads(); // previous tile fully consumed
-        const uint32_t r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records(bufs, n, stride, p0, np, tile);
+        const uint32_t r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records<NT>(bufs, n, stride, p0, np, tile);
         __syncthreads();
         if (pipe && p0 + PK_BLOCK < c1)   // next tile's loads fly while this one is classified
-            stage_issue(bufs, n, stride, p0 + PK_BLOCK, c1 - p0 - PK_BLOCK < PK_BLOCK ? c1 - p0 - PK_BLOCK : PK_BLOCK, st);
+            stage_issue<NT>(bufs, n, stride, p0 + PK_BLOCK, c1 - p0 - PK_BLOCK < PK_BLOCK ? c1 - p0 - PK_BLOCK : PK_BLOCK, st);
         // classify one record per lane
         uint32_t cls = 0, id = 0; // 0 skip, 1 insert, 2 reset
         const uint64_t pi = p0 + threadIdx.x;
@@ -217,7 +218,9 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
         if (int e = scratch_acquire(ctx, s)) return e;
         uint64_t *partials = (uint64_t *)ctx->d_scratch;
 #define QK_PKT_FUSED(NB_, NA_, SG_)                                                                          \
-    hipLaunchKernelGGL((k_pkt_kernel<bsgs::Cfg<NB_, NA_, SG_>>), dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs,    \
+    hipLaunchKernelGGL((ctx->knobs.pkt_nt ? k_pkt_kernel<bsgs::Cfg<NB_, NA_, SG_>, true>                          \
+                                          : k_pkt_kernel<bsgs::Cfg<NB_, NA_, SG_>, false>),                       \
+                       dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs,                                                \
                        (uint64_t)n, (uint32_t)stride, d_meta, my_ip_le, check_reset, chunk, (uint32_t *)nullptr,   \
                        d_stats, t, partials)
         hipEvent_t e0 = prof_begin(ctx, s);
@@ -261,7 +264,8 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
         }
         // a reset in the batch: the exact path
     }
-    hipLaunchKernelGGL(k_pkt_kernel<NoEncode>, dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs, (uint64_t)n,
+    auto kx = ctx->knobs.pkt_nt ? k_pkt_kernel<NoEncode, true> : k_pkt_kernel<NoEncode, false>;
+    hipLaunchKernelGGL(kx, dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs, (uint64_t)n,
                        (uint32_t)stride, d_meta, my_ip_le, check_reset, chunk, d_ids, d_stats, 0u,
                        (uint64_t *)nullptr);
     if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
                                                     const uint32_t *__restrict__ dtot,
                                                     uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
                                                     uint8_t *__restrict__ nd_out = nullptr, uint32_t nshift = 0,
-                                                    uint32_t nmask = 0) {
+                                                    uint32_t nmask = 0, uint32_t nt = 0) {
     constexpr uint32_t RD = 1u << D, TILE = BLK * K;
     constexpr int NW = BLK / 64;
     constexpr int DPT = RD >= (uint32_t)BLK ? RD / BLK : 1;   // digits per thread in the per-digit steps
@@ -240,8 +240,22 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint64_t p = wbase + (uint64_t)k * 64 + lane;
-            if constexpr (IP) it[k] = p < c1 ? reinterpret_cast<const uint2 *>(keys)[p] : make_uint2(0u, 0u);
-            else it[k] = p < c1 ? make_uint2(keys[p], vals[p]) : make_uint2(0u, 0u);
+            // nt bit 0: the pass's input read nontemporal (read once; the
+            // scattered output runs keep L2 for write combining)
+            if (nt & 1) {
+                if constexpr (IP) {
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    const u32x2 x = p < c1 ? __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(keys) + p)
+                                           : u32x2{0u, 0u};
+                    it[k] = make_uint2(x.x, x.y);
+                } else {
+                    it[k] = p < c1 ? make_uint2(__builtin_nontemporal_load(keys + p), __builtin_nontemporal_load(vals + p))
+                                   : make_uint2(0u, 0u);
+                }
+            } else {
+                if constexpr (IP) it[k] = p < c1 ? reinterpret_cast<const uint2 *>(keys)[p] : make_uint2(0u, 0u);
+                else it[k] = p < c1 ? make_uint2(keys[p], vals[p]) : make_uint2(0u, 0u);
+            }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -319,7 +333,15 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
         for (uint32_t i = tid; i < nsub; i += BLK) {
             const uint2 v = stage[i];
             const uint32_t dst = dl[(v.x >> shift) & mask] + i;
-            if constexpr (OP) {
+            if (nt & 2) {   // nt bit 1: the output written nontemporal
+                if constexpr (OP) {
+                    __builtin_nontemporal_store(v.x, keys_out + 2 * (size_t)dst);
+                    __builtin_nontemporal_store(v.y, keys_out + 2 * (size_t)dst + 1);
+                } else {
+                    __builtin_nontemporal_store(v.x, keys_out + dst);
+                    __builtin_nontemporal_store(v.y, vals_out + dst);
+                }
+            } else if constexpr (OP) {
                 reinterpret_cast<uint2 *>(keys_out)[dst] = v;
             } else {
                 keys_out[dst] = v.x;

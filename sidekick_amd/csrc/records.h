@@ -13,10 +13,24 @@ namespace qk {
 constexpr int REC_TILE = 256;      // records per LDS tile (one per thread)
 constexpr uint32_t REC_UDP = 17;   // IPPROTO_UDP
 
+// A 16-byte load of the record stream, nontemporal when NT (the stream is
+// read once: kept out of the way of data that is reused, e.g. a flow table)
+template <bool NT>
+__device__ __forceinline__ uint4 rec_ld16(const uint8_t *p) {
+    if constexpr (NT) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
+}
+
 // Copy records [p0, p0+np) of `bufs` (stride bytes each, n records in all)
 // into `tile` with 16-byte loads aligned on the absolute address; returns the
 // byte offset of record p0 inside `tile`.  Bytes outside [0, n*stride) are
 // never read.  Caller brackets with __syncthreads().
+template <bool NT = false>
 __device__ __forceinline__ uint32_t stage_records(const uint8_t *__restrict__ bufs, uint64_t n, uint32_t stride,
                                                   uint64_t p0, uint64_t np, uint8_t *tile) {
     const uintptr_t base = (uintptr_t)bufs;
@@ -41,7 +55,7 @@ __device__ __forceinline__ uint32_t stage_records(const uint8_t *__restrict__ bu
             const uint32_t v = v0 + k * blockDim.x + threadIdx.x;
             const uint64_t off = a_lo + 16ull * v; // relative to bufs, mod 2^64
             ok[k] = v < nvec && off < total && off + 16 <= total;
-            r[k] = *reinterpret_cast<const uint4 *>(bufs + (ok[k] ? off : safe));
+            r[k] = rec_ld16<NT>(bufs + (ok[k] ? off : safe));
         }
         // pin the loads here (otherwise each is sunk into its store's branch
         // and waited for alone)
@@ -84,6 +98,7 @@ __device__ __forceinline__ bool stage_pipelined(uint32_t stride, uint32_t thread
     return ((uint64_t)REC_TILE * stride + 15) / 16 + 1 <= (uint64_t)STAGE_VEC * threads;
 }
 
+template <bool NT = false>
 __device__ __forceinline__ void stage_issue(const uint8_t *__restrict__ bufs, uint64_t n, uint32_t stride,
                                             uint64_t p0, uint64_t np, TileStage &st) {
     const uintptr_t base = (uintptr_t)bufs;
@@ -101,7 +116,7 @@ __device__ __forceinline__ void stage_issue(const uint8_t *__restrict__ bufs, ui
         const uint64_t off = st.a_lo + 16ull * v;
         const bool ok = v < st.nvec && off < total && off + 16 <= total;
         st.ok |= (uint32_t)ok << k;
-        st.r[k] = *reinterpret_cast<const uint4 *>(bufs + (ok ? off : safe));
+        st.r[k] = rec_ld16<NT>(bufs + (ok ? off : safe));
     }
 }
 

@@ -258,14 +258,16 @@ def test_hit_and_stop_slot_boundaries(nhit):
     assert q.root_test_shard(c, dev(log2), stop_value=stop_value) == (want, int(spos[0]))
 
 
-@pytest.mark.parametrize("u", [2, 4])
-def test_scan_loads_per_iteration(u, root_test_mode):
+@pytest.mark.parametrize("u,nt", [(2, 1), (4, 1), (1, 0), (2, 0)])
+def test_scan_loads_per_iteration(u, nt, root_test_mode):
     """The root-set scan with 2 / 4 loads per lane per iteration (knob
-    rt_scan_u, measurements; the product takes 1): ragged length, a
+    rt_scan_u, measurements; the product takes 1) and with nontemporal loads
+    (knob rt_scan_nt, the product's; 0 = plain loads): ragged length, a
     misaligned start, both widths, against the oracle."""
     import sidekick_amd as skm
     ctx = skm.get_context(0)
     ctx.set_knob("rt_scan_u", u)
+    ctx.set_knob("rt_scan_nt", nt)
     try:
         for bits in (32, 64):
             log = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(90 + u + bits, 100_007)
@@ -278,6 +280,7 @@ def test_scan_loads_per_iteration(u, root_test_mode):
             assert q.root_test(c, d) == want
     finally:
         ctx.set_knob("rt_scan_u", 1)
+        ctx.set_knob("rt_scan_nt", 1)
 
 
 def test_undecodable_and_empty():

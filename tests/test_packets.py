@@ -152,20 +152,22 @@ def test_gpu_packets_fused_thresholds(golden, t):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wgpc", [1, 12])
-def test_gpu_packets_workgroups_per_cu(wgpc):
+@pytest.mark.parametrize("wgpc,nt", [(1, 1), (12, 1), (4, 0)])
+def test_gpu_packets_workgroups_per_cu(wgpc, nt):
     """The chunking by knob pkt_wgpc (measurements; 4 is the product's):
     fewer or more chunks give the same sums, counts and reset bookkeeping,
-    fused (t = 12) and two-pass (t = 32), with resets."""
+    fused (t = 12) and two-pass (t = 32), with resets; and the plain-load
+    record staging (knob pkt_nt = 0; the product's loads are nontemporal)."""
     import torch
     import sidekick_amd as sk
     from sidekick_amd.quack import encode_packets
     ctx = sk.get_context(0)
     ctx.set_knob("pkt_wgpc", wgpc)
+    ctx.set_knob("pkt_nt", nt)
     try:
         for t, resets in ((12, ()), (32, (77_777,)), (32, ())):
             n = 300_007
-            bufs, meta = make_batch(n, seed=wgpc * 100 + t, reset_at=resets, p_filter=0.05)
+            bufs, meta = make_batch(n, seed=wgpc * 100 + t + nt, reset_at=resets, p_filter=0.05)
             q = sk.PowerSumQuackU32(t)
             st = encode_packets(q, torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
                                 meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_ipv4=MY_IP)
@@ -174,3 +176,4 @@ def test_gpu_packets_workgroups_per_cu(wgpc):
             assert st["inserted"] == len(ids) and st["last_reset_index"] == last
     finally:
         ctx.set_knob("pkt_wgpc", 4)
+        ctx.set_knob("pkt_nt", 1)
