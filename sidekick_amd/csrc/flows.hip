@@ -387,7 +387,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
         uint64_t src = 0, dst = 0;
         uint32_t id = 0;
         int cls = 0; // 0 skip, 1 insert, 2 reset
-        const qk_pkt_meta m = valid ? record_meta(meta, i) : qk_pkt_meta{};
+        const qk_pkt_meta m = valid ? record_meta<NT>(meta, i) : qk_pkt_meta{};
         if (valid && record_is_incoming_udp(m, rec)) {
             // AddrKey halves, big-endian so numeric order == byte order
             src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
             valid = threadIdx.x < np;
             const uint8_t *rec = tile + r0 + threadIdx.x * stride;
             int cls = 0;
-            const qk_pkt_meta m = valid ? record_meta(meta, i) : qk_pkt_meta{};
+            const qk_pkt_meta m = valid ? record_meta<NT>(meta, i) : qk_pkt_meta{};
             if (valid && record_is_incoming_udp(m, rec)) {
                 src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
                       ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restri
         const uint64_t pi = p0 + threadIdx.x;
         if (threadIdx.x < np) {
             const uint8_t *rec = tile + r0 + threadIdx.x * stride;
-            const qk_pkt_meta m = record_meta(meta, pi);
+            const qk_pkt_meta m = record_meta<NT>(meta, pi);
             if (record_is_incoming_udp(m, rec)) {
                 const uint32_t dst = (uint32_t)rec[30] | ((uint32_t)rec[31] << 8) | ((uint32_t)rec[32] << 16) |
                                      ((uint32_t)rec[33] << 24);

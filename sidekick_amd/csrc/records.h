@@ -144,10 +144,18 @@ __device__ __forceinline__ uint32_t stage_commit(const uint8_t *__restrict__ buf
     return st.r0;
 }
 
+template <bool NT = false>
 __device__ __forceinline__ qk_pkt_meta record_meta(const qk_pkt_meta *__restrict__ meta, uint64_t i) {
+    static_assert(sizeof(qk_pkt_meta) == 8, "qk_pkt_meta is one 8-byte word");
     qk_pkt_meta m;
-    if (meta) m = meta[i];
-    else {
+    if (meta) {
+        if constexpr (NT) {   // read once, like the records (rec_ld16)
+            const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(meta) + i);
+            __builtin_memcpy(&m, &v, 8);
+        } else {
+            m = meta[i];
+        }
+    } else {
         m.pkttype = 0;          // PACKET_HOST
         m.reserved = 0;
         m.protocol_be = 0x0008; // htons(ETH_P_IP) as stored
