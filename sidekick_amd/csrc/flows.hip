@@ -986,11 +986,13 @@ static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs, uint32_
 // records (so), the rest by the work items from seg_items (d_items holds
 // items.size() entries) into the accumulator rows item.seg of d_acc (u64,
 // acc_rows rows, zeroed here).
+// small_done: the caller already launched k_seg_small (before it waited
+// for the work-item list)
 static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs,
                       const std::vector<SegItem> &items, size_t nseg, uint32_t T, unsigned long long *d_acc,
-                      size_t acc_rows, SegItem *d_items, const SmallOut &so, hipStream_t s) {
+                      size_t acc_rows, SegItem *d_items, const SmallOut &so, hipStream_t s, bool small_done = false) {
     if (acc_rows) QK_HIP_TRY(hipMemsetAsync(d_acc, 0, acc_rows * T * sizeof(uint64_t), s));
-    if (small_ok(T) && nseg) {
+    if (small_ok(T) && nseg && !small_done) {
         hipEvent_t e0 = prof_begin(ctx, s);
         const int rs = seg_small_launch(ctx->knobs.flow_prio, T, d_ids, d_offs, (uint32_t)nseg, d_acc, so, s);
         prof_end(ctx, s, e0);
@@ -1527,6 +1529,20 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         }
         // by slot / histogram: segment g is output rank rseg[g]; by rank: g
         const uint32_t *seg_rank = by_slot || hist ? rseg : nullptr;
+        // the small flows' records straight from k_seg_small, the work-item
+        // flows' through their accumulator rows and k_flow_finalize_big
+        SmallOut so;
+        so.rec = d_rec;
+        so.rseg = seg_rank;
+        so.lastid = hist ? lastid : nullptr;
+        // k_seg_small needs no host decision: it goes first, and the host's
+        // wait for the work-item list below overlaps it
+        const bool small_first = small_ok(T) && nf;
+        if (!rc && small_first) {
+            hipEvent_t e0 = prof_begin(ctx, s);
+            rc = seg_small_launch(ctx->knobs.flow_prio, T, id_s, d_offs, nf, acc, so, s);
+            prof_end(ctx, s, e0);
+        }
         // only the flows that need work items come back to the host (none
         // in the many-small-flows case): 8 bytes of counts, then their seeds
         uint32_t hsel[2] = {0, 0};
@@ -1547,13 +1563,9 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipStreamSynchronize(s) != hipSuccess)
                 rc = QK_E_HIP;
         }
-        // the small flows' records straight from k_seg_small, the work-item
-        // flows' through their accumulator rows and k_flow_finalize_big
-        SmallOut so;
-        so.rec = d_rec;
-        so.rseg = seg_rank;
-        so.lastid = hist ? lastid : nullptr;
-        if (!rc) rc = seg_encode(ctx, id_s, d_offs, seg_items_from_big(bigs), nf, T, acc, hsel[1], d_items, so, s);
+        if (!rc)
+            rc = seg_encode(ctx, id_s, d_offs, seg_items_from_big(bigs), nf, T, acc, hsel[1], d_items, so, s,
+                            small_first);
         if (!rc && hsel[1]) {
             const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)hsel[1] * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);
