@@ -34,6 +34,8 @@ struct qk_knobs {
                            // staging (direct scatter)
     int pkt_nt = 1;        // the packet-batch kernels: records read nontemporal (t = 32, 1e8 records:
                            // 1.83-1.84 -> 1.74-1.76 ms, profiles/r05/packets_nt/)
+    int flow_side_lo = 0;  // flow batches: the key-ranking branch on the lowest-priority stream (1e6 flows
+                           // 5.92 vs 5.89 ms, 1e4 equal: no contention to speak of, profiles/r05/flows_side/)
     int flow_rs_nt = 1;    // grouping-sort scatters: bit 0 input read, bit 1 output written nontemporal
                            // (bit 0: 1e6 flows 6.16 -> 6.02 ms, 1e4 4.01 -> 3.89; bit 1: +15 %,
                            // profiles/r05/flows_nt/ab_rsnt.jsonl)
@@ -64,6 +66,7 @@ struct qk_ctx {
     hipStream_t stream = nullptr;      // own stream (host-input pipeline, comm collectives); a NULL
                                        // stream argument is the HIP null stream, not this one
     hipStream_t copy_stream = nullptr; // second stream for the host-input pipeline
+    hipStream_t side_stream = nullptr; // lowest-priority stream: the flow batches' key-ranking branch
     uint32_t grid_override = 0;
     qk_knobs knobs;
 

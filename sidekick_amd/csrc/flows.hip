@@ -1431,7 +1431,9 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
         const bool by_slot = (cbits + 7) / 8 <= (fbits + 7) / 8;
         const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
-        hipStream_t s2 = s == ctx->copy_stream ? ctx->stream : ctx->copy_stream;
+        hipStream_t s2 = ctx->knobs.flow_side_lo && s != ctx->side_stream ? ctx->side_stream
+                         : s == ctx->copy_stream                          ? ctx->stream
+                                                                          : ctx->copy_stream;
         if (!rc && (hipEventRecord(ctx->flow_ev[0], s) != hipSuccess || hipStreamWaitEvent(s2, ctx->flow_ev[0], 0) != hipSuccess))
             rc = QK_E_HIP;
         auto side = [&]() -> int {
@@ -1580,6 +1582,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     }
     (void)hipStreamSynchronize(s); // the arenas are reused by the next call
     (void)hipStreamSynchronize(s == ctx->copy_stream ? ctx->stream : ctx->copy_stream);   // the flow-key branch
+    if (s != ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
     if (stats) *stats = st;
     return rc;
 }
