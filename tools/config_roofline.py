@@ -26,17 +26,18 @@ import os
 import sys
 
 PEAK_GBPS = 8000.0
-# (kernel name prefix, grid size of the config's launch, units, bytes per unit, config)
-# (kernel name prefix, grid, units, bytes per unit, config, issue_roofline.json key)
-ROWS = [("void qk::k_encode_u64_bsgs<10, 16>", "262144", 1_000_000_000, 8,
+# (kernel name prefix, units, bytes per unit, config, issue_roofline.json key):
+# the first profiled kernel whose name starts with the prefix (the template
+# arguments change between rounds), its most frequent grid in the PMC files
+ROWS = [("void qk::k_encode_u64_bsgs<10,", 1_000_000_000, 8,
          "configs[2]: encode 1e9 u64 ids, t=80", "encode_u64_t80"),
-        ("void qk::k_root_scan<unsigned int, 1>", "524288", 100_000_000, 4,
+        ("void qk::k_root_scan<unsigned int, 1", 100_000_000, 4,
          "configs[4]: root test of 1e8 u32 candidates, d=32 — root-set scan (the default)", "root_scan_u32_d32"),
-        ("void qk::k_root_test_u32<32>", "458752", 100_000_000, 4,
+        ("void qk::k_root_test_u32<32>", 100_000_000, 4,
          "configs[4]: root test of 1e8 u32 candidates, d=32 — Horner", "root_test_u32_d32"),
-        ("void qk::k_root_scan<unsigned long, 1>", "524288", 100_000_000, 8,
+        ("void qk::k_root_scan<unsigned long, 1", 100_000_000, 8,
          "root test of 1e8 u64 candidates, d=32 — root-set scan (the default)", "root_scan_u64_d32"),
-        ("void qk::k_root_test_u64_bsgs<0>", "458752", 100_000_000, 8,
+        ("void qk::k_root_test_u64_bsgs<0>", 100_000_000, 8,
          "root test of 1e8 u64 candidates, d=32 — baby-step/giant-step Horner", "root_test_u64_d32")]
 
 
@@ -51,9 +52,11 @@ def main(d):
     if os.path.exists(ip):
         issue = json.load(open(ip))["kernels"]
     out = []
-    for name, grid, units, bpu, cfg, ikey in ROWS:
+    for prefix, units, bpu, cfg, ikey in ROWS:
+        name = next(n for n in stats if n.startswith(prefix))
         s = stats[name]
-        c = {k: sum(v) / len(v) for k, v in ctr[(name, grid)].items()}
+        key = max((k for k in ctr if k[0] == name), key=lambda k: len(ctr[k]["FETCH_SIZE"]))
+        c = {k: sum(v) / len(v) for k, v in ctr[key].items()}
         avg_s = float(s["AverageNs"]) * 1e-9
         alg = units * bpu
         traffic = c["FETCH_SIZE"] * 1024 * 2

@@ -11,4 +11,4 @@ cd "$ROOT"
 mkdir -p gpurun_out
 timeout -k 10 200 ./tools/prof_roots 32 200 > gpurun_out/prof_roots.txt 2>&1 || exit 3
 CONFIGS_ARGS="u64 decode decode64 flows packets" \
-STEPS="smoke pytest bench prof pmc configs roots dist2full profcfg" bash tools/gpu_check.sh
+STEPS="smoke pytest bench prof pmc configs roots dist2full profcfg pmccfg proflows" bash tools/gpu_check.sh
