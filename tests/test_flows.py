@@ -367,7 +367,8 @@ def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
     0: the extract's chunk histogram off), the pipelined extract's
     (flow_pipe = 1: table reads one tile ahead), the plain-load extract's
     (flow_nt = 0), the plain-load scatters' (flow_rs_nt = 0) and the
-    nontemporal-store scatters' (flow_rs_nt = 3) byte for byte; flow_hist on and off (the table is above its few-flow size, so both
+    nontemporal-store scatters' (flow_rs_nt = 3) and the key-ranking branch
+    on the lowest-priority stream (flow_side_lo = 1) byte for byte; flow_hist on and off (the table is above its few-flow size, so both
     take the sort)."""
     import torch
     from sidekick_amd.quack import Context, encode_flows
@@ -378,9 +379,10 @@ def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
     d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
     d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
     recs = {}
-    for mode, fuse0, pipe, nt, rsnt in ((2, 1, 0, 1, 1), (1, 1, 0, 1, 1), (7, 1, 0, 1, 1), (2, 0, 0, 1, 1),
-                                        (5, 1, 0, 1, 1), (2, 1, 1, 1, 1), (2, 1, 0, 0, 1), (2, 1, 0, 1, 0),
-                                        (2, 1, 0, 1, 3)):
+    for mode, fuse0, pipe, nt, rsnt, side in ((2, 1, 0, 1, 1, 0), (1, 1, 0, 1, 1, 0), (7, 1, 0, 1, 1, 0),
+                                              (2, 0, 0, 1, 1, 0), (5, 1, 0, 1, 1, 0), (2, 1, 1, 1, 1, 0),
+                                              (2, 1, 0, 0, 1, 0), (2, 1, 0, 1, 0, 0), (2, 1, 0, 1, 3, 0),
+                                              (2, 1, 0, 1, 1, 1)):
         ctx = Context(0)
         ctx.set_knob("flow_hist", hist)
         ctx.set_knob("flow_sort", mode)
@@ -388,14 +390,15 @@ def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
         ctx.set_knob("flow_pipe", pipe)
         ctx.set_knob("flow_nt", nt)
         ctx.set_knob("flow_rs_nt", rsnt)
+        ctx.set_knob("flow_side_lo", side)
         keys, qs, st = encode_flows(d_bufs, 32, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
         assert st["resets"] == nres and st["inserted"] == sum(len(v) for v in want.values())
         assert keys == sorted(want)
-        recs[(mode, fuse0, pipe, nt, rsnt)] = [bytes(q._buf.raw) for q in qs]
-        if (mode, fuse0, pipe, nt, rsnt) == (2, 1, 0, 1, 1):
+        recs[(mode, fuse0, pipe, nt, rsnt, side)] = [bytes(q._buf.raw) for q in qs]
+        if (mode, fuse0, pipe, nt, rsnt, side) == (2, 1, 0, 1, 1, 0):
             for k, q in zip(keys, qs):
                 ids = want[k]
                 assert q.count() == len(ids) and q.last_value() == ids[-1], k.hex()
                 assert q.power_sums() == coracle.encode_u32(np.array(ids, dtype=np.uint32), 32), k.hex()
         ctx.close()
-    assert all(r == recs[(2, 1, 0, 1, 1)] for r in recs.values())
+    assert all(r == recs[(2, 1, 0, 1, 1, 0)] for r in recs.values())
