@@ -481,12 +481,14 @@ int qk_ctx_create(int device, qk_ctx **out) {
         hipStreamCreateWithPriority(&ctx->side_stream, hipStreamNonBlocking, prio_least) != hipSuccess ||
         hipMalloc(&ctx->d_small, SMALL_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&ctx->h_small, SMALL_WORDS * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&ctx->h_flow, 8 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipHostGetDevicePointer((void **)&ctx->h_small_dev, ctx->h_small, 0) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->stage_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->stage_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->flow_ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->flow_ev[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&ctx->flow_ev[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->flow_ev[2], hipEventDisableTiming) != hipSuccess) {
         qk_ctx_destroy(ctx);
         return QK_E_HIP;
     }
@@ -515,6 +517,7 @@ void qk_ctx_destroy(qk_ctx *ctx) {
     for (void *r : ctx->retired) hipFree(r);
     if (ctx->d_small) hipFree(ctx->d_small);
     if (ctx->h_small) hipHostFree(ctx->h_small);
+    if (ctx->h_flow) hipHostFree(ctx->h_flow);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     if (ctx->copy_stream) hipStreamDestroy(ctx->copy_stream);
     if (ctx->side_stream) hipStreamDestroy(ctx->side_stream);
@@ -591,7 +594,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 1, 9},
         {"flow_fuse0", &qk_knobs::flow_fuse0, 0, 1},    {"flow_pipe", &qk_knobs::flow_pipe, 0, 1},
         {"flow_nt", &qk_knobs::flow_nt, 0, 1},          {"flow_rs_nt", &qk_knobs::flow_rs_nt, 0, 3},
-        {"flow_side_lo", &qk_knobs::flow_side_lo, 0, 1},
+        {"flow_side_lo", &qk_knobs::flow_side_lo, 0, 1},   {"flow_spec", &qk_knobs::flow_spec, 0, 1},
         {"pkt_nt", &qk_knobs::pkt_nt, 0, 1},
         {"flow_prio", &qk_knobs::flow_prio, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},
         {"pkt_wgpc", &qk_knobs::pkt_wgpc, 1, 16},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},

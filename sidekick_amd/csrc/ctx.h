@@ -34,6 +34,9 @@ struct qk_knobs {
                            // staging (direct scatter)
     int pkt_nt = 1;        // the packet-batch kernels: records read nontemporal (t = 32, 1e8 records:
                            // 1.83-1.84 -> 1.74-1.76 ms, profiles/r05/packets_nt/)
+    int flow_spec = 0;     // flow batches: the by-slot grouping sort launched before the host reads the
+                           // extract's counters (16 / 1e4 / 1e6 flows: equal within 0.5 %,
+                           // profiles/r05/flows_spec/: the launch gap it removes is not on the path)
     int flow_side_lo = 0;  // flow batches: the key-ranking branch on the lowest-priority stream (1e6 flows
                            // 5.92 vs 5.89 ms, 1e4 equal: no contention to speak of, profiles/r05/flows_side/)
     int flow_rs_nt = 1;    // grouping-sort scatters: bit 0 input read, bit 1 output written nontemporal
@@ -104,7 +107,8 @@ struct qk_ctx {
     hipEvent_t scratch_ev = nullptr;
     bool scratch_ev_valid = false;
     // per-flow batches: fork/join of the flow-key branch on the second stream
-    hipEvent_t flow_ev[2] = {nullptr, nullptr};
+    hipEvent_t flow_ev[3] = {nullptr, nullptr, nullptr};
+    uint64_t *h_flow = nullptr;   // pinned: the flow extract's counters (read back without a staging copy)
 
     // grown-out device buffers, freed by qk_ctx_trim / qk_ctx_destroy (hipFree
     // synchronises the whole device; growth must not)

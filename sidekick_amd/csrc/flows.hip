@@ -1289,6 +1289,15 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     const uint32_t hg = std::max<uint32_t>(1, ((uint32_t)ctx->knobs.flow_wgpc + RS_WGPC_MAX - 1) / RS_WGPC_MAX);
     auto sort_plan = [&]() { return RsPlan{(xpl.nwg + hg - 1) / hg, xpl.chunk * hg}; };
     const bool fuse0 = rs_digit_bits(ctx) == 8 && ctx->knobs.flow_fuse0;   // the extract writes the sort's first counts
+    // speculation (knob flow_spec): the by-slot grouping sort of the pass's
+    // packets is enqueued right behind the extract, before the host has read
+    // the extract's counters (so the GPU does not idle through that round
+    // trip).  Valid when the pass ends the batch (no table regrow, no reset
+    // after it) and the table is above the histogram grouping's size — the
+    // grouping then uses it as is, by slot; otherwise the next extract (same
+    // stream) starts over and the sorted copies are simply overwritten.
+    bool spec = false;
+    int spec_where = 0;
     auto pass1 = [&](uint64_t p_from) -> int {
         const uint64_t pn = n - p_from;
         const uint8_t *pb = d_bufs + p_from * stride;
@@ -1319,10 +1328,23 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                                    dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
                                    pb, pn, (uint32_t)stride, pm, my_key, xpl.chunk, tab, (uint32_t)(C - 1), probe_limit,
                                    slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr, hg);
+            // the counters into pinned memory (an async copy to pageable memory
+            // would hold the host until the extract ends); flow_ev[0]: the
+            // table is complete (the key-ranking branch waits for it, not for
+            // a speculated sort behind it)
             if (hipGetLastError() != hipSuccess ||
-                hipMemcpyAsync(hc, counters, 40, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess)
+                hipMemcpyAsync(ctx->h_flow, counters, 40, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipEventRecord(ctx->flow_ev[2], s) != hipSuccess || hipEventRecord(ctx->flow_ev[0], s) != hipSuccess)
                 return QK_E_HIP;
+            spec = ctx->knobs.flow_spec && pn && !(C <= HIST_MAX && ctx->knobs.flow_hist);
+            if (spec) {
+                const RsPlan spl = sort_plan();
+                const int e = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, pn, cb, rs, s, spec_where, &spl, true)
+                                    : rs_sort(ctx, slots, ids, key_s, id_s, pn, cb, rs, s, spec_where);
+                if (e) return e;
+            }
+            if (hipEventSynchronize(ctx->flow_ev[2]) != hipSuccess) return QK_E_HIP;
+            std::copy(ctx->h_flow, ctx->h_flow + 5, hc);
             if (!(hc[3] & FT_OVERFLOW)) return QK_OK;
             if (C == cmax) return QK_E_NOMEM;   // > 2^31 flows: no table size left
             C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(16 * C, 4 * hc[2])));
@@ -1429,12 +1451,13 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         //     their host launch time).  Otherwise by rank (slot -> rank remap
         //     per packet, bit_width(flows) bits), which waits for s2 first.
         const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
-        const bool by_slot = (cbits + 7) / 8 <= (fbits + 7) / 8;
+        // (a speculated sort is by slot: always a valid grouping)
+        const bool by_slot = spec || (cbits + 7) / 8 <= (fbits + 7) / 8;
         const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
         hipStream_t s2 = ctx->knobs.flow_side_lo && s != ctx->side_stream ? ctx->side_stream
                          : s == ctx->copy_stream                          ? ctx->stream
                                                                           : ctx->copy_stream;
-        if (!rc && (hipEventRecord(ctx->flow_ev[0], s) != hipSuccess || hipStreamWaitEvent(s2, ctx->flow_ev[0], 0) != hipSuccess))
+        if (!rc && hipStreamWaitEvent(s2, ctx->flow_ev[0], 0) != hipSuccess)   // (recorded behind the last extract)
             rc = QK_E_HIP;
         auto side = [&]() -> int {
             // the occupied slots in slot order
@@ -1495,10 +1518,11 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             // the grouping sort (radix.h); with the extract's fused histogram
             // its first pass reads no keys and every pass keeps the extract's
             // chunking
-            int where = 0;
+            int where = spec_where;
             const RsPlan spl = sort_plan();
-            rc = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where, &spl, true)
-                       : rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where);
+            if (!spec)
+                rc = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where, &spl, true)
+                           : rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where);
             if (!rc && where == 0) {   // even number of passes: the result is in (slots, ids)
                 std::swap(slots, key_s);
                 std::swap(ids, id_s);

@@ -368,7 +368,8 @@ def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
     (flow_pipe = 1: table reads one tile ahead), the plain-load extract's
     (flow_nt = 0), the plain-load scatters' (flow_rs_nt = 0) and the
     nontemporal-store scatters' (flow_rs_nt = 3) and the key-ranking branch
-    on the lowest-priority stream (flow_side_lo = 1) byte for byte; flow_hist on and off (the table is above its few-flow size, so both
+    on the lowest-priority stream (flow_side_lo = 1) and the speculated
+    grouping sort (flow_spec = 1) byte for byte; flow_hist on and off (the table is above its few-flow size, so both
     take the sort)."""
     import torch
     from sidekick_amd.quack import Context, encode_flows
@@ -382,7 +383,7 @@ def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
     for mode, fuse0, pipe, nt, rsnt, side in ((2, 1, 0, 1, 1, 0), (1, 1, 0, 1, 1, 0), (7, 1, 0, 1, 1, 0),
                                               (2, 0, 0, 1, 1, 0), (5, 1, 0, 1, 1, 0), (2, 1, 1, 1, 1, 0),
                                               (2, 1, 0, 0, 1, 0), (2, 1, 0, 1, 0, 0), (2, 1, 0, 1, 3, 0),
-                                              (2, 1, 0, 1, 1, 1)):
+                                              (2, 1, 0, 1, 1, 1), (2, 1, 0, 1, 1, 2)):
         ctx = Context(0)
         ctx.set_knob("flow_hist", hist)
         ctx.set_knob("flow_sort", mode)
@@ -390,7 +391,8 @@ def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
         ctx.set_knob("flow_pipe", pipe)
         ctx.set_knob("flow_nt", nt)
         ctx.set_knob("flow_rs_nt", rsnt)
-        ctx.set_knob("flow_side_lo", side)
+        ctx.set_knob("flow_side_lo", side & 1)
+        ctx.set_knob("flow_spec", side >> 1)
         keys, qs, st = encode_flows(d_bufs, 32, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
         assert st["resets"] == nres and st["inserted"] == sum(len(v) for v in want.values())
         assert keys == sorted(want)
