@@ -15,9 +15,10 @@
 //     tools/issue_model.py); the kernel issues 1.19 VALU + 0.76 SALU
 //     wave-instructions per id, each id's MAC phase at raised wave priority
 //     (s_setprio, knob bsgs_prio), over encode grids of three rounds of
-//     resident workgroups (knob grid_mult), and runs at 0.84-0.89 of the
+//     resident workgroups (knob grid_mult), and runs at 0.86-0.89 of the
 //     anchor at the bench run's own shader clock (bench.py roofline.valu,
-//     DESIGN.md §4) and 0.20-0.22 of the HBM read roofline (4 B/id).
+//     DESIGN.md §4) and ~0.20-0.21 of the HBM read roofline (4 B/id; the
+//     line moves with the box's shader clock, 2.0-2.1 GHz).
 //   * 14 <= t <= 80 (u64) — k_encode_u64_bsgs<NA,SG,F> (bsgs64.h): the
 //     same split with the babies/giants of a 256-id tile shared through LDS,
 //     each wave owning two babies' MAC rows (paired, at raised priority).
