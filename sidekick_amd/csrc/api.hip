@@ -591,7 +591,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"u64_passes", &qk_knobs::u64_passes, 0, 1},
         {"u64_xcache", &qk_knobs::u64_xcache, 0, 1},   {"u64_kmax", &qk_knobs::u64_kmax, 4, 40},
         {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
-        {"flow_hist", &qk_knobs::flow_hist, 0, 1},      {"flow_sort", &qk_knobs::flow_sort, 1, 9},
+        {"flow_hist", &qk_knobs::flow_hist, 0, 1 << 20},      {"flow_sort", &qk_knobs::flow_sort, 1, 9},
         {"flow_fuse0", &qk_knobs::flow_fuse0, 0, 1},    {"flow_pipe", &qk_knobs::flow_pipe, 0, 1},
         {"flow_nt", &qk_knobs::flow_nt, 0, 1},          {"flow_rs_nt", &qk_knobs::flow_rs_nt, 0, 3},
         {"flow_side_lo", &qk_knobs::flow_side_lo, 0, 1},   {"flow_spec", &qk_knobs::flow_spec, 0, 1},

@@ -27,7 +27,9 @@ struct qk_knobs {
     int u64_kmax = 40;     // u64 power chain: accumulators per lane
     int flow_load = 4;     // flow-table slots per expected flow
     int flow_wgpc = 12;    // flow extract: workgroups per CU
-    int flow_hist = 1;     // 0: few-flow batches grouped by the radix sort instead of per-workgroup slot histograms
+    int flow_hist = 32;    // batches of at most this many flows (and a table of <= 8192 slots) are grouped by
+                           // per-workgroup slot histograms instead of the radix sort (0: never); 16 flows
+                           // 2.76 vs 2.90 ms, 64: 3.17 vs 3.05, 1000: 5.80 vs 3.68 (profiles/r05/flows_hist/)
     int flow_sort = 2;     // grouping sort (radix.h, flows.hip rs_sort): 1: 8-bit digits, 256 threads, two arrays
                            // throughout; 2: pair arrays between the first and last pass; 3 / 4: 512 / 1024
                            // threads; 5 / 6: 11-bit digits, 512 / 1024 threads; 7-9: as 2, 5, 6 without LDS

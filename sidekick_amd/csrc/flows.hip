@@ -745,9 +745,19 @@ __global__ void k_rank_perm(const FlowSlot *__restrict__ tab, const uint32_t *__
 // packet index, so nothing depends on it.
 constexpr uint32_t HIST_MAX = 8192;   // slots (LDS counters per workgroup: 32 KB)
 
+// nt: the per-packet arrays read nontemporal (knob flow_rs_nt bit 0, as the
+// grouping sort's scatters)
+__device__ __forceinline__ uint4 ld_u4(const uint32_t *p, uint32_t nt) {
+    if (nt) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    }
+    return *reinterpret_cast<const uint4 *>(p);
+}
 __global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__ slots, uint64_t n, uint64_t chunk,
                                                     uint32_t C, uint32_t nwg, uint32_t *__restrict__ hist,
-                                                    uint32_t *__restrict__ last) {
+                                                    uint32_t *__restrict__ last, uint32_t nt) {
     extern __shared__ uint32_t lh[];   // C counts, C last indices (+1)
     uint32_t *lc = lh, *ll = lh + C;
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) { lc[j] = 0; ll[j] = 0; }
@@ -763,7 +773,7 @@ __global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__
     };
     const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
     for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
-        const uint4 sv = *reinterpret_cast<const uint4 *>(slots + i);
+        const uint4 sv = ld_u4(slots + i, nt);
         one(sv.x, i); one(sv.y, i + 1); one(sv.z, i + 2); one(sv.w, i + 3);
     }
     for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) one(slots[i], i);
@@ -780,7 +790,7 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ ids, uint64_t n, uint64_t chunk,
                                                       uint32_t C, uint32_t nwg, const uint32_t *__restrict__ base,
                                                       const uint32_t *__restrict__ spre,
-                                                      uint32_t *__restrict__ grouped) {
+                                                      uint32_t *__restrict__ grouped, uint32_t nt) {
     extern __shared__ uint32_t lc[];   // C running counts
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) lc[j] = 0;
     __syncthreads();
@@ -793,8 +803,8 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
     };
     const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
     for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
-        const uint4 sv = *reinterpret_cast<const uint4 *>(slots + i);
-        const uint4 iv = *reinterpret_cast<const uint4 *>(ids + i);
+        const uint4 sv = ld_u4(slots + i, nt);
+        const uint4 iv = ld_u4(ids + i, nt);
         one(sv.x, iv.x); one(sv.y, iv.y); one(sv.z, iv.z); one(sv.w, iv.w);
     }
     for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) one(slots[i], ids[i]);
@@ -1336,7 +1346,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipMemcpyAsync(ctx->h_flow, counters, 40, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipEventRecord(ctx->flow_ev[2], s) != hipSuccess || hipEventRecord(ctx->flow_ev[0], s) != hipSuccess)
                 return QK_E_HIP;
-            spec = ctx->knobs.flow_spec && pn && !(C <= HIST_MAX && ctx->knobs.flow_hist);
+            spec = ctx->knobs.flow_spec && pn && !(C <= HIST_MAX && ctx->knobs.flow_hist > 0);
             if (spec) {
                 const RsPlan spl = sort_plan();
                 const int e = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, pn, cb, rs, s, spec_where, &spl, true)
@@ -1384,8 +1394,11 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         uint32_t *kA = nullptr, *vA = nullptr, *kB = nullptr, *vB = nullptr, *wcnt = nullptr, *lastid = nullptr;
         SegItem *big = nullptr;
         uint8_t *d_keys = nullptr;
-        // histogram grouping: few flows (a table of <= HIST_MAX slots)
-        const bool hist = C <= HIST_MAX && ctx->knobs.flow_hist;
+        // histogram grouping: few flows (a table of <= HIST_MAX slots and at
+        // most knob flow_hist flows: above a few dozen flows every workgroup
+        // scatters into that many runs and the radix sort is faster,
+        // profiles/r05/flows_hist/)
+        const bool hist = !spec && C <= HIST_MAX && nf <= (uint32_t)ctx->knobs.flow_hist;
         const uint32_t hnwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->num_cus * 4,
                                                                                   (n_eff + 4095) / 4096));
         const uint64_t hchunk = ((n_eff + hnwg - 1) / hnwg + 3) & ~(uint64_t)3;   // a multiple of 4 (16-byte reads)
@@ -1498,13 +1511,14 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipMemsetAsync(hlast, 0, (size_t)C * 4, s) != hipSuccess)
                 rc = QK_E_HIP;
             if (!rc) {
+                const uint32_t hnt = (uint32_t)ctx->knobs.flow_rs_nt & 1u;
                 hipLaunchKernelGGL(k_hist_count, dim3(hnwg), dim3(256), (size_t)C * 8, s, slots, n_eff, hchunk, (uint32_t)C,
-                                   hnwg, hcnt, hlast);
+                                   hnwg, hcnt, hlast, hnt);
                 // slot-major counts -> each slot's workgroup prefixes, then the slots' prefix
                 hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3((uint32_t)C), dim3(256), 0, s, hcnt, hnwg, hpre, htot);
                 hipLaunchKernelGGL(rsort::k_tot_scan<1024>, dim3(1), dim3(1024), 0, s, htot, (uint32_t)C, hspre);
                 hipLaunchKernelGGL(k_hist_scatter, dim3(hnwg), dim3(256), (size_t)C * 4, s, slots, ids, n_eff, hchunk,
-                                   (uint32_t)C, hnwg, hpre, hspre, id_s);
+                                   (uint32_t)C, hnwg, hpre, hspre, id_s, hnt);
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
             if (!rc) rc = side();

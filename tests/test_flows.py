@@ -262,7 +262,9 @@ def test_gpu_flows_histogram_grouping(nflows, t, p_reset, skew):
     order inside a flow is arbitrary, so the counts, last ids (from the last
     packet index) and sums must match the oracle, and the records must be the
     radix-sort path's (knob flow_hist = 0) byte for byte — one flow, skewed
-    flows, resets, and the work-item path (t > 32) included."""
+    flows, resets, and the work-item path (t > 32) included.  flow_hist =
+    8192 forces the histogram path at every flow count here (the product
+    takes it up to 32 flows)."""
     import torch
     from sidekick_amd.quack import Context, encode_flows
     bufs, meta = make_flows(250_000 + nflows, nflows, seed=nflows + t, p_reset=p_reset, skew=skew)
@@ -270,7 +272,7 @@ def test_gpu_flows_histogram_grouping(nflows, t, p_reset, skew):
     d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
     d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
     recs = {}
-    for mode in (1, 0):
+    for mode in (8192, 0):
         ctx = Context(0)
         ctx.set_knob("flow_hist", mode)
         keys, qs, st = encode_flows(d_bufs, t, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
@@ -283,7 +285,7 @@ def test_gpu_flows_histogram_grouping(nflows, t, p_reset, skew):
             assert qs[i].power_sums() == coracle.encode_u32(np.array(want[keys[i]], dtype=np.uint32), t)
         recs[mode] = [bytes(q._buf.raw) for q in qs]
         ctx.close()
-    assert recs[1] == recs[0]
+    assert recs[8192] == recs[0]
 
 
 @pytest.mark.gpu
