@@ -772,9 +772,23 @@ __global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__
         }
     };
     const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
+    const int lane = threadIdx.x & 63;
     for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
         const uint4 sv = ld_u4(slots + i, nt);
-        one(sv.x, i); one(sv.y, i + 1); one(sv.z, i + 2); one(sv.w, i + 3);
+        // a wave whose packets all hold one slot (one flow, or a skewed
+        // batch) adds them with one LDS atomic instead of 256 on one counter
+        const uint32_t s0 = __builtin_amdgcn_readfirstlane(sv.x);
+        if (__all(sv.x == s0 && sv.y == s0 && sv.z == s0 && sv.w == s0) && s0 != SLOT_NONE) {
+            const uint64_t act = __ballot(1);
+            const int first = __ffsll((unsigned long long)act) - 1, last = 63 - __clzll((long long)act);
+            const uint64_t ilast = (uint64_t)__shfl((unsigned long long)i, last);
+            if (lane == first) {
+                atomicAdd(&lc[s0], 4u * (uint32_t)__popcll(act));
+                atomicMax(&ll[s0], (uint32_t)ilast + 4u);   // the wave's last packet + 1
+            }
+        } else {
+            one(sv.x, i); one(sv.y, i + 1); one(sv.z, i + 2); one(sv.w, i + 3);
+        }
     }
     for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) one(slots[i], i);
     __syncthreads();
@@ -802,10 +816,27 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
         }
     };
     const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
+    const int lane = threadIdx.x & 63;
     for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
         const uint4 sv = ld_u4(slots + i, nt);
         const uint4 iv = ld_u4(ids + i, nt);
-        one(sv.x, iv.x); one(sv.y, iv.y); one(sv.z, iv.z); one(sv.w, iv.w);
+        // one slot across the wave (as k_hist_count): one LDS atomic reserves
+        // the wave's places, each lane takes four in lane order
+        const uint32_t s0 = __builtin_amdgcn_readfirstlane(sv.x);
+        if (__all(sv.x == s0 && sv.y == s0 && sv.z == s0 && sv.w == s0) && s0 != SLOT_NONE) {
+            const uint64_t act = __ballot(1);
+            const int first = __ffsll((unsigned long long)act) - 1;
+            uint32_t r = 0;
+            if (lane == first) r = atomicAdd(&lc[s0], 4u * (uint32_t)__popcll(act));
+            r = (uint32_t)__shfl((int)r, first) + 4u * rsort::lanes_below(act);
+            uint32_t *g = grouped + spre[s0] + base[(size_t)s0 * nwg + blockIdx.x] + r;
+            g[0] = iv.x;
+            g[1] = iv.y;
+            g[2] = iv.z;
+            g[3] = iv.w;
+        } else {
+            one(sv.x, iv.x); one(sv.y, iv.y); one(sv.z, iv.z); one(sv.w, iv.w);
+        }
     }
     for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) one(slots[i], ids[i]);
 }
@@ -1465,7 +1496,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         //     per packet, bit_width(flows) bits), which waits for s2 first.
         const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
         // (a speculated sort is by slot: always a valid grouping)
-        const bool by_slot = spec || (cbits + 7) / 8 <= (fbits + 7) / 8;
+        const bool by_slot = spec || ctx->knobs.flow_byslot || (cbits + 7) / 8 <= (fbits + 7) / 8;
         const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
         hipStream_t s2 = ctx->knobs.flow_side_lo && s != ctx->side_stream ? ctx->side_stream
                          : s == ctx->copy_stream                          ? ctx->stream
