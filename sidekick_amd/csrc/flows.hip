@@ -1496,7 +1496,13 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         //     per packet, bit_width(flows) bits), which waits for s2 first.
         const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
         // (a speculated sort is by slot: always a valid grouping)
-        const bool by_slot = spec || ctx->knobs.flow_byslot || (cbits + 7) / 8 <= (fbits + 7) / 8;
+        // By rank costs a remap pass over the packets (k_slot_to_rank) and the
+        // wait for s2 before the sort, ~one sort pass and more: it is taken
+        // when it saves two passes, or leaves one (knob flow_byslot: 0 this
+        // rule, 1 by slot, 2 by rank; profiles/r05/flows_byslot/)
+        const int sp = (cbits + 7) / 8, rp = (fbits + 7) / 8;
+        const bool by_slot = spec || (ctx->knobs.flow_byslot == 0 ? !(sp >= rp + 2 || (rp <= 1 && sp > 1))
+                                                                  : ctx->knobs.flow_byslot == 1);
         const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
         hipStream_t s2 = ctx->knobs.flow_side_lo && s != ctx->side_stream ? ctx->side_stream
                          : s == ctx->copy_stream                          ? ctx->stream

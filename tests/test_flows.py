@@ -236,21 +236,38 @@ def test_gpu_flows_edge_keys_and_table_growth():
 
 @pytest.mark.gpu
 def test_gpu_flows_group_by_slot_and_by_rank():
-    """The grouping sort runs by table slot when log2(table size) needs no more
-    radix passes than bit_width(flows) (10 000 flows, table sized from the
-    previous batch: 16 vs 14 bits), else by flow rank (16 flows: 12 vs 5
-    bits).  Both must give the oracle's tables, in ascending key order."""
+    """The grouping sort keys the packets by table slot or by flow rank (a
+    slot -> rank remap first); by rank is taken when it saves two 8-bit
+    passes or leaves one (knob flow_byslot = 0), and flow_byslot = 1 / 2
+    force either key.  Every mode must give the oracle's tables in ascending
+    key order, and the records byte for byte alike: 10 000 flows (16 vs 14
+    bits), 40 flows (12 vs 6 bits: by rank under the rule), 3 000 flows and
+    30 000 flows (17 vs 15 bits: by slot under the rule), with
+    resets; flow_hist = 0 so that few flows take the sort too."""
     import torch
-    import sidekick_amd as sk
-    for nflows, seed in ((10_000, 1), (10_000, 2), (16, 3), (10_000, 4)):
+    from sidekick_amd.quack import Context, encode_flows
+    for nflows, seed in ((10_000, 1), (40, 3), (3_000, 4), (30_000, 5)):
         bufs, meta = make_flows(200_000, nflows, seed=seed, p_reset=0.02)
         want, nres, _ = vector_flows(bufs, meta)
-        table = sk.FlowQuacks(24)
-        st = table.insert_packets(torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
-                                  meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_addr=MY_ADDR)
-        assert st["resets"] == nres
-        check_flows_table(table, want, 24)
-        assert list(table.senders()) == sorted(want)
+        d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
+        d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
+        recs = {}
+        for mode in (0, 1, 2):
+            ctx = Context(0)
+            ctx.set_knob("flow_hist", 0)
+            ctx.set_knob("flow_byslot", mode)
+            for _ in range(2):   # the second batch's table is sized from the first's flows
+                keys, qs, st = encode_flows(d_bufs, 24, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
+            assert st["resets"] == nres
+            assert keys == sorted(want)
+            for k, q in zip(keys, qs):
+                ids = want[k]
+                assert q.count() == len(ids) and q.last_value() == ids[-1], (mode, k.hex())
+                if mode == 0:
+                    assert q.power_sums() == coracle.encode_u32(np.array(ids, dtype=np.uint32), 24), k.hex()
+            recs[mode] = [bytes(q._buf.raw) for q in qs]
+            ctx.close()
+        assert recs[1] == recs[0] and recs[2] == recs[0], nflows
 
 
 @pytest.mark.gpu
