@@ -36,6 +36,7 @@ struct qk_knobs {
                            // staging (direct scatter)
     int pkt_nt = 1;        // the packet-batch kernels: records read nontemporal (t = 32, 1e8 records:
                            // 1.83-1.84 -> 1.74-1.76 ms, profiles/r05/packets_nt/)
+    int flow_nd = 1;       // 1: each radix scatter writes the next pass's digit bytes (count from them); 0: count from the pairs
     int flow_byslot = 0;   // grouping sort key: 0 by the pass-count rule, 1 slot, 2 flow rank (A/B)
     int flow_spec = 0;     // flow batches: the by-slot grouping sort launched before the host reads the
                            // extract's counters (16 / 1e4 / 1e6 flows: equal within 0.5 %,

@@ -1202,7 +1202,7 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
         const uint32_t mask = left >= dd ? (1u << dd) - 1 : (1u << left) - 1;
         const bool ip = PAIRS && q > 0, op = PAIRS && q + 1 < passes;
         auto count = ip ? rsort::k_rs_count<D, true> : rsort::k_rs_count<D, false>;
-        if (D == 8 && q > 0)   // the previous scatter wrote this pass's digits as bytes
+        if (D == 8 && q > 0 && ctx->knobs.flow_nd)   // the previous scatter wrote this pass's digits as bytes
             hipLaunchKernelGGL(rsort::k_rs_count8, dim3(pl.nwg), dim3(256), 0, s, sc.dig, n, pl.chunk, pl.nwg, sc.cnt);
         else if (!(pre0 && q == 0))
             hipLaunchKernelGGL(count, dim3(pl.nwg), dim3(256), 0, s, ki, n, pl.chunk, shift, mask, pl.nwg, sc.cnt);
@@ -1216,7 +1216,7 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
                        : (op ? rsort::k_rs_scatter<D, BLK, K, false, true, DIRECT>
                              : rsort::k_rs_scatter<D, BLK, K, false, false, DIRECT>);
         // the next pass's digit as a byte beside each item (8-bit digits)
-        const bool nd = D == 8 && q + 1 < passes;
+        const bool nd = D == 8 && q + 1 < passes && ctx->knobs.flow_nd;
         const uint32_t nshift = (uint32_t)((q + 1) * dd);
         const int nleft = bits - (q + 1) * dd;
         const uint32_t nmask = nleft >= dd ? (1u << dd) - 1 : (1u << (nleft > 0 ? nleft : 0)) - 1;
