@@ -596,6 +596,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"flow_nt", &qk_knobs::flow_nt, 0, 1},          {"flow_rs_nt", &qk_knobs::flow_rs_nt, 0, 3},
         {"flow_side_lo", &qk_knobs::flow_side_lo, 0, 1},   {"flow_spec", &qk_knobs::flow_spec, 0, 1},
         {"flow_byslot", &qk_knobs::flow_byslot, 0, 2},
+        {"flow_bail", &qk_knobs::flow_bail, 0, 1 << 16},
         {"flow_nd", &qk_knobs::flow_nd, 0, 1},
         {"pkt_nt", &qk_knobs::pkt_nt, 0, 1},
         {"flow_prio", &qk_knobs::flow_prio, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},

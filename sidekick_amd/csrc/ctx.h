@@ -37,6 +37,7 @@ struct qk_knobs {
     int pkt_nt = 1;        // the packet-batch kernels: records read nontemporal (t = 32, 1e8 records:
                            // 1.83-1.84 -> 1.74-1.76 ms, profiles/r05/packets_nt/)
     int flow_nd = 1;       // 1: each radix scatter writes the next pass's digit bytes (count from them); 0: count from the pairs
+    int flow_bail = 64;    // the flow extract stops on its own overflow, or on any (flag read every flow_bail-th tile); 0: never
     int flow_byslot = 0;   // grouping sort key: 0 by the pass-count rule, 1 slot, 2 flow rank (A/B)
     int flow_spec = 0;     // flow batches: the by-slot grouping sort launched before the host reads the
                            // extract's counters (16 / 1e4 / 1e6 flows: equal within 0.5 %,

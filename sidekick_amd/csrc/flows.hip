@@ -347,8 +347,11 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
                                                            uint32_t *__restrict__ ids,
                                                            unsigned long long *__restrict__ counters,
                                                            uint32_t hmask, uint32_t *__restrict__ hcnt,
-                                                           uint32_t hgroup) {
+                                                           uint32_t hgroup, uint32_t bail) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    __shared__ uint32_t l_stop;
+    uint32_t since = 0;   // tiles since the last overflow check
+    if (threadIdx.x == 0) l_stop = 0;   // (read only after the loop's first barrier)
     __shared__ uint32_t l_hist[rsort::R];
     if (hcnt)
         for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) l_hist[j] = 0;
@@ -375,9 +378,20 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     for (uint64_t p0 = c0; p0 < c1; p0 += REC_TILE) {
         const uint64_t np = c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE;
         __syncthreads();   // previous tile fully consumed
+        // bail (knob flow_bail, 0 never): stop once this workgroup's own
+        // probes overflowed, or (flag read every bail-th tile) any other's —
+        // the pass is rerun on a regrown table and its outputs dropped
+        const bool chk = bail && ++since >= bail;   // every bail-th tile (a load per tile measured 5 % slower)
+        if (chk) since = 0;
+        const uint64_t fl = chk && threadIdx.x == 0
+                                ? __hip_atomic_load(&counters[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0ull;
         const uint32_t r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records<NT>(bufs, n, stride, p0, np, tile);
         for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
+        if (fl & FT_OVERFLOW) l_stop = 1;
         __syncthreads();
+        if (l_stop) break;   // uniform: set only before the barrier above (0 -> 1 once)
+        // (since: same count in every thread, so chk is uniform too)
         if (pipe && p0 + REC_TILE < c1)   // next tile's loads fly while this one is classified
             stage_issue<NT>(bufs, n, stride, p0 + REC_TILE,
                         c1 - p0 - REC_TILE < (uint64_t)REC_TILE ? c1 - p0 - REC_TILE : REC_TILE, st);
@@ -415,8 +429,11 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
                 if (l_src[o] == src && l_dst[o] == dst) { lead = o; break; }
                 h = (h + 1) & (LH - 1);
             }
-            if (lead == threadIdx.x)
-                l_slot[threadIdx.x] = ft_find_or_insert(tab, mask, probe_limit, src, dst, counters, n_new);
+            if (lead == threadIdx.x) {
+                const uint32_t sl = ft_find_or_insert(tab, mask, probe_limit, src, dst, counters, n_new);
+                l_slot[threadIdx.x] = sl;
+                if (sl == SLOT_NONE && bail) l_stop = 1;   // this workgroup overflowed: it leaves at the next tile
+            }
         }
         __syncthreads();
         if (valid) {
@@ -468,8 +485,11 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
                                                                 uint32_t *__restrict__ ids,
                                                                 unsigned long long *__restrict__ counters,
                                                                 uint32_t hmask, uint32_t *__restrict__ hcnt,
-                                                           uint32_t hgroup) {
+                                                           uint32_t hgroup, uint32_t bail) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    __shared__ uint32_t l_stop;
+    uint32_t since = 0;   // tiles since the last overflow check
+    if (threadIdx.x == 0) l_stop = 0;   // (read only after the loop's first barrier)
     __shared__ uint32_t l_hist[rsort::R];
     if (hcnt)
         for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) l_hist[j] = 0;
@@ -499,12 +519,19 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
         const bool have = p0 < c1;   // a tile this iteration (else: drain the previous one)
         const uint64_t np = have ? (c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE) : 0;
         __syncthreads();   // the previous election's LDS reads are done
+        const bool chk = bail && ++since >= bail;
+        if (chk) since = 0;
+        const uint64_t fl = chk && threadIdx.x == 0
+                                ? __hip_atomic_load(&counters[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0ull;
         uint32_t r0 = 0;
         if (have) {
             r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records<NT>(bufs, n, stride, p0, np, tile);
             for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
         }
+        if (fl & FT_OVERFLOW) l_stop = 1;
         __syncthreads();
+        if (l_stop) break;   // as k_flow_extract's bail (the pending outputs are dropped with the pass)
         bool valid = false, leader = false;
         uint64_t i = p0 + threadIdx.x, src = 0, dst = 0;
         uint32_t id = 0, lead = SLOT_NONE;
@@ -548,9 +575,11 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *_
             }
         }
         // the previous tile's leaders resolve their slots (its read has landed)
-        if (pv_leader)
-            l_slot[buf ^ 1][threadIdx.x] = ft_find_or_insert(tab, mask, probe_limit, pv_src, pv_dst, counters, n_new,
-                                                              &pv_e);
+        if (pv_leader) {
+            const uint32_t sl = ft_find_or_insert(tab, mask, probe_limit, pv_src, pv_dst, counters, n_new, &pv_e);
+            l_slot[buf ^ 1][threadIdx.x] = sl;
+            if (sl == SLOT_NONE && bail) l_stop = 1;
+        }
         __syncthreads();
         if (pv_valid) {
             const uint32_t sl = pv_lead != SLOT_NONE ? l_slot[buf ^ 1][pv_lead] : SLOT_NONE;
@@ -1368,7 +1397,8 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                                    dim3(xpl.nwg),
                                    dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
                                    pb, pn, (uint32_t)stride, pm, my_key, xpl.chunk, tab, (uint32_t)(C - 1), probe_limit,
-                                   slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr, hg);
+                                   slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr, hg,
+                                   (uint32_t)ctx->knobs.flow_bail);
             // the counters into pinned memory (an async copy to pageable memory
             // would hold the host until the extract ends); flow_ev[0]: the
             // table is complete (the key-ranking branch waits for it, not for

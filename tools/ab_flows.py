@@ -29,12 +29,14 @@ def main():
     ap.add_argument("--t", type=int, default=32)
     ap.add_argument("--host-check", type=int, default=0,
                     help="1: compare outputs on the host (pageable copies between calls), 0: on the device")
+    ap.add_argument("--cold", type=int, default=0,
+                    help="1: every call on a fresh context (no flow-count hint: the table starts small and regrows)")
     ap.add_argument("--default", type=int, default=None, help="knob value restored afterwards (default: the first mode)")
     a = ap.parse_args()
     import torch
     import sidekick_amd as sk
     from sidekick_amd._lib import lib
-    from sidekick_amd.quack import PktStats
+    from sidekick_amd.quack import Context, PktStats
     ctx = sk.get_context(0)
     dev = "cuda:0"
     n, stride, t = int(a.npkts), 67, a.t
@@ -59,6 +61,8 @@ def main():
         same = {m: True for m in modes}
         for r in range(a.rounds + 1):
             for m in modes:
+                if a.cold:
+                    ctx = Context(0)
                 ctx.set_knob(a.knob, m)
                 nf, st = C.c_size_t(), PktStats()
                 torch.cuda.synchronize()
@@ -70,6 +74,8 @@ def main():
                 dt = time.perf_counter() - t0
                 if rc != 0:
                     raise SystemExit(f"rc={rc} at {a.knob}={m}")
+                if a.cold:
+                    torch.cuda.synchronize()
                 if r:
                     times[m].append(dt)
                 if a.host_check:
@@ -82,7 +88,10 @@ def main():
                     ref = (keys[: nf.value].clone(), sks[: nf.value].clone())
                 elif not (torch.equal(keys[: nf.value], ref[0]) and torch.equal(sks[: nf.value], ref[1])):
                     same[m] = False
-        ctx.set_knob(a.knob, modes[0] if a.default is None else a.default)
+                if a.cold:
+                    ctx.close()
+        if not a.cold:
+            ctx.set_knob(a.knob, modes[0] if a.default is None else a.default)
         print(json.dumps({"flows": nflows, "n_packets": n, "t": t, "knob": a.knob,
                           "median_ms": {str(m): float(np.median(times[m])) * 1e3 for m in modes},
                           "min_ms": {str(m): float(np.min(times[m])) * 1e3 for m in modes},
