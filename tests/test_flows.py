@@ -235,6 +235,36 @@ def test_gpu_flows_edge_keys_and_table_growth():
 
 
 @pytest.mark.gpu
+def test_gpu_flows_regrow_bail():
+    """A batch of 60 000 flows on a fresh context (table from 4096 slots):
+    the overflowing passes stop early (knob flow_bail; 0 = finish every
+    pass) and the batch reruns on regrown tables; the records must be the
+    oracle's and byte for byte the no-bail path's, also with resets (the
+    rerun after the last reset) and with the pipelined extract."""
+    import torch
+    from sidekick_amd.quack import Context, encode_flows
+    bufs, meta = make_flows(400_000, 60_000, seed=77, p_reset=0.0005, reset_until=0.3)
+    want, nres, _ = vector_flows(bufs, meta)
+    d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
+    d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
+    recs = {}
+    for bail, pipe in ((64, 0), (0, 0), (1, 0), (64, 1)):
+        ctx = Context(0)
+        ctx.set_knob("flow_bail", bail)
+        ctx.set_knob("flow_pipe", pipe)
+        keys, qs, st = encode_flows(d_bufs, 16, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
+        assert st["resets"] == nres and keys == sorted(want)
+        if bail == 64 and pipe == 0:
+            for k, q in zip(keys, qs):
+                ids = want[k]
+                assert q.count() == len(ids) and q.last_value() == ids[-1], k.hex()
+                assert q.power_sums() == coracle.encode_u32(np.array(ids, dtype=np.uint32), 16), k.hex()
+        recs[(bail, pipe)] = [bytes(q._buf.raw) for q in qs]
+        ctx.close()
+    assert all(r == recs[(64, 0)] for r in recs.values())
+
+
+@pytest.mark.gpu
 def test_gpu_flows_group_by_slot_and_by_rank():
     """The grouping sort keys the packets by table slot or by flow rank (a
     slot -> rank remap first); by rank is taken when it saves two 8-bit
