@@ -38,6 +38,11 @@ Rank 0 prints ONE JSON line.  Alongside the metric it reports
                 (two sharded encodes, the difference, decode_sharded's
                 broadcast and all-gathers) against rank 0's single-GPU root
                 test: equal hit lists, every drop recovered;
+  configs       N = 1, untimed, after the headline: configs[2] (u64 t=80),
+                configs[4] (decode-missing, and its u64 twin) and SURVEY §8f's
+                flow and packet batches, each with its kernel / wall times,
+                roofline fractions and an independent check of its result
+                (secondary_configs; --configs 0 skips it);
   cpu_baseline  the oracle's scalar C restatement of the reference insert
                 loop on ONE host core over a bounded prefix of the same
                 stream (rank 0, N = 1 only), timed in the crate's own unit
@@ -220,6 +225,284 @@ def decode_check(comm, ctx, ids, n_per_gpu, rank, world, bits):
             "drops_recovered": bool(set(drops.tolist()) <= set(hits)), "decode_sharded_ms": dec_ms}
 
 
+# ---------------------------------------------------------------------------
+# N = 1, untimed, after the headline: every other single-GPU config of
+# BASELINE.json (and SURVEY §8f's two batch paths) measured and checked in the
+# same run, so the driver's record carries them (reported under "configs").
+# Kernel times come from HIP events on the launch stream (qk_ctx profiling);
+# wall times from perf_counter around synchronised calls; each block checks
+# its own result independently of the kernel it times.
+# ---------------------------------------------------------------------------
+# configs[2]: digest of the folded power sums of 1e9 u64 ids (seed
+# 0x5EED0003) at t = 80, recorded by this block's first run (BENCH line of
+# profiles/r06/), equal across every u64 kernel change since.
+RECORDED_U64_DIGEST = {(64, 80, 1_000_000_000, 0x5EED0003): "9d86f76bad8351be"}
+
+
+def cfg_u64(ctx, dev_index, steps=10):
+    """configs[2]: encode 1e9 u64 ids at t = 80, device-resident: kernel ms,
+    ids/s, algorithmic HBM fraction, the issue-anchor fraction on the same
+    method as the headline's roofline.valu, the digest against the recorded
+    one, and the first 1e6 ids against the oracle's scalar C encode of the
+    same stream generated on the host."""
+    import numpy as np
+    import torch
+    import sidekick_amd as sk
+    from oracle import coracle
+    from sidekick_amd import dist as skd
+    from sidekick_amd.quack import encode_device_async, fill_splitmix, partial_words
+    n, t, seed, m = 1_000_000_000, 80, 0x5EED0003, 1_000_000
+    dev = f"cuda:{dev_index}"
+    ids = torch.empty(n, dtype=torch.int64, device=dev)
+    fill_splitmix(ctx, ids, seed, bits=64)
+    part = torch.zeros(partial_words(t, 64), dtype=torch.int64, device=dev)
+
+    def step():
+        encode_device_async(ctx, ids, t, part, bits=64)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    ctx.kernel_stats()
+    ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    ctx.set_profiling(False)
+    kms, launches = ctx.kernel_stats()
+    kern = kms / max(launches, 1)
+    S, count = skd.fold_partial_sum(part.cpu().numpy().view(np.uint64), t, 64)
+    digest = digest_of(S, count)
+    clock = measure_clock(ctx, step, dev_index, kern)
+    torch.cuda.synchronize()
+    q = sk.PowerSumQuackU64(t)
+    q.insert_batch(ids[:m], ctx=ctx)
+    want = coracle.encode_u64(coracle.splitmix_u64(seed, m), t)
+    rec = RECORDED_U64_DIGEST.get((64, t, n, seed))
+    del ids
+    return {"workload": f"configs[2]: encode {n:.0e} u64 ids at t={t}, device-resident (seed {hex(seed)})",
+            "kernel_ms": kern, "launches": launches, "ms_per_step": wall * 1e3, "ids_per_s": n / wall,
+            "hbm_frac": 8 * n / (kern * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            "valu": valu_roofline(64, t, n, kern, clock), "clock_ghz": clock,
+            "digest": digest, "recorded_digest": rec, "equals_recorded": (digest == rec) if rec else None,
+            "oracle_prefix": {"ids": m, "equal": q.power_sums() == want}}
+
+
+def cfg_decode(ctx, dev_index, bits=32, reps=30):
+    """configs[4] (u32; its u64 twin with bits = 64): a 1e8-id candidate log,
+    32 seeded drops; quack_A = encode(log), quack_B = encode(log without the
+    drops), diff = A - B; the timed call is qk_u*_decode_device(diff, log,
+    stop_at_last) — to_coeffs, the host root finding, the root-set scan and
+    the hand-back — by perf_counter around the C call, the scan kernel by HIP
+    events.  Check: the hits equal the positions whose id is one of the
+    dropped ids (torch.isin on the device, no polynomial involved)."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import sidekick_amd as sk
+    from sidekick_amd._lib import lib
+    from sidekick_amd.quack import fill_splitmix
+    n, t = DECODE_N, DECODE_T
+    seed = DECODE_SEED + (bits == 64)
+    dev = f"cuda:{dev_index}"
+    log_ = torch.empty(n, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
+    fill_splitmix(ctx, log_, seed, bits=bits)
+    drops = np.sort(np.random.default_rng(seed).choice(n, DECODE_DROPS, replace=False))
+    d_drops = torch.from_numpy(drops).to(dev)
+    keep = torch.ones(n, dtype=torch.bool, device=dev)
+    keep[d_drops] = False
+    Q = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+    A, B = Q(t), Q(t)
+    A.insert_batch(log_, ctx=ctx)
+    B.insert_batch(log_[keep].contiguous(), ctx=ctx)
+    diff = A.clone()
+    diff.sub_assign(B)
+    expected = torch.isin(log_, log_[d_drops]).nonzero().flatten().cpu().tolist()
+    del keep
+    torch.cuda.synchronize()
+    fn = getattr(lib(), f"qk_u{bits}_decode_device")
+    cap = 1 << 12
+    hits = (C.c_uint64 * cap)()
+    nh = C.c_size_t()
+    walls, kerns, ok = [], [], True
+    for r in range(reps + 2):
+        ctx.kernel_stats()
+        ctx.set_profiling(True)
+        t0 = time.perf_counter()
+        rc = fn(ctx.handle, diff._buf, log_.data_ptr(), n, 1, hits, cap, C.byref(nh), None)
+        wall = time.perf_counter() - t0
+        ctx.set_profiling(False)
+        kms, k = ctx.kernel_stats()
+        got = [int(h) for h in hits[:nh.value]] if rc == 0 else None
+        ok = ok and got == expected
+        if r >= 2:
+            walls.append(wall * 1e6)
+            kerns.append(kms * 1e3 / max(k, 1))
+    b = bits // 8
+    scan = float(np.median(kerns))
+    del log_
+    return {"workload": f"configs[4]{'' if bits == 32 else ' (u64 twin)'}: decode-missing over a {n:.0e}-id u{bits} "
+                        f"log (seed {hex(seed)}), {DECODE_DROPS} drops, t={t}: qk_u{bits}_decode_device with "
+                        f"stop_at_last (to_coeffs + host roots + root-set scan + hand-back)",
+            "wall_us_median": float(np.median(walls)), "wall_us_min": float(np.min(walls)),
+            "scan_kernel_us_median": scan, "scan_hbm_frac": b * n / (scan * 1e-6) / (HBM_PEAK_GBS * 1e9),
+            "d": diff.count(), "hits": len(expected), "hits_equal_expected": ok,
+            "drops_recovered": bool(set(drops.tolist()) <= set(expected)) and ok, "reps": reps}
+
+
+def make_records(dev, n, seed, stride=67):
+    """n synthetic 67-byte captured records in HBM: random bytes, UDP, a
+    foreign destination (192.168.0.9:8080, src port 0x115C), id at byte 63."""
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    raw = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+    raw.random_(0, 256, generator=g)
+    rec = raw.view(n, stride)
+    rec[:, 23] = 17
+    rec[:, 30:38] = torch.tensor([192, 168, 0, 9, 0x11, 0x5C, 0x1F, 0x90], dtype=torch.uint8, device=dev)
+    return raw, rec, g
+
+
+def record_ids(rec_rows):
+    """The big-endian u32 identifiers (buffer.rs:99-106) of CUDA record rows,
+    as a host uint32 array."""
+    import numpy as np
+    import torch
+    b = rec_rows[:, 63:67].to(torch.int64)
+    v = (b[:, 0] << 24) | (b[:, 1] << 16) | (b[:, 2] << 8) | b[:, 3]
+    return v.cpu().numpy().astype(np.uint32)
+
+
+def cfg_flows(dev_index, n=100_000_000, nflows=1_000_000, t=32, steps=10):
+    """one SidekickMulti batch of n records over nflows
+    flows (src ip = flow number), device-resident output, on a FRESH context
+    (its first batch sizes the flow table from nothing).  First-batch and
+    steady (median) wall ms.  Check: flow count and inserts, and 8 sampled
+    flows' records against the oracle's scalar encode of their ids gathered
+    by torch in packet order."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import sidekick_amd as sk
+    from oracle import coracle
+    from sidekick_amd._lib import lib
+    from sidekick_amd.quack import Context, PktStats
+    dev = f"cuda:{dev_index}"
+    raw, rec, g = make_records(dev, n, 11)
+    f = torch.randint(0, nflows, (n,), device=dev, generator=g, dtype=torch.int64)
+    for k in range(4):
+        rec[:, 26 + k] = ((f >> (8 * k)) & 255).to(torch.uint8)
+    distinct = int(torch.unique(f).numel())
+    rsz = lib().qk_u32_size(t)
+    keys = torch.empty((nflows, 12), dtype=torch.uint8, device=dev)
+    sks = torch.empty((nflows, rsz // 4), dtype=torch.int32, device=dev)
+    ctx = Context(dev_index)
+    times, nf, st = [], C.c_size_t(), PktStats()
+    for _ in range(steps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rc = lib().qk_u32_encode_flows_device(ctx.handle, raw.data_ptr(), n, 67, None, None, t, keys.data_ptr(),
+                                              sks.data_ptr(), nflows, C.byref(nf), C.byref(st), None)
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+        if rc != 0:
+            raise RuntimeError(f"qk_u32_encode_flows_device rc={rc}")
+    m = int(nf.value)
+    kh = keys[:m].cpu().numpy()
+    rng = np.random.default_rng(0xF1)
+    sample = sorted({0, 1, nflows // 2, nflows - 1, *rng.integers(0, nflows, 4).tolist()})
+    ok = True
+    for fid in sample:
+        key = np.array([*(fid >> (8 * k) & 255 for k in range(4)), 0x11, 0x5C, 192, 168, 0, 9, 0x1F, 0x90], np.uint8)
+        row = np.nonzero(np.all(kh == key, axis=1))[0]
+        want_ids = record_ids(rec[f == fid])
+        if len(want_ids) == 0:
+            ok = ok and len(row) == 0
+            continue
+        if len(row) != 1:
+            ok = False
+            continue
+        q = sk.PowerSumQuackU32.__new__(sk.PowerSumQuackU32)
+        q._t = t
+        q._buf = C.create_string_buffer(sks[int(row[0])].cpu().numpy().tobytes(), rsz)
+        ok = ok and (q.power_sums() == coracle.encode_u32(want_ids, t) and q.count() == len(want_ids)
+                     and q.last_value() == int(want_ids[-1]))
+    ctx.close()
+    del raw, rec, f, keys, sks
+    steady = float(np.median(times[1:]))
+    return {"workload": f"SURVEY 8f row 1: per-flow batch, {n:.0e} 67-byte records of {nflows:.0e} flows -> one "
+                        f"quACK per AddrKey, t={t}, device-resident output, fresh context",
+            "first_batch_ms": times[0], "steady_ms_median": steady, "steady_ms_min": float(np.min(times[1:])),
+            "first_over_steady": times[0] / steady, "record_hbm_frac": n * 67 / (steady * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            "flows": m, "flows_expected": distinct, "inserted": int(st.inserted),
+            "check": {"flows_equal": m == distinct, "inserted_equal": int(st.inserted) == n,
+                      "sampled_flows": len(sample), "sampled_flows_equal_oracle": ok}}
+
+
+def cfg_packets(ctx, dev_index, n=100_000_000, t=32, steps=10):
+    """one sniff-loop batch (sidekick.rs:76-124) of n
+    records -> one quACK.  Median wall ms.  Check: the batch's quACK equals
+    the GPU encode of the ids torch extracts from the same records, and a
+    1e6-record prefix batch equals the oracle's scalar encode."""
+    import numpy as np
+    import torch
+    import sidekick_amd as sk
+    from oracle import coracle
+    from sidekick_amd.quack import encode_packets
+    dev = f"cuda:{dev_index}"
+    raw, rec, _ = make_records(dev, n, 7)
+    ip = (10, 0, 2, 1)
+    times = []
+    for _ in range(steps + 1):
+        q = sk.PowerSumQuackU32(t)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = encode_packets(q, raw, stride=67, my_ipv4=ip, ctx=ctx)
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+    b = rec[:, 63:67].to(torch.int64)
+    ids = ((b[:, 0] << 24) | (b[:, 1] << 16) | (b[:, 2] << 8) | b[:, 3]).to(torch.int32)
+    del b
+    ref = sk.PowerSumQuackU32(t)
+    ref.insert_batch(ids, ctx=ctx)
+    m = 1_000_000
+    qp = sk.PowerSumQuackU32(t)
+    encode_packets(qp, raw[:m * 67], stride=67, my_ipv4=ip, ctx=ctx)
+    want = coracle.encode_u32(ids[:m].cpu().numpy().view(np.uint32), t)
+    del raw, rec, ids
+    tm = float(np.median(times[1:]))
+    return {"workload": f"SURVEY 8f row 2: sniff-loop batch, {n:.0e} 67-byte records in HBM -> extract + encode "
+                        f"u32 t={t}",
+            "ms_median": tm, "ms_min": float(np.min(times[1:])), "packets_per_s": n / (tm * 1e-3),
+            "record_hbm_frac": n * 67 / (tm * 1e-3) / (HBM_PEAK_GBS * 1e9), "inserted": st["inserted"],
+            "check": {"inserted_equal": st["inserted"] == n, "equals_gpu_encode_of_extracted_ids": q == ref,
+                      "prefix_ids": m, "prefix_equals_oracle": qp.power_sums() == want}}
+
+
+def secondary_configs(ctx, dev_index):
+    """The N = 1 configs block: each entry is its own record or an error
+    string (a failure here never voids the measured headline)."""
+    import torch
+    out = {}
+    for name, fn in (("configs2_u64_t80", lambda: cfg_u64(ctx, dev_index)),
+                     ("configs4_decode_u32", lambda: cfg_decode(ctx, dev_index, 32)),
+                     ("configs4_decode_u64_twin", lambda: cfg_decode(ctx, dev_index, 64)),
+                     ("f1_flows_1e6", lambda: cfg_flows(dev_index)),
+                     ("f2_packets", lambda: cfg_packets(ctx, dev_index))):
+        tc = time.perf_counter()
+        try:
+            out[name] = fn()
+        except Exception as e:  # noqa: BLE001 — reported in the line
+            log(f"config {name} failed: {e!r}")
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+        out[name]["block_s"] = time.perf_counter() - tc
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return out
+
+
 # The published crate at the metric's threshold: benchmark_construct on one
 # core of a Xeon E5, `-e 1000 --trials 100`, in its own units — avg_cycles
 # (rdtsc around the insert loop) / 1000 ids and avg_us / 1000 ids; t = 32 and
@@ -338,6 +621,9 @@ def main():
     ap.add_argument("--bits", type=int, default=32, choices=(32, 64))
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     ap.add_argument("--cpu-sample", type=float, default=1e8, help="ids for the CPU baseline (0 disables)")
+    ap.add_argument("--configs", type=int, default=1,
+                    help="N = 1: after the headline, the untimed self-checked block of the other single-GPU configs "
+                         "(configs[2], configs[4] and its u64 twin, SURVEY 8f flows / packets); 0 skips it")
     ap.add_argument("--grid", type=int, default=0, help="override workgroups per launch")
     ap.add_argument("--knob", action="append", default=[], help="NAME=VALUE measurement knob (qk_ctx_set_knob)")
     ap.add_argument("--comm", action="store_true",
@@ -554,6 +840,8 @@ def main():
                            "devices": [r["rccl_device"] for r in ranks],
                            "user_ranks": [r["rccl_rank"] for r in ranks]}
 
+    if world == 1 and args.configs and bits == 32 and t == 32:
+        out["configs"] = secondary_configs(ctx, dev_index)
     if world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"], out["cpu_baseline_all_cores"] = cpu_baselines(args, bits, t, start, cnt, ids)
     print(json.dumps(out), flush=True)

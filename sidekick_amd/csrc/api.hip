@@ -18,6 +18,8 @@ using namespace qk;
 
 namespace qk {
 
+QK_WARM_KERNEL(api)
+
 // NULL is the HIP null (legacy default) stream, as in every HIP API: work
 // enqueued there is ordered with the caller's default-stream work (torch's
 // default stream has handle 0).
@@ -489,6 +491,17 @@ int qk_ctx_create(int device, qk_ctx **out) {
         hipEventCreateWithFlags(&ctx->flow_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->flow_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->flow_ev[2], hipEventDisableTiming) != hipSuccess) {
+        qk_ctx_destroy(ctx);
+        return QK_E_HIP;
+    }
+    // every code object resident and the pageable-copy path set up now, not
+    // inside the caller's first batch (ctx.h QK_WARM_KERNEL)
+    uint64_t pageable[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (warm_api(ctx->stream) || warm_encode(ctx->stream) || warm_decode(ctx->stream) ||
+        warm_packets(ctx->stream) || warm_flows(ctx->stream) || warm_comm(ctx->stream) ||
+        hipMemcpyAsync(ctx->d_small, pageable, sizeof pageable, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(pageable, ctx->d_small, sizeof pageable, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
         qk_ctx_destroy(ctx);
         return QK_E_HIP;
     }

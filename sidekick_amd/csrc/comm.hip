@@ -105,6 +105,8 @@ struct qk_comm {
 
 namespace qk {
 
+QK_WARM_KERNEL(comm)
+
 using Local = qk_comm::Local;
 
 // Words of every payload buffer: the largest encode payload, the decode

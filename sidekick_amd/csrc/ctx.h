@@ -150,6 +150,27 @@ constexpr size_t SMALL_HITPF_N = SMALL_STOPS - SMALL_HITPF;
 // the same slots relative to SMALL_NHITS (the kernel's hout)
 constexpr size_t RT_STOP0 = SMALL_STOPS - SMALL_NHITS;
 
+// One no-op kernel per translation unit.  HIP loads a translation unit's code
+// object at the first launch of any of its kernels, and sets up its staging
+// path for pageable copies at the first such copy; qk_ctx_create does both
+// (warm_* and two 64-byte pageable copies) so that neither lands inside a
+// caller's first batch (a process's first flow batch had a 7.7 ms idle gap
+// before its first pageable hand-back, profiles/r05/final5/flows_per_call.txt:20).
+#define QK_WARM_KERNEL(name)                                                                                     \
+    __global__ void k_warm_##name(int *p) {                                                                      \
+        if (p) p[threadIdx.x] = 0;                                                                               \
+    }                                                                                                            \
+    int warm_##name(hipStream_t s) {                                                                             \
+        hipLaunchKernelGGL(k_warm_##name, dim3(1), dim3(64), 0, s, nullptr);                                     \
+        return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;                                               \
+    }
+int warm_api(hipStream_t s);
+int warm_encode(hipStream_t s);
+int warm_decode(hipStream_t s);
+int warm_packets(hipStream_t s);
+int warm_flows(hipStream_t s);
+int warm_comm(hipStream_t s);
+
 hipStream_t pick_stream(qk_ctx *ctx, void *stream);
 // order stream s after the previous user of the context's scratch buffers
 int scratch_acquire(qk_ctx *ctx, hipStream_t s);

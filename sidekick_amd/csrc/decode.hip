@@ -23,6 +23,8 @@
 
 namespace qk {
 
+QK_WARM_KERNEL(decode)
+
 constexpr int RT_BLOCK = 256;
 
 // hout (optional, k_root_scan): the hit / stop also into pinned host memory

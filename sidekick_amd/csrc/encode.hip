@@ -51,6 +51,8 @@
 
 namespace qk {
 
+QK_WARM_KERNEL(encode)
+
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
 

@@ -57,6 +57,8 @@
 
 namespace qk {
 
+QK_WARM_KERNEL(flows)
+
 static_assert(sizeof(qk_flow_key) == 12, "qk_flow_key is 12 packed bytes");
 static_assert(sizeof(qk_u32) == 16, "qk_u32 header is 4 words (k_seg_small / k_flow_finalize_big write it)");
 

@@ -37,6 +37,8 @@
 
 namespace qk {
 
+QK_WARM_KERNEL(packets)
+
 constexpr int PK_BLOCK = REC_TILE;
 
 struct ChunkStat {       // per workgroup chunk, written by lane 0
