@@ -155,15 +155,14 @@ int qk_ctx_kernel_stats(qk_ctx *ctx, double *total_ms, uint64_t *launches);
 int qk_ctx_trim(qk_ctx *ctx);
 /* Tuning knobs (0 = automatic): workgroups per launch. */
 int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
-/* Measurement knobs of this context (the defaults are the
- * product's measured choices — tools/ and the variant tests set them):
- * "bsgs_sg", "bsgs_shapes", "bsgs_prio", "grid_mult" (1..8: encode grids of that many rounds of
- * resident workgroups), "u32_passes", "u32_xcache", "bsgs64_sg", "bsgs64_off", "bsgs64_tmin", "bsgs64_shapes", "bsgs64_prio", "u64_passes",
- * "u64_xcache", "u64_kmax", "flow_load" (2..64), "flow_wgpc", "flow_hist", "flow_sort", "flow_prio",
- * "pkt_fused", "rt64_horner",
- * "root_test" (0 automatic, 1 Horner, 2 root-set scan), "rt_direct" (0: the
- * root-set scan's results by copies, not its pinned host slots), "comm_fault" (tests:
- * the k-th collective's payload staging of this context's rank fails once).
+/* Knobs of this context that select between live product paths (DESIGN.md
+ * §3; the defaults are the product's measured choices — tools/ and the
+ * tests set them): "grid_mult" (1..8: encode grids of that many rounds of
+ * resident workgroups), "flow_hist" (per-flow batches of at most this many
+ * flows are grouped by slot histograms, 0: never), "flow_byslot" (0 the
+ * rule, 1 / 2 force the by-slot / by-rank grouping key), "root_test" (0
+ * automatic, 1 Horner, 2 root-set scan), "comm_fault" (tests: the k-th
+ * collective's payload staging of this context's rank fails once).
  * Unknown name or out-of-range value -> QK_E_INVAL. */
 int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value);
 /* Shader-clock probe (measurement): one wave on `stream` spins for

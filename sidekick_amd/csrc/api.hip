@@ -102,6 +102,24 @@ int ensure_stage(qk_ctx *ctx, size_t bytes) {
     return QK_OK;
 }
 
+int ensure_items(qk_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->h_items_bytes) return QK_OK;
+    // the previous buffer is idle: every user synchronises before returning
+    if (ctx->h_items) hipHostFree(ctx->h_items);
+    ctx->h_items = ctx->h_items_dev = nullptr;
+    ctx->h_items_bytes = 0;
+    bytes = std::max(bytes, (size_t)1 << 20);
+    if (hipHostMalloc(&ctx->h_items, bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostGetDevicePointer(&ctx->h_items_dev, ctx->h_items, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        if (ctx->h_items) hipHostFree(ctx->h_items);
+        ctx->h_items = ctx->h_items_dev = nullptr;
+        return QK_E_NOMEM;
+    }
+    ctx->h_items_bytes = bytes;
+    return QK_OK;
+}
+
 bool is_device_ptr(const void *p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
@@ -290,9 +308,6 @@ template <typename T> int root_test_plan(const qk_ctx *ctx, const T *coeffs, uin
     plan.scan = rt_scan_table<T>(r.data(), k, plan.set, plan.tab) &&
                 plan.set.words * sizeof(T) <= (SMALL_NHITS - RT_C) * 8;
     if (!plan.scan) plan.tab.clear();
-    // begin and finish must agree on the form even if the knob changes in
-    // between (comm.hip releases ctx->mu between the two)
-    plan.direct = plan.scan && ctx->knobs.rt_direct;
     return QK_OK;
 }
 
@@ -304,7 +319,7 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
     uint64_t *d_counters = ctx->d_small;
     T *d_c = (T *)(ctx->d_small + RT_C);
     uint64_t *h_c = ctx->h_small + RT_C;
-    const bool scan = n && plan.scan, direct = scan && plan.direct;
+    const bool scan = n && plan.scan;
     size_t cbytes = (size_t)d * sizeof(T);
     if (scan) {
         cbytes = (size_t)plan.set.words * sizeof(T);
@@ -321,7 +336,7 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
     ctx->h_small[1] = ~0ull;
     ctx->h_small[2] = 0;
     ctx->h_small[3] = 0;
-    if (direct) {   // the direct form's slots (decode.hip rt_record): empty, no overflow
+    if (scan) {   // the scan's host slots (decode.hip rt_record): empty, no overflow
         std::fill(ctx->h_small + SMALL_HITPF, ctx->h_small + SMALL_WORDS, ~0ull);
         ctx->h_small[SMALL_OVF] = 0;
     }
@@ -329,25 +344,21 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
                               hipMemcpyHostToDevice, s));
     if (int rc = ensure_hits(ctx, 4096, s)) return rc;
     if (n) {
-        int rc;
-        if (direct) {
+        if (scan) {
             // the scan writes its hits and stops into h_small's slots itself
             // (rt_record); root_test_finish derives count and stop from them
+            // (a D2H copy of the counters and hits instead measured slower,
+            // profiles/r05/decode_nt/)
             return launch_root_scan<T>(ctx, d_c, plan.set, d_log, n, use_stop, stop_value, ctx->d_hits,
                                        (uint64_t)ctx->hits_cap, d_counters, ctx->h_small_dev + SMALL_NHITS, s);
-        }
-        if (scan) {
-            rc = launch_root_scan<T>(ctx, d_c, plan.set, d_log, n, use_stop, stop_value, ctx->d_hits,
-                                     (uint64_t)ctx->hits_cap, d_counters, nullptr, s);
-            if (rc) return rc;
         }
         int (*launch)(qk_ctx *, const T *, uint32_t, const T *, size_t, int, T, uint64_t *, uint64_t, uint64_t *,
                       hipStream_t);
         if constexpr (sizeof(T) == 4) launch = launch_root_test_u32;
         else launch = launch_root_test_u64;
-        if (!scan) rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap,
-                               d_counters, s);
-        if (rc) return rc;
+        if (int rc = launch(ctx, d_c, d, d_log, n, use_stop, stop_value, ctx->d_hits, (uint64_t)ctx->hits_cap,
+                            d_counters, s))
+            return rc;
     }
     QK_HIP_TRY(hipMemcpyAsync(ctx->h_small + SMALL_NHITS, d_counters, 16, hipMemcpyDeviceToHost, s));
     // and the first hits with them: a decode finds ~d hits, so one
@@ -361,11 +372,11 @@ template <typename T>
 int root_test_finish(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_t d, const T *d_log, size_t n,
                      int use_stop, T stop_value, hipStream_t s, std::vector<uint64_t> &hits, uint64_t &stop_index) {
     // count and stop into h_small[SMALL_NHITS], [SMALL_STOP]: the Horner
-    // form copied them; the direct form (the scan) has its slots, or on
-    // overflow the device counters are copied now
+    // form copied them; the scan has its slots, or on overflow the device
+    // counters are copied now
     auto counts = [&]() -> int {
         QK_HIP_TRY(hipStreamSynchronize(s));
-        if (!(n && plan.scan && plan.direct)) return QK_OK;
+        if (!(n && plan.scan)) return QK_OK;
         uint64_t *h = ctx->h_small;
         if (h[SMALL_OVF]) {
             QK_HIP_TRY(hipMemcpyAsync(h + SMALL_NHITS, ctx->d_small, 16, hipMemcpyDeviceToHost, s));
@@ -476,11 +487,9 @@ int qk_ctx_create(int device, qk_ctx **out) {
     if (!ctx) return QK_E_NOMEM;
     ctx->device = device;
     ctx->num_cus = prop.multiProcessorCount;
-    int prio_least = 0, prio_greatest = 0;   // the flow batches' side branch runs at the lowest priority
-    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_least = prio_greatest = 0;
+    if (prop.maxThreadsPerMultiProcessor > 0) ctx->max_threads_per_cu = prop.maxThreadsPerMultiProcessor;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->side_stream, hipStreamNonBlocking, prio_least) != hipSuccess ||
         hipMalloc(&ctx->d_small, SMALL_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&ctx->h_small, SMALL_WORDS * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&ctx->h_flow, 8 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
@@ -495,9 +504,10 @@ int qk_ctx_create(int device, qk_ctx **out) {
         return QK_E_HIP;
     }
     // every code object resident and the pageable-copy path set up now, not
-    // inside the caller's first batch (ctx.h QK_WARM_KERNEL)
+    // inside the caller's first batch (ctx.h QK_WARM_KERNEL); the per-flow
+    // work-item buffer (1 MiB) allocated
     uint64_t pageable[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (warm_api(ctx->stream) || warm_encode(ctx->stream) || warm_decode(ctx->stream) ||
+    if (ensure_items(ctx, (size_t)1 << 20) || warm_api(ctx->stream) || warm_encode(ctx->stream) || warm_decode(ctx->stream) ||
         warm_packets(ctx->stream) || warm_flows(ctx->stream) || warm_comm(ctx->stream) ||
         hipMemcpyAsync(ctx->d_small, pageable, sizeof pageable, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
         hipMemcpyAsync(pageable, ctx->d_small, sizeof pageable, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
@@ -531,9 +541,9 @@ void qk_ctx_destroy(qk_ctx *ctx) {
     if (ctx->d_small) hipFree(ctx->d_small);
     if (ctx->h_small) hipHostFree(ctx->h_small);
     if (ctx->h_flow) hipHostFree(ctx->h_flow);
+    if (ctx->h_items) hipHostFree(ctx->h_items);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     if (ctx->copy_stream) hipStreamDestroy(ctx->copy_stream);
-    if (ctx->side_stream) hipStreamDestroy(ctx->side_stream);
     delete ctx;
 }
 
@@ -595,27 +605,11 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         int64_t lo, hi;
     };
     static const K table[] = {
-        {"bsgs_sg", &qk_knobs::bsgs_sg, -1, 64},       {"u32_passes", &qk_knobs::u32_passes, 0, 1},
-        {"u32_xcache", &qk_knobs::u32_xcache, 0, 1},     {"bsgs_shapes", &qk_knobs::bsgs_shapes, 0, 1},
-        {"bsgs_prio", &qk_knobs::bsgs_prio, 0, 1},      {"grid_mult", &qk_knobs::grid_mult, 1, 8},
-        {"bsgs64_sg", &qk_knobs::bsgs64_sg, -1, 64},   {"bsgs64_off", &qk_knobs::bsgs64_off, 0, 1},
-        {"bsgs64_tmin", &qk_knobs::bsgs64_tmin, 9, 81}, {"bsgs64_shapes", &qk_knobs::bsgs64_shapes, 0, 1},
-        {"bsgs64_prio", &qk_knobs::bsgs64_prio, 0, 1},
-        {"u64_passes", &qk_knobs::u64_passes, 0, 1},
-        {"u64_xcache", &qk_knobs::u64_xcache, 0, 1},   {"u64_kmax", &qk_knobs::u64_kmax, 4, 40},
-        {"flow_load", &qk_knobs::flow_load, 2, 64},    {"flow_wgpc", &qk_knobs::flow_wgpc, 1, 32},
-        {"flow_hist", &qk_knobs::flow_hist, 0, 1 << 20},      {"flow_sort", &qk_knobs::flow_sort, 1, 9},
-        {"flow_fuse0", &qk_knobs::flow_fuse0, 0, 1},    {"flow_pipe", &qk_knobs::flow_pipe, 0, 1},
-        {"flow_nt", &qk_knobs::flow_nt, 0, 1},          {"flow_rs_nt", &qk_knobs::flow_rs_nt, 0, 3},
-        {"flow_side_lo", &qk_knobs::flow_side_lo, 0, 1},   {"flow_spec", &qk_knobs::flow_spec, 0, 1},
+        {"grid_mult", &qk_knobs::grid_mult, 1, 8},
+        {"flow_hist", &qk_knobs::flow_hist, 0, 1 << 20},
         {"flow_byslot", &qk_knobs::flow_byslot, 0, 2},
-        {"flow_bail", &qk_knobs::flow_bail, 0, 1 << 16},
-        {"flow_nd", &qk_knobs::flow_nd, 0, 1},
-        {"pkt_nt", &qk_knobs::pkt_nt, 0, 1},
-        {"flow_prio", &qk_knobs::flow_prio, 0, 1},    {"pkt_fused", &qk_knobs::pkt_fused, 0, 1},
-        {"pkt_wgpc", &qk_knobs::pkt_wgpc, 1, 16},     {"rt64_horner", &qk_knobs::rt64_horner, 0, 1},
-        {"root_test", &qk_knobs::root_test, 0, 2},      {"rt_direct", &qk_knobs::rt_direct, 0, 1},
-        {"rt_scan_u", &qk_knobs::rt_scan_u, 1, 4},      {"rt_scan_nt", &qk_knobs::rt_scan_nt, 0, 1},      {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
+        {"root_test", &qk_knobs::root_test, 0, 2},
+        {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
     };
     for (const K &k : table)
         if (strcmp(k.name, name) == 0) {

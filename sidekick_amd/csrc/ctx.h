@@ -7,63 +7,19 @@
 
 #include "quack_hip.h"
 
-// Measurement knobs (qk_ctx_set_knob; only tools/ and tests set them — the
-// defaults below are the product's choices, each backed by a measurement in
-// DESIGN.md).  Per context, so one process can compare variants.
+// Per-context knobs (qk_ctx_set_knob).  Round 6 removed every knob that
+// selected a measured-and-rejected variant ("measured and
+// removed"); what is left selects between live product paths — the defaults
+// below are the product's own choices — or injects a test fault.
 struct qk_knobs {
-    int bsgs_sg = -1;      // u32 BSGS: scalar-counted wrap groups (-1: the per-shape default)
-    int u32_passes = 1;    // 0: u32 t > 80 on the power chain instead of BSGS passes
-    int bsgs_shapes = 1;   // 0: the round-2 u32 BSGS shapes (t 17..36, 41..42, 65..72)
-    int bsgs_prio = 1;     // 0: u32 BSGS without wave priority over the accumulation (bsgs.h Cfg PRIO 4)
     int grid_mult = 3;     // encode launches: resident workgroups x this (1: one round; grid_for, encode.hip)
-    int u32_xcache = 1;    // 0: u32 offset passes raise x^8 to base/8 themselves (no per-id x^base cache)
-    int bsgs64_sg = -1;    // u64 BSGS MAC mode override (-1: default)
-    int bsgs64_off = 0;    // 1: u64 on the power chain instead of BSGS
-    int bsgs64_shapes = 1; // 0: u64 t = 14..20, 25..28, 33..36 with 8 babies per id instead of 4
-    int bsgs64_prio = 1;   // 0: u64 BSGS without s_setprio in the MAC step and without paired MACs (round 3)
-    int bsgs64_tmin = 14;  // lowest u64 threshold on BSGS (below: the power chain; round 2: 21)
-    int u64_passes = 1;    // 0: u64 t > 80 on the power chain instead of BSGS passes
-    int u64_xcache = 1;    // 0: u64 offset passes raise x^8 to base/8 themselves (no per-id x^base cache)
-    int u64_kmax = 40;     // u64 power chain: accumulators per lane
-    int flow_load = 4;     // flow-table slots per expected flow
-    int flow_wgpc = 12;    // flow extract: workgroups per CU
-    int flow_hist = 32;    // batches of at most this many flows (and a table of <= 8192 slots) are grouped by
-                           // per-workgroup slot histograms instead of the radix sort (0: never); 16 flows
-                           // 2.76 vs 2.90 ms, 64: 3.17 vs 3.05, 1000: 5.80 vs 3.68 (profiles/r05/flows_hist/)
-    int flow_sort = 2;     // grouping sort (radix.h, flows.hip rs_sort): 1: 8-bit digits, 256 threads, two arrays
-                           // throughout; 2: pair arrays between the first and last pass; 3 / 4: 512 / 1024
-                           // threads; 5 / 6: 11-bit digits, 512 / 1024 threads; 7-9: as 2, 5, 6 without LDS
-                           // staging (direct scatter)
-    int pkt_nt = 1;        // the packet-batch kernels: records read nontemporal (t = 32, 1e8 records:
-                           // 1.83-1.84 -> 1.74-1.76 ms, profiles/r05/packets_nt/)
-    int flow_nd = 1;       // 1: each radix scatter writes the next pass's digit bytes (count from them); 0: count from the pairs
-    int flow_bail = 64;    // the flow extract stops on its own overflow, or on any (flag read every flow_bail-th tile); 0: never
-    int flow_byslot = 0;   // grouping sort key: 0 by the pass-count rule, 1 slot, 2 flow rank (A/B)
-    int flow_spec = 0;     // flow batches: the by-slot grouping sort launched before the host reads the
-                           // extract's counters (16 / 1e4 / 1e6 flows: equal within 0.5 %,
-                           // profiles/r05/flows_spec/: the launch gap it removes is not on the path)
-    int flow_side_lo = 0;  // flow batches: the key-ranking branch on the lowest-priority stream (1e6 flows
-                           // 5.92 vs 5.89 ms, 1e4 equal: no contention to speak of, profiles/r05/flows_side/)
-    int flow_rs_nt = 1;    // grouping-sort scatters: bit 0 input read, bit 1 output written nontemporal
-                           // (bit 0: 1e6 flows 6.16 -> 6.02 ms, 1e4 4.01 -> 3.89; bit 1: +15 %,
-                           // profiles/r05/flows_nt/ab_rsnt.jsonl)
-    int flow_nt = 1;       // k_flow_extract: records read / (slot, id) written nontemporal (1e6 flows
-                           // 6.04 -> 5.93 ms, 16 flows 2.88 -> 2.81 ms, profiles/r05/flows_nt/)
-    int flow_pipe = 0;     // 1: the flow extract reads its table one tile ahead (k_flow_extract_pipe: slower,
-                           // 1e6 flows 7.14 vs 6.25 ms, 1e4 4.42 vs 4.11; profiles/r05/check4/ab_pipe.log)
-    int flow_fuse0 = 1;    // 0: the grouping sort's first-digit counts by its own pass, not fused into the extract
-                           // (1e6 flows 6.71 vs 6.61 ms, 1e4 4.46 vs 4.42; profiles/r05/check4/ab_fuse0.log)
-    int flow_prio = 0;     // 1: per-flow encode kernels with s_setprio around the MACs (1e6 flows: 7.57 vs
-                           // 6.80 ms, 16 / 1e4 flows even; profiles/r04/prio/ab_flows_prio.jsonl)
-    int pkt_wgpc = 4;      // packet batches: workgroups per CU
-    int pkt_fused = 1;     // 0: packet batches t 5..12 in two passes (extract, encode)
-    int rt64_horner = 0;   // 1: u64 root test by Horner instead of baby-step/giant-step
-    int root_test = 0;     // 0: automatic, 1: Horner, 2: root-set scan (decode.hip)
-    int rt_scan_nt = 1;    // root-set scan: nontemporal 16-byte loads of the log (u32 kernel 72 -> 66 us,
-                           // u64 135 -> 125 us at configs[4], profiles/r05/decode_nt/)
-    int rt_scan_u = 1;     // root-set scan: 16-byte loads per lane per iteration (1, 2, 4; 3 runs as 2; 1: u32
-                           // kernel 70 vs 84 / 78 us at 2 / 4, profiles/r04/decode_scan_u/)
-    int rt_direct = 1;     // 0: the root-set scan's results by D2H copies instead of its host slots
+    int flow_hist = 32;    // per-flow batches of at most this many flows (and a table of <= 8192 slots) are
+                           // grouped by per-workgroup slot histograms instead of the radix sort (0: never);
+                           // 16 flows 2.76 vs 2.90 ms, 64: 3.17 vs 3.05, 1000: 5.80 vs 3.68
+                           // (profiles/r05/flows_hist/)
+    int flow_byslot = 0;   // per-flow grouping-sort key: 0 the pass-count rule (flows.hip), 1 force by slot,
+                           // 2 force by flow rank (tests cover both product paths)
+    int root_test = 0;     // 0: automatic (cost model, api.hip rt_use_scan), 1: Horner, 2: root-set scan
     int comm_fault = 0;    // k > 0 (tests): this rank's payload staging for the k-th collective of its
                            // next sharded operation fails, once (comm.hip fault_now)
 };
@@ -71,10 +27,11 @@ struct qk_knobs {
 struct qk_ctx {
     int device = 0;
     int num_cus = 256;
+    int max_threads_per_cu = 2048;     // hipDeviceProp_t::maxThreadsPerMultiProcessor
+    uint32_t max_blocks_per_cu(uint32_t block) const { return (uint32_t)max_threads_per_cu / block; }
     hipStream_t stream = nullptr;      // own stream (host-input pipeline, comm collectives); a NULL
                                        // stream argument is the HIP null stream, not this one
     hipStream_t copy_stream = nullptr; // second stream for the host-input pipeline
-    hipStream_t side_stream = nullptr; // lowest-priority stream: the flow batches' key-ranking branch
     uint32_t grid_override = 0;
     qk_knobs knobs;
 
@@ -95,6 +52,15 @@ struct qk_ctx {
     void *d_flow[3] = {nullptr, nullptr, nullptr};
     size_t flow_bytes[3] = {0, 0, 0};
     size_t flow_hint = 0;
+    // work items of the per-flow encode, written by the host into pinned
+    // memory the kernels read directly (h_items_dev): no H2D copy — a
+    // process's first pageable H2D copy cost 7 ms (SDMA set-up) inside its
+    // first flow batch: 16 flows 9.97 ms against 2.89 steady, 3.23 after
+    // (profiles/r06/s1/, s2/flows_cold.jsonl); grow-only, used only inside
+    // synchronous calls
+    void *h_items = nullptr;
+    void *h_items_dev = nullptr;
+    size_t h_items_bytes = 0;
 
     // host-input pipeline: pinned staging + device chunk buffers (2 slots)
     void *h_stage[2] = {nullptr, nullptr};
@@ -182,6 +148,7 @@ int ensure_scratch(qk_ctx *ctx, size_t bytes, hipStream_t s);
 int ensure_hits(qk_ctx *ctx, size_t cap, hipStream_t s);
 int ensure_flow(qk_ctx *ctx, int which, size_t bytes, hipStream_t s);
 int ensure_stage(qk_ctx *ctx, size_t bytes);
+int ensure_items(qk_ctx *ctx, size_t bytes);
 bool is_device_ptr(const void *p);
 hipEvent_t prof_begin(qk_ctx *ctx, hipStream_t s);
 void prof_end(qk_ctx *ctx, hipStream_t s, hipEvent_t begin);
@@ -231,8 +198,7 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
 // root_test_begin enqueues on s; root_test_finish waits and collects the
 // sorted hit positions (all of them) and the first stop position
 template <typename T> struct RtPlan {
-    bool scan = false;
-    bool direct = false;  // the scan writes its hits into pinned host slots (knob rt_direct, read once at plan time)
+    bool scan = false;    // the root-set scan, writing its hits into pinned host slots (else Horner)
     RtScanSet set;
     std::vector<T> tab;   // the root set (scan)
 };

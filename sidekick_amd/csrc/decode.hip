@@ -351,7 +351,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_test_u64_bsgs(const uint64_t 
 }
 
 bool rt64_use_bsgs(const qk_ctx *ctx, uint32_t d) {
-    return !ctx->knobs.rt64_horner && d >= RT64_BSGS_MIND && d <= RT64_BSGS_MAXD;
+    (void)ctx;
+    return d >= RT64_BSGS_MIND && d <= RT64_BSGS_MAXD;
 }
 
 // host: the limb-shifted coefficient table of the BSGS kernel into out[]
@@ -547,27 +548,18 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
     if (a & (sizeof(T) - 1)) return QK_E_INVAL;
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / sizeof(T));
     const size_t lds = (size_t)set.words * sizeof(T);
-    const int U = ctx->knobs.rt_scan_u;
-    const uint64_t units = (n + U * (16 / sizeof(T)) - 1) / (U * (16 / sizeof(T)));
+    // one nontemporal 16-byte load per lane per iteration: u32 kernel 70 us
+    // against 84 / 78 us with 2 / 4 in flight (profiles/r04/decode_scan_u/);
+    // nontemporal 72 -> 66 us, u64 135 -> 125 us (profiles/r05/decode_nt/)
+    const uint64_t units = (n + (16 / sizeof(T)) - 1) / (16 / sizeof(T));
     hipEvent_t e0 = prof_begin(ctx, s);
-#define QK_RS(SS, UU)                                                                                         \
-    do {                                                                                                      \
-        if (ctx->knobs.rt_scan_nt) QK_RSN(SS, UU, true);                                                      \
-        else QK_RSN(SS, UU, false);                                                                           \
-    } while (0)
-#define QK_RSN(SS, UU, NT_)                                                                                   \
-    hipLaunchKernelGGL((k_root_scan<T, SS, UU, NT_>), dim3(rs_grid(ctx, k_root_scan<T, SS, UU, NT_>, units, lds)), \
+#define QK_RS(SS)                                                                                             \
+    hipLaunchKernelGGL((k_root_scan<T, SS, 1, true>), dim3(rs_grid(ctx, k_root_scan<T, SS, 1, true>, units, lds)), \
                        dim3(RT_BLOCK), lds, s, log, (uint64_t)n, head, d_tab, set.words, set.m1, set.m2, set.shift, \
                        use_stop, stop_value, hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N)
-    if (set.S == 1) {
-        if (U == 4) QK_RS(1, 4);
-        else if (U == 1) QK_RS(1, 1);
-        else QK_RS(1, 2);
-    } else {
-        QK_RS(4, 1);
-    }
+    if (set.S == 1) QK_RS(1);
+    else QK_RS(4);
 #undef QK_RS
-#undef QK_RSN
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());
     return QK_OK;

@@ -630,12 +630,14 @@ static uint32_t grid_for(qk_ctx *ctx, KernelT kern, uint64_t units, uint32_t per
 }
 
 // An upper bound on grid_for over every kernel a multi-pass encode may
-// launch, whatever its occupancy (which depends on the knob-selected
-// instantiation): at most 8 workgroups of 256 threads per CU (32 waves).
-// The x^base cache is placed after the largest partials this allows.
+// launch, whatever its occupancy: the device's resident threads per CU
+// (hipDeviceAttributeMaxThreadsPerMultiProcessor, read at context creation)
+// in workgroups of BLOCK threads.  The x^base cache is placed after the
+// largest partials this allows.
 static uint32_t grid_cap(const qk_ctx *ctx, uint64_t units, uint32_t per_block, int mult = 0) {
     if (ctx->grid_override) return ctx->grid_override;
-    const uint64_t full = (uint64_t)ctx->num_cus * 8u * (uint64_t)(mult > 0 ? mult : ctx->knobs.grid_mult);
+    const uint64_t full = (uint64_t)ctx->num_cus * (uint64_t)ctx->max_blocks_per_cu(BLOCK) *
+                          (uint64_t)(mult > 0 ? mult : ctx->knobs.grid_mult);
     uint64_t need = (units + per_block - 1) / per_block;
     if (need < 1) need = 1;
     return (uint32_t)(need < full ? need : full);
@@ -718,18 +720,16 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
     // writes x^80, the middle passes read and write, the last one reads.  The
     // cache lives in the scratch after the partials, sized once for every
     // pass (a regrow between passes would drop it), with the ids' address
-    // modulo 16 so that both are read in the same 16-byte groups; knob
-    // u32_xcache = 0 keeps the square-and-multiply form.
+    // modulo 16 so that both are read in the same 16-byte groups.
     const uint32_t npass = T <= 80 ? 0 : (T - 80 + 47) / 48;   // offset passes
     uint32_t *xc = nullptr;
-    if (npass >= 1 && ctx->knobs.u32_xcache) {
+    if (npass >= 1) {
         const uint32_t nbmax = grid_cap(ctx, (n + 3) / 4, BLOCK, 1);   // run_pass: one round
         const size_t poff = ((size_t)nbmax * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
         if (ensure_scratch(ctx, poff + 16 + (size_t)n * 4, s) == QK_OK)
             xc = (uint32_t *)((char *)ctx->d_scratch + poff + ((uintptr_t)ids & 15));
         // else: no room for the cache, each pass raises x^8 itself
     }
-    const bool prio = ctx->knobs.bsgs_prio;   // s_setprio around the MAC phase (knob bsgs_prio)
     uint32_t pass = 0;
     for (uint32_t base = 0; base < T; ++pass) {
         const uint32_t Tp = std::min<uint32_t>(base == 0 ? 80 : 48, T - base);
@@ -738,13 +738,12 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
         const int xcm = !xc ? 0 : (pass > 0 ? 1 : 0) | (pass < npass ? 2 : 0);
         int rc;
         if (base == 0 && xc)
-            rc = run_pass<2>(ctx, prio ? k_encode_u32_bsgs_x80<16, 1> : k_encode_u32_bsgs_x80<16, 0>, 80, ids, n, head,
-                             Tp, 0, out, meta, acc, s, nullptr, xc);
+            rc = run_pass<2>(ctx, k_encode_u32_bsgs_x80<16, 1>, 80, ids, n, head, Tp, 0, out, meta, acc, s, nullptr,
+                             xc);
         else if (base == 0)
-            rc = run_pass<0>(ctx, prio ? k_encode_u32_bsgs<8, 10, 16, 1> : k_encode_u32_bsgs<8, 10, 16, 0>, 80, ids, n,
-                             head, Tp, 0, out, meta, acc, s);
+            rc = run_pass<0>(ctx, k_encode_u32_bsgs<8, 10, 16, 1>, 80, ids, n, head, Tp, 0, out, meta, acc, s);
         else if (Tp <= 40) {   // the last pass (npass >= 1): NA = ceil(Tp / 8) giant rows
-#define QK_OFF32(NA_, XC_) (prio ? k_encode_u32_bsgs_off<NA_, 2 * NA_, XC_, 1> : k_encode_u32_bsgs_off<NA_, 2 * NA_, XC_, 0>)
+#define QK_OFF32(NA_, XC_) k_encode_u32_bsgs_off<NA_, 2 * NA_, XC_, 1>
 #define QK_LAST32(NA_)                                                                                       \
     (xcm & 1 ? run_pass<1>(ctx, QK_OFF32(NA_, 1), 8 * NA_, ids, n, head, Tp, base,                            \
                               out + base, meta, acc, s, xc, nullptr)                                          \
@@ -783,7 +782,7 @@ static int enc32_passes_chunk(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32
 constexpr size_t XC_CHUNK32 = (size_t)1 << 28;
 static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
                         int acc, hipStream_t s) {
-    if (n <= XC_CHUNK32 || !ctx->knobs.u32_xcache) return enc32_passes_chunk(ctx, ids, n, head, T, out, acc, s);
+    if (n <= XC_CHUNK32) return enc32_passes_chunk(ctx, ids, n, head, T, out, acc, s);
     for (size_t c0 = 0; c0 < n; c0 += XC_CHUNK32) {
         const uint32_t *p = ids + c0;
         const uint32_t hd = (uint32_t)(((16 - ((uintptr_t)p & 15)) & 15) / 4);
@@ -800,7 +799,7 @@ static int enc32_passes(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t hea
 template <int NA, int XC = 0>
 static int run_pass64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t Tp, uint32_t base,
                       uint64_t *out, uint64_t *meta, int acc, hipStream_t s, uint64_t *xc = nullptr) {
-    auto kern = ctx->knobs.bsgs64_prio ? k_encode_u64_bsgs_off<NA, XC, 1> : k_encode_u64_bsgs_off<NA, XC, 0>;
+    auto kern = k_encode_u64_bsgs_off<NA, XC, 1>;
     const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
     if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 8 * NA * sizeof(uint64_t), s)) return rc;
     uint64_t *partials = (uint64_t *)ctx->d_scratch;
@@ -821,20 +820,19 @@ static int enc64_passes_chunk(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32
     uint64_t *meta = out + 2 * T;
     // x^(next base) goes from pass to pass through a per-id cache (8 B read +
     // 8 B written per id and pass; pass 0 writes x^80) instead of each offset
-    // pass raising x^8 to base/8 (as enc32_passes; knob u64_xcache).  The
-    // cache follows the partials in the scratch, sized once.
+    // pass raising x^8 to base/8 (as enc32_passes).  The cache follows the
+    // partials in the scratch, sized once.
     const uint32_t npass = (T - 80 + 79) / 80;
     uint64_t *xc = nullptr;
-    if (npass >= 1 && ctx->knobs.u64_xcache) {
+    if (npass >= 1) {
         const uint64_t tiles = (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK;
         const uint32_t nbmax = grid_cap(ctx, tiles, 1);
         const size_t poff = ((size_t)nbmax * 2 * 80 * sizeof(uint64_t) + 255) & ~(size_t)255;
         if (ensure_scratch(ctx, poff + (size_t)n * 8, s) == QK_OK) xc = (uint64_t *)((char *)ctx->d_scratch + poff);
     }
     {   // pass 0: powers 1..80 (+ x^80 per id for pass 1 when the cache is on)
-        const bool f1 = ctx->knobs.bsgs64_prio;
-        auto kern = f1 ? k_encode_u64_bsgs<10, 16, 1> : k_encode_u64_bsgs<10, 16, 0>;
-        auto kx80 = f1 ? k_encode_u64_bsgs_x80<1> : k_encode_u64_bsgs_x80<0>;
+        auto kern = k_encode_u64_bsgs<10, 14, 1>;
+        auto kx80 = k_encode_u64_bsgs_x80<1>;
         const uint32_t nb = grid_for(ctx, kern, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1);
         if (int rc = ensure_scratch(ctx, (size_t)nb * 2 * 80 * sizeof(uint64_t), s)) return rc;
         uint64_t *partials = (uint64_t *)ctx->d_scratch;
@@ -889,7 +887,7 @@ static int enc64_passes_chunk(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32
 constexpr size_t XC_CHUNK64 = (size_t)1 << 27;
 static int enc64_passes(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t head, uint32_t T, uint64_t *out,
                         int acc, hipStream_t s) {
-    if (n <= XC_CHUNK64 || !ctx->knobs.u64_xcache) return enc64_passes_chunk(ctx, ids, n, head, T, out, acc, s);
+    if (n <= XC_CHUNK64) return enc64_passes_chunk(ctx, ids, n, head, T, out, acc, s);
     for (size_t c0 = 0; c0 < n; c0 += XC_CHUNK64) {
         const uint64_t *p = ids + c0;
         const uint32_t hd = (uint32_t)(((16 - ((uintptr_t)p & 15)) & 15) / 8);
@@ -1007,61 +1005,42 @@ static int enc32(qk_ctx *ctx, const uint32_t *ids, size_t n, uint32_t T, uint64_
     // wave sees at most 64 * (4 * trips + 2) wraps per accumulator, so trips
     // must stay < 2^24 - 1 — true for any n < 2^40 at >= 1 workgroup per CU;
     // a tiny override grid over a huge n takes the all-VALU form.
-    // knob bsgs_sg overrides the number of scalar-counted groups
-    // (measurements; tools/tune_bsgs.hip).
-    const int sg_env = ctx->knobs.bsgs_sg;
     const uint64_t min_grid = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
     const bool sc_ok = n / (4ull * BLOCK * min_grid) < (1ull << 24) - 2;
-    auto sg = [&](int dflt) { return sc_ok ? (sg_env >= 0 ? sg_env : dflt) : 0; };
-    const int prio = ctx->knobs.bsgs_prio;
-#define QK_BSGS_P(NB_, NA_, G_, P_)                                                                          \
-    run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_, P_>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
-                         (n + 3) / 4, BLOCK, out, acc, s, NB_ * NA_ > 48 ? 1 : 0)
 #define QK_BSGS(NB_, NA_, G_)                                                                                 \
-    (prio ? QK_BSGS_P(NB_, NA_, G_, 1) : QK_BSGS_P(NB_, NA_, G_, 0))
-    if (T >= 5 && T <= 8 && sg(1)) return QK_BSGS(4, 2, 1);
-    if (T >= 9 && T <= 12) return sg(3) ? QK_BSGS(4, 3, 3) : QK_BSGS(4, 3, 0);
-    if (T >= 13 && T <= 16) return sg(4) ? QK_BSGS(4, 4, 4) : QK_BSGS(4, 4, 0);
-    // Round-3 shapes (knob bsgs_shapes = 0: the round-2 ones): the (NB, NA)
-    // with the fewest issue cycles for the powers actually needed — modmuls
-    // NB - 1 + NA - 2 at ~17 cycles, MACs NB (NA - 1) and row-0 adds NB at
-    // ~4.2, measured: 17..28 four babies and ceil(T / 4)
-    // giant rows (every group 4 wide, scalar-counted; (6,4) / (8,4) computed
-    // 24 / 32 powers), 29..30 (6,5), 33..36 (6,6), 41..42 (6,7), 65..72 (8,9)
-    const bool r3 = ctx->knobs.bsgs_shapes;
-    if (r3 && T >= 17 && T <= 20 && sg(5)) return QK_BSGS(4, 5, 5);
-    if (r3 && T >= 21 && T <= 24 && sg(6)) return QK_BSGS(4, 6, 6);
-    if (r3 && T >= 25 && T <= 28 && sg(7)) return QK_BSGS(4, 7, 7);
-    if (r3 && T >= 29 && T <= 30 && sg(5)) return QK_BSGS(6, 5, 5);
-    if (r3 && T >= 33 && T <= 36 && sg(6)) return QK_BSGS(6, 6, 6);
-    if (r3 && T >= 41 && T <= 42 && sg(7)) return QK_BSGS(6, 7, 7);
-    if (r3 && T >= 65 && T <= 72 && sg(14)) return QK_BSGS(8, 9, 14);
-    if (T >= 17 && T <= 24) return sg(4) ? QK_BSGS(6, 4, 4) : QK_BSGS(6, 4, 0);
-    if (T >= 25 && T <= 32) {
-        switch (sg(QK_BSGS_SG_T32)) {
-        case 0: return QK_BSGS(8, 4, 0);
-        case 1: return QK_BSGS(8, 4, 1);
-        case 2: return QK_BSGS(8, 4, 2);
-        case 3: return QK_BSGS(8, 4, 3);
-        case 4: return QK_BSGS(8, 4, 4);
-        case 5: return QK_BSGS(8, 4, 5);
-        case 6: return QK_BSGS(8, 4, 6);
-        case 7: return QK_BSGS(8, 4, 7);
-        default: return QK_BSGS(8, 4, 8);
-        }
+    run_encode<uint32_t>(ctx, k_encode_u32_bsgs<NB_, NA_, G_, 1>, k_finalize_u32, NB_ * NA_, 1, ids, n, head, T, \
+                         (n + 3) / 4, BLOCK, out, acc, s, NB_ * NA_ > 48 ? 1 : 0)
+    if (T >= 5 && T <= 8 && sc_ok) return QK_BSGS(4, 2, 1);
+    if (T >= 9 && T <= 12) return sc_ok ? QK_BSGS(4, 3, 3) : QK_BSGS(4, 3, 0);
+    if (T >= 13 && T <= 16) return sc_ok ? QK_BSGS(4, 4, 4) : QK_BSGS(4, 4, 0);
+    // Round-3 shapes: the (NB, NA) with the fewest issue cycles for the
+    // powers actually needed — modmuls NB - 1 + NA - 2 at ~17 cycles, MACs
+    // NB (NA - 1) and row-0 adds NB at ~4.2, measured: 17..28
+    // four babies and ceil(T / 4) giant rows (every group 4 wide,
+    // scalar-counted; (6,4) / (8,4) computed 24 / 32 powers), 29..30 (6,5),
+    // 33..36 (6,6), 41..42 (6,7), 65..72 (8,9)
+    if (sc_ok) {
+        if (T >= 17 && T <= 20) return QK_BSGS(4, 5, 5);
+        if (T >= 21 && T <= 24) return QK_BSGS(4, 6, 6);
+        if (T >= 25 && T <= 28) return QK_BSGS(4, 7, 7);
+        if (T >= 29 && T <= 30) return QK_BSGS(6, 5, 5);
+        if (T >= 31 && T <= 32) return QK_BSGS(8, 4, QK_BSGS_SG_T32);
+        if (T >= 33 && T <= 36) return QK_BSGS(6, 6, 6);
+        if (T >= 37 && T <= 40) return QK_BSGS(8, 5, 10);
+        if (T >= 41 && T <= 42) return QK_BSGS(6, 7, 7);
+        if (T >= 43 && T <= 48) return QK_BSGS(8, 6, 12);
+        if (T >= 49 && T <= 56) return QK_BSGS(8, 7, 14);
+        if (T >= 57 && T <= 64) return QK_BSGS(8, 8, 16);
+        if (T >= 65 && T <= 72) return QK_BSGS(8, 9, 14);
+        if (T >= 73 && T <= 80) return QK_BSGS(8, 10, 16);
+        if (T > 80) return enc32_passes(ctx, ids, n, head, T, out, acc, s);
+    } else {
+        // the all-VALU forms that fit the registers; t 33..80 would spill, so
+        // a grid too small for scalar counts takes the power chain there
+        if (T >= 17 && T <= 24) return QK_BSGS(6, 4, 0);
+        if (T >= 25 && T <= 32) return QK_BSGS(8, 4, 0);
     }
-    // t 33..40: one more giant row (118 VGPRs, 4 waves/SIMD); its all-VALU
-    // form would spill, so a grid too small for scalar counts takes the chain
-    if (T >= 33 && T <= 40 && sg(10)) return QK_BSGS(8, 5, 10);
-    if (T >= 41 && T <= 48 && sg(12)) return QK_BSGS(8, 6, 12);
-    if (T >= 49 && T <= 56 && sg(14)) return QK_BSGS(8, 7, 14);
-    if (T >= 57 && T <= 64 && sg(16)) return QK_BSGS(8, 8, 16);
-    if (T >= 65 && T <= 80 && sg(16)) return QK_BSGS(8, 10, 16);
-    // knob u32_passes = 0 keeps t > 80 on the power chain (measurements)
-    const int passes_env = ctx->knobs.u32_passes;
-    if (T > 80 && sg(16) && passes_env) return enc32_passes(ctx, ids, n, head, T, out, acc, s);
 #undef QK_BSGS
-#undef QK_BSGS_P
     int G, K;
     choose_gk(T, 32, K32_G1, 10, K32_GN, 4, G, K);
     switch (G) {
@@ -1082,29 +1061,24 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
     const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / 8);
     // baby-step / giant-step for 14 <= T <= 80 (configs[2] is T = 80; below
     // 14 powers the 8 modmuls of the babies and x^8 cost more than the chain
-    // they save: knob bsgs64_tmin, profiles/r03/shapes/sweep64_tmin_ab.jsonl —
-    // 21 before round 3, BSGS +3..9 % at t = 14..20): NA = ceil(T / 8)
-    // giant rows; its per-wave 32-bit carry totals need < 2^31 ids per
-    // workgroup.  knob bsgs64_sg (T > 72 only) picks a carry mode
-    // for measurements (tools/tune_u64.hip); knob bsgs64_off = 1 forces the
-    // power chain.
-    const int sg64 = ctx->knobs.bsgs64_sg;
-    const int no64 = ctx->knobs.bsgs64_off;
-    const bool f64 = ctx->knobs.bsgs64_prio;   // s_setprio + paired MACs (knob bsgs64_prio)
+    // they save: profiles/r03/shapes/sweep64_tmin_ab.jsonl — 21 before round
+    // 3, BSGS +3..9 % at t = 14..20): NA = ceil(T / 8) giant rows; its
+    // per-wave 32-bit carry totals need < 2^31 ids per workgroup.  Every form
+    // runs with s_setprio around the MACs and paired MACs (F = 1).
     const uint64_t min_grid64 = ctx->grid_override ? ctx->grid_override : (uint64_t)ctx->num_cus;
-    if (T >= (uint32_t)ctx->knobs.bsgs64_tmin && T <= 80 && !no64 && n / min_grid64 < (1ull << 30)) {
+    const bool bsgs_ok = n / min_grid64 < (1ull << 30);
+    if (T >= 14 && T <= 80 && bsgs_ok) {
 #define QK_BSGS64(NA_, SG_)                                                                           \
-    run_encode<uint64_t>(ctx, f64 ? k_encode_u64_bsgs<NA_, SG_, 1> : k_encode_u64_bsgs<NA_, SG_, 0>,         \
-                         k_finalize_u64, 8 * NA_, 2, ids, n, head, T,                                          \
+    run_encode<uint64_t>(ctx, k_encode_u64_bsgs<NA_, SG_, 1>, k_finalize_u64, 8 * NA_, 2, ids, n, head, T,   \
                          (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
 #define QK_BSGS64_4(NA_)                                                                              \
-    run_encode<uint64_t>(ctx, f64 ? k_encode_u64_bsgs4<NA_, 1> : k_encode_u64_bsgs4<NA_, 0>, k_finalize_u64,  \
-                         4 * NA_, 2, ids, n, head, T, (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
-        // four babies per id and ceil(T/4) giant rows (knob bsgs64_shapes)
-        // where 8 babies would compute 4+ powers more: t = 14..20, 25..28,
-        // 33..36 (+8..17 %, profiles/r03/shapes/sweep64_four_babies_ab.jsonl;
-        // at t = 21..24, 29..32 even, at 37..40 7 % slower: not used)
-        if (ctx->knobs.bsgs64_shapes && T <= 36) switch ((T + 3) / 4) {
+    run_encode<uint64_t>(ctx, k_encode_u64_bsgs4<NA_, 1>, k_finalize_u64, 4 * NA_, 2, ids, n, head, T,      \
+                         (n + bsgs64::BLOCK - 1) / bsgs64::BLOCK, 1, out, acc, s)
+        // four babies per id and ceil(T/4) giant rows where 8 babies would
+        // compute 4+ powers more: t = 14..20, 25..28, 33..36 (+8..17 %,
+        // profiles/r03/shapes/sweep64_four_babies_ab.jsonl; at t = 21..24,
+        // 29..32 even, at 37..40 7 % slower: not used)
+        if (T <= 36) switch ((T + 3) / 4) {
             case 4: return QK_BSGS64_4(4);
             case 5: return QK_BSGS64_4(5);
             case 7: return QK_BSGS64_4(7);
@@ -1121,29 +1095,18 @@ static int enc64(qk_ctx *ctx, const uint64_t *ids, size_t n, uint32_t T, uint64_
         case 7: return QK_BSGS64(7, 16);
         case 8: return QK_BSGS64(8, 16);
         case 9: return QK_BSGS64(9, 16);
-        default:
-            // knob bsgs64_sg (measurements): scalar-counted MACs of the 18; the
-            // default 14 with the paired-MAC form (22.65 vs 23.19 ms at 16,
-            // twice, profiles/r04/prio/tune_u64_prio.json), 16 without it
-            switch (sg64 >= 0 ? sg64 : f64 ? 14 : 16) {
-            case 8: return QK_BSGS64(10, 8);
-            case 12: return QK_BSGS64(10, 12);
-            case 14: return QK_BSGS64(10, 14);
-            case 18: return QK_BSGS64(10, 18);
-            default: return QK_BSGS64(10, 16);
-            }
+        // NA = 10: 14 of the 18 MACs scalar-counted with the paired-MAC form
+        // (22.65 vs 23.19 ms at 16, twice, profiles/r04/prio/tune_u64_prio.json)
+        default: return QK_BSGS64(10, 14);
         }
 #undef QK_BSGS64
     }
-    // knob u64_passes = 0 keeps t > 80 on the power chain (measurements)
-    const int passes64 = ctx->knobs.u64_passes;
-    if (T > 80 && !no64 && passes64 && n / min_grid64 < (1ull << 30)) return enc64_passes(ctx, ids, n, head, T, out, acc, s);
+    if (T > 80 && bsgs_ok) return enc64_passes(ctx, ids, n, head, T, out, acc, s);
     int G, K;
     // K <= 40 accumulators per lane (120 VGPRs, 3 waves/SIMD) beat K <= 20 at
     // 5 waves by needing fewer lanes per id (t = 80: 2 x (39 + 1) steps vs
-    // 4 x (19 + 3)); knob u64_kmax overrides for measurements.
-    const int kmax = ctx->knobs.u64_kmax;
-    choose_gk(T, kmax, K64_G1, 10, K64_GN, 6, G, K);
+    // 4 x (19 + 3)).
+    choose_gk(T, 40, K64_G1, 10, K64_GN, 6, G, K);
     switch (G) {
     case 1: return enc64_g<1>(ctx, K, ids, n, head, T, out, acc, s);
     case 2: return enc64_g<2>(ctx, K, ids, n, head, T, out, acc, s);

@@ -137,7 +137,9 @@ __global__ __launch_bounds__(SG_BLOCK) void k_seg_encode(const uint32_t *__restr
 // headline kernel's baby-step/giant-step body (bsgs.h).  All lanes of the
 // workgroup belong to one flow, so the wave-level scalar wrap counts stay
 // valid; the workgroup's sums go to the flow's accumulator row by atomicAdd.
-template <int NB, int NA, int SG, int PRIO>
+// (no s_setprio around the MACs: with it 1e6 flows took 7.57 vs 6.80 ms,
+// profiles/r04/prio/ab_flows_prio.jsonl)
+template <int NB, int NA, int SG>
 __global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 : NB * NA > 40 ? 3 : 4)) void k_seg_bsgs(
     const uint32_t *__restrict__ ids, const SegItem *__restrict__ items, uint32_t T,
     unsigned long long *__restrict__ acc_out) {
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(bsgs::BLOCK, (NB * NA == 32 ? 5 : NB * NA > 64 ? 2 
     const uint32_t *p = ids + it.lo;
     const uint32_t head = (uint32_t)(((16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u) >> 2);   // ids to 16-B alignment
     unsigned long long *row = acc_out + (size_t)it.seg * T;
-    bsgs::body_gen<bsgs::Cfg<NB, NA, SG, 1, 1, false, false, 0, false, PRIO>>(p, it.hi - it.lo, head, T, threadIdx.x,
+    bsgs::body_gen<bsgs::Cfg<NB, NA, SG, 1, 1, false, false, 0, false, 0>>(p, it.hi - it.lo, head, T, threadIdx.x,
                                                                              (uint64_t)bsgs::BLOCK,
                                           [=](uint32_t m, uint64_t s) {
                                               atomicAdd(&row[m], (unsigned long long)fold64_32(s));
@@ -229,18 +231,17 @@ __global__ __launch_bounds__(SG_BLOCK, 4) void k_seg_small(const uint32_t *__res
     }
 }
 
-// per-lane (VALU) wrap counters: SG = 0; P: s_setprio around the MACs
+// per-lane (VALU) wrap counters: SG = 0; no s_setprio
 // where k_seg_small writes (SmallOut: acc rows, or records by rank)
 struct SmallOut {
     uint32_t *rec = nullptr;
     const uint32_t *rseg = nullptr, *lastid = nullptr;
 };
-template <int P>
-static void seg_small_launch_p(uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
-                               unsigned long long *acc, const SmallOut &so, hipStream_t s) {
+static int seg_small_launch(uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
+                            unsigned long long *acc, const SmallOut &so, hipStream_t s) {
     const dim3 grid((nseg + SG_BLOCK - 1) / SG_BLOCK), block(SG_BLOCK);
 #define QK_SMALL(NB_, NA_)                                                                                         \
-    hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<NB_, NA_, 0, 1, 1, false, false, 0, false, P>>), grid, block, 0, s, ids, \
+    hipLaunchKernelGGL((k_seg_small<bsgs::Cfg<NB_, NA_, 0, 1, 1, false, false, 0, false, 0>>), grid, block, 0, s, ids, \
                        d_offs, nseg, T, acc, so.rec, so.rseg, so.lastid)
     if (T <= 8) QK_SMALL(4, 2);
     else if (T <= 12) QK_SMALL(4, 3);
@@ -248,11 +249,6 @@ static void seg_small_launch_p(uint32_t T, const uint32_t *ids, const uint64_t *
     else if (T <= 24) QK_SMALL(6, 4);
     else QK_SMALL(8, 4);
 #undef QK_SMALL
-}
-static int seg_small_launch(int prio, uint32_t T, const uint32_t *ids, const uint64_t *d_offs, uint32_t nseg,
-                            unsigned long long *acc, const SmallOut &so, hipStream_t s) {
-    if (prio) seg_small_launch_p<1>(T, ids, d_offs, nseg, acc, so, s);
-    else seg_small_launch_p<0>(T, ids, d_offs, nseg, acc, so, s);
     return hipGetLastError() == hipSuccess ? QK_OK : QK_E_HIP;
 }
 
@@ -301,17 +297,12 @@ __device__ __forceinline__ uint32_t ft_home(uint64_t src, uint64_t dst, uint32_t
 
 // slot of (src, dst), inserting it if absent (++created when this call made
 // the flow); SLOT_NONE (and a flag) when the probe limit is reached.
-// first: the home slot's entry read earlier (k_flow_extract_pipe issues that
-// read one tile ahead) or null to read it here.  Any earlier read is as good
-// as a fresh one: a nonzero word is final, and a zero word is resolved by
-// the CAS below whatever was written since.
 __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t probe_limit, uint64_t src,
-                                      uint64_t dst, unsigned long long *counters, uint32_t &created,
-                                      const FlowSlot *first = nullptr) {
+                                      uint64_t dst, unsigned long long *counters, uint32_t &created) {
     const uint64_t a0 = ft_w0(src, dst), a1 = ft_w1(dst);
     uint32_t slot = ft_home(src, dst, mask);
     for (uint32_t probe = 0; probe < probe_limit; ++probe, slot = slot + 1 == mask ? 0 : slot + 1) {
-        const FlowSlot e = probe == 0 && first ? *first : tab[slot];   // one 16-byte read: the common cases
+        const FlowSlot e = tab[slot];   // one 16-byte read: the common cases
         if (e.w0 == a0 && e.w1 == a1) return slot;
         if (e.w0 != 0 && (e.w0 != a0 || e.w1 != 0)) continue;
         if (ft_settle(&tab[slot].w0, a0) != a0) continue;
@@ -339,8 +330,15 @@ __device__ uint32_t ft_find_or_insert(FlowSlot *tab, uint32_t mask, uint32_t pro
 // digit (slot & hmask, SLOT_NONE included), digit-major as k_rs_count writes
 // it, added into the sort's chunk (hgroup consecutive extract chunks; hcnt
 // zeroed first): the sort's first pass then reads no keys.
-// NT (knob flow_nt): the records read and the (slot, id) written nontemporal
-template <bool NT>
+// The records are read and the (slot, id) written nontemporal (1e6 flows
+// 6.04 -> 5.93 ms, 16 flows 2.88 -> 2.81 ms, profiles/r05/flows_nt/): the
+// table's lines stay cached instead of being pushed out by the records.
+// Bail: an overflowing pass stops early (it is rerun on a regrown table and
+// its outputs dropped) — a workgroup whose own probe overflowed leaves at its
+// next tile, and every FLOW_BAIL-th tile thread 0 reads the global overflow
+// flag (a load per tile measured 5 % slower; a fresh context's 1e6-flow
+// batch 64.5 -> 7.3 ms, profiles/r05/flows_bail/).
+constexpr uint32_t FLOW_BAIL = 64;
 __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__restrict__ bufs, uint64_t n,
                                                            uint32_t stride, const qk_pkt_meta *__restrict__ meta,
                                                            uint64_t my_key_lo, uint64_t chunk,
@@ -349,7 +347,8 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
                                                            uint32_t *__restrict__ ids,
                                                            unsigned long long *__restrict__ counters,
                                                            uint32_t hmask, uint32_t *__restrict__ hcnt,
-                                                           uint32_t hgroup, uint32_t bail) {
+                                                           uint32_t hgroup) {
+    constexpr bool NT = true;
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
     __shared__ uint32_t l_stop;
     uint32_t since = 0;   // tiles since the last overflow check
@@ -380,10 +379,9 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
     for (uint64_t p0 = c0; p0 < c1; p0 += REC_TILE) {
         const uint64_t np = c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE;
         __syncthreads();   // previous tile fully consumed
-        // bail (knob flow_bail, 0 never): stop once this workgroup's own
-        // probes overflowed, or (flag read every bail-th tile) any other's —
-        // the pass is rerun on a regrown table and its outputs dropped
-        const bool chk = bail && ++since >= bail;   // every bail-th tile (a load per tile measured 5 % slower)
+        // bail: stop once this workgroup's own probes overflowed, or (flag
+        // read every FLOW_BAIL-th tile) any other's
+        const bool chk = ++since >= FLOW_BAIL;
         if (chk) since = 0;
         const uint64_t fl = chk && threadIdx.x == 0
                                 ? __hip_atomic_load(&counters[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -434,19 +432,14 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
             if (lead == threadIdx.x) {
                 const uint32_t sl = ft_find_or_insert(tab, mask, probe_limit, src, dst, counters, n_new);
                 l_slot[threadIdx.x] = sl;
-                if (sl == SLOT_NONE && bail) l_stop = 1;   // this workgroup overflowed: it leaves at the next tile
+                if (sl == SLOT_NONE) l_stop = 1;   // this workgroup overflowed: it leaves at the next tile
             }
         }
         __syncthreads();
         if (valid) {
             const uint32_t sl = cls == 1 ? l_slot[lead] : SLOT_NONE;
-            if constexpr (NT) {
-                __builtin_nontemporal_store(sl, &slots[i]);
-                __builtin_nontemporal_store(id, &ids[i]);
-            } else {
-                slots[i] = sl;
-                ids[i] = id;
-            }
+            __builtin_nontemporal_store(sl, &slots[i]);
+            __builtin_nontemporal_store(id, &ids[i]);
             if (hcnt) atomicAdd(&l_hist[sl & hmask], 1u);
         }
         n_ins += cls == 1;   // summed once per workgroup below (no per-tile barrier count)
@@ -462,152 +455,6 @@ __global__ __launch_bounds__(REC_TILE) void k_flow_extract(const uint8_t *__rest
             if (l_hist[j]) atomicAdd(&hcnt[(size_t)j * ((gridDim.x + hgroup - 1) / hgroup) + blockIdx.x / hgroup], l_hist[j]);
     // one atomic per workgroup (a per-packet atomic on one address
     // serialises: 1.2 s per 1e8 packets)
-    if (threadIdx.x == 0) {
-        if (l_ins) atomicAdd(&counters[0], l_ins);
-        if (l_rsts) atomicAdd(&counters[1], l_rsts);
-        if (l_new) atomicAdd(&counters[2], (unsigned long long)l_new);
-        if (l_rst) atomicMax(&counters[4], l_rst);
-    }
-}
-
-// k_flow_extract with the table probes one tile behind (knob flow_pipe): a
-// leader issues its home slot's read right after its tile's election and
-// resolves it (hit, or the probe / CAS loop) during the NEXT tile's
-// iteration, after that tile's records are classified and elected, so the
-// read's latency (a random line of a table far larger than L2 at 1e6 flows)
-// overlaps a tile of other work instead of stalling its own.  Outputs (slot,
-// id, the fused histogram) are written one iteration late; l_slot is double
-// buffered.  Same arguments and results as k_flow_extract.
-template <bool NT>
-__global__ __launch_bounds__(REC_TILE) void k_flow_extract_pipe(const uint8_t *__restrict__ bufs, uint64_t n,
-                                                                uint32_t stride, const qk_pkt_meta *__restrict__ meta,
-                                                                uint64_t my_key_lo, uint64_t chunk,
-                                                                FlowSlot *__restrict__ tab, uint32_t mask,
-                                                                uint32_t probe_limit, uint32_t *__restrict__ slots,
-                                                                uint32_t *__restrict__ ids,
-                                                                unsigned long long *__restrict__ counters,
-                                                                uint32_t hmask, uint32_t *__restrict__ hcnt,
-                                                           uint32_t hgroup, uint32_t bail) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
-    __shared__ uint32_t l_stop;
-    uint32_t since = 0;   // tiles since the last overflow check
-    if (threadIdx.x == 0) l_stop = 0;   // (read only after the loop's first barrier)
-    __shared__ uint32_t l_hist[rsort::R];
-    if (hcnt)
-        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE) l_hist[j] = 0;
-    constexpr uint32_t LH = 2 * REC_TILE;                // LDS election table
-    __shared__ uint64_t l_src[REC_TILE], l_dst[REC_TILE];
-    __shared__ uint32_t l_lead[LH];
-    __shared__ uint32_t l_slot[2][REC_TILE];
-    const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
-    const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
-    uint32_t n_ins = 0, n_rst = 0;
-    __shared__ unsigned long long l_ins, l_rsts, l_rst;
-    __shared__ uint32_t l_new;
-    if (threadIdx.x == 0) { l_ins = l_rsts = l_rst = 0; l_new = 0; }
-    uint64_t my_rst = 0;
-    uint32_t n_new = 0;
-    const bool pipe = stage_pipelined(stride, REC_TILE);
-    TileStage st;
-    if (pipe && c0 < c1) stage_issue<NT>(bufs, n, stride, c0, c1 - c0 < (uint64_t)REC_TILE ? c1 - c0 : REC_TILE, st);
-    // the previous tile's state: its packet, and for its leaders the key and
-    // the home slot's entry in flight
-    bool pv_valid = false, pv_leader = false;
-    uint64_t pv_i = 0, pv_src = 0, pv_dst = 0;
-    uint32_t pv_id = 0, pv_lead = SLOT_NONE;
-    FlowSlot pv_e{0, 0};
-    uint32_t buf = 0;   // l_slot buffer of the current tile
-    for (uint64_t p0 = c0;; p0 += REC_TILE) {
-        const bool have = p0 < c1;   // a tile this iteration (else: drain the previous one)
-        const uint64_t np = have ? (c1 - p0 < (uint64_t)REC_TILE ? c1 - p0 : (uint64_t)REC_TILE) : 0;
-        __syncthreads();   // the previous election's LDS reads are done
-        const bool chk = bail && ++since >= bail;
-        if (chk) since = 0;
-        const uint64_t fl = chk && threadIdx.x == 0
-                                ? __hip_atomic_load(&counters[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : 0ull;
-        uint32_t r0 = 0;
-        if (have) {
-            r0 = pipe ? stage_commit(bufs, n, stride, st, tile) : stage_records<NT>(bufs, n, stride, p0, np, tile);
-            for (uint32_t h = threadIdx.x; h < LH; h += REC_TILE) l_lead[h] = SLOT_NONE;
-        }
-        if (fl & FT_OVERFLOW) l_stop = 1;
-        __syncthreads();
-        if (l_stop) break;   // as k_flow_extract's bail (the pending outputs are dropped with the pass)
-        bool valid = false, leader = false;
-        uint64_t i = p0 + threadIdx.x, src = 0, dst = 0;
-        uint32_t id = 0, lead = SLOT_NONE;
-        FlowSlot e{0, 0};
-        if (have) {
-            if (pipe && p0 + REC_TILE < c1)
-                stage_issue<NT>(bufs, n, stride, p0 + REC_TILE,
-                            c1 - p0 - REC_TILE < (uint64_t)REC_TILE ? c1 - p0 - REC_TILE : REC_TILE, st);
-            valid = threadIdx.x < np;
-            const uint8_t *rec = tile + r0 + threadIdx.x * stride;
-            int cls = 0;
-            const qk_pkt_meta m = valid ? record_meta<NT>(meta, i) : qk_pkt_meta{};
-            if (valid && record_is_incoming_udp(m, rec)) {
-                src = ((uint64_t)rec[26] << 40) | ((uint64_t)rec[27] << 32) | ((uint64_t)rec[28] << 24) |
-                      ((uint64_t)rec[29] << 16) | ((uint64_t)rec[34] << 8) | (uint64_t)rec[35];
-                dst = ((uint64_t)rec[30] << 40) | ((uint64_t)rec[31] << 32) | ((uint64_t)rec[32] << 24) |
-                      ((uint64_t)rec[33] << 16) | ((uint64_t)rec[36] << 8) | (uint64_t)rec[37];
-                if (dst == my_key_lo) {
-                    cls = 2;
-                    my_rst = i + 1;
-                } else if (m.len == QK_BUFFER_SIZE) {
-                    cls = 1;
-                    id = record_identifier(rec);
-                }
-            }
-            n_ins += cls == 1;
-            n_rst += cls == 2;
-            l_src[threadIdx.x] = src;
-            l_dst[threadIdx.x] = dst;
-            __syncthreads();
-            if (cls == 1) {
-                uint32_t h = ft_hash(src, dst) & (LH - 1);
-                for (;;) {   // at most REC_TILE claims in LH slots: terminates
-                    const uint32_t o = atomicCAS(&l_lead[h], SLOT_NONE, threadIdx.x);
-                    if (o == SLOT_NONE) { lead = threadIdx.x; break; }
-                    if (l_src[o] == src && l_dst[o] == dst) { lead = o; break; }
-                    h = (h + 1) & (LH - 1);
-                }
-                leader = lead == threadIdx.x;
-                if (leader) e = tab[ft_home(src, dst, mask)];   // resolved next iteration
-            }
-        }
-        // the previous tile's leaders resolve their slots (its read has landed)
-        if (pv_leader) {
-            const uint32_t sl = ft_find_or_insert(tab, mask, probe_limit, pv_src, pv_dst, counters, n_new, &pv_e);
-            l_slot[buf ^ 1][threadIdx.x] = sl;
-            if (sl == SLOT_NONE && bail) l_stop = 1;
-        }
-        __syncthreads();
-        if (pv_valid) {
-            const uint32_t sl = pv_lead != SLOT_NONE ? l_slot[buf ^ 1][pv_lead] : SLOT_NONE;
-            slots[pv_i] = sl;
-            ids[pv_i] = pv_id;
-            if (hcnt) atomicAdd(&l_hist[sl & hmask], 1u);
-        }
-        if (!have) break;
-        pv_valid = valid;
-        pv_leader = leader;
-        pv_i = i;
-        pv_src = src;
-        pv_dst = dst;
-        pv_id = id;
-        pv_lead = lead;
-        pv_e = e;
-        buf ^= 1;
-    }
-    if (n_new) atomicAdd(&l_new, n_new);
-    if (my_rst) atomicMax(&l_rst, (unsigned long long)my_rst);
-    if (n_ins) atomicAdd(&l_ins, (unsigned long long)n_ins);
-    if (n_rst) atomicAdd(&l_rsts, (unsigned long long)n_rst);
-    __syncthreads();
-    if (hcnt)
-        for (uint32_t j = threadIdx.x; j < rsort::R; j += REC_TILE)
-            if (l_hist[j]) atomicAdd(&hcnt[(size_t)j * ((gridDim.x + hgroup - 1) / hgroup) + blockIdx.x / hgroup], l_hist[j]);
     if (threadIdx.x == 0) {
         if (l_ins) atomicAdd(&counters[0], l_ins);
         if (l_rsts) atomicAdd(&counters[1], l_rsts);
@@ -776,19 +623,16 @@ __global__ void k_rank_perm(const FlowSlot *__restrict__ tab, const uint32_t *__
 // packet index, so nothing depends on it.
 constexpr uint32_t HIST_MAX = 8192;   // slots (LDS counters per workgroup: 32 KB)
 
-// nt: the per-packet arrays read nontemporal (knob flow_rs_nt bit 0, as the
-// grouping sort's scatters)
-__device__ __forceinline__ uint4 ld_u4(const uint32_t *p, uint32_t nt) {
-    if (nt) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-        return make_uint4(x.x, x.y, x.z, x.w);
-    }
-    return *reinterpret_cast<const uint4 *>(p);
+// the per-packet arrays read nontemporal (read once, as the grouping sort's
+// scatters read theirs)
+__device__ __forceinline__ uint4 ld_u4(const uint32_t *p) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
 }
 __global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__ slots, uint64_t n, uint64_t chunk,
                                                     uint32_t C, uint32_t nwg, uint32_t *__restrict__ hist,
-                                                    uint32_t *__restrict__ last, uint32_t nt) {
+                                                    uint32_t *__restrict__ last) {
     extern __shared__ uint32_t lh[];   // C counts, C last indices (+1)
     uint32_t *lc = lh, *ll = lh + C;
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) { lc[j] = 0; ll[j] = 0; }
@@ -805,7 +649,7 @@ __global__ __launch_bounds__(256) void k_hist_count(const uint32_t *__restrict__
     const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
     const int lane = threadIdx.x & 63;
     for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
-        const uint4 sv = ld_u4(slots + i, nt);
+        const uint4 sv = ld_u4(slots + i);
         // a wave whose packets all hold one slot (one flow, or a skewed
         // batch) adds them with one LDS atomic instead of 256 on one counter
         const uint32_t s0 = __builtin_amdgcn_readfirstlane(sv.x);
@@ -835,7 +679,7 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ ids, uint64_t n, uint64_t chunk,
                                                       uint32_t C, uint32_t nwg, const uint32_t *__restrict__ base,
                                                       const uint32_t *__restrict__ spre,
-                                                      uint32_t *__restrict__ grouped, uint32_t nt) {
+                                                      uint32_t *__restrict__ grouped) {
     extern __shared__ uint32_t lc[];   // C running counts
     for (uint32_t j = threadIdx.x; j < C; j += blockDim.x) lc[j] = 0;
     __syncthreads();
@@ -849,8 +693,8 @@ __global__ __launch_bounds__(256) void k_hist_scatter(const uint32_t *__restrict
     const uint64_t v1 = c0 + ((c1 - c0) & ~(uint64_t)3);
     const int lane = threadIdx.x & 63;
     for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
-        const uint4 sv = ld_u4(slots + i, nt);
-        const uint4 iv = ld_u4(ids + i, nt);
+        const uint4 sv = ld_u4(slots + i);
+        const uint4 iv = ld_u4(ids + i);
         // one slot across the wave (as k_hist_count): one LDS atomic reserves
         // the wave's places, each lane takes four in lane order
         const uint32_t s0 = __builtin_amdgcn_readfirstlane(sv.x);
@@ -1055,26 +899,27 @@ static std::vector<SegItem> seg_items(const std::vector<uint64_t> &offs, uint32_
 
 // Segmented encode of a grouped id array: the small flows by k_seg_small
 // (d_offs: the nseg + 1 offsets on the device) into accumulator rows or
-// records (so), the rest by the work items from seg_items (d_items holds
-// items.size() entries) into the accumulator rows item.seg of d_acc (u64,
-// acc_rows rows, zeroed here).
+// records (so), the rest by the work items from seg_items into the
+// accumulator rows item.seg of d_acc (u64, acc_rows rows, zeroed here).  The
+// items go to the kernels through the context's pinned item buffer, read in
+// place over the bus (one 24-byte item per workgroup), not by an H2D copy.
 // small_done: the caller already launched k_seg_small (before it waited
 // for the work-item list)
 static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs,
                       const std::vector<SegItem> &items, size_t nseg, uint32_t T, unsigned long long *d_acc,
-                      size_t acc_rows, SegItem *d_items, const SmallOut &so, hipStream_t s, bool small_done = false) {
+                      size_t acc_rows, const SmallOut &so, hipStream_t s, bool small_done = false) {
     if (acc_rows) QK_HIP_TRY(hipMemsetAsync(d_acc, 0, acc_rows * T * sizeof(uint64_t), s));
     if (small_ok(T) && nseg && !small_done) {
         hipEvent_t e0 = prof_begin(ctx, s);
-        const int rs = seg_small_launch(ctx->knobs.flow_prio, T, d_ids, d_offs, (uint32_t)nseg, d_acc, so, s);
+        const int rs = seg_small_launch(T, d_ids, d_offs, (uint32_t)nseg, d_acc, so, s);
         prof_end(ctx, s, e0);
         if (rs) return rs;
     }
-    // the caller's host offsets / items vectors must outlive their async copies
+    // the caller's host offsets vector must outlive its async copy
     if (items.empty()) return hipStreamSynchronize(s) == hipSuccess ? QK_OK : QK_E_HIP;
-    int rc = QK_OK;
-    if (hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(SegItem), hipMemcpyHostToDevice, s) != hipSuccess)
-        rc = QK_E_HIP;
+    int rc = ensure_items(ctx, items.size() * sizeof(SegItem));
+    const SegItem *d_items = (const SegItem *)ctx->h_items_dev;
+    if (!rc) memcpy(ctx->h_items, items.data(), items.size() * sizeof(SegItem));
     if (!rc) {
         int G, K;
         seg_choose(T, G, K);
@@ -1082,10 +927,8 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
         hipEvent_t e0 = prof_begin(ctx, s);
         const dim3 grid(ni), block(bsgs::BLOCK);
         if (T >= 5 && T <= 80) {   // same configurations as the headline encode
-            const bool fp = ctx->knobs.flow_prio;   // s_setprio around the MACs (knob flow_prio)
 #define QK_SEGB(NB_, NA_, SG_)                                                                                     \
-    hipLaunchKernelGGL((fp ? k_seg_bsgs<NB_, NA_, SG_, 1> : k_seg_bsgs<NB_, NA_, SG_, 0>), grid, block, 0, s, d_ids, \
-                       d_items, T, d_acc)
+    hipLaunchKernelGGL((k_seg_bsgs<NB_, NA_, SG_>), grid, block, 0, s, d_ids, d_items, T, d_acc)
             if (T <= 8) QK_SEGB(4, 2, 1);
             else if (T <= 12) QK_SEGB(4, 3, 3);
             else if (T <= 16) QK_SEGB(4, 4, 4);
@@ -1112,7 +955,7 @@ static int seg_encode(qk_ctx *ctx, const uint32_t *d_ids, const uint64_t *d_offs
         }
         prof_end(ctx, s, e0);
     }
-    // the host vector `items` must outlive the async copy
+    // the pinned items must outlive the kernels
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = QK_E_HIP;
     return rc;
 }
@@ -1145,18 +988,16 @@ extern "C" int qk_u32_encode_segments_device(qk_ctx *ctx, const uint32_t *d_ids,
     const std::vector<SegItem> items = seg_items(offs, T);
     Carve probe{nullptr};
     probe.take<unsigned long long>(nseg * T);
-    probe.take<SegItem>(items.size());
     probe.take<uint32_t>(nseg);
     probe.take<uint64_t>(nseg + 1);
     if (int e = ensure_flow(ctx, 1, probe.off, s)) return e;
     Carve cv{(char *)ctx->d_flow[1]};
     unsigned long long *d_acc = cv.take<unsigned long long>(nseg * T);
-    SegItem *d_items = cv.take<SegItem>(items.size());
     uint32_t *d_last = cv.take<uint32_t>(nseg);
     uint64_t *d_offs = cv.take<uint64_t>(nseg + 1);
     int rc = QK_OK;
     if (hipMemcpyAsync(d_offs, offs.data(), (nseg + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess) rc = QK_E_HIP;
-    if (!rc) rc = seg_encode(ctx, d_ids, d_offs, items, nseg, T, d_acc, nseg, d_items, SmallOut{}, s);
+    if (!rc) rc = seg_encode(ctx, d_ids, d_offs, items, nseg, T, d_acc, nseg, SmallOut{}, s);
     std::vector<uint64_t> acc(nseg * T);
     std::vector<uint32_t> last(nseg, 0);
     if (!rc && hipMemcpyAsync(acc.data(), d_acc, acc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -1199,9 +1040,9 @@ struct RsScratch {
     uint32_t *cnt, *base, *tot;
     uint8_t *dig;
     template <class Carver> void take(Carver &c, uint32_t nwg, uint64_t n) {
-        cnt = c.template take<uint32_t>((size_t)rsort::RMAX * nwg);
-        base = c.template take<uint32_t>((size_t)rsort::RMAX * nwg);
-        tot = c.template take<uint32_t>(rsort::RMAX);
+        cnt = c.template take<uint32_t>((size_t)rsort::R * nwg);
+        base = c.template take<uint32_t>((size_t)rsort::R * nwg);
+        tot = c.template take<uint32_t>(rsort::R);
         dig = c.template take<uint8_t>(n + 16);
     }
 };
@@ -1209,21 +1050,23 @@ struct RsScratch {
 // ping-ponging between region X = (k0, v0) and region Y = (k1, v1); each
 // region must also hold n (key, value) pairs from k0 / k1 (arena layout: the
 // value array follows the key array).  The first pass reads two arrays, the
-// last writes two, the passes between use pair arrays (knob flow_sort 2, 3;
-// 1: two arrays throughout).  Returns in `where` the region holding the
-// result: 1 = Y, 0 = X (an even number of passes).
+// last writes two, the passes between use pair arrays.  Every scatter writes
+// the next pass's digit as a byte beside each item, so the later passes
+// count 1 byte per item (k_rs_count8) instead of 8.  Returns in `where` the
+// region holding the result: 1 = Y, 0 = X (an even number of passes).
 // plan: the chunking to use instead of rs_plan's (pre0: sc.cnt already holds
 // the first pass's counts for it — k_flow_extract's fused histogram; the
-// scratch must hold RMAX x plan->nwg counts)
-template <int D, int BLK, int K, bool PAIRS, uint32_t WGPC, bool DIRECT = false>
+// scratch must hold R x plan->nwg counts)
+template <int BLK, int K, uint32_t WGPC>
 static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, uint64_t n, int bits,
                      const RsScratch &sc, hipStream_t s, int &where, const RsPlan *plan = nullptr, bool pre0 = false) {
     static_assert(WGPC <= RS_WGPC_MAX, "scratch is sized for RS_WGPC_MAX");
+    constexpr int D = rsort::DBITS;
     where = 0;
     if (n == 0 || bits <= 0) return QK_OK;
     const RsPlan pl0 = plan ? *plan : rs_plan(ctx, n, WGPC);
     // the digit byte stream needs 16-item chunks (k_rs_count8's loads)
-    const RsPlan pl = D == 8 ? RsPlan{pl0.nwg, (pl0.chunk + 15) & ~(uint64_t)15} : pl0;
+    const RsPlan pl = RsPlan{pl0.nwg, (pl0.chunk + 15) & ~(uint64_t)15};
     const int passes = (bits + D - 1) / D;
     const int dd = (bits + passes - 1) / passes;   // the digit width actually used (<= D): balanced passes
     uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
@@ -1231,29 +1074,25 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
         const uint32_t shift = (uint32_t)(q * dd);
         const int left = bits - q * dd;
         const uint32_t mask = left >= dd ? (1u << dd) - 1 : (1u << left) - 1;
-        const bool ip = PAIRS && q > 0, op = PAIRS && q + 1 < passes;
-        auto count = ip ? rsort::k_rs_count<D, true> : rsort::k_rs_count<D, false>;
-        if (D == 8 && q > 0 && ctx->knobs.flow_nd)   // the previous scatter wrote this pass's digits as bytes
+        const bool ip = q > 0, op = q + 1 < passes;
+        if (q > 0)   // the previous scatter wrote this pass's digits as bytes
             hipLaunchKernelGGL(rsort::k_rs_count8, dim3(pl.nwg), dim3(256), 0, s, sc.dig, n, pl.chunk, pl.nwg, sc.cnt);
-        else if (!(pre0 && q == 0))
-            hipLaunchKernelGGL(count, dim3(pl.nwg), dim3(256), 0, s, ki, n, pl.chunk, shift, mask, pl.nwg, sc.cnt);
+        else if (!pre0)
+            hipLaunchKernelGGL(rsort::k_rs_count, dim3(pl.nwg), dim3(256), 0, s, ki, n, pl.chunk, shift, mask, pl.nwg,
+                               sc.cnt);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
         // digit-major counts -> each digit's chunk prefixes + the digit totals
         // (the scatter scans the totals itself)
         hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3(1u << D), dim3(256), 0, s, sc.cnt, pl.nwg, sc.base, sc.tot);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
-        auto kern = ip ? (op ? rsort::k_rs_scatter<D, BLK, K, true, true, DIRECT>
-                             : rsort::k_rs_scatter<D, BLK, K, true, false, DIRECT>)
-                       : (op ? rsort::k_rs_scatter<D, BLK, K, false, true, DIRECT>
-                             : rsort::k_rs_scatter<D, BLK, K, false, false, DIRECT>);
-        // the next pass's digit as a byte beside each item (8-bit digits)
-        const bool nd = D == 8 && q + 1 < passes && ctx->knobs.flow_nd;
+        auto kern = ip ? (op ? rsort::k_rs_scatter<D, BLK, K, true, true> : rsort::k_rs_scatter<D, BLK, K, true, false>)
+                       : (op ? rsort::k_rs_scatter<D, BLK, K, false, true> : rsort::k_rs_scatter<D, BLK, K, false, false>);
+        // the next pass's digit as a byte beside each item
         const uint32_t nshift = (uint32_t)((q + 1) * dd);
         const int nleft = bits - (q + 1) * dd;
         const uint32_t nmask = nleft >= dd ? (1u << dd) - 1 : (1u << (nleft > 0 ? nleft : 0)) - 1;
         hipLaunchKernelGGL(kern, dim3(pl.nwg), dim3(BLK), 0, s, ki, vi, n, pl.chunk, shift, mask, pl.nwg, sc.base,
-                           sc.tot, ko, vo, nd ? sc.dig : (uint8_t *)nullptr, nshift, nmask,
-                           (uint32_t)ctx->knobs.flow_rs_nt);
+                           sc.tot, ko, vo, op ? sc.dig : (uint8_t *)nullptr, nshift, nmask);
         if (hipGetLastError() != hipSuccess) return QK_E_HIP;
         std::swap(ki, ko);
         std::swap(vi, vo);
@@ -1261,37 +1100,20 @@ static int rs_sort_k(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1
     where = passes % 2;
     return QK_OK;
 }
-// the digit width of the knob-selected variant (flow_sort 5, 6, 8, 9: 11 bits)
-static int rs_digit_bits(const qk_ctx *ctx) {
-    const int m = ctx->knobs.flow_sort;
-    return m == 5 || m == 6 || m == 8 || m == 9 ? 11 : 8;
-}
+// the grouping sort: 256 threads x 16 items per sub-tile, 4 workgroups per CU
 static int rs_sort(const qk_ctx *ctx, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1, uint64_t n, int bits,
                    const RsScratch &sc, hipStream_t s, int &where, const RsPlan *plan = nullptr, bool pre0 = false) {
-#define QK_RS(D, BLK, K, PAIRS, WGPC, ...)                                                              \
-    return rs_sort_k<D, BLK, K, PAIRS, WGPC, ##__VA_ARGS__>(ctx, k0, v0, k1, v1, n, bits, sc, s, where, plan, \
-                                                           pre0 && D == 8)
-    switch (ctx->knobs.flow_sort) {
-    case 1: QK_RS(8, 256, 16, false, 4);
-    case 2: QK_RS(8, 256, 16, true, 4);
-    case 3: QK_RS(8, 512, 16, true, 2);
-    case 4: QK_RS(8, 1024, 16, true, 1);
-    case 5: QK_RS(11, 512, 16, true, 1);
-    case 6: QK_RS(11, 1024, 8, true, 1);
-    case 7: QK_RS(8, 256, 16, true, 4, true);
-    case 8: QK_RS(11, 512, 16, true, 1, true);
-    default: QK_RS(11, 1024, 8, true, 1, true);
-    }
-#undef QK_RS
+    return rs_sort_k<256, 16, 4>(ctx, k0, v0, k1, v1, n, bits, sc, s, where, plan, pre0);
 }
 
 // k_flow_extract's chunking of pn packets: >= 4 tiles per workgroup, enough
-// workgroups to cover the chip (knob flow_wgpc: workgroups per CU; 4, 6, 8,
-// 12 measured, 12 best at 1e4 and 1e6 flows).  With the fused first-digit
+// workgroups to cover the chip (FLOW_WGPC workgroups per CU; 4, 6, 8, 12
+// measured, 12 best at 1e4 and 1e6 flows).  With the fused first-digit
 // histogram the grouping sort keeps this chunking (RsPlan).
+constexpr uint32_t FLOW_WGPC = 12;
 static RsPlan extract_plan(const qk_ctx *ctx, uint64_t pn) {
     const uint64_t ntiles = (pn + REC_TILE - 1) / REC_TILE;
-    const uint64_t wg = (uint64_t)ctx->num_cus * (uint64_t)ctx->knobs.flow_wgpc;
+    const uint64_t wg = (uint64_t)ctx->num_cus * FLOW_WGPC;
     const uint64_t chunk = std::max<uint64_t>(4, (ntiles + wg - 1) / wg) * REC_TILE;
     return {(uint32_t)std::max<uint64_t>(1, (pn + chunk - 1) / chunk), chunk};
 }
@@ -1325,8 +1147,9 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     // Arena 2: the flow table (C slots) and slot -> rank.  Arena 1, per flow:
     // see below.
     const uint64_t cmax = std::min<uint64_t>(next_pow2(2 * (uint64_t)n + 2), 1ull << 31);
-    // table slots per expected flow (knob flow_load, [2, 64], for measurements)
-    const uint64_t spf = (uint64_t)ctx->knobs.flow_load;
+    // table slots per expected flow (2 / 8 measured slower at 1e6 / 1e4 flows,
+    // profiles/r02/s3/flows_load/, profiles/r05/flows_nd/)
+    const uint64_t spf = 4;
     uint64_t C = std::min<uint64_t>(cmax, next_pow2(std::max<uint64_t>(4096, spf * (uint64_t)ctx->flow_hint)));
     // the grouping sort's chunk counts: its own plan's, or the extract's
     const uint32_t rs_nwg = std::max(rs_plan(ctx, n, RS_WGPC_MAX).nwg, extract_plan(ctx, n).nwg);
@@ -1358,18 +1181,10 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     // the grouping sort's chunks when the extract counts its first digit: hg
     // consecutive extract chunks each (~RS_WGPC_MAX workgroups per CU: the
     // scatter's LDS allows 4; the extract's 12 per CU measured slower)
-    const uint32_t hg = std::max<uint32_t>(1, ((uint32_t)ctx->knobs.flow_wgpc + RS_WGPC_MAX - 1) / RS_WGPC_MAX);
+    const uint32_t hg = (FLOW_WGPC + RS_WGPC_MAX - 1) / RS_WGPC_MAX;
     auto sort_plan = [&]() { return RsPlan{(xpl.nwg + hg - 1) / hg, xpl.chunk * hg}; };
-    const bool fuse0 = rs_digit_bits(ctx) == 8 && ctx->knobs.flow_fuse0;   // the extract writes the sort's first counts
-    // speculation (knob flow_spec): the by-slot grouping sort of the pass's
-    // packets is enqueued right behind the extract, before the host has read
-    // the extract's counters (so the GPU does not idle through that round
-    // trip).  Valid when the pass ends the batch (no table regrow, no reset
-    // after it) and the table is above the histogram grouping's size — the
-    // grouping then uses it as is, by slot; otherwise the next extract (same
-    // stream) starts over and the sorted copies are simply overwritten.
-    bool spec = false;
-    int spec_where = 0;
+    // the extract writes the by-slot sort's first-digit counts (1e6 flows
+    // 6.71 -> 6.61 ms, profiles/r05/check4/ab_fuse0.log)
     auto pass1 = [&](uint64_t p_from) -> int {
         const uint64_t pn = n - p_from;
         const uint8_t *pb = d_bufs + p_from * stride;
@@ -1387,35 +1202,23 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             }
             if (hipMemsetAsync(tab, 0, C * sizeof(FlowSlot), s) != hipSuccess ||
                 hipMemsetAsync(counters, 0, 5 * 8, s) != hipSuccess ||
-                (fuse0 && hipMemsetAsync(rs.cnt, 0, (size_t)rsort::R * sort_plan().nwg * 4, s) != hipSuccess))
+                hipMemsetAsync(rs.cnt, 0, (size_t)rsort::R * sort_plan().nwg * 4, s) != hipSuccess)
                 return QK_E_HIP;
             const uint32_t probe_limit = C == cmax ? (uint32_t)C - 1 : 64u;   // load <= 1/4 when sized from the hint
             // the by-slot sort's first digit (8-bit variants): its passes and
             // width as rs_sort_k cuts bits(C - 1)
             const int cb = bit_width32((uint32_t)(C - 1)), np = (cb + 7) / 8, dd = (cb + np - 1) / np;
             if (pn)
-                hipLaunchKernelGGL(ctx->knobs.flow_pipe ? (ctx->knobs.flow_nt ? k_flow_extract_pipe<true> : k_flow_extract_pipe<false>)
-                                                        : (ctx->knobs.flow_nt ? k_flow_extract<true> : k_flow_extract<false>),
-                                   dim3(xpl.nwg),
-                                   dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
+                hipLaunchKernelGGL(k_flow_extract, dim3(xpl.nwg), dim3(REC_TILE), (size_t)REC_TILE * stride + 32, s,
                                    pb, pn, (uint32_t)stride, pm, my_key, xpl.chunk, tab, (uint32_t)(C - 1), probe_limit,
-                                   slots, ids, counters, (1u << dd) - 1, fuse0 ? rs.cnt : (uint32_t *)nullptr, hg,
-                                   (uint32_t)ctx->knobs.flow_bail);
+                                   slots, ids, counters, (1u << dd) - 1, rs.cnt, hg);
             // the counters into pinned memory (an async copy to pageable memory
             // would hold the host until the extract ends); flow_ev[0]: the
-            // table is complete (the key-ranking branch waits for it, not for
-            // a speculated sort behind it)
+            // table is complete (the key-ranking branch waits for it)
             if (hipGetLastError() != hipSuccess ||
                 hipMemcpyAsync(ctx->h_flow, counters, 40, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipEventRecord(ctx->flow_ev[2], s) != hipSuccess || hipEventRecord(ctx->flow_ev[0], s) != hipSuccess)
                 return QK_E_HIP;
-            spec = ctx->knobs.flow_spec && pn && !(C <= HIST_MAX && ctx->knobs.flow_hist > 0);
-            if (spec) {
-                const RsPlan spl = sort_plan();
-                const int e = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, pn, cb, rs, s, spec_where, &spl, true)
-                                    : rs_sort(ctx, slots, ids, key_s, id_s, pn, cb, rs, s, spec_where);
-                if (e) return e;
-            }
             if (hipEventSynchronize(ctx->flow_ev[2]) != hipSuccess) return QK_E_HIP;
             std::copy(ctx->h_flow, ctx->h_flow + 5, hc);
             if (!(hc[3] & FT_OVERFLOW)) return QK_OK;
@@ -1446,13 +1249,10 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     const bool dev_out = keys && sketches && is_device_ptr(keys);
     if (!rc && keys && sketches && dev_out != is_device_ptr(sketches)) rc = QK_E_INVAL;
     if (!rc && nf) {
-        // per-flow arena 1: the work-item accumulator rows and items (at most
-        // one per flow plus one per SEG_CHUNK ids), output records and keys,
-        // offsets, and the flow-key sort buffers
-        const size_t items_max = (size_t)nf + inserted / SEG_CHUNK + 1;
+        // per-flow arena 1: the work-item accumulator rows, output records
+        // and keys, offsets, and the flow-key sort buffers
         const size_t rec = qk_u32_size(T);
         uint64_t *d_offs = nullptr;
-        SegItem *d_items = nullptr;
         uint32_t *d_rec = nullptr, *used = nullptr, *sl3 = nullptr, *nsel = nullptr, *rseg = nullptr;
         uint32_t *kA = nullptr, *vA = nullptr, *kB = nullptr, *vB = nullptr, *wcnt = nullptr, *lastid = nullptr;
         SegItem *big = nullptr;
@@ -1461,7 +1261,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         // most knob flow_hist flows: above a few dozen flows every workgroup
         // scatters into that many runs and the radix sort is faster,
         // profiles/r05/flows_hist/)
-        const bool hist = !spec && C <= HIST_MAX && nf <= (uint32_t)ctx->knobs.flow_hist;
+        const bool hist = C <= HIST_MAX && nf <= (uint32_t)ctx->knobs.flow_hist;
         const uint32_t hnwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->num_cus * 4,
                                                                                   (n_eff + 4095) / 4096));
         const uint64_t hchunk = ((n_eff + hnwg - 1) / hnwg + 3) & ~(uint64_t)3;   // a multiple of 4 (16-byte reads)
@@ -1485,7 +1285,6 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             // them for t <= 32; every flow for t > 32), row j = list entry j
             acc = c.take<unsigned long long>((size_t)(small_ok(T) ? std::min<uint64_t>(nf, inserted / (SMALL_SEG + 1))
                                                                    : nf) * T);
-            d_items = c.take<SegItem>(items_max);
             d_rec = dev_out ? (uint32_t *)sketches : (uint32_t *)c.take<uint8_t>((size_t)nf * rec);
             d_keys = dev_out ? (uint8_t *)keys : c.take<uint8_t>((size_t)nf * 12);
             d_offs = c.take<uint64_t>((size_t)nf + 1);
@@ -1527,18 +1326,15 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         //     their host launch time).  Otherwise by rank (slot -> rank remap
         //     per packet, bit_width(flows) bits), which waits for s2 first.
         const int fbits = bit_width32(nf), cbits = bit_width32((uint32_t)(C - 1));
-        // (a speculated sort is by slot: always a valid grouping)
         // By rank costs a remap pass over the packets (k_slot_to_rank) and the
         // wait for s2 before the sort, ~one sort pass and more: it is taken
         // when it saves two passes, or leaves one (knob flow_byslot: 0 this
         // rule, 1 by slot, 2 by rank; profiles/r05/flows_byslot/)
         const int sp = (cbits + 7) / 8, rp = (fbits + 7) / 8;
-        const bool by_slot = spec || (ctx->knobs.flow_byslot == 0 ? !(sp >= rp + 2 || (rp <= 1 && sp > 1))
-                                                                  : ctx->knobs.flow_byslot == 1);
+        const bool by_slot = ctx->knobs.flow_byslot == 0 ? !(sp >= rp + 2 || (rp <= 1 && sp > 1))
+                                                         : ctx->knobs.flow_byslot == 1;
         const uint32_t ob = (uint32_t)std::min<uint64_t>((inserted + 255) / 256, (uint64_t)ctx->num_cus * 8);
-        hipStream_t s2 = ctx->knobs.flow_side_lo && s != ctx->side_stream ? ctx->side_stream
-                         : s == ctx->copy_stream                          ? ctx->stream
-                                                                          : ctx->copy_stream;
+        hipStream_t s2 = s == ctx->copy_stream ? ctx->stream : ctx->copy_stream;
         if (!rc && hipStreamWaitEvent(s2, ctx->flow_ev[0], 0) != hipSuccess)   // (recorded behind the last extract)
             rc = QK_E_HIP;
         auto side = [&]() -> int {
@@ -1559,7 +1355,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                                        q ? (uint32_t *)nullptr : vA);
                     if (hipGetLastError() != hipSuccess) return QK_E_HIP;
                     int where = 1;
-                    if (int e = rs_sort_k<8, 256, 16, true, RS_WGPC_MAX>(ctx, kA, vA, kB, vB, nf, 32, krs, s2, where))
+                    if (int e = rs_sort_k<256, 16, RS_WGPC_MAX>(ctx, kA, vA, kB, vB, nf, 32, krs, s2, where))
                         return e;
                     if (where != 0) return QK_E_HIP;   // four passes: the result is back in (kA, vA)
                 }
@@ -1580,14 +1376,13 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 hipMemsetAsync(hlast, 0, (size_t)C * 4, s) != hipSuccess)
                 rc = QK_E_HIP;
             if (!rc) {
-                const uint32_t hnt = (uint32_t)ctx->knobs.flow_rs_nt & 1u;
                 hipLaunchKernelGGL(k_hist_count, dim3(hnwg), dim3(256), (size_t)C * 8, s, slots, n_eff, hchunk, (uint32_t)C,
-                                   hnwg, hcnt, hlast, hnt);
+                                   hnwg, hcnt, hlast);
                 // slot-major counts -> each slot's workgroup prefixes, then the slots' prefix
                 hipLaunchKernelGGL(rsort::k_row_scan<256>, dim3((uint32_t)C), dim3(256), 0, s, hcnt, hnwg, hpre, htot);
                 hipLaunchKernelGGL(rsort::k_tot_scan<1024>, dim3(1), dim3(1024), 0, s, htot, (uint32_t)C, hspre);
                 hipLaunchKernelGGL(k_hist_scatter, dim3(hnwg), dim3(256), (size_t)C * 4, s, slots, ids, n_eff, hchunk,
-                                   (uint32_t)C, hnwg, hpre, hspre, id_s, hnt);
+                                   (uint32_t)C, hnwg, hpre, hspre, id_s);
                 if (hipGetLastError() != hipSuccess) rc = QK_E_HIP;
             }
             if (!rc) rc = side();
@@ -1601,11 +1396,9 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
             // the grouping sort (radix.h); with the extract's fused histogram
             // its first pass reads no keys and every pass keeps the extract's
             // chunking
-            int where = spec_where;
+            int where = 0;
             const RsPlan spl = sort_plan();
-            if (!spec)
-                rc = fuse0 ? rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where, &spl, true)
-                           : rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where);
+            rc = rs_sort(ctx, slots, ids, key_s, id_s, n_eff, cbits, rs, s, where, &spl, true);
             if (!rc && where == 0) {   // even number of passes: the result is in (slots, ids)
                 std::swap(slots, key_s);
                 std::swap(ids, id_s);
@@ -1649,7 +1442,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
         const bool small_first = small_ok(T) && nf;
         if (!rc && small_first) {
             hipEvent_t e0 = prof_begin(ctx, s);
-            rc = seg_small_launch(ctx->knobs.flow_prio, T, id_s, d_offs, nf, acc, so, s);
+            rc = seg_small_launch(T, id_s, d_offs, nf, acc, so, s);
             prof_end(ctx, s, e0);
         }
         // only the flows that need work items come back to the host (none
@@ -1673,8 +1466,7 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
                 rc = QK_E_HIP;
         }
         if (!rc)
-            rc = seg_encode(ctx, id_s, d_offs, seg_items_from_big(bigs), nf, T, acc, hsel[1], d_items, so, s,
-                            small_first);
+            rc = seg_encode(ctx, id_s, d_offs, seg_items_from_big(bigs), nf, T, acc, hsel[1], so, s, small_first);
         if (!rc && hsel[1]) {
             const uint32_t fb = (uint32_t)std::min<uint64_t>(((uint64_t)hsel[1] * (4 + T) + 255) / 256,
                                                              (uint64_t)ctx->num_cus * 16);
@@ -1689,7 +1481,6 @@ extern "C" int qk_u32_encode_flows_device(qk_ctx *ctx, const uint8_t *d_bufs, si
     }
     (void)hipStreamSynchronize(s); // the arenas are reused by the next call
     (void)hipStreamSynchronize(s == ctx->copy_stream ? ctx->stream : ctx->copy_stream);   // the flow-key branch
-    if (s != ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
     if (stats) *stats = st;
     return rc;
 }

@@ -40,6 +40,7 @@ namespace qk {
 QK_WARM_KERNEL(packets)
 
 constexpr int PK_BLOCK = REC_TILE;
+constexpr uint64_t PK_WGPC = 4;   // workgroups per CU
 
 struct ChunkStat {       // per workgroup chunk, written by lane 0
     int64_t last_reset;  // absolute packet index of the last reset in the chunk, -1 if none
@@ -189,10 +190,10 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     QK_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = pick_stream(ctx, stream);
 
-    // chunking: >= 4 tiles per workgroup, pkt_wgpc workgroups per CU (each
+    // chunking: >= 4 tiles per workgroup, PK_WGPC workgroups per CU (each
     // keeps one staged tile of loads in flight)
     const uint64_t tiles = (n + PK_BLOCK - 1) / PK_BLOCK;
-    const uint64_t wgs = (uint64_t)ctx->num_cus * (uint64_t)ctx->knobs.pkt_wgpc;
+    const uint64_t wgs = (uint64_t)ctx->num_cus * PK_WGPC;
     uint64_t tiles_per_chunk = std::max<uint64_t>(4, (tiles + wgs - 1) / wgs);
     const uint64_t chunk = tiles_per_chunk * PK_BLOCK;
     const uint32_t nchunks = (uint32_t)((n + chunk - 1) / chunk);
@@ -213,16 +214,13 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     // occupancy (182 VGPRs at t = 32, 2 waves/SIMD) below what the record
     // stream needs — measured per 1e8 records, fused vs two-pass: t = 12
     // 1.40 vs 1.68 ms, 16 1.89 vs 1.69, 24 1.95 vs 1.75, 32 2.06 vs 1.81.
-    const int fused_env = ctx->knobs.pkt_fused;   // knob pkt_fused (measurements)
-    if (fused_env && t >= 5 && t <= 12) {
+    if (t >= 5 && t <= 12) {
         int frc = QK_OK;
         if (int e = ensure_scratch(ctx, (size_t)nchunks * 32 * sizeof(uint64_t), s)) return e;
         if (int e = scratch_acquire(ctx, s)) return e;
         uint64_t *partials = (uint64_t *)ctx->d_scratch;
 #define QK_PKT_FUSED(NB_, NA_, SG_)                                                                          \
-    hipLaunchKernelGGL((ctx->knobs.pkt_nt ? k_pkt_kernel<bsgs::Cfg<NB_, NA_, SG_>, true>                          \
-                                          : k_pkt_kernel<bsgs::Cfg<NB_, NA_, SG_>, false>),                       \
-                       dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs,                                                \
+    hipLaunchKernelGGL((k_pkt_kernel<bsgs::Cfg<NB_, NA_, SG_>, true>), dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs,                                                \
                        (uint64_t)n, (uint32_t)stride, d_meta, my_ip_le, check_reset, chunk, (uint32_t *)nullptr,   \
                        d_stats, t, partials)
         hipEvent_t e0 = prof_begin(ctx, s);
@@ -266,7 +264,9 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
         }
         // a reset in the batch: the exact path
     }
-    auto kx = ctx->knobs.pkt_nt ? k_pkt_kernel<NoEncode, true> : k_pkt_kernel<NoEncode, false>;
+    // records read nontemporal (t = 32, 1e8 records: 1.83-1.84 -> 1.74-1.76
+    // ms, profiles/r05/packets_nt/)
+    auto kx = k_pkt_kernel<NoEncode, true>;
     hipLaunchKernelGGL(kx, dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs, (uint64_t)n,
                        (uint32_t)stride, d_meta, my_ip_le, check_reset, chunk, d_ids, d_stats, 0u,
                        (uint64_t *)nullptr);

@@ -37,42 +37,31 @@
 namespace qk {
 namespace rsort {
 
-constexpr int DBITS = 8;                  // the default digit width
+constexpr int DBITS = 8;                  // the digit width
 constexpr uint32_t R = 1u << DBITS;
-constexpr uint32_t RMAX = 1u << 11;       // the widest digit (scratch sizing)
 
-// chunk is a multiple of 4 and keys is 16-byte aligned (arena buffers).  IP:
-// the input is an array of (key, value) pairs instead of a key array.
-template <int D, bool IP>
+// The first pass's chunk histograms from the key array (the later passes
+// count from the digit bytes, k_rs_count8; the per-flow batch's by-slot sort
+// has its first pass counted by k_flow_extract).  chunk is a multiple of 4
+// and keys is 16-byte aligned (arena buffers).
 __global__ __launch_bounds__(256) void k_rs_count(const uint32_t *__restrict__ keys, uint64_t n, uint64_t chunk,
                                                   uint32_t shift, uint32_t mask, uint32_t nwg,
                                                   uint32_t *__restrict__ cnt) {
-    constexpr uint32_t RD = 1u << D;
-    __shared__ uint32_t h[RD];
-    for (uint32_t j = threadIdx.x; j < RD; j += blockDim.x) h[j] = 0;
+    __shared__ uint32_t h[R];
+    for (uint32_t j = threadIdx.x; j < R; j += blockDim.x) h[j] = 0;
     __syncthreads();
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
-    if constexpr (IP) {   // two pairs per 16-byte load
-        const uint64_t v1 = c0 < c1 ? c0 + ((c1 - c0) & ~(uint64_t)1) : c0;
-        for (uint64_t i = c0 + 2 * threadIdx.x; i < v1; i += 2 * blockDim.x) {
-            const uint4 k = *reinterpret_cast<const uint4 *>(keys + 2 * i);
-            atomicAdd(&h[(k.x >> shift) & mask], 1u);
-            atomicAdd(&h[(k.z >> shift) & mask], 1u);
-        }
-        for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) atomicAdd(&h[(keys[2 * i] >> shift) & mask], 1u);
-    } else {
-        const uint64_t v1 = c0 < c1 ? c0 + ((c1 - c0) & ~(uint64_t)3) : c0;
-        for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
-            const uint4 k = *reinterpret_cast<const uint4 *>(keys + i);
-            atomicAdd(&h[(k.x >> shift) & mask], 1u);
-            atomicAdd(&h[(k.y >> shift) & mask], 1u);
-            atomicAdd(&h[(k.z >> shift) & mask], 1u);
-            atomicAdd(&h[(k.w >> shift) & mask], 1u);
-        }
-        for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
+    const uint64_t v1 = c0 < c1 ? c0 + ((c1 - c0) & ~(uint64_t)3) : c0;
+    for (uint64_t i = c0 + 4 * threadIdx.x; i < v1; i += 4 * blockDim.x) {
+        const uint4 k = *reinterpret_cast<const uint4 *>(keys + i);
+        atomicAdd(&h[(k.x >> shift) & mask], 1u);
+        atomicAdd(&h[(k.y >> shift) & mask], 1u);
+        atomicAdd(&h[(k.z >> shift) & mask], 1u);
+        atomicAdd(&h[(k.w >> shift) & mask], 1u);
     }
+    for (uint64_t i = v1 + threadIdx.x; i < c1; i += blockDim.x) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < RD; j += blockDim.x) cnt[(size_t)j * nwg + blockIdx.x] = h[j];
+    for (uint32_t j = threadIdx.x; j < R; j += blockDim.x) cnt[(size_t)j * nwg + blockIdx.x] = h[j];
 }
 
 // the same histogram from a byte per item: the digit the previous pass's
@@ -182,21 +171,23 @@ __global__ __launch_bounds__(BLK) void k_tot_scan(const uint32_t *__restrict__ t
 // D: digit bits; BLK threads; K items per thread and sub-tile.  IP / OP:
 // input / output as one array of (key, value) pairs (keys / keys_out then
 // point at it; vals / vals_out are unused) instead of two arrays — the passes
-// between the first and the last: one 8-byte store per item.
-// DIRECT: no LDS staging — every item goes straight from its lane to its
-// output position (wc then holds the global position of wave w's first item
-// of each digit).  nd_out != null: also the item's next digit
-// ((key >> nshift) & nmask, < 256) as a byte at its output position, for the
-// next pass's k_rs_count8.
-template <int D, int BLK, int K, bool IP, bool OP, bool DIRECT = false>
+// between the first and the last: one 8-byte store per item.  The input is
+// read nontemporal (read once; the scattered output runs keep L2 for write
+// combining: 1e6 flows 6.16 -> 6.02 ms, nontemporal stores +15 %,
+// profiles/r05/flows_nt/ab_rsnt.jsonl).  (Round 4-5 variants measured and
+// removed: a direct scatter without LDS staging, 11-bit digits with 512 /
+// 1024 threads, two arrays throughout, 8 and 24 items per thread; DESIGN
+// §3.6.)  nd_out != null: also the item's next digit ((key >> nshift) &
+// nmask, < 256) as a byte at its output position, for the next pass's
+// k_rs_count8.
+template <int D, int BLK, int K, bool IP, bool OP>
 __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__ keys,
                                                     const uint32_t *__restrict__ vals, uint64_t n, uint64_t chunk,
                                                     uint32_t shift, uint32_t mask, uint32_t nwg,
                                                     const uint32_t *__restrict__ base,
                                                     const uint32_t *__restrict__ dtot,
                                                     uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out,
-                                                    uint8_t *__restrict__ nd_out = nullptr, uint32_t nshift = 0,
-                                                    uint32_t nmask = 0, uint32_t nt = 0) {
+                                                    uint8_t *__restrict__ nd_out, uint32_t nshift, uint32_t nmask) {
     constexpr uint32_t RD = 1u << D, TILE = BLK * K;
     constexpr int NW = BLK / 64;
     constexpr int DPT = RD >= (uint32_t)BLK ? RD / BLK : 1;   // digits per thread in the per-digit steps
@@ -204,13 +195,13 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
     static_assert(RD % BLK == 0 || BLK % RD == 0, "digits over threads");
     // counts and staged places stay below TILE <= 2^16: 16-bit when the
     // 32-bit table would not fit beside the staging area
-    using WT = std::conditional_t<(NW * RD * 4 > 65536 && !DIRECT), uint16_t, uint32_t>;
+    using WT = std::conditional_t<(NW * RD * 4 > 65536), uint16_t, uint32_t>;
     static_assert(TILE <= 65536 || sizeof(WT) == 4, "16-bit wave counters");
     __shared__ WT wc[NW][RD];         // per wave: running digit counts, then the staged place of its first item
     __shared__ uint32_t dl[RD];       // output position of the sub-tile's run start of the digit, minus its
                                       // staged start (dst = dl[d] + staged index)
     __shared__ uint32_t ws[NW];
-    __shared__ uint2 stage[DIRECT ? 1 : TILE];
+    __shared__ uint2 stage[TILE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
     // this thread's digits: tid * DPT .. + DPT (when RD < BLK: digit tid, threads past RD idle)
@@ -240,21 +231,14 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint64_t p = wbase + (uint64_t)k * 64 + lane;
-            // nt bit 0: the pass's input read nontemporal (read once; the
-            // scattered output runs keep L2 for write combining)
-            if (nt & 1) {
-                if constexpr (IP) {
-                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                    const u32x2 x = p < c1 ? __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(keys) + p)
-                                           : u32x2{0u, 0u};
-                    it[k] = make_uint2(x.x, x.y);
-                } else {
-                    it[k] = p < c1 ? make_uint2(__builtin_nontemporal_load(keys + p), __builtin_nontemporal_load(vals + p))
-                                   : make_uint2(0u, 0u);
-                }
+            if constexpr (IP) {
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 x = p < c1 ? __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(keys) + p)
+                                       : u32x2{0u, 0u};
+                it[k] = make_uint2(x.x, x.y);
             } else {
-                if constexpr (IP) it[k] = p < c1 ? reinterpret_cast<const uint2 *>(keys)[p] : make_uint2(0u, 0u);
-                else it[k] = p < c1 ? make_uint2(keys[p], vals[p]) : make_uint2(0u, 0u);
+                it[k] = p < c1 ? make_uint2(__builtin_nontemporal_load(keys + p), __builtin_nontemporal_load(vals + p))
+                               : make_uint2(0u, 0u);
             }
         }
 #pragma unroll
@@ -298,7 +282,7 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
             const uint32_t d = (uint32_t)tid * DPT + j;
             if (dth) {
                 dl[d] = gp[j] - ls;
-                uint32_t a = DIRECT ? gp[j] : ls;
+                uint32_t a = ls;
 #pragma unroll
                 for (int w = 0; w < NW; ++w) {
                     wc[w][d] = (WT)a;
@@ -308,40 +292,16 @@ __global__ __launch_bounds__(BLK) void k_rs_scatter(const uint32_t *__restrict__
             ls += tot[j];
         }
         __syncthreads();
-        if constexpr (DIRECT) {
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (dg[k] != NOD) {
-                    const uint32_t dst = (uint32_t)wc[wave][dg[k]] + pw[k];
-                    if constexpr (OP) {
-                        reinterpret_cast<uint2 *>(keys_out)[dst] = it[k];
-                    } else {
-                        keys_out[dst] = it[k].x;
-                        vals_out[dst] = it[k].y;
-                    }
-                    if (nd_out) nd_out[dst] = (uint8_t)((it[k].x >> nshift) & nmask);
-                }
-            nsub = 0;   // (nothing staged)
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (dg[k] != NOD) stage[wc[wave][dg[k]] + pw[k]] = it[k];
-        }
+        for (int k = 0; k < K; ++k)
+            if (dg[k] != NOD) stage[wc[wave][dg[k]] + pw[k]] = it[k];
         __syncthreads();
         // out in staged order: consecutive lanes write consecutive positions
         // of a digit's run
         for (uint32_t i = tid; i < nsub; i += BLK) {
             const uint2 v = stage[i];
             const uint32_t dst = dl[(v.x >> shift) & mask] + i;
-            if (nt & 2) {   // nt bit 1: the output written nontemporal
-                if constexpr (OP) {
-                    __builtin_nontemporal_store(v.x, keys_out + 2 * (size_t)dst);
-                    __builtin_nontemporal_store(v.y, keys_out + 2 * (size_t)dst + 1);
-                } else {
-                    __builtin_nontemporal_store(v.x, keys_out + dst);
-                    __builtin_nontemporal_store(v.y, vals_out + dst);
-                }
-            } else if constexpr (OP) {
+            if constexpr (OP) {
                 reinterpret_cast<uint2 *>(keys_out)[dst] = v;
             } else {
                 keys_out[dst] = v.x;

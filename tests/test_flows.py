@@ -237,31 +237,31 @@ def test_gpu_flows_edge_keys_and_table_growth():
 @pytest.mark.gpu
 def test_gpu_flows_regrow_bail():
     """A batch of 60 000 flows on a fresh context (table from 4096 slots):
-    the overflowing passes stop early (knob flow_bail; 0 = finish every
-    pass) and the batch reruns on regrown tables; the records must be the
-    oracle's and byte for byte the no-bail path's, also with resets (the
-    rerun after the last reset) and with the pipelined extract."""
+    the overflowing passes stop early (k_flow_extract's bail: a workgroup
+    whose probe overflowed leaves, the others read the flag every 64th tile)
+    and the batch reruns on regrown tables; the records must be the oracle's,
+    also with resets (the rerun after the last reset), and byte for byte the
+    records of the next batch on the same context (its table sized from this
+    one's flows: no regrow)."""
     import torch
     from sidekick_amd.quack import Context, encode_flows
     bufs, meta = make_flows(400_000, 60_000, seed=77, p_reset=0.0005, reset_until=0.3)
     want, nres, _ = vector_flows(bufs, meta)
     d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
     d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
-    recs = {}
-    for bail, pipe in ((64, 0), (0, 0), (1, 0), (64, 1)):
-        ctx = Context(0)
-        ctx.set_knob("flow_bail", bail)
-        ctx.set_knob("flow_pipe", pipe)
+    ctx = Context(0)
+    recs = []
+    for call in range(2):
         keys, qs, st = encode_flows(d_bufs, 16, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
         assert st["resets"] == nres and keys == sorted(want)
-        if bail == 64 and pipe == 0:
+        if call == 0:
             for k, q in zip(keys, qs):
                 ids = want[k]
                 assert q.count() == len(ids) and q.last_value() == ids[-1], k.hex()
                 assert q.power_sums() == coracle.encode_u32(np.array(ids, dtype=np.uint32), 16), k.hex()
-        recs[(bail, pipe)] = [bytes(q._buf.raw) for q in qs]
-        ctx.close()
-    assert all(r == recs[(64, 0)] for r in recs.values())
+        recs.append([bytes(q._buf.raw) for q in qs])
+    ctx.close()
+    assert recs[0] == recs[1]
 
 
 @pytest.mark.gpu
@@ -402,24 +402,19 @@ def test_gpu_flows_device_resident_output(nflows):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nflows,skew,p_reset,hist", [(80_000, False, 0.002, 1), (120_000, True, 0.0, 1),
+@pytest.mark.parametrize("nflows,skew,p_reset,hist", [(80_000, False, 0.002, 32), (120_000, True, 0.0, 32),
                                                        (80_000, False, 0.0, 0)])
 def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
     """More than 65 536 flows over 1e6 records: the flow table has > 2^16
-    slots, so the default grouping sort (radix.h, knob flow_sort = 2) runs
-    three digit passes — key/value arrays in, the pair array in and out in
-    the middle pass, arrays out (sidekick_multi.rs:65-90's per-flow map for a
-    batch).  Against the literal sniff loop's tables: every flow's sums,
-    count and last_value, in ascending key order; the records must equal the
-    two-array sort's (flow_sort = 1), the direct-scatter sort's (7), the
-    11-bit sort's (5, two passes) and the unfused first pass's (flow_fuse0 =
-    0: the extract's chunk histogram off), the pipelined extract's
-    (flow_pipe = 1: table reads one tile ahead), the plain-load extract's
-    (flow_nt = 0), the plain-load scatters' (flow_rs_nt = 0) and the
-    nontemporal-store scatters' (flow_rs_nt = 3) and the key-ranking branch
-    on the lowest-priority stream (flow_side_lo = 1) and the speculated
-    grouping sort (flow_spec = 1) byte for byte; flow_hist on and off (the table is above its few-flow size, so both
-    take the sort)."""
+    slots, so the grouping sort (radix.h) runs three digit passes — key/value
+    arrays in (the first pass's counts fused into the extract), the pair
+    array in and out in the middle pass, arrays out (sidekick_multi.rs:65-90's
+    per-flow map for a batch).  Against the literal sniff loop's tables:
+    every flow's sums, count and last_value, in ascending key order; the
+    records of both grouping keys (knob flow_byslot 1 / 2: by slot, three
+    passes; by flow rank after the slot -> rank remap) must equal the rule's
+    byte for byte.  flow_hist at its default (32 flows) and 0 (never): the
+    table is above the few-flow size, so both take the sort."""
     import torch
     from sidekick_amd.quack import Context, encode_flows
     bufs, meta = make_flows(1_000_000, nflows, seed=nflows + int(skew), p_reset=p_reset, skew=skew,
@@ -429,27 +424,18 @@ def test_gpu_flows_three_pass_grouping_sort(nflows, skew, p_reset, hist):
     d_bufs = torch.from_numpy(bufs.reshape(-1).copy()).cuda()
     d_meta = torch.from_numpy(meta.view(np.int64).copy()).cuda()
     recs = {}
-    for mode, fuse0, pipe, nt, rsnt, side in ((2, 1, 0, 1, 1, 0), (1, 1, 0, 1, 1, 0), (7, 1, 0, 1, 1, 0),
-                                              (2, 0, 0, 1, 1, 0), (5, 1, 0, 1, 1, 0), (2, 1, 1, 1, 1, 0),
-                                              (2, 1, 0, 0, 1, 0), (2, 1, 0, 1, 0, 0), (2, 1, 0, 1, 3, 0),
-                                              (2, 1, 0, 1, 1, 1), (2, 1, 0, 1, 1, 2)):
+    for byslot in (0, 1, 2):
         ctx = Context(0)
         ctx.set_knob("flow_hist", hist)
-        ctx.set_knob("flow_sort", mode)
-        ctx.set_knob("flow_fuse0", fuse0)
-        ctx.set_knob("flow_pipe", pipe)
-        ctx.set_knob("flow_nt", nt)
-        ctx.set_knob("flow_rs_nt", rsnt)
-        ctx.set_knob("flow_side_lo", side & 1)
-        ctx.set_knob("flow_spec", side >> 1)
+        ctx.set_knob("flow_byslot", byslot)
         keys, qs, st = encode_flows(d_bufs, 32, meta=d_meta, my_addr=MY_ADDR, ctx=ctx)
         assert st["resets"] == nres and st["inserted"] == sum(len(v) for v in want.values())
         assert keys == sorted(want)
-        recs[(mode, fuse0, pipe, nt, rsnt, side)] = [bytes(q._buf.raw) for q in qs]
-        if (mode, fuse0, pipe, nt, rsnt, side) == (2, 1, 0, 1, 1, 0):
+        recs[byslot] = [bytes(q._buf.raw) for q in qs]
+        if byslot == 0:
             for k, q in zip(keys, qs):
                 ids = want[k]
                 assert q.count() == len(ids) and q.last_value() == ids[-1], k.hex()
                 assert q.power_sums() == coracle.encode_u32(np.array(ids, dtype=np.uint32), 32), k.hex()
         ctx.close()
-    assert all(r == recs[(2, 1, 0, 1, 1, 0)] for r in recs.values())
+    assert recs[1] == recs[0] and recs[2] == recs[0]

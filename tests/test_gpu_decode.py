@@ -24,19 +24,17 @@ def QT(bits):
     return sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
 
 
-@pytest.fixture(autouse=True, params=["horner", "scan", "scan_copies"])
+@pytest.fixture(autouse=True, params=["horner", "scan", "auto"])
 def root_test_mode(request):
     """Every test of this module runs three times: the root test by Horner
     per candidate (k_root_test_*), by host root finding + the root-set scan
     (roots.cpp, k_root_scan; forced for 2 <= d <= 256) handing its results
-    over through pinned host slots (the default), and the same scan with its
-    results copied back (knob rt_direct = 0): the same hit lists."""
+    over through pinned host slots, and as the cost model picks (the
+    default): the same hit lists."""
     ctx = sk.get_context(0)
-    ctx.set_knob("root_test", 1 if request.param == "horner" else 2)
-    ctx.set_knob("rt_direct", 0 if request.param == "scan_copies" else 1)
+    ctx.set_knob("root_test", {"horner": 1, "scan": 2, "auto": 0}[request.param])
     yield request.param
     ctx.set_knob("root_test", 0)
-    ctx.set_knob("rt_direct", 1)
 
 
 def _poly_mul(a, b, p):
@@ -258,29 +256,20 @@ def test_hit_and_stop_slot_boundaries(nhit):
     assert q.root_test_shard(c, dev(log2), stop_value=stop_value) == (want, int(spos[0]))
 
 
-@pytest.mark.parametrize("u,nt", [(2, 1), (4, 1), (1, 0), (2, 0)])
-def test_scan_loads_per_iteration(u, nt, root_test_mode):
-    """The root-set scan with 2 / 4 loads per lane per iteration (knob
-    rt_scan_u, measurements; the product takes 1) and with nontemporal loads
-    (knob rt_scan_nt, the product's; 0 = plain loads): ragged length, a
-    misaligned start, both widths, against the oracle."""
-    import sidekick_amd as skm
-    ctx = skm.get_context(0)
-    ctx.set_knob("rt_scan_u", u)
-    ctx.set_knob("rt_scan_nt", nt)
-    try:
-        for bits in (32, 64):
-            log = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(90 + u + bits, 100_007)
-            q = QT(bits)(16)
-            for i in (0, 1, 777, 23_456, 100_006):
-                q.insert(int(log[i]))
-            c = q.to_coeffs()
-            d = dev(log, bits)[1:]
-            want = qo.root_test_indices(list(c), log[1:].tolist(), qo.P32 if bits == 32 else qo.P64)
-            assert q.root_test(c, d) == want
-    finally:
-        ctx.set_knob("rt_scan_u", 1)
-        ctx.set_knob("rt_scan_nt", 1)
+@pytest.mark.parametrize("off,n", [(1, 100_007), (2, 100_000), (3, 5), (0, 17)])
+def test_scan_ragged_and_misaligned(off, n, root_test_mode):
+    """The root test over a log starting 0-3 entries past a 16-byte boundary
+    with ragged lengths (head, body of 16-byte loads, tail), both widths,
+    against the oracle."""
+    for bits in (32, 64):
+        log = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(90 + off + bits, n + off)
+        q = QT(bits)(16)
+        for i in sorted({0, 1, n // 7, n // 2, n - 1}):
+            q.insert(int(log[off + i]))
+        c = q.to_coeffs()
+        d = dev(log, bits)[off:]
+        want = qo.root_test_indices(list(c), log[off:].tolist(), qo.P32 if bits == 32 else qo.P64)
+        assert q.root_test(c, d) == want
 
 
 def test_undecodable_and_empty():

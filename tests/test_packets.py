@@ -152,28 +152,20 @@ def test_gpu_packets_fused_thresholds(golden, t):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wgpc,nt", [(1, 1), (12, 1), (4, 0)])
-def test_gpu_packets_workgroups_per_cu(wgpc, nt):
-    """The chunking by knob pkt_wgpc (measurements; 4 is the product's):
-    fewer or more chunks give the same sums, counts and reset bookkeeping,
-    fused (t = 12) and two-pass (t = 32), with resets; and the plain-load
-    record staging (knob pkt_nt = 0; the product's loads are nontemporal)."""
+@pytest.mark.parametrize("n", [1, 255, 257, 4097, 300_007, 1_500_013])
+def test_gpu_packets_chunk_edges(n):
+    """Batch sizes around the chunking (one record; a partial tile; one tile
+    and one record; many chunks of 4+ tiles): the same sums, counts and reset
+    bookkeeping as the literal loop, fused (t = 12) and two-pass (t = 32),
+    with and without a reset."""
     import torch
     import sidekick_amd as sk
     from sidekick_amd.quack import encode_packets
-    ctx = sk.get_context(0)
-    ctx.set_knob("pkt_wgpc", wgpc)
-    ctx.set_knob("pkt_nt", nt)
-    try:
-        for t, resets in ((12, ()), (32, (77_777,)), (32, ())):
-            n = 300_007
-            bufs, meta = make_batch(n, seed=wgpc * 100 + t + nt, reset_at=resets, p_filter=0.05)
-            q = sk.PowerSumQuackU32(t)
-            st = encode_packets(q, torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
-                                meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_ipv4=MY_IP)
-            ids, last = vector_sniff(bufs, meta)
-            assert q.power_sums() == coracle.encode_u32(ids, t), (wgpc, t, resets)
-            assert st["inserted"] == len(ids) and st["last_reset_index"] == last
-    finally:
-        ctx.set_knob("pkt_wgpc", 4)
-        ctx.set_knob("pkt_nt", 1)
+    for t, resets in ((12, ()), (32, (n // 3,)), (32, ())):
+        bufs, meta = make_batch(n, seed=n % 1000 + t, reset_at=resets, p_filter=0.05)
+        q = sk.PowerSumQuackU32(t)
+        st = encode_packets(q, torch.from_numpy(bufs.reshape(-1).copy()).cuda(), stride=67,
+                            meta=torch.from_numpy(meta.view(np.int64).copy()).cuda(), my_ipv4=MY_IP)
+        ids, last = vector_sniff(bufs, meta)
+        assert q.power_sums() == coracle.encode_u32(ids, t), (n, t, resets)
+        assert st["inserted"] == len(ids) and st["last_reset_index"] == last

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Same-process A/B of an encode knob (default bsgs_prio): per threshold the
+"""Same-process A/B of an encode knob (default grid_mult): per threshold the
 knob values alternate for several rounds over the same device-resident ids,
 each value's partial sums must equal the first value's, and the median
 kernel time per encode (the context's profiled launches) is reported.
 
-    python tools/ab_encode.py [--knob bsgs_prio] [--values 1,0] [--bits 32]
+    python tools/ab_encode.py [--knob grid_mult] [--values 3,1] [--bits 32]
                               [--t 8,16,20,32,40,64,80] [--n 2.5e8] [--rounds 6]
 """
 import argparse
@@ -21,8 +21,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--knob", default="bsgs_prio")
-    ap.add_argument("--values", default="1,0")
+    ap.add_argument("--knob", default="grid_mult")
+    ap.add_argument("--values", default="3,1")
     ap.add_argument("--bits", type=int, default=32)
     ap.add_argument("--t", default="8,12,16,20,24,28,30,32,36,40,42,48,56,64,72,80")
     ap.add_argument("--n", type=float, default=2.5e8)

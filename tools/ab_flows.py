@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Same-process A/B of a flow-batch knob (default flow_sort: the variants of
-the grouping sort in radix.h): per flow count, the modes alternate,
+"""Same-process A/B of a flow-batch knob (default flow_hist: the few-flow
+histogram grouping against the radix sort): per flow count, the modes alternate,
 every mode's output (keys + sketches, device-resident) must equal mode 0's
 byte for byte, and the median wall time of the synchronous call is reported.
 
-    python tools/ab_flows.py [--knob flow_sort] [--modes 2,1] [--flows 10000,1000000] [--rounds 4]
+    python tools/ab_flows.py [--knob flow_hist] [--modes 32,0] [--flows 10000,1000000] [--rounds 4]
 """
 import argparse
 import ctypes as C
@@ -21,8 +21,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--knob", default="flow_sort")
-    ap.add_argument("--modes", default="2,1")
+    ap.add_argument("--knob", default="flow_hist")
+    ap.add_argument("--modes", default="32,0")
     ap.add_argument("--flows", default="10000,1000000")
     ap.add_argument("--npkts", type=float, default=1e8)
     ap.add_argument("--rounds", type=int, default=4)

@@ -333,7 +333,7 @@ def run_sweep64(args, ctx):
     n = int(args.nsweep)
     ids = torch.empty(n, dtype=torch.int64, device=DEV)
     fill_splitmix(ctx, ids, 0x5EED0003, bits=64)
-    path = "chain" if "bsgs64_off=1" in args.knob else "default"
+    path = "default"
     for t in sweep_ts(args, (8, 9, 12, 16, 17, 20, 24, 32, 40, 48, 56, 64, 72, 80, 81, 128, 160, 256, 512, 1024)):
         wall, kern = time_encode(ctx, ids, t, 64, max(3, args.steps // 2))
         emit({"config": f"encode u64 t={t} ({path})", "n": n, "ids_per_s": n / kern,

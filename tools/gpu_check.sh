@@ -27,10 +27,6 @@ for s in $STEPS; do
     pytest) step pytest 1200 python3 -u -m pytest tests -m gpu -q -x -p no:cacheprovider -rA --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     pytestf) step pytestf 1200 python3 -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q -x -p no:cacheprovider -rA --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}; rc=$?; ok_or_testfail $rc || exit 3 ;;
     bench) step bench 600 python3 -u bench.py ${BENCH_ARGS:-} || exit 3 ;;
-    sgsweep)
-      for g in ${SG_LIST:-0 2 4 6 8}; do
-        step sg$g 300 python3 -u bench.py --steps 10 --warmup 2 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
-      done ;;
     configsab)  # the same configs with knob settings alternated: CONFIGS_AB="k=v1 k=v2", CONFIGS_ROUNDS rounds
       for r in $(seq ${CONFIGS_ROUNDS:-2}); do
         for kv in ${CONFIGS_AB}; do
@@ -38,10 +34,6 @@ for s in $STEPS; do
         done
       done ;;
     configs) step configs 900 python3 -u tools/bench_configs.py ${CONFIGS_ARGS:-u64 decode host sweep --cpu} || exit 3 ;;
-    pktab)  # packet batch: fused extract+encode vs the two-pass path
-      step pkt_fused 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 || exit 3
-      step pkt_twopass 300 python3 -u tools/bench_configs.py packets --pkt-t 12,16,24,32 --knob pkt_fused=0 || exit 3 ;;
-    configs20) step configs20 900 python3 -u tools/bench_configs.py u64 --knob u64_kmax=20 || exit 3 ;;
     prof)
       export TMPDIR=/tmp
       step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 1 --cpu-sample 0 || exit 3 ;;
@@ -67,12 +59,6 @@ for s in $STEPS; do
     proflows)
       export TMPDIR=/tmp
       step proflows 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proflows" -o run -- python3 "$ROOT/tools/bench_configs.py" flows packets --steps 4 || exit 3 ;;
-    pmcab)  # SQ stall/issue counters for two BSGS variants (A/B), two counter passes each
-      export TMPDIR=/tmp
-      for g in ${SG_AB:-0 8}; do
-        step pmcab_a$g 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmcab_a$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
-        step pmcab_b$g 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcab_b$g" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --cpu-sample 0 --knob bsgs_sg=$g || exit 3
-      done ;;
     proftrace)  # kernel + memory-copy + HIP runtime trace (no counters) of one command, for the gaps between them
       export TMPDIR=/tmp
       step proftrace 600 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --stats --output-format csv -d "$OUT/proftrace" -o run -- python3 "$ROOT/tools/bench_configs.py" ${PROFTRACE_ARGS:-decode --rt-modes 2} --steps 10 || exit 3 ;;
@@ -86,10 +72,6 @@ for s in $STEPS; do
     decshape) step decshape 600 python3 -u tools/bench_decode.py ${DECSHAPE_ARGS:-} || exit 3 ;;
     tuneu64) step tuneu64 600 ./tools/tune_u64 || exit 3 ;;
     flowsbench) step flowsbench 600 python3 -u tools/bench_configs.py flows --steps 6 || exit 3 ;;
-    flowswg)
-      for w in ${WG_LIST:-4 6 8}; do
-        step flowswg$w 300 python3 -u tools/bench_configs.py flows --steps 6 --knob flow_wgpc=$w || exit 3
-      done ;;
     dec64)  # u64 root test: BSGS (default) vs Horner
       step dec64_bsgs 300 python3 -u tools/bench_configs.py decode64 --steps 10 --cpu || exit 3
       step dec64_horner 300 python3 -u tools/bench_configs.py decode64 --steps 10 --knob rt64_horner=1 || exit 3 ;;
