@@ -548,6 +548,17 @@ def usable_cpus():
     return n, how
 
 
+def cgroup_throttling():
+    """nr_periods / nr_throttled / throttled_usec of this process's cgroup
+    (cgroup v2 cpu.stat), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            d = dict(line.split() for line in f if line.strip())
+        return {k: int(d[k]) for k in ("nr_periods", "nr_throttled", "throttled_usec") if k in d}
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baselines(args, bits, t, start, cnt, ids):
     """The oracle's scalar restatement of the reference insert loop, timed on
     this host over a bounded prefix of the same stream, with the ids
@@ -560,8 +571,14 @@ def cpu_baselines(args, bits, t, start, cnt, ids):
     host_ids = (coracle.splitmix_u32 if bits == 32 else coracle.splitmix_u64)(args.seed, m, start)
     # the insert loop timed in the crate's own unit (rdtsc, as its
     # benchmark_construct's avg_cycles) and by the monotonic clock over the
-    # same region: the TSC rate comes from this run, not from /proc/cpuinfo
-    cpu_S, tsc, ns = coracle.encode_timed(host_ids, t)
+    # same region (the TSC rate comes from this run, not from /proc/cpuinfo),
+    # and in core cycles: perf_event_open's user-mode cycle count where the
+    # kernel allows it, and the core clock read by a dependent-add chain just
+    # before and after the loop; the cgroup's CPU throttling over the region
+    thr0 = cgroup_throttling()
+    cpu_S, cyc = coracle.encode_cycles(host_ids, t)
+    thr1 = cgroup_throttling()
+    tsc, ns = cyc["tsc"], cyc["ns"]
     cpu_s = ns * 1e-9
     q = (sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64)(t)
     q.insert_batch(ids[:m])                    # GPU on the same prefix: bit-exact parity check
@@ -574,18 +591,43 @@ def cpu_baselines(args, bits, t, start, cnt, ids):
     ns_id = cpu_s / m * 1e9
     tsc_id = tsc / m if tsc else None
     tsc_ghz = tsc / ns if tsc else None
+    clk = cyc["clock_probe_ghz"]
+    if cyc["core_cycles"]:
+        core_id, core_how = cyc["core_cycles"] / m, "perf_event_open user-mode cycles"
+    elif clk:
+        core_id, core_how = ns_id * clk, (f"ns x the core clock of a dependent-add chain ({clk:.2f} GHz; "
+                                          f"perf_event_open refused, errno {cyc['perf_errno']})")
+    else:
+        core_id, core_how = None, "unavailable"
+    throttled = None
+    if thr0 and thr1:
+        throttled = {k: thr1[k] - thr0.get(k, 0) for k in thr1}
     one = {
         "value": m / cpu_s, "unit": "identifiers/s", "cores": 1, "kind": "port",
         "ns_per_id": ns_id, "tsc_cycles_per_id": tsc_id, "tsc_cycles_per_power": tsc_id / t if tsc_id else None,
         "tsc_ghz": tsc_ghz,
+        "core_cycles_per_id": core_id, "core_cycles_per_power": core_id / t if core_id else None,
+        "core_cycles_source": core_how, "core_clock_probe_ghz": clk,
+        "instructions_per_id": cyc["instructions"] / m if cyc["instructions"] else None,
+        "cgroup_throttling_during_loop": throttled,
         "sample": f"first {m} ids of the same stream (seed {hex(args.seed)}), pre-generated, inserted by the "
-                  f"scalar C restatement of the reference insert loop (oracle/quack_oracle.c qo_encode_timed), "
-                  f"1 core, {cpu_s:.1f} s = {ns_id:.1f} ns/id"
+                  f"scalar C restatement of the reference insert loop (oracle/quack_oracle.c qo_encode_cycles: "
+                  f"t - 1 dependent mul + mod-by-constant steps per id, the sums' conditional subtract as a "
+                  f"mask), 1 core, {cpu_s:.1f} s = {ns_id:.1f} ns/id"
                   + (f" = {tsc_id:.1f} TSC cycles/id (rdtsc around the loop, TSC at {tsc_ghz:.3f} GHz from the "
-                     f"same region)" if tsc_id else "") + f"; {host}"
+                     f"same region)" if tsc_id else "")
+                  + (f" = {core_id:.1f} core cycles/id, {core_id / t:.1f} per power ({core_how})" if core_id else "")
+                  + (f"; cgroup throttling over the loop: {throttled}" if throttled is not None else "")
+                  + f"; {host}"
                   + (f"; the published crate in the same units: {pub_cyc:.1f} TSC cycles/id = {pub_ns:.1f} ns/id "
                      f"at u{bits} t={t} on one Xeon E5 core (benchmark_construct avg_cycles / 1000 ids; "
-                     f"BASELINE.md), so this port takes {tsc_id / pub_cyc:.2f}x the crate's TSC cycles per id"
+                     f"BASELINE.md): this port takes {tsc_id / pub_cyc:.2f}x the crate's TSC cycles per id. "
+                     f"A power step is one dependent chain of a 64-bit multiply and the modulo by the constant "
+                     f"prime (multiply-high, shifts, subtracts), so the loop is latency-bound: "
+                     + (f"{core_id / (t - 1):.1f} core cycles per step here" if core_id and t > 1 else "")
+                     + f"; the TSC ratio to the crate follows the two hosts' core-clock / TSC ratios. (Until round "
+                     f"5 the port's modular add compiled to a branch that mispredicted every other power: 1.77x "
+                     f"the crate.)"
                      if pub_cyc and tsc_id else ""),
         "published_crate_ns_per_id": pub_ns,
         "published_crate_tsc_cycles_per_id": pub_cyc,

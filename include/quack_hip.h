@@ -162,7 +162,9 @@ int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
  * flows are grouped by slot histograms, 0: never), "flow_byslot" (0 the
  * rule, 1 / 2 force the by-slot / by-rank grouping key), "root_test" (0
  * automatic, 1 Horner, 2 root-set scan), "comm_fault" (tests: the k-th
- * collective's payload staging of this context's rank fails once).
+ * collective's payload staging of this context's rank fails once),
+ * "comm_delay_ms" (tests: a kernel of that many ms runs before this rank's
+ * next RCCL collective, once).
  * Unknown name or out-of-range value -> QK_E_INVAL. */
 int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value);
 /* Shader-clock probe (measurement): one wave on `stream` spins for
@@ -348,7 +350,8 @@ int qk_u64_decode_device(qk_ctx *ctx, const qk_u64 *diff, const uint64_t *d_log,
  * in another process is released by its own timeout: every wait on an RCCL
  * collective polls ncclCommGetAsyncError and aborts after the communicator's
  * timeout (qk_comm_set_timeout; a host channel's callbacks time out
- * themselves).
+ * themselves), and the rank's own work in front of the collective is waited
+ * for under 4 x that timeout, also polling the asynchronous error.
  * ---------------------------------------------------------------------- */
 typedef struct qk_comm qk_comm;
 #define QK_COMM_ID_BYTES 128

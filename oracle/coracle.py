@@ -48,6 +48,7 @@ def lib():
             "qo_bench_construct": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, u64p]),
             "qo_bench_decode": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, u64p]),
             "qo_encode_timed": (None, [C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, u64p, u64p]),
+            "qo_encode_cycles": (None, [C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -106,6 +107,21 @@ def encode_timed(ids, t):
     tsc, ns = C.c_uint64(), C.c_uint64()
     lib().qo_encode_timed(bits, ids.ctypes.data, len(ids), t, S.ctypes.data, C.byref(tsc), C.byref(ns))
     return [int(v) for v in S], tsc.value, ns.value
+
+
+def encode_cycles(ids, t):
+    """encode_timed with the core's view of the same region (quack_oracle.c
+    qo_encode_cycles): (power sums, dict of core cycles and instructions
+    from perf_event_open (None where refused, with its errno), TSC ticks, ns,
+    and the core clock read by a dependent-add chain around the loop)."""
+    bits = 32 if ids.dtype == np.uint32 else 64
+    ids = np.ascontiguousarray(ids)
+    S = np.zeros(t, dtype=np.uint32 if bits == 32 else np.uint64)
+    out = (C.c_uint64 * 6)()
+    lib().qo_encode_cycles(bits, ids.ctypes.data, len(ids), t, S.ctypes.data, C.cast(out, C.POINTER(C.c_uint64)))
+    return [int(v) for v in S], {"core_cycles": out[0] or None, "instructions": out[1] or None, "tsc": out[2],
+                                 "ns": out[3], "clock_probe_ghz": out[4] / 1e6 if out[4] else None,
+                                 "perf_errno": out[5] or None}
 
 
 def encode_mt(ids, t, threads):

@@ -21,7 +21,7 @@
  * Decode (media_client.rs:295-313): Newton's identities (to_coeffs) and the
  * Horner root test (arithmetic::eval(&coeffs, id).value() == 0).
  */
-#define _POSIX_C_SOURCE 200809L
+#define _GNU_SOURCE
 #include <pthread.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -52,9 +52,14 @@ void qo_splitmix_u64(uint64_t seed, uint64_t start, uint64_t n, uint64_t *out) {
 }
 
 /* ---- GF(p32) ---------------------------------------------------------- */
+/* The conditional subtract as a mask, not a branch: s >= p is a coin flip
+ * per add for random operands, and gcc compiled the ternary into a jump that
+ * mispredicted every other power (~8 of the ~24 core cycles per power of the
+ * insert loop; the crate's LLVM build selects instead). */
 static inline uint32_t add32(uint32_t a, uint32_t b) {
-    uint64_t s = (uint64_t)a + b;
-    return (uint32_t)(s >= QO_P32 ? s - QO_P32 : s);
+    const uint64_t s = (uint64_t)a + b;
+    const uint64_t m = (uint64_t)0 - (uint64_t)(s >= QO_P32);
+    return (uint32_t)(s - (m & QO_P32));
 }
 static inline uint32_t sub32(uint32_t a, uint32_t b) { return a >= b ? a - b : (uint32_t)((uint64_t)a + QO_P32 - b); }
 static inline uint32_t mul32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) % QO_P32); }
@@ -115,9 +120,10 @@ uint64_t qo_root_test_u32(const uint32_t *c, uint32_t d, const uint32_t *log, ui
 }
 
 /* ---- GF(p64) ---------------------------------------------------------- */
-static inline uint64_t add64(uint64_t a, uint64_t b) {
-    u128 s = (u128)a + b;
-    return (uint64_t)(s >= QO_P64 ? s - QO_P64 : s);
+static inline uint64_t add64(uint64_t a, uint64_t b) {   /* as add32: a mask, not a branch */
+    const u128 s = (u128)a + b;
+    const u128 m = (u128)0 - (u128)(s >= QO_P64);
+    return (uint64_t)(s - (m & QO_P64));
 }
 static inline uint64_t sub64(uint64_t a, uint64_t b) { return a >= b ? a - b : (uint64_t)((u128)a + QO_P64 - b); }
 static inline uint64_t mul64(uint64_t a, uint64_t b) { return (uint64_t)(((u128)a * b) % QO_P64); }
@@ -285,6 +291,93 @@ void qo_encode_timed(uint32_t bits, const void *ids, uint64_t n, uint32_t t, voi
     const uint64_t c1 = qo_tsc(), n1 = qo_now_ns();
     *tsc = c1 - c0;
     *ns = n1 - n0;
+}
+
+/* The same region read in core cycles, so that the baseline can say how its
+ * TSC figure relates to the work the core did (a TSC tick is not a core
+ * cycle on a boosting CPU):
+ *   out[0] core cycles, out[1] instructions retired (perf_event_open,
+ *          user-mode only, this thread; 0 where the kernel refuses —
+ *          perf_event_paranoid, a container's seccomp),
+ *   out[2] TSC ticks, out[3] ns (as qo_encode_timed),
+ *   out[4] the core clock in kHz from a chain of dependent adds (1 cycle
+ *          each) timed just before and just after the loop — an unprivileged
+ *          reading of the clock the core runs at, whatever perf allows,
+ *   out[5] errno of a refused perf_event_open (0 if it opened). */
+#if defined(__linux__)
+#include <errno.h>
+#include <linux/perf_event.h>
+#include <sys/ioctl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+static int qo_perf_open(uint64_t config, int group) {
+    struct perf_event_attr a;
+    memset(&a, 0, sizeof a);
+    a.type = PERF_TYPE_HARDWARE;
+    a.size = sizeof a;
+    a.config = config;
+    a.disabled = group < 0;
+    a.exclude_kernel = 1;
+    a.exclude_hv = 1;
+    return (int)syscall(SYS_perf_event_open, &a, 0, -1, group, 0);
+}
+#endif
+/* kHz of this core: 2^26 dependent adds (1 cycle each on x86-64) */
+static uint64_t qo_clock_khz(void) {
+#if defined(__x86_64__)
+    uint64_t best = 0;
+    for (int rep = 0; rep < 3; ++rep) {
+        uint64_t x = 0, k = 1u << 22;
+        const uint64_t t0 = qo_now_ns();
+        uint64_t one = 1;
+        __asm__ volatile("" : "+r"(one));   /* a register operand: no immediate-add folding in the renamer */
+        for (uint64_t i = 0; i < k; ++i)
+            __asm__ volatile("add %1, %0\n\tadd %1, %0\n\tadd %1, %0\n\tadd %1, %0\n\t"
+                             "add %1, %0\n\tadd %1, %0\n\tadd %1, %0\n\tadd %1, %0\n\t"
+                             "add %1, %0\n\tadd %1, %0\n\tadd %1, %0\n\tadd %1, %0\n\t"
+                             "add %1, %0\n\tadd %1, %0\n\tadd %1, %0\n\tadd %1, %0"
+                             : "+r"(x)
+                             : "r"(one));
+        const uint64_t dt = qo_now_ns() - t0;
+        const uint64_t khz = dt ? x * 1000000ull / dt : 0;   /* x adds in dt ns */
+        if (khz > best) best = khz;
+    }
+    return best;
+#else
+    return 0;
+#endif
+}
+void qo_encode_cycles(uint32_t bits, const void *ids, uint64_t n, uint32_t t, void *S, uint64_t *out) {
+    memset(out, 0, 6 * sizeof(uint64_t));
+    const uint64_t khz0 = qo_clock_khz();
+    int fc = -1, fi = -1;
+#if defined(__linux__)
+    fc = qo_perf_open(PERF_COUNT_HW_CPU_CYCLES, -1);
+    if (fc < 0) out[5] = (uint64_t)errno;
+    else fi = qo_perf_open(PERF_COUNT_HW_INSTRUCTIONS, fc);
+    if (fc >= 0) {
+        ioctl(fc, PERF_EVENT_IOC_RESET, PERF_IOC_FLAG_GROUP);
+        ioctl(fc, PERF_EVENT_IOC_ENABLE, PERF_IOC_FLAG_GROUP);
+    }
+#endif
+    const uint64_t n0 = qo_now_ns(), c0 = qo_tsc();
+    if (bits == 32) qo_encode_u32((const uint32_t *)ids, n, t, (uint32_t *)S);
+    else qo_encode_u64((const uint64_t *)ids, n, t, (uint64_t *)S);
+    const uint64_t c1 = qo_tsc(), n1 = qo_now_ns();
+#if defined(__linux__)
+    if (fc >= 0) {
+        ioctl(fc, PERF_EVENT_IOC_DISABLE, PERF_IOC_FLAG_GROUP);
+        uint64_t v = 0;
+        if (read(fc, &v, sizeof v) == (ssize_t)sizeof v) out[0] = v;
+        if (fi >= 0 && read(fi, &v, sizeof v) == (ssize_t)sizeof v) out[1] = v;
+        close(fc);
+        if (fi >= 0) close(fi);
+    }
+#endif
+    const uint64_t khz1 = qo_clock_khz();
+    out[2] = c1 - c0;
+    out[3] = n1 - n0;
+    out[4] = (khz0 + khz1) / 2;
 }
 
 /* CPU port of quack's benchmark_decode (figures/fig2_microbenchmarks.py:

@@ -610,6 +610,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"flow_byslot", &qk_knobs::flow_byslot, 0, 2},
         {"root_test", &qk_knobs::root_test, 0, 2},
         {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
+        {"comm_delay_ms", &qk_knobs::comm_delay_ms, 0, 600000},
     };
     for (const K &k : table)
         if (strcmp(k.name, name) == 0) {

@@ -187,19 +187,57 @@ static int abort_comm(qk_comm *c) {
     return QK_E_COMM;
 }
 
+// Test knob comm_delay_ms = k on a local rank's context: a one-wave kernel
+// that spins k ms (s_memrealtime, 100 MHz; s_sleep between reads) is put in
+// front of that rank's next collective, once — slow or hung local work
+// before a collective (wait_local's bounded pre-collective wait).
+__global__ void k_comm_delay(uint64_t ticks) {
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - r0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
 // Mark the end of a local rank's own work (its encode, the caller's work
 // ordered in by enter, the payload staging) just before an RCCL collective.
 static void mark_pre(Local &L) {
     (void)hipSetDevice(L.device);
+    int &dl = L.ctx->knobs.comm_delay_ms;
+    if (dl > 0) {
+        hipLaunchKernelGGL(k_comm_delay, dim3(1), dim3(64), 0, L.ctx->stream, (uint64_t)dl * 100000ull);
+        (void)hipGetLastError();
+        dl = 0;
+    }
     L.pre = hipEventRecord(L.ev_pre, L.ctx->stream) == hipSuccess;
+}
+
+// Poll until `done` reports completion; every poll also reads the
+// communicator's asynchronous error.  Past limit_ms (0: none) or on an
+// asynchronous error the communicator is aborted: QK_E_COMM.
+template <class Done> static int poll_bounded(qk_comm *c, Local &L, int64_t limit_ms, Done done) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+        const hipError_t q = done();
+        if (q == hipSuccess) return QK_OK;
+        if (q != hipErrorNotReady) return QK_E_HIP;
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(L.nc, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress))
+            return abort_comm(c);
+        if (limit_ms > 0 &&
+            std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
+                limit_ms)
+            return abort_comm(c);
+        if (spin >= 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
 }
 
 // Drain the local rank's stream.  With RCCL work in it, the wait polls the
 // communicator's asynchronous error and gives up after the timeout (a peer
 // that never reaches the collective): the communicator is aborted, QK_E_COMM.
-// The timeout covers the collective only: the local work recorded before it
-// (mark_pre) is waited for first, without a limit — slow local work is not a
-// missing peer.
+// The local work recorded before the collective (mark_pre) is waited for
+// first under its own, longer limit — PRE_TIMEOUT_MULT x the timeout: slow
+// local work is not a missing peer, but local work that never ends (a hung
+// kernel, a caller stream waiting on an event that never fires) must not
+// hang the rank either.
+constexpr int64_t PRE_TIMEOUT_MULT = 4;
 static int wait_local(qk_comm *c, Local &L) {
     QK_HIP_TRY(hipSetDevice(L.device));
     if (c->host || !L.nc) {
@@ -208,22 +246,10 @@ static int wait_local(qk_comm *c, Local &L) {
     }
     if (L.pre) {
         L.pre = false;
-        QK_HIP_TRY(hipEventSynchronize(L.ev_pre));
+        if (int rc = poll_bounded(c, L, c->timeout_ms * PRE_TIMEOUT_MULT, [&] { return hipEventQuery(L.ev_pre); }))
+            return rc;
     }
-    const auto t0 = std::chrono::steady_clock::now();
-    for (unsigned spin = 0;; ++spin) {
-        const hipError_t q = hipStreamQuery(L.ctx->stream);
-        if (q == hipSuccess) return QK_OK;
-        if (q != hipErrorNotReady) return QK_E_HIP;
-        ncclResult_t ae = ncclSuccess;
-        if (ncclCommGetAsyncError(L.nc, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress))
-            return abort_comm(c);
-        if (c->timeout_ms > 0 &&
-            std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
-                c->timeout_ms)
-            return abort_comm(c);
-        if (spin >= 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
+    return poll_bounded(c, L, c->timeout_ms, [&] { return hipStreamQuery(L.ctx->stream); });
 }
 
 // Test knob comm_fault = k on a local rank's context (qk_ctx_set_knob): the

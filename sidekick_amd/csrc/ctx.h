@@ -22,6 +22,8 @@ struct qk_knobs {
     int root_test = 0;     // 0: automatic (cost model, api.hip rt_use_scan), 1: Horner, 2: root-set scan
     int comm_fault = 0;    // k > 0 (tests): this rank's payload staging for the k-th collective of its
                            // next sharded operation fails, once (comm.hip fault_now)
+    int comm_delay_ms = 0; // k > 0 (tests): a k-ms kernel in front of this rank's next RCCL collective,
+                           // once (comm.hip mark_pre: the bounded wait for pre-collective work)
 };
 
 struct qk_ctx {

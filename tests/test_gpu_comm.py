@@ -376,6 +376,49 @@ def test_rccl_world1_local_failure_leaves_q_untouched(comm):
     assert q.count() == 5001
 
 
+@pytest.mark.parametrize("how", ["create", "init_rank"])
+def test_rccl_world1_pre_collective_wait_is_bounded(how):
+    """Local work in front of an RCCL collective (knob comm_delay_ms: a kernel
+    of that many ms on the rank's stream before its reduce) is waited for
+    under its own limit, 4 x the communicator's timeout: a delay inside the
+    limit completes bit-exactly; one past it aborts the communicator with
+    QK_E_COMM within about that limit (no unbounded hipEventSynchronize), q
+    untouched, and later calls on it fail fast."""
+    import time
+    import ctypes as C
+    import sidekick_amd as sk
+    from sidekick_amd._lib import QK_E_COMM, QK_OK, lib
+    from sidekick_amd.dist import Comm
+    host, ids = _ids(32, 200_003, 0x3D)
+    want = sk.PowerSumQuackU32(32)
+    want.insert_batch(ids)
+    c = Comm.create([0]) if how == "create" else Comm.init_rank(Comm.unique_id(), 0, 1, 0)
+    try:
+        c.set_timeout(200)                     # collective 200 ms, local work before it 800 ms
+        q = sk.PowerSumQuackU32(32)
+        c.context(0).set_knob("comm_delay_ms", 300)
+        c.encode_sharded([ids], q)
+        assert q == want
+        q = sk.PowerSumQuackU32(32)
+        q.insert(7)
+        c.context(0).set_knob("comm_delay_ms", 3000)
+        t0 = time.time()
+        rc = lib().qk_u32_encode_sharded(c.handle, (C.c_void_p * 1)(ids.data_ptr()), (C.c_size_t * 1)(len(host)),
+                                         q._buf, 0, None)
+        dt = time.time() - t0
+        assert rc == QK_E_COMM, rc
+        assert 0.7 < dt < 2.5, dt              # the 800 ms limit, not the 3 s kernel
+        assert q.count() == 1 and q.power_sums()[0] == 7
+        rc = lib().qk_u32_encode_sharded(c.handle, (C.c_void_p * 1)(ids.data_ptr()), (C.c_size_t * 1)(len(host)),
+                                         q._buf, 0, None)
+        assert rc == QK_E_COMM and q.count() == 1
+        assert rc != QK_OK
+    finally:
+        import torch
+        torch.cuda.synchronize()               # the 3 s kernel drains before the context goes
+        c.close()
+
+
 def test_host_channel_staging_fault_at_every_step_same_status_everywhere():
     """A rank whose payload staging fails (knob comm_fault = k: the copy into
     its k-th collective of the call) keeps joining and sends the failure as
