@@ -164,7 +164,8 @@ int qk_ctx_set_grid(qk_ctx *ctx, uint32_t blocks);
  * automatic, 1 Horner, 2 root-set scan), "comm_fault" (tests: the k-th
  * collective's payload staging of this context's rank fails once),
  * "comm_delay_ms" (tests: a kernel of that many ms runs before this rank's
- * next RCCL collective, once).
+ * next RCCL collective, once), "rt_karg" (1: a root-set scan whose set fits
+ * the kernel arguments takes them; 0: always by copy).
  * Unknown name or out-of-range value -> QK_E_INVAL. */
 int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value);
 /* Shader-clock probe (measurement): one wave on `stream` spins for

@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -305,7 +306,7 @@ template <typename T> int root_test_plan(const qk_ctx *ctx, const T *coeffs, uin
     if constexpr (sizeof(T) == 4) rc = qk_u32_roots(coeffs, d, r.data(), d, &k);
     else rc = qk_u64_roots(coeffs, d, r.data(), d, &k);
     if (rc) return rc;
-    plan.scan = rt_scan_table<T>(r.data(), k, plan.set, plan.tab) &&
+    plan.scan = rt_scan_table<T>(r.data(), k, plan.set, plan.tab, false) &&
                 plan.set.words * sizeof(T) <= (SMALL_NHITS - RT_C) * 8;
     if (!plan.scan) plan.tab.clear();
     return QK_OK;
@@ -330,11 +331,11 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
     } else {
         memcpy(h_c, coeffs, cbytes);
     }
-    // one copy carries the zeroed counters and the table (or coefficients):
-    // no counter-initialising launch
+    // one copy carries the zeroed counters, the scan's hash multipliers and
+    // the table (or coefficients): no counter-initialising launch
     ctx->h_small[0] = 0;
     ctx->h_small[1] = ~0ull;
-    ctx->h_small[2] = 0;
+    ctx->h_small[2] = scan ? (uint64_t)plan.set.m1 | (uint64_t)plan.set.m2 << 32 : 0;
     ctx->h_small[3] = 0;
     if (scan) {   // the scan's host slots (decode.hip rt_record): empty, no overflow
         std::fill(ctx->h_small + SMALL_HITPF, ctx->h_small + SMALL_WORDS, ~0ull);
@@ -425,6 +426,72 @@ template int root_test_finish<uint64_t>(qk_ctx *, const RtPlan<uint64_t> &, cons
                                         const uint64_t *, size_t, int, uint64_t, hipStream_t, std::vector<uint64_t> &,
                                         uint64_t &);
 
+// The root-set scan with its set in the kernel arguments (single GPU, sets
+// of at most RT_KTAB_BYTES: the compact layout, k = 32 roots -> 256 buckets,
+// 1 KB u32 / 2 KB u64): the host finds the roots, builds the set and
+// launches — no H2D
+// copy and no counter reset in front of the scan (the hit / stop tickets
+// run on from the values the previous call left, ctx->rt_hbase / rt_sbase,
+// in their own words of d_small, SMALL_KT).  The scan hands its hits and
+// stops over through the pinned slots; a slot overflow (more than the slots
+// hold) returns 1, the caller reruns by the two-phase form, and the tickets
+// are reset before the next kernel-argument call.
+template <typename T>
+static int root_test_scan_k(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop,
+                            T stop_value, hipStream_t s, std::vector<uint64_t> &h, uint64_t &stop) {
+    std::vector<T> r(d);
+    uint32_t k = 0;
+    int rc;
+    if constexpr (sizeof(T) == 4) rc = qk_u32_roots(coeffs, d, r.data(), d, &k);
+    else rc = qk_u64_roots(coeffs, d, r.data(), d, &k);
+    if (rc) return rc;
+    RtScanSet set;
+    std::vector<T> tab;
+    if (!rt_scan_table<T>(r.data(), k, set, tab, true) || set.words * sizeof(T) > RT_KTAB_BYTES) return 1;
+    if (int e = ensure_hits(ctx, 4096, s)) return e;
+    uint64_t *hs = ctx->h_small;
+    if (!ctx->rt_bases_valid) {   // after a two-phase call (or none): reset the tickets once
+        QK_HIP_TRY(hipMemsetAsync(ctx->d_small + SMALL_KT, 0, 4 * sizeof(uint64_t), s));
+        ctx->rt_hbase = ctx->rt_sbase = 0;
+    }
+    std::fill(hs + SMALL_HITPF, hs + SMALL_WORDS, ~0ull);
+    hs[SMALL_OVF] = 0;
+    if (int e = launch_root_scan_k<T>(ctx, tab, set, d_log, n, use_stop, stop_value, ctx->d_hits,
+                                      (uint64_t)ctx->hits_cap, ctx->d_small + SMALL_KT, ctx->h_small_dev + SMALL_NHITS,
+                                      ctx->rt_hbase, ctx->rt_sbase, s)) {
+        ctx->rt_bases_valid = false;
+        return e;
+    }
+    ctx->rt_bases_valid = true;
+    // wait by polling: a sleeping synchronisation wakes ~5 µs late
+    for (unsigned spin = 0;; ++spin) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) {
+            ctx->rt_bases_valid = false;
+            return QK_E_HIP;
+        }
+        if (spin >= 20000) std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
+    if (hs[SMALL_OVF]) {   // past the slots: the two-phase form reruns it (and resets the tickets)
+        ctx->rt_bases_valid = false;
+        return 1;
+    }
+    uint64_t c = 0;
+    while (c < SMALL_HITPF_N && hs[SMALL_HITPF + c] != ~0ull) ++c;
+    uint64_t st = ~0ull, ns = 0;
+    for (uint32_t q = 0; q < RT_NSTOP; ++q) {
+        st = std::min(st, hs[SMALL_STOPS + q]);
+        ns += hs[SMALL_STOPS + q] != ~0ull;
+    }
+    ctx->rt_hbase += c;
+    ctx->rt_sbase += ns;
+    h.assign(hs + SMALL_HITPF, hs + SMALL_HITPF + c);
+    std::sort(h.begin(), h.end());
+    stop = use_stop ? std::min<uint64_t>(st, (uint64_t)n) : (uint64_t)n;
+    return QK_OK;
+}
+
 template <typename T>
 static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_log, size_t n, int use_stop,
                           T stop_value, uint64_t *hits, size_t cap, size_t *n_hits, void *stream,
@@ -443,12 +510,19 @@ static int root_test_impl(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d_l
     std::lock_guard<std::mutex> g(ctx->mu);
     QK_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = pick_stream(ctx, stream);
-    RtPlan<T> plan;
-    if (int rc = root_test_plan<T>(ctx, coeffs, d, n, plan)) return rc;
-    if (int rc = root_test_begin<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
     std::vector<uint64_t> h;
     uint64_t stop = n;
-    if (int rc = root_test_finish<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s, h, stop)) return rc;
+    int ov = 1;
+    if (ctx->knobs.rt_karg && rt_use_scan<T>(ctx, d, n)) {
+        ov = root_test_scan_k<T>(ctx, coeffs, d, d_log, n, use_stop, stop_value, s, h, stop);
+        if (ov < 0) return ov;
+    }
+    if (ov) {   // Horner, a set too large for the kernel arguments, or a slot overflow
+        RtPlan<T> plan;
+        if (int rc = root_test_plan<T>(ctx, coeffs, d, n, plan)) return rc;
+        if (int rc = root_test_begin<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s)) return rc;
+        if (int rc = root_test_finish<T>(ctx, plan, coeffs, d, d_log, n, use_stop, stop_value, s, h, stop)) return rc;
+    }
     const size_t m = (size_t)(std::lower_bound(h.begin(), h.end(), stop) - h.begin());
     if (stop_index) *stop_index = stop;
     *n_hits = m;
@@ -611,6 +685,7 @@ int qk_ctx_set_knob(qk_ctx *ctx, const char *name, int64_t value) {
         {"root_test", &qk_knobs::root_test, 0, 2},
         {"comm_fault", &qk_knobs::comm_fault, 0, 1 << 20},
         {"comm_delay_ms", &qk_knobs::comm_delay_ms, 0, 600000},
+        {"rt_karg", &qk_knobs::rt_karg, 0, 1},
     };
     for (const K &k : table)
         if (strcmp(k.name, name) == 0) {

@@ -93,6 +93,7 @@ struct qk_comm {
     bool host = false;                // collectives through ops (qk_comm_init_host)
     qk_comm_host_ops ops{};
     bool broken = false;              // a collective failed: unusable
+    bool abort_pending = false;       // broken by local work that outlasted its limit: abort at destroy
     int64_t timeout_ms = 300000;      // waits on RCCL collectives give up (and abort) after this; 0: never
     int step = 0;                     // collectives of the operation in progress (fault injection)
     // sharded encode in flight (qk_*_encode_sharded_async -> _wait)
@@ -210,9 +211,13 @@ static void mark_pre(Local &L) {
 }
 
 // Poll until `done` reports completion; every poll also reads the
-// communicator's asynchronous error.  Past limit_ms (0: none) or on an
-// asynchronous error the communicator is aborted: QK_E_COMM.
-template <class Done> static int poll_bounded(qk_comm *c, Local &L, int64_t limit_ms, Done done) {
+// communicator's asynchronous error.  On an asynchronous error, or past
+// limit_ms (0: none) with abort_late, the communicator is aborted: QK_E_COMM.
+// Past the limit without abort_late it is only marked broken (QK_E_COMM,
+// every later call fails at once) and aborted by qk_comm_destroy: RCCL's
+// abort frees its buffers, and hipFree waits for the device — here, for the
+// very local work that outlasted the limit.
+template <class Done> static int poll_bounded(qk_comm *c, Local &L, int64_t limit_ms, bool abort_late, Done done) {
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned spin = 0;; ++spin) {
         const hipError_t q = done();
@@ -223,8 +228,12 @@ template <class Done> static int poll_bounded(qk_comm *c, Local &L, int64_t limi
             return abort_comm(c);
         if (limit_ms > 0 &&
             std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
-                limit_ms)
-            return abort_comm(c);
+                limit_ms) {
+            if (abort_late) return abort_comm(c);
+            c->broken = true;
+            c->abort_pending = true;
+            return QK_E_COMM;
+        }
         if (spin >= 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
 }
@@ -246,10 +255,11 @@ static int wait_local(qk_comm *c, Local &L) {
     }
     if (L.pre) {
         L.pre = false;
-        if (int rc = poll_bounded(c, L, c->timeout_ms * PRE_TIMEOUT_MULT, [&] { return hipEventQuery(L.ev_pre); }))
+        if (int rc = poll_bounded(c, L, c->timeout_ms * PRE_TIMEOUT_MULT, false,
+                                  [&] { return hipEventQuery(L.ev_pre); }))
             return rc;
     }
-    return poll_bounded(c, L, c->timeout_ms, [&] { return hipStreamQuery(L.ctx->stream); });
+    return poll_bounded(c, L, c->timeout_ms, true, [&] { return hipStreamQuery(L.ctx->stream); });
 }
 
 // Test knob comm_fault = k on a local rank's context (qk_ctx_set_knob): the
@@ -744,6 +754,16 @@ int qk_comm_init_host(const qk_comm_host_ops *ops, int rank, int world, int devi
 
 void qk_comm_destroy(qk_comm *comm) {
     if (!comm) return;
+    if (comm->abort_pending) {
+        // the collective never started (its local work outlasted the limit):
+        // abort now — this waits until that local work has drained (hipFree)
+        for (auto &L : comm->local)
+            if (L.nc) {
+                (void)hipSetDevice(L.device);
+                ncclCommAbort(L.nc);
+                L.nc = nullptr;
+            }
+    }
     for (auto &L : comm->local)
         if (L.ctx) (void)wait_local(comm, L);   // (a peer that never arrives: the timeout aborts)
     for (auto &L : comm->local) destroy_local(L);

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -22,6 +23,10 @@ struct qk_knobs {
     int root_test = 0;     // 0: automatic (cost model, api.hip rt_use_scan), 1: Horner, 2: root-set scan
     int comm_fault = 0;    // k > 0 (tests): this rank's payload staging for the k-th collective of its
                            // next sharded operation fails, once (comm.hip fault_now)
+    int rt_karg = 1;       // 1: a root-set scan whose set fits the kernel arguments takes them (api.hip
+                           // root_test_scan_k; configs[4] u64 wall 172 -> 167 us, u32 even,
+                           // profiles/r06/s6_karg_s1/); 0: always the set by an H2D copy (the path of
+                           // larger sets and of the sharded decode; tests compare the two)
     int comm_delay_ms = 0; // k > 0 (tests): a k-ms kernel in front of this rank's next RCCL collective,
                            // once (comm.hip mark_pre: the bounded wait for pre-collective work)
 };
@@ -43,6 +48,10 @@ struct qk_ctx {
     uint64_t *d_small = nullptr;       // partial output / hit counters (small, fixed)
     uint64_t *h_small = nullptr;       // pinned mirror of d_small
     uint64_t *h_small_dev = nullptr;   // h_small as the device addresses it
+    // the kernel-argument root-set scan keeps its hit / stop tickets
+    // (d_small[0], [3]) running across calls: their values now, when valid
+    uint64_t rt_hbase = 0, rt_sbase = 0;
+    bool rt_bases_valid = false;
     uint64_t *d_hits = nullptr;
     size_t hits_cap = 0;
 
@@ -117,6 +126,10 @@ constexpr size_t SMALL_STOPS = SMALL_WORDS - RT_NSTOP;
 constexpr size_t SMALL_HITPF_N = SMALL_STOPS - SMALL_HITPF;
 // the same slots relative to SMALL_NHITS (the kernel's hout)
 constexpr size_t RT_STOP0 = SMALL_STOPS - SMALL_NHITS;
+// d_small[SMALL_KT ..+4): the kernel-argument root-set scan's counters (hit
+// ticket, stop minimum, -, stop ticket), apart from everything else that
+// writes d_small (encode partials, the two-phase root test's header)
+constexpr size_t SMALL_KT = SMALL_WORDS - 8;
 
 // One no-op kernel per translation unit.  HIP loads a translation unit's code
 // object at the first launch of any of its kernels, and sets up its staging
@@ -188,7 +201,17 @@ int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uin
 struct RtScanSet {
     uint32_t S = 1, words = 0, m1 = 1, m2 = 1, shift = 28;
 };
-template <typename T> bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &out);
+template <typename T>
+bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &out, bool compact = false);
+// the root-set scan with its set in the kernel arguments (decode.hip)
+constexpr size_t RT_KTAB_BYTES = 2048;
+struct RtKTab {
+    uint64_t w[RT_KTAB_BYTES / 8];
+};
+template <typename T>
+int launch_root_scan_k(qk_ctx *ctx, const std::vector<T> &tab, const RtScanSet &set, const T *log, size_t n,
+                       int use_stop, T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,
+                       uint64_t hbase, uint64_t sbase, hipStream_t s);
 template <typename T>
 int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
                      T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,

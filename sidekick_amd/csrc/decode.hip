@@ -13,7 +13,9 @@
 // atomic ticket; the host sorts them into log order.  The `break` at the
 // first log entry equal to diff.last_value() becomes an atomicMin of that
 // position; the host drops hits at or after it.
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -27,11 +29,15 @@ QK_WARM_KERNEL(decode)
 
 constexpr int RT_BLOCK = 256;
 
-// hout (optional, k_root_scan): the hit / stop also into pinned host memory
+// hout (optional, k_root_scan): the hit / stop also into pinned host memory.
+// hbase / sbase: the values the hit / stop tickets (counters[0], [3]) start
+// from in this launch (0 after the host reset them; the kernel-argument form
+// of the scan keeps them running across calls instead of resetting them)
 __device__ __forceinline__ void rt_record(uint64_t pos, bool hit, bool stop, uint64_t *hits, uint64_t cap,
-                                          uint64_t *counters, uint64_t *hout = nullptr, uint32_t nhpf = 0) {
+                                          uint64_t *counters, uint64_t *hout = nullptr, uint32_t nhpf = 0,
+                                          uint64_t hbase = 0, uint64_t sbase = 0) {
     if (hit) {
-        const uint64_t slot = atomicAdd((unsigned long long *)&counters[0], 1ull);
+        const uint64_t slot = atomicAdd((unsigned long long *)&counters[0], 1ull) - hbase;
         if (slot < cap) hits[slot] = pos;
         if (hout) {
             if (slot < nhpf) hout[4 + slot] = pos;
@@ -41,7 +47,7 @@ __device__ __forceinline__ void rt_record(uint64_t pos, bool hit, bool stop, uin
     if (stop) {
         atomicMin((unsigned long long *)&counters[1], (unsigned long long)pos);
         if (hout) {
-            const uint64_t k = atomicAdd((unsigned long long *)&counters[3], 1ull);
+            const uint64_t k = atomicAdd((unsigned long long *)&counters[3], 1ull) - sbase;
             if (k < RT_NSTOP) hout[RT_STOP0 + k] = pos;
             else hout[2] = 1;
         }
@@ -423,16 +429,16 @@ __device__ __forceinline__ bool rs_member(T x, const T *__restrict__ set, uint32
 // counters[3]) — and a slot past either sets the overflow flag hout[2], so
 // the host reads the result after the kernel with no copy behind it (the
 // slots are pre-filled with ~0 by the host; a decode finds ~d hits).
-// U: 16-byte loads per lane per iteration (knob rt_scan_u; 1 is the fastest
-// measured)
-// NT: the log's 16-byte loads nontemporal (knob rt_scan_nt)
-template <typename T, int S, int U = 1, bool NT = false>
-__global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ log, uint64_t n, uint32_t head,
-                                                        const T *__restrict__ tab, uint32_t words, uint32_t m1,
-                                                        uint32_t m2, uint32_t shift, int use_stop, T stop_value,
-                                                        uint64_t *__restrict__ hits, uint64_t cap,
-                                                        uint64_t *__restrict__ counters, uint64_t *hout,
-                                                        uint32_t nhpf) {
+// One 16-byte load per lane per iteration (2 / 4 in flight measured slower,
+// DESIGN.md §3.4), nontemporal (the log is read once).  tab: the set in
+// device memory (k_root_scan: copied with the counters, multipliers from
+// counters[2]) or in the kernel arguments (k_root_scan_k).
+template <typename T, int S>
+__device__ __forceinline__ void root_scan_body(const T *__restrict__ log, uint64_t n, uint32_t head, const T *tab,
+                                               uint32_t words, uint32_t m1, uint32_t m2, uint32_t shift, int use_stop,
+                                               T stop_value, uint64_t *__restrict__ hits, uint64_t cap,
+                                               uint64_t *__restrict__ counters, uint64_t *hout, uint32_t nhpf,
+                                               uint64_t hbase, uint64_t sbase) {
     extern __shared__ __align__(16) unsigned char rs_lds[];
     T *set = reinterpret_cast<T *>(rs_lds);
     for (uint32_t i = threadIdx.x; i < words; i += RT_BLOCK) set[i] = tab[i];
@@ -444,73 +450,79 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ lo
     const uint64_t h = head < n ? head : n;
     const uint64_t body = (n - h) / V;
     const Vec *__restrict__ v = reinterpret_cast<const Vec *>(log + h);
-    // U loads in flight per lane
-    uint64_t i = gtid;
-    for (; i + (U - 1) * nthr < body; i += U * nthr) {
-        Vec w[U];
+    for (uint64_t i = gtid; i < body; i += nthr) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(&v[i]));
+        Vec w;
+        __builtin_memcpy(&w, &x, 16);
+        const T *e = reinterpret_cast<const T *>(&w);
+        bool any = false, hit[V], st[V];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if constexpr (NT) {
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(&v[i + u * nthr]));
-                __builtin_memcpy(&w[u], &x, 16);
-            } else {
-                w[u] = v[i + u * nthr];
-            }
-        }
-        bool any = false, hit[U][V], st[U][V];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const T *e = reinterpret_cast<const T *>(&w[u]);
-#pragma unroll
-            for (int j = 0; j < V; ++j) {
-                hit[u][j] = rs_member<T, S>(e[j], set, m1, m2, shift);
-                st[u][j] = use_stop && e[j] == stop_value;
-                any |= hit[u][j] | st[u][j];
-            }
+        for (int j = 0; j < V; ++j) {
+            hit[j] = rs_member<T, S>(e[j], set, m1, m2, shift);
+            st[j] = use_stop && e[j] == stop_value;
+            any |= hit[j] | st[j];
         }
         if (any) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int j = 0; j < V; ++j)
-                    rt_record(h + (uint64_t)V * (i + u * nthr) + j, hit[u][j], st[u][j], hits, cap, counters, hout,
-                              nhpf);
-        }
-    }
-    for (; i < body; i += nthr) {   // the last < U loads of this lane
-        const Vec w0 = v[i];
-        const T *e0 = reinterpret_cast<const T *>(&w0);
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const bool hit = rs_member<T, S>(e0[j], set, m1, m2, shift);
-            const bool st = use_stop && e0[j] == stop_value;
-            if (hit | st) rt_record(h + (uint64_t)V * i + j, hit, st, hits, cap, counters, hout, nhpf);
+            for (int j = 0; j < V; ++j)
+                rt_record(h + (uint64_t)V * i + j, hit[j], st[j], hits, cap, counters, hout, nhpf, hbase, sbase);
         }
     }
     const uint64_t tail0 = h + body * V;
     if (gtid < h) {
         const T x = log[gtid];
         rt_record(gtid, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters,
-                  hout, nhpf);
+                  hout, nhpf, hbase, sbase);
     }
     if (gtid < n - tail0) {
         const uint64_t pos = tail0 + gtid;
         const T x = log[pos];
         rt_record(pos, rs_member<T, S>(x, set, m1, m2, shift), use_stop && x == stop_value, hits, cap, counters,
-                  hout, nhpf);
+                  hout, nhpf, hbase, sbase);
     }
+}
+
+template <typename T, int S>
+__global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ log, uint64_t n, uint32_t head,
+                                                        const T *__restrict__ tab, uint32_t words, uint32_t shift,
+                                                        int use_stop, T stop_value, uint64_t *__restrict__ hits,
+                                                        uint64_t cap, uint64_t *__restrict__ counters, uint64_t *hout,
+                                                        uint32_t nhpf) {
+    const uint64_t mm = counters[2];   // m1 | m2 << 32, copied with the set
+    root_scan_body<T, S>(log, n, head, tab, words, (uint32_t)mm, (uint32_t)(mm >> 32), shift, use_stop, stop_value,
+                         hits, cap, counters, hout, nhpf, 0, 0);
+}
+
+// The set in the kernel arguments (a table of at most RT_KTAB_BYTES): no
+// copy in front of the scan — at configs[4] (d = 32) the H2D copy's API call
+// and blit kernel were ~8 of the call's ~100 µs.  The tickets run on from
+// hbase / sbase (no counter reset either).
+template <typename T, int S>
+__global__ __launch_bounds__(RT_BLOCK) void k_root_scan_k(const T *__restrict__ log, uint64_t n, uint32_t head,
+                                                          RtKTab tab, uint32_t words, uint32_t m1, uint32_t m2,
+                                                          uint32_t shift, int use_stop, T stop_value,
+                                                          uint64_t *__restrict__ hits, uint64_t cap,
+                                                          uint64_t *__restrict__ counters, uint64_t *hout,
+                                                          uint32_t nhpf, uint64_t hbase, uint64_t sbase) {
+    root_scan_body<T, S>(log, n, head, reinterpret_cast<const T *>(tab.w), words, m1, m2, shift, use_stop, stop_value,
+                         hits, cap, counters, hout, nhpf, hbase, sbase);
 }
 
 // host: the hash set of the roots (see k_root_scan).  S = 1 for up to 32
 // roots (2^b >= 2 k^2 buckets: a multiplier pair without collisions is found
 // in ~1.3 tries on average), else S = 4 with 2^b >= 2k buckets (mean load
-// 1/2).  Returns false when no multipliers fit within the attempt limit.
+// 1/2).  compact: S = 1 with 2^b >= k^2 / 6 — a table small enough for the
+// kernel arguments (k = 32: 256 words; a collision-free multiplier pair is
+// then found in ~e^(k^2 / 2^(b+1)) = 7 tries, a few hundred host hashes).
+// (S = 4 with 2^b >= 2k, the other small layout, costs the u32 scan 84
+// against 65 µs at configs[4]: four compares per candidate.)  Returns false
+// when no multipliers fit within the attempt limit.
 template <typename T>
-bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &out) {
-    set.S = k <= 32 ? 1 : 4;
+bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &out, bool compact) {
+    set.S = k <= 32 || compact ? 1 : 4;
     uint32_t b = 4;
-    const uint64_t want = set.S == 1 ? 2ull * k * k : 2ull * k;
+    const uint64_t want = compact ? ((uint64_t)k * k + 5) / 6 : set.S == 1 ? 2ull * k * k : 2ull * k;
     while ((1ull << b) < want) ++b;
     set.shift = 32 - b;
     const uint32_t nb = 1u << b;
@@ -537,8 +549,8 @@ bool rt_scan_table(const T *roots, uint32_t k, RtScanSet &set, std::vector<T> &o
     }
     return false;
 }
-template bool rt_scan_table<uint32_t>(const uint32_t *, uint32_t, RtScanSet &, std::vector<uint32_t> &);
-template bool rt_scan_table<uint64_t>(const uint64_t *, uint32_t, RtScanSet &, std::vector<uint64_t> &);
+template bool rt_scan_table<uint32_t>(const uint32_t *, uint32_t, RtScanSet &, std::vector<uint32_t> &, bool);
+template bool rt_scan_table<uint64_t>(const uint64_t *, uint32_t, RtScanSet &, std::vector<uint64_t> &, bool);
 
 template <typename T>
 int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
@@ -554,9 +566,9 @@ int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T 
     const uint64_t units = (n + (16 / sizeof(T)) - 1) / (16 / sizeof(T));
     hipEvent_t e0 = prof_begin(ctx, s);
 #define QK_RS(SS)                                                                                             \
-    hipLaunchKernelGGL((k_root_scan<T, SS, 1, true>), dim3(rs_grid(ctx, k_root_scan<T, SS, 1, true>, units, lds)), \
-                       dim3(RT_BLOCK), lds, s, log, (uint64_t)n, head, d_tab, set.words, set.m1, set.m2, set.shift, \
-                       use_stop, stop_value, hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N)
+    hipLaunchKernelGGL((k_root_scan<T, SS>), dim3(rs_grid(ctx, k_root_scan<T, SS>, units, lds)), dim3(RT_BLOCK), \
+                       lds, s, log, (uint64_t)n, head, d_tab, set.words, set.shift, use_stop, stop_value, hits, cap, \
+                       counters, hout, (uint32_t)SMALL_HITPF_N)
     if (set.S == 1) QK_RS(1);
     else QK_RS(4);
 #undef QK_RS
@@ -627,6 +639,33 @@ int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uin
     QK_HIP_TRY(hipGetLastError());
     return QK_OK;
 }
+
+template <typename T>
+int launch_root_scan_k(qk_ctx *ctx, const std::vector<T> &tabv, const RtScanSet &set, const T *log, size_t n,
+                       int use_stop, T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,
+                       uint64_t hbase, uint64_t sbase, hipStream_t s) {
+    const uintptr_t a = (uintptr_t)log;
+    if (a & (sizeof(T) - 1)) return QK_E_INVAL;
+    if (set.words * sizeof(T) > RT_KTAB_BYTES || set.S != 1) return QK_E_INVAL;
+    RtKTab tab;
+    memcpy(tab.w, tabv.data(), (size_t)set.words * sizeof(T));
+    const uint32_t head = (uint32_t)(((16 - (a & 15)) & 15) / sizeof(T));
+    const size_t lds = (size_t)set.words * sizeof(T);
+    const uint64_t units = (n + (16 / sizeof(T)) - 1) / (16 / sizeof(T));
+    hipEvent_t e0 = prof_begin(ctx, s);
+    hipLaunchKernelGGL((k_root_scan_k<T, 1>), dim3(rs_grid(ctx, k_root_scan_k<T, 1>, units, lds)), dim3(RT_BLOCK), lds,
+                       s, log, (uint64_t)n, head, tab, set.words, set.m1, set.m2, set.shift, use_stop, stop_value,
+                       hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N, hbase, sbase);
+    prof_end(ctx, s, e0);
+    QK_HIP_TRY(hipGetLastError());
+    return QK_OK;
+}
+template int launch_root_scan_k<uint32_t>(qk_ctx *, const std::vector<uint32_t> &, const RtScanSet &,
+                                          const uint32_t *, size_t, int, uint32_t, uint64_t *, uint64_t, uint64_t *,
+                                          uint64_t *, uint64_t, uint64_t, hipStream_t);
+template int launch_root_scan_k<uint64_t>(qk_ctx *, const std::vector<uint64_t> &, const RtScanSet &,
+                                          const uint64_t *, size_t, int, uint64_t, uint64_t *, uint64_t, uint64_t *,
+                                          uint64_t *, uint64_t, uint64_t, hipStream_t);
 
 template int launch_root_scan<uint32_t>(qk_ctx *, const uint32_t *, const RtScanSet &, const uint32_t *, size_t, int,
                                         uint32_t, uint64_t *, uint64_t, uint64_t *, uint64_t *, hipStream_t);

@@ -381,9 +381,12 @@ def test_rccl_world1_pre_collective_wait_is_bounded(how):
     """Local work in front of an RCCL collective (knob comm_delay_ms: a kernel
     of that many ms on the rank's stream before its reduce) is waited for
     under its own limit, 4 x the communicator's timeout: a delay inside the
-    limit completes bit-exactly; one past it aborts the communicator with
-    QK_E_COMM within about that limit (no unbounded hipEventSynchronize), q
-    untouched, and later calls on it fail fast."""
+    limit completes bit-exactly; one past it returns QK_E_COMM within about
+    that limit (no unbounded hipEventSynchronize), q untouched, the
+    communicator broken — later calls fail at once — and its destroy aborts
+    RCCL once the local work has drained.  (A world-1 in-place ncclReduce
+    enqueues no kernel: profiles/r06/comm1/, so nothing of RCCL's runs after
+    the abort.)"""
     import time
     import ctypes as C
     import sidekick_amd as sk
@@ -407,11 +410,12 @@ def test_rccl_world1_pre_collective_wait_is_bounded(how):
                                          q._buf, 0, None)
         dt = time.time() - t0
         assert rc == QK_E_COMM, rc
-        assert 0.7 < dt < 2.5, dt              # the 800 ms limit, not the 3 s kernel
+        assert 0.7 < dt < 2.0, dt              # the 800 ms limit, not the 3 s kernel
         assert q.count() == 1 and q.power_sums()[0] == 7
+        t0 = time.time()
         rc = lib().qk_u32_encode_sharded(c.handle, (C.c_void_p * 1)(ids.data_ptr()), (C.c_size_t * 1)(len(host)),
                                          q._buf, 0, None)
-        assert rc == QK_E_COMM and q.count() == 1
+        assert rc == QK_E_COMM and q.count() == 1 and time.time() - t0 < 0.5
         assert rc != QK_OK
     finally:
         import torch

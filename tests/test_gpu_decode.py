@@ -256,6 +256,58 @@ def test_hit_and_stop_slot_boundaries(nhit):
     assert q.root_test_shard(c, dev(log2), stop_value=stop_value) == (want, int(spos[0]))
 
 
+def test_scan_kernel_args_tickets_run_on(root_test_mode):
+    """The root-set scan with its set in the kernel arguments keeps its hit
+    and stop tickets running across calls (no reset in front of the scan):
+    a sequence of decodes with different hit and stop counts, interleaved
+    with encodes (which write the context's small buffer), a Horner call, a
+    shard call, a call past the hit slots (the two-phase rerun, which
+    invalidates the running tickets) and a stop value past the stop slots,
+    every one against the oracle; knob rt_karg = 0 (the set by copy) gives
+    the same lists."""
+    import sidekick_amd as skm
+    ctx = skm.get_context(0)
+    results = {}
+    for karg in (1, 0):
+        rng = np.random.default_rng(77)   # the same sequence of cases for both forms
+        base = rng.integers(0, 1 << 32, size=300_000, dtype=np.uint64).astype(np.uint32)
+        ctx.set_knob("rt_karg", karg)
+        try:
+            out = []
+            for it, (nhit, nstop) in enumerate(((3, 0), (40, 2), (1, 1), (1100, 0), (7, 0), (20, 30), (5, 1),
+                                                 (2, 17), (9, 0))):
+                roots = [int(r) for r in rng.integers(1, 1 << 31, size=3)]
+                log = base.copy()
+                log[np.isin(log, roots)] = 11
+                pos = np.sort(rng.choice(len(log), size=nhit, replace=False))
+                log[pos] = np.array(roots, dtype=np.uint32)[np.arange(nhit) % 3]
+                q = sk.PowerSumQuackU32(8)
+                for r in roots:
+                    q.insert(r)
+                c = q.to_coeffs()
+                stop_value = None
+                if nstop:
+                    stop_value = 0xFEEDBEE
+                    log[log == stop_value] = 12
+                    free = np.setdiff1d(np.arange(len(log)), pos)
+                    log[np.sort(rng.choice(free, size=nstop, replace=False))] = stop_value
+                want = qo.root_test_indices(list(c), log.tolist(), qo.P32, stop_value=stop_value)
+                got = q.root_test(c, dev(log), stop_value=stop_value)
+                assert got == want, (karg, it, nhit, nstop)
+                out.append(got)
+                if it == 2:   # an encode through the same context (its partial goes to the small buffer)
+                    e = sk.PowerSumQuackU32(16)
+                    e.insert_batch(dev(log[:5000]))
+                    assert e.power_sums() == coracle.encode_u32(log[:5000], 16)
+                if it == 4:
+                    got2, _ = q.root_test_shard(c, dev(log), stop_value=stop_value)
+                    assert got2 == want
+            results[karg] = out
+        finally:
+            ctx.set_knob("rt_karg", 1)
+    assert results[1] == results[0]
+
+
 @pytest.mark.parametrize("off,n", [(1, 100_007), (2, 100_000), (3, 5), (0, 17)])
 def test_scan_ragged_and_misaligned(off, n, root_test_mode):
     """The root test over a log starting 0-3 entries past a 16-byte boundary
