@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; parity tests through the C ABI")
+    config.addinivalue_line("markers", "slow: a full-size GPU test (tens of GB, ~10 s); deselect with -m 'not slow'")
 
 
 @pytest.fixture(scope="session")
