@@ -582,7 +582,7 @@ int qk_ctx_create(int device, qk_ctx **out) {
     // work-item buffer (1 MiB) allocated
     uint64_t pageable[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (ensure_items(ctx, (size_t)1 << 20) || warm_api(ctx->stream) || warm_encode(ctx->stream) || warm_decode(ctx->stream) ||
-        warm_packets(ctx->stream) || warm_flows(ctx->stream) || warm_comm(ctx->stream) ||
+        warm_packets(ctx->stream) || warm_flows(ctx->stream) || warm_segments(ctx->stream) || warm_comm(ctx->stream) ||
         hipMemcpyAsync(ctx->d_small, pageable, sizeof pageable, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
         hipMemcpyAsync(pageable, ctx->d_small, sizeof pageable, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {

@@ -150,6 +150,7 @@ int warm_encode(hipStream_t s);
 int warm_decode(hipStream_t s);
 int warm_packets(hipStream_t s);
 int warm_flows(hipStream_t s);
+int warm_segments(hipStream_t s);
 int warm_comm(hipStream_t s);
 
 hipStream_t pick_stream(qk_ctx *ctx, void *stream);
