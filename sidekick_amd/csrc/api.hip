@@ -341,6 +341,7 @@ int root_test_begin(qk_ctx *ctx, const RtPlan<T> &plan, const T *coeffs, uint32_
         std::fill(ctx->h_small + SMALL_HITPF, ctx->h_small + SMALL_WORDS, ~0ull);
         ctx->h_small[SMALL_OVF] = 0;
     }
+    ctx->rt_slots_clean = false;   // this call's hits / stops (or Horner's copy) land in the slots
     QK_HIP_TRY(hipMemcpyAsync(ctx->d_small, ctx->h_small, (RT_C + (cbytes + 7) / 8) * sizeof(uint64_t),
                               hipMemcpyHostToDevice, s));
     if (int rc = ensure_hits(ctx, 4096, s)) return rc;
@@ -454,25 +455,43 @@ static int root_test_scan_k(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d
         QK_HIP_TRY(hipMemsetAsync(ctx->d_small + SMALL_KT, 0, 4 * sizeof(uint64_t), s));
         ctx->rt_hbase = ctx->rt_sbase = 0;
     }
-    std::fill(hs + SMALL_HITPF, hs + SMALL_WORDS, ~0ull);
-    hs[SMALL_OVF] = 0;
+    if (!ctx->rt_slots_clean) {
+        std::fill(hs + SMALL_HITPF, hs + SMALL_WORDS, ~0ull);
+        hs[SMALL_OVF] = 0;
+    }
+    ctx->rt_slots_clean = false;
+    const uint64_t gen = ++ctx->rt_gen;
     if (int e = launch_root_scan_k<T>(ctx, tab, set, d_log, n, use_stop, stop_value, ctx->d_hits,
                                       (uint64_t)ctx->hits_cap, ctx->d_small + SMALL_KT, ctx->h_small_dev + SMALL_NHITS,
-                                      ctx->rt_hbase, ctx->rt_sbase, s)) {
+                                      ctx->rt_hbase, ctx->rt_sbase, ctx->d_small + RT_DONE, gen, s)) {
         ctx->rt_bases_valid = false;
         return e;
     }
     ctx->rt_bases_valid = true;
-    // wait by polling: a sleeping synchronisation wakes ~5 µs late
+    // wait by polling the completion mark the kernel's last workgroup writes
+    // (decode.hip k_root_scan_k: the result is in the slots ~3-5 µs before
+    // the stream reports the kernel done), the stream asked now and then: an
+    // error fails the call; a finished stream without the mark (completion
+    // tickets left off by an earlier aborted launch) still has the result,
+    // and the tickets are cleared for the next launch
+    const volatile uint64_t *done = hs + SMALL_DONE;
     for (unsigned spin = 0;; ++spin) {
-        const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) {
-            ctx->rt_bases_valid = false;
-            return QK_E_HIP;
+        if (*done == gen) break;
+        if ((spin & 63) == 63) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                ctx->rt_bases_valid = false;
+                return QK_E_HIP;
+            }
+            if (q == hipSuccess) {
+                if (*done == gen) break;
+                QK_HIP_TRY(hipMemsetAsync(ctx->d_small + RT_DONE, 0, (SMALL_DEV_WORDS - RT_DONE) * sizeof(uint64_t), s));
+                break;
+            }
         }
-        if (spin >= 20000) std::this_thread::sleep_for(std::chrono::microseconds(5));
+        if (spin >= 200000) std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
+    std::atomic_thread_fence(std::memory_order_acquire);
     if (hs[SMALL_OVF]) {   // past the slots: the two-phase form reruns it (and resets the tickets)
         ctx->rt_bases_valid = false;
         return 1;
@@ -487,6 +506,11 @@ static int root_test_scan_k(qk_ctx *ctx, const T *coeffs, uint32_t d, const T *d
     ctx->rt_hbase += c;
     ctx->rt_sbase += ns;
     h.assign(hs + SMALL_HITPF, hs + SMALL_HITPF + c);
+    // the next call finds the slots empty: the c hit slots and the stop
+    // slots back to ~0 (the kernel wrote no others: no overflow)
+    std::fill(hs + SMALL_HITPF, hs + SMALL_HITPF + c, ~0ull);
+    std::fill(hs + SMALL_STOPS, hs + SMALL_WORDS, ~0ull);
+    ctx->rt_slots_clean = true;
     std::sort(h.begin(), h.end());
     stop = use_stop ? std::min<uint64_t>(st, (uint64_t)n) : (uint64_t)n;
     return QK_OK;
@@ -564,7 +588,7 @@ int qk_ctx_create(int device, qk_ctx **out) {
     if (prop.maxThreadsPerMultiProcessor > 0) ctx->max_threads_per_cu = prop.maxThreadsPerMultiProcessor;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&ctx->d_small, SMALL_WORDS * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&ctx->d_small, SMALL_DEV_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&ctx->h_small, SMALL_WORDS * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&ctx->h_flow, 8 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipHostGetDevicePointer((void **)&ctx->h_small_dev, ctx->h_small, 0) != hipSuccess ||
@@ -583,6 +607,7 @@ int qk_ctx_create(int device, qk_ctx **out) {
     uint64_t pageable[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (ensure_items(ctx, (size_t)1 << 20) || warm_api(ctx->stream) || warm_encode(ctx->stream) || warm_decode(ctx->stream) ||
         warm_packets(ctx->stream) || warm_flows(ctx->stream) || warm_segments(ctx->stream) || warm_comm(ctx->stream) ||
+        hipMemsetAsync(ctx->d_small, 0, SMALL_DEV_WORDS * sizeof(uint64_t), ctx->stream) != hipSuccess ||
         hipMemcpyAsync(ctx->d_small, pageable, sizeof pageable, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
         hipMemcpyAsync(pageable, ctx->d_small, sizeof pageable, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {

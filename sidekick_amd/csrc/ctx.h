@@ -52,6 +52,14 @@ struct qk_ctx {
     // (d_small[0], [3]) running across calls: their values now, when valid
     uint64_t rt_hbase = 0, rt_sbase = 0;
     bool rt_bases_valid = false;
+    // the pinned hit / stop slots hold ~0 everywhere (the kernel-argument
+    // scan restores the few it used instead of re-filling all 1020 words)
+    bool rt_slots_clean = false;
+    // k_root_scan_k<u32 / u64, 1> workgroups per CU (0: not yet asked)
+    int rt_occ_k[2] = {0, 0};
+    // the value the next kernel-argument scan's last workgroup writes to
+    // h_small[SMALL_DONE] (the host polls that word, not the stream)
+    uint64_t rt_gen = 0;
     uint64_t *d_hits = nullptr;
     size_t hits_cap = 0;
 
@@ -120,6 +128,7 @@ constexpr size_t RT_C = 4;             // root tests: coefficients / root set fr
 constexpr size_t SMALL_NHITS = 3072;   // h_small: hit count
 constexpr size_t SMALL_STOP = 3073;    // h_small: first stop index
 constexpr size_t SMALL_OVF = 3074;     // h_small: a hit or stop slot past the direct form's room
+constexpr size_t SMALL_DONE = 3075;    // h_small: the kernel-argument scan's completion mark
 constexpr size_t SMALL_HITPF = 3076;   // h_small: the first hits
 constexpr uint32_t RT_NSTOP = 16;      // stop slots of the direct form
 constexpr size_t SMALL_STOPS = SMALL_WORDS - RT_NSTOP;
@@ -130,6 +139,13 @@ constexpr size_t RT_STOP0 = SMALL_STOPS - SMALL_NHITS;
 // ticket, stop minimum, -, stop ticket), apart from everything else that
 // writes d_small (encode partials, the two-phase root test's header)
 constexpr size_t SMALL_KT = SMALL_WORDS - 8;
+// d_small[RT_DONE ..) (device only, past h_small's mirror): the scan's
+// completion tickets, one 128-byte line per workgroup group and one for the
+// groups (a single ticket that every workgroup of the grid takes at its end
+// serialises: +15 µs); zeroed at context creation, each reset by its taker
+constexpr uint32_t RT_DONE_GROUPS = 32;
+constexpr size_t RT_DONE = SMALL_WORDS;
+constexpr size_t SMALL_DEV_WORDS = RT_DONE + 16 * (RT_DONE_GROUPS + 1);
 
 // One no-op kernel per translation unit.  HIP loads a translation unit's code
 // object at the first launch of any of its kernels, and sets up its staging
@@ -212,7 +228,7 @@ struct RtKTab {
 template <typename T>
 int launch_root_scan_k(qk_ctx *ctx, const std::vector<T> &tab, const RtScanSet &set, const T *log, size_t n,
                        int use_stop, T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,
-                       uint64_t hbase, uint64_t sbase, hipStream_t s);
+                       uint64_t hbase, uint64_t sbase, uint64_t *done, uint64_t gen, hipStream_t s);
 template <typename T>
 int launch_root_scan(qk_ctx *ctx, const T *d_tab, const RtScanSet &set, const T *log, size_t n, int use_stop,
                      T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,

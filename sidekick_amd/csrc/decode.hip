@@ -36,20 +36,23 @@ constexpr int RT_BLOCK = 256;
 __device__ __forceinline__ void rt_record(uint64_t pos, bool hit, bool stop, uint64_t *hits, uint64_t cap,
                                           uint64_t *counters, uint64_t *hout = nullptr, uint32_t nhpf = 0,
                                           uint64_t hbase = 0, uint64_t sbase = 0) {
+    // the slots in pinned host memory by system-scope stores (written
+    // through the L2: no write-back needed before the host reads them)
+    auto put = [&](size_t i, uint64_t v) { __hip_atomic_store(&hout[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
     if (hit) {
         const uint64_t slot = atomicAdd((unsigned long long *)&counters[0], 1ull) - hbase;
         if (slot < cap) hits[slot] = pos;
         if (hout) {
-            if (slot < nhpf) hout[4 + slot] = pos;
-            else hout[2] = 1;
+            if (slot < nhpf) put(4 + slot, pos);
+            else put(2, 1);
         }
     }
     if (stop) {
         atomicMin((unsigned long long *)&counters[1], (unsigned long long)pos);
         if (hout) {
             const uint64_t k = atomicAdd((unsigned long long *)&counters[3], 1ull) - sbase;
-            if (k < RT_NSTOP) hout[RT_STOP0 + k] = pos;
-            else hout[2] = 1;
+            if (k < RT_NSTOP) put(RT_STOP0 + k, pos);
+            else put(2, 1);
         }
     }
 }
@@ -497,16 +500,44 @@ __global__ __launch_bounds__(RT_BLOCK) void k_root_scan(const T *__restrict__ lo
 // The set in the kernel arguments (a table of at most RT_KTAB_BYTES): no
 // copy in front of the scan — at configs[4] (d = 32) the H2D copy's API call
 // and blit kernel were ~8 of the call's ~100 µs.  The tickets run on from
-// hbase / sbase (no counter reset either).
+// hbase / sbase (no counter reset either).  Completion: each workgroup,
+// its hits and stops written, takes a ticket of its group (workgroup index
+// mod G, G = min(grid, RT_DONE_GROUPS), done[16 g]); the last of a group
+// takes a ticket of the groups (done[16 G_max]), and the last of those
+// writes gen to hout[SMALL_DONE - SMALL_NHITS], the word the host polls — it
+// sees the result without waiting for the end-of-kernel signal.  Each last
+// taker resets its ticket for the next launch.
 template <typename T, int S>
 __global__ __launch_bounds__(RT_BLOCK) void k_root_scan_k(const T *__restrict__ log, uint64_t n, uint32_t head,
                                                           RtKTab tab, uint32_t words, uint32_t m1, uint32_t m2,
                                                           uint32_t shift, int use_stop, T stop_value,
                                                           uint64_t *__restrict__ hits, uint64_t cap,
                                                           uint64_t *__restrict__ counters, uint64_t *hout,
-                                                          uint32_t nhpf, uint64_t hbase, uint64_t sbase) {
+                                                          uint32_t nhpf, uint64_t hbase, uint64_t sbase,
+                                                          uint64_t *__restrict__ done, uint64_t gen) {
     root_scan_body<T, S>(log, n, head, reinterpret_cast<const T *>(tab.w), words, m1, m2, shift, use_stop, stop_value,
                          hits, cap, counters, hout, nhpf, hbase, sbase);
+    // every wave's stores performed — the hits and stops went to the pinned
+    // slots through the L2 (rt_record) — before the workgroup's ticket (the
+    // barrier itself waits for LDS only).  No system-scope fence: an L2
+    // write-back per workgroup costs +75 µs over the grid, and one in each
+    // of the ~d workgroups that recorded something +20 µs of the u32 scan
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t G = gridDim.x < RT_DONE_GROUPS ? gridDim.x : RT_DONE_GROUPS;
+        const uint32_t g = blockIdx.x % G;
+        unsigned long long *cg = reinterpret_cast<unsigned long long *>(done) + 16 * g;
+        unsigned long long *ct = reinterpret_cast<unsigned long long *>(done) + 16 * RT_DONE_GROUPS;
+        if (__hip_atomic_fetch_add(cg, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (gridDim.x - g + G - 1) / G - 1) {
+            __hip_atomic_store(cg, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(ct, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+                __hip_atomic_store(ct, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&hout[SMALL_DONE - SMALL_NHITS], gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
 }
 
 // host: the hash set of the roots (see k_root_scan).  S = 1 for up to 32
@@ -643,7 +674,7 @@ int launch_root_test_u64(qk_ctx *ctx, const uint64_t *d_c, uint32_t d, const uin
 template <typename T>
 int launch_root_scan_k(qk_ctx *ctx, const std::vector<T> &tabv, const RtScanSet &set, const T *log, size_t n,
                        int use_stop, T stop_value, uint64_t *hits, uint64_t cap, uint64_t *counters, uint64_t *hout,
-                       uint64_t hbase, uint64_t sbase, hipStream_t s) {
+                       uint64_t hbase, uint64_t sbase, uint64_t *done, uint64_t gen, hipStream_t s) {
     const uintptr_t a = (uintptr_t)log;
     if (a & (sizeof(T) - 1)) return QK_E_INVAL;
     if (set.words * sizeof(T) > RT_KTAB_BYTES || set.S != 1) return QK_E_INVAL;
@@ -653,19 +684,28 @@ int launch_root_scan_k(qk_ctx *ctx, const std::vector<T> &tabv, const RtScanSet 
     const size_t lds = (size_t)set.words * sizeof(T);
     const uint64_t units = (n + (16 / sizeof(T)) - 1) / (16 / sizeof(T));
     hipEvent_t e0 = prof_begin(ctx, s);
-    hipLaunchKernelGGL((k_root_scan_k<T, 1>), dim3(rs_grid(ctx, k_root_scan_k<T, 1>, units, lds)), dim3(RT_BLOCK), lds,
+    // workgroups per CU asked once per context (the runtime's occupancy
+    // query costs microseconds of a ~100 µs call), at the largest table
+    int &occ = ctx->rt_occ_k[sizeof(T) == 8];
+    if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_root_scan_k<T, 1>, RT_BLOCK, RT_KTAB_BYTES) !=
+                     hipSuccess || occ < 1))
+        occ = 1;
+    const uint64_t need = std::max<uint64_t>(1, (units + RT_BLOCK - 1) / RT_BLOCK);
+    const uint32_t grid =
+        ctx->grid_override ? ctx->grid_override : (uint32_t)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * occ);
+    hipLaunchKernelGGL((k_root_scan_k<T, 1>), dim3(grid), dim3(RT_BLOCK), lds,
                        s, log, (uint64_t)n, head, tab, set.words, set.m1, set.m2, set.shift, use_stop, stop_value,
-                       hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N, hbase, sbase);
+                       hits, cap, counters, hout, (uint32_t)SMALL_HITPF_N, hbase, sbase, done, gen);
     prof_end(ctx, s, e0);
     QK_HIP_TRY(hipGetLastError());
     return QK_OK;
 }
 template int launch_root_scan_k<uint32_t>(qk_ctx *, const std::vector<uint32_t> &, const RtScanSet &,
                                           const uint32_t *, size_t, int, uint32_t, uint64_t *, uint64_t, uint64_t *,
-                                          uint64_t *, uint64_t, uint64_t, hipStream_t);
+                                          uint64_t *, uint64_t, uint64_t, uint64_t *, uint64_t, hipStream_t);
 template int launch_root_scan_k<uint64_t>(qk_ctx *, const std::vector<uint64_t> &, const RtScanSet &,
                                           const uint64_t *, size_t, int, uint64_t, uint64_t *, uint64_t, uint64_t *,
-                                          uint64_t *, uint64_t, uint64_t, hipStream_t);
+                                          uint64_t *, uint64_t, uint64_t, uint64_t *, uint64_t, hipStream_t);
 
 template int launch_root_scan<uint32_t>(qk_ctx *, const uint32_t *, const RtScanSet &, const uint32_t *, size_t, int,
                                         uint32_t, uint64_t *, uint64_t, uint64_t *, uint64_t *, hipStream_t);

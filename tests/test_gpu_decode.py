@@ -256,6 +256,39 @@ def test_hit_and_stop_slot_boundaries(nhit):
     assert q.root_test_shard(c, dev(log2), stop_value=stop_value) == (want, int(spos[0]))
 
 
+@pytest.mark.parametrize("bits", [32, 64])
+def test_scan_completion_mark_grids(bits):
+    """The kernel-argument scan's completion mark (decode.hip k_root_scan_k:
+    per-group tickets, then a ticket of the groups) at grids below, at and
+    above the group count, uneven groups included, and back-to-back calls
+    with alternating grids (each last taker resets its ticket): every call's
+    hits equal the log positions of the roots."""
+    import sidekick_amd as skm
+    ctx = skm.get_context(0)
+    rng = np.random.default_rng(91 + bits)
+    n = 1_000_003
+    dt = np.uint32 if bits == 32 else np.uint64
+    log = rng.integers(0, 1 << bits, size=n, dtype=np.uint64).astype(dt)
+    roots = [int(r) for r in rng.integers(1, 1 << (bits - 1), size=5)]
+    log[np.isin(log, np.array(roots, dtype=dt))] = 3
+    pos = np.sort(rng.choice(n, size=23, replace=False))
+    log[pos] = np.array(roots, dtype=dt)[np.arange(23) % 5]
+    Q = sk.PowerSumQuackU32 if bits == 32 else sk.PowerSumQuackU64
+    q = Q(8)
+    for r in roots:
+        q.insert(r)
+    c = q.to_coeffs()
+    d_log = dev(log, bits)
+    want = pos.tolist()
+    try:
+        for grid in (1, 5, 31, 32, 33, 100, 977, 0, 7, 0, 64, 1):
+            ctx.set_grid(grid)
+            for _ in range(2):
+                assert q.root_test(c, d_log) == want, grid
+    finally:
+        ctx.set_grid(0)
+
+
 def test_scan_kernel_args_tickets_run_on(root_test_mode):
     """The root-set scan with its set in the kernel arguments keeps its hit
     and stop tickets running across calls (no reset in front of the scan):
