@@ -289,7 +289,7 @@ def cfg_u64(ctx, dev_index, steps=10):
             "oracle_prefix": {"ids": m, "equal": q.power_sums() == want}}
 
 
-def cfg_decode(ctx, dev_index, bits=32, reps=30):
+def cfg_decode(ctx, dev_index, bits=32, reps=60, warm=8):
     """configs[4] (u32; its u64 twin with bits = 64): a 1e8-id candidate log,
     32 seeded drops; quack_A = encode(log), quack_B = encode(log without the
     drops), diff = A - B; the timed call is qk_u*_decode_device(diff, log,
@@ -329,7 +329,7 @@ def cfg_decode(ctx, dev_index, bits=32, reps=30):
     # wall times without the profiling events (two event records per call);
     # the scan kernel's time from separate profiled calls
     for prof in (False, True):
-        for r in range(reps + 2):
+        for r in range(reps + warm):
             if prof:
                 ctx.kernel_stats()
                 ctx.set_profiling(True)
@@ -341,9 +341,9 @@ def cfg_decode(ctx, dev_index, bits=32, reps=30):
             if prof:
                 ctx.set_profiling(False)
                 kms, k = ctx.kernel_stats()
-                if r >= 2:
+                if r >= warm:
                     kerns.append(kms * 1e3 / max(k, 1))
-            elif r >= 2:
+            elif r >= warm:
                 walls.append(wall * 1e6)
     b = bits // 8
     scan = float(np.median(kerns))
