@@ -289,6 +289,25 @@ def test_scan_completion_mark_grids(bits):
         ctx.set_grid(0)
 
 
+def test_scan_completion_mark_many_calls():
+    """Two hundred back-to-back kernel-argument scans over one resident log,
+    each with another root set (1-40 roots drawn from the log, so the hits
+    move across the whole grid every call): every hit list equals the log
+    positions of its roots (numpy), i.e. no call reads its pinned slots
+    before the workgroups that found hits wrote them."""
+    rng = np.random.default_rng(2026)
+    n = 2_000_003
+    log = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    d_log = dev(log)
+    for it in range(200):
+        k = int(rng.integers(1, 41))
+        roots = np.unique(log[rng.choice(n, size=k, replace=False)])
+        q = sk.PowerSumQuackU32(len(roots))
+        for r in roots.tolist():
+            q.insert(int(r))
+        want = np.flatnonzero(np.isin(log, roots)).tolist()
+        assert q.root_test(q.to_coeffs(), d_log) == want, it
+
 def test_scan_kernel_args_tickets_run_on(root_test_mode):
     """The root-set scan with its set in the kernel arguments keeps its hit
     and stop tickets running across calls (no reset in front of the scan):
