@@ -59,8 +59,27 @@ struct ChunkStat {       // per workgroup chunk, written by lane 0
 // chunk, resets included: the host uses them only when the batch has no
 // reset (otherwise it reruns the exact extract + encode-from-last-reset).
 struct NoEncode {};
-template <class C> struct AccOf { using type = bsgs::Acc<C::NB, C::NA, C::ROWS>; };
-template <> struct AccOf<NoEncode> { using type = int; };
+// Shared<NA> (13 <= t <= 32, t <= 8 NA): the (8, NA) baby-step/giant-step
+// sums with the work of a tile split across the workgroup's waves through
+// LDS, as the u64 kernel does (bsgs64.h): every lane computes its record's
+// babies x^1..x^8 and giants x^16 .. x^(8 (NA-1)) (7 + NA - 2 lazy modmuls)
+// into LDS, then wave w runs, over the tile's 256 ids (4 per lane), the
+// a = 0 row and the NA - 1 MAC rows of babies 2w+1 and 2w+2 — 4 NA
+// accumulator VGPRs per lane instead of the lane-private form's (182 VGPRs
+// at t = 32, 2 waves/SIMD: slower than the two passes, below).  Wraps
+// counted per lane (v_addc): the record stream, not the arithmetic, bounds
+// the kernel.
+template <int NA_> struct Shared {
+    static constexpr int NA = NA_;
+    using Pw = bsgs::Cfg<8, NA_, 0, 1, 1>;   // the powers (min-tracked lazy folds)
+};
+template <class C> struct IsShared : std::false_type {};
+template <int NA> struct IsShared<Shared<NA>> : std::true_type {};
+template <class C, bool SH = IsShared<C>::value> struct AccOf { using type = bsgs::Acc<C::NB, C::NA, C::ROWS>; };
+template <class C> struct AccOf<C, true> { using type = int; };
+template <> struct AccOf<NoEncode, false> { using type = int; };
+template <class C, bool SH = IsShared<C>::value> struct ShNA { static constexpr int value = 1; };
+template <class C> struct ShNA<C, true> { static constexpr int value = C::NA; };
 // NT (knob pkt_nt): the records read nontemporal
 template <class C, bool NT = false>
 __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restrict__ bufs, uint64_t n,
@@ -68,8 +87,20 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restri
                                                          uint32_t my_ip_le, int check_reset, uint64_t chunk,
                                                          uint32_t *__restrict__ ids_out, ChunkStat *stats,
                                                          uint32_t T, uint64_t *__restrict__ partials) {
-    constexpr bool FUSED = !std::is_same<C, NoEncode>::value;
+    constexpr bool SH = IsShared<C>::value;
+    constexpr bool FUSED = !std::is_same<C, NoEncode>::value && !SH;
+    constexpr int SNA = ShNA<C>::value;   // Shared: giant rows (a = 0 .. SNA-1)
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    // Shared: the tile's babies x^1..x^8 (rows 0-7) and giants x^16 ..
+    // (rows 8 ..), [value][record]; this wave's accumulators: rows a of
+    // babies 2w+1, 2w+2, and the MAC rows' per-lane wrap counts
+    __shared__ uint32_t sh_v[SH ? 8 + SNA - 2 : 1][SH ? PK_BLOCK : 1];
+    [[maybe_unused]] uint64_t sh_acc[SNA][2];
+    [[maybe_unused]] uint32_t sh_c[SNA][2];
+    if constexpr (SH) {
+#pragma unroll
+        for (int a = 0; a < SNA; ++a) sh_acc[a][0] = sh_acc[a][1] = 0, sh_c[a][0] = sh_c[a][1] = 0;
+    }
     __shared__ int64_t s_reset[PK_BLOCK / 64], s_insert[PK_BLOCK / 64];
     __shared__ uint64_t s_cnt[PK_BLOCK / 64], s_nres[PK_BLOCK / 64], s_nins[PK_BLOCK / 64], s_iid[PK_BLOCK / 64];
     [[maybe_unused]] typename AccOf<C>::type S;
@@ -110,9 +141,21 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restri
                     id = record_identifier(rec);
                 }
             }
-            if constexpr (!FUSED) ids_out[pi] = cls == 1 ? id : 0u;
+            if constexpr (std::is_same<C, NoEncode>::value) ids_out[pi] = cls == 1 ? id : 0u;   // the extract pass only
         }
         if constexpr (FUSED) bsgs::one<C>(S, cls == 1 ? id : 0u);   // every lane: EXEC full
+        if constexpr (SH) {   // this record's powers into LDS (read after the barrier below)
+            using Pw = typename C::Pw;
+            uint32_t B[8], A[Pw::ROWS];   // A[r] = x^(8 (r + 1))
+            const uint32_t w = bsgs::powers<Pw>(cls == 1 ? id : 0u, B, A);
+            if (__builtin_expect(__any(w), 0)) {
+                if (w) bsgs::powers_exact<Pw>(B, A);
+            }
+#pragma unroll
+            for (int b = 0; b < 8; ++b) sh_v[b][threadIdx.x] = B[b];
+#pragma unroll
+            for (int r = 1; r < Pw::ROWS; ++r) sh_v[7 + r][threadIdx.x] = A[r];
+        }
         // tile bookkeeping: last reset in tile, inserts after it, last insert
         const unsigned long long rmask = __ballot(cls == 2);
         const unsigned long long imask = __ballot(cls == 1);
@@ -138,6 +181,18 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restri
             s_iid[wave] = last_id;
         }
         __syncthreads();
+        if constexpr (SH) {   // this wave's rows over the tile's 256 records (wave-uniform)
+            const int b0 = 2 * wave;
+#pragma unroll
+            for (int q = 0; q < PK_BLOCK / 64; ++q) {
+                const int j = q * 64 + lane;
+                const uint32_t B0 = sh_v[b0][j], B1 = sh_v[b0 + 1][j];
+                bsgs::row2m(sh_acc[0][0], sh_acc[0][1], B0, B1);
+#pragma unroll
+                for (int a = 1; a < SNA; ++a)   // giant x^(8a): baby 8 (row 7), then rows 8 ..
+                    bsgs::mac2v(sh_acc[a][0], sh_acc[a][1], sh_c[a][0], sh_c[a][1], sh_v[6 + a][j], B0, B1);
+            }
+        }
         if (threadIdx.x == 0) {
             for (int w = 0; w < PK_BLOCK / 64; ++w) { // waves in packet order
                 blk_nres += s_nres[w];
@@ -163,6 +218,22 @@ __global__ __launch_bounds__(PK_BLOCK) void k_pkt_kernel(const uint8_t *__restri
     }
     if constexpr (FUSED)
         bsgs::finish<C>(S, T, [=](uint32_t m, uint64_t v) { partials[(size_t)m * gridDim.x + blockIdx.x] = v; });
+    if constexpr (SH) {   // power 8a + b + 1 is owned by the wave of baby b: lane sums, written by lane 0
+#pragma unroll
+        for (int a = 0; a < SNA; ++a) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t m = 8 * a + 2 * wave + k;
+                // value = acc + c 2^64 with 2^64 == 25 (mod p) for the MAC rows
+                uint64_t x = a == 0 ? fold64_32(sh_acc[0][k])
+                                    : (uint64_t)fold64_32(sh_acc[a][k]) + fold64_32((uint64_t)sh_c[a][k] * 25u);
+                x = fold64_32(x);
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) x += bsgs::shfl_xor_u64(x, off);   // < 2^38
+                if (lane == 0 && m < T) partials[(size_t)m * gridDim.x + blockIdx.x] = x;
+            }
+        }
+    }
 }
 
 } // namespace qk
@@ -214,7 +285,7 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     // occupancy (182 VGPRs at t = 32, 2 waves/SIMD) below what the record
     // stream needs — measured per 1e8 records, fused vs two-pass: t = 12
     // 1.40 vs 1.68 ms, 16 1.89 vs 1.69, 24 1.95 vs 1.75, 32 2.06 vs 1.81.
-    if (t >= 5 && t <= 12) {
+    if (t >= 5 && t <= 32) {
         int frc = QK_OK;
         if (int e = ensure_scratch(ctx, (size_t)nchunks * 32 * sizeof(uint64_t), s)) return e;
         if (int e = scratch_acquire(ctx, s)) return e;
@@ -229,8 +300,16 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
         // accumulators cannot live across the tile loop's divergent
         // bookkeeping (the compiler rejects it)
         if (t <= 8) QK_PKT_FUSED(4, 2, 0);
-        else QK_PKT_FUSED(4, 3, 0);
+        else if (t <= 12) QK_PKT_FUSED(4, 3, 0);
 #undef QK_PKT_FUSED
+#define QK_PKT_SHARED(NA_)                                                                                       \
+    hipLaunchKernelGGL((k_pkt_kernel<Shared<NA_>, true>), dim3(nchunks), dim3(PK_BLOCK), lds, s, d_bufs, (uint64_t)n, \
+                       (uint32_t)stride, d_meta, my_ip_le, check_reset, chunk, (uint32_t *)nullptr, d_stats, t,         \
+                       partials)
+        else if (t <= 16) QK_PKT_SHARED(2);
+        else if (t <= 24) QK_PKT_SHARED(3);
+        else QK_PKT_SHARED(4);
+#undef QK_PKT_SHARED
         prof_end(ctx, s, e0);
         if (hipGetLastError() != hipSuccess) frc = QK_E_HIP;
         if (!frc) frc = launch_finalize_powers_u32(partials, nchunks, t, ctx->d_small, s);

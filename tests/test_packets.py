@@ -122,17 +122,20 @@ def test_gpu_packets_no_meta_no_ip():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("t", [4, 5, 8, 9, 12, 13, 16, 32, 33])
+@pytest.mark.parametrize("t", [4, 5, 8, 9, 12, 13, 16, 24, 25, 28, 31, 32, 33])
 def test_gpu_packets_fused_thresholds(golden, t):
-    """5 <= t <= 12 without a reset in the batch takes the fused kernel
-    (records -> baby-step/giant-step sums, no id array); the lazy-fold wrap ids
-    of the matching configuration sit in records so the exact-recompute branch
-    runs inside it; t = 4 / 13+ and a batch with a reset take the two-pass
-    path.  All against the sniff-loop restatement."""
+    """5 <= t <= 32 without a reset in the batch takes the fused kernel
+    (records -> baby-step/giant-step sums, no id array: lane-private
+    accumulators up to t = 12, the (8, NA) sums split across the waves
+    through LDS from 13 on); the lazy-fold wrap ids of the matching
+    configuration sit in records so the exact-recompute branch runs inside
+    it; t = 4, 33+ and a batch with a reset take the two-pass path.  All
+    against the sniff-loop restatement."""
     import torch
     import sidekick_amd as sk
     from sidekick_amd.quack import encode_packets
-    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "4x4" if t <= 16 else "8x4" if t <= 32 else "8x5"
+    cfg = "4x2" if t <= 8 else "4x3" if t <= 12 else "8x2" if t <= 16 else "8x3" if t <= 24 else "8x4" if t <= 32 \
+        else "8x5"
     wraps = np.array(golden["bsgs_wrap_ids"][cfg], dtype=np.uint32)
     for resets in ((), (31_000,)):
         n = 50_001
@@ -156,8 +159,8 @@ def test_gpu_packets_fused_thresholds(golden, t):
 def test_gpu_packets_chunk_edges(n):
     """Batch sizes around the chunking (one record; a partial tile; one tile
     and one record; many chunks of 4+ tiles): the same sums, counts and reset
-    bookkeeping as the literal loop, fused (t = 12) and two-pass (t = 32),
-    with and without a reset."""
+    bookkeeping as the literal loop, fused (t = 12, and t = 32 without a
+    reset) and two-pass (t = 32 with a reset)."""
     import torch
     import sidekick_amd as sk
     from sidekick_amd.quack import encode_packets
