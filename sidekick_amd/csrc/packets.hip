@@ -11,9 +11,11 @@
 //     sc.insert_packet(parse_identifier(&buf))  /* BE u32 at byte 63 */   (:103-115)
 // (buffer.rs:6-7,80-83,88-90,99-106).
 //
-// Fused (5 <= t <= 12, batches without a reset): k_pkt_kernel<Cfg> classifies
-// the staged records and feeds the ids straight into the headline kernel's
-// baby-step/giant-step accumulators — one pass over the records, no id array.
+// Fused (5 <= t <= 32, batches without a reset): k_pkt_kernel<Cfg> (t <= 12)
+// classifies the staged records and feeds the ids straight into the headline
+// kernel's baby-step/giant-step accumulators, k_pkt_kernel<Shared<NA>>
+// (13 <= t <= 32) the same sums split across the workgroup's waves through
+// LDS — one pass over the records, no id array.
 //
 // Pass 1 (k_pkt_kernel<NoEncode>): each workgroup owns a contiguous chunk of packets
 // and walks it in tiles of 256 records staged into LDS with coalesced 16-byte
@@ -278,13 +280,15 @@ extern "C" int qk_u32_encode_packets_device(qk_ctx *ctx, const uint8_t *d_bufs, 
     const size_t lds = (size_t)PK_BLOCK * stride + 32;
     int rc = QK_OK;
     std::vector<ChunkStat> hs(nchunks);
-    // Fused fast path (5 <= t <= 12): records -> baby-step/giant-step sums in
+    // Fused fast path (5 <= t <= 32): records -> baby-step/giant-step sums in
     // one kernel, no id array.  Used when the batch holds no reset (the
     // common case); a batch with a reset takes the exact two-pass path below.
-    // Larger t stays two-pass: the accumulators cut the fused kernel's
+    // Lane-private accumulators up to t = 12; above, they cut the kernel's
     // occupancy (182 VGPRs at t = 32, 2 waves/SIMD) below what the record
-    // stream needs — measured per 1e8 records, fused vs two-pass: t = 12
-    // 1.40 vs 1.68 ms, 16 1.89 vs 1.69, 24 1.95 vs 1.75, 32 2.06 vs 1.81.
+    // stream needs (per 1e8 records, lane-private fused vs two-pass: t = 12
+    // 1.40 vs 1.68 ms, 16 1.89 vs 1.69, 24 1.95 vs 1.75, 32 2.06 vs 1.81), so
+    // 13 <= t <= 32 splits the sums across the waves (Shared<NA>): t = 16 /
+    // 24 / 32 1.37 / 1.44 / 1.45-1.56 ms (profiles/r06/s8_packets_shared/).
     if (t >= 5 && t <= 32) {
         int frc = QK_OK;
         if (int e = ensure_scratch(ctx, (size_t)nchunks * 32 * sizeof(uint64_t), s)) return e;
