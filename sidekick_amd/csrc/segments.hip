@@ -149,9 +149,15 @@ __global__ __launch_bounds__(SG_BLOCK, 4) void k_seg_small(const uint32_t *__res
     // 0, which adds nothing): the 64 lanes of a wave read 64 different lines,
     // so 4-byte loads moved a whole cache line from L2 per id.  A 16-byte
     // block never straddles a page, so the partial end blocks are safe reads.
+    // The next block's load is issued before this block's four ids are
+    // encoded (one block ahead: the load's latency under the arithmetic).
     const uintptr_t lo = (uintptr_t)(ids + b), hi = (uintptr_t)(ids + e);
-    for (uintptr_t blk = lo & ~(uintptr_t)15; blk < hi; blk += 16) {
-        uint4 w = *reinterpret_cast<const uint4 *>(blk);
+    uintptr_t blk = lo & ~(uintptr_t)15;
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (blk < hi) nxt = *reinterpret_cast<const uint4 *>(blk);
+    for (; blk < hi; blk += 16) {
+        uint4 w = nxt;
+        if (blk + 16 < hi) nxt = *reinterpret_cast<const uint4 *>(blk + 16);
         if (blk < lo || blk + 16 > hi) {
             w.x = blk + 0 >= lo && blk + 0 < hi ? w.x : 0u;
             w.y = blk + 4 >= lo && blk + 4 < hi ? w.y : 0u;
