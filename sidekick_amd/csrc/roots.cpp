@@ -702,6 +702,21 @@ struct F32 {
     }
 };
 
+// Small factors of a u32 split (degree <= small_split_deg, the factors of
+// 3-4 roots a 38-way split leaves): split 10 ways (E = 2, LO = 5) — 10
+// class gcds instead of 38 for a handful of roots, the one exponentiation
+// the same length
+#ifndef SPLIT32S
+#define SPLIT32S 5
+#endif
+struct F32s : F32 {
+    static constexpr uint32_t L = SPLIT32S;
+    static constexpr uint32_t E = L & (0u - L);
+    static constexpr uint32_t LO = L / E;
+};
+template <class F> struct SmallSplit;
+template <> struct SmallSplit<F32> { using type = F32s; };
+
 struct F64 {
     using T = uint64_t;
     using A = unsigned __int128;
@@ -746,6 +761,18 @@ struct F64 {
         return mul64(r, r) == n;
     }
 };
+// and of a u64 split: the factors of a group share one exponentiation
+// mod their product (group_deg); a group of small factors only takes it
+// with SPLIT64S classes
+#ifndef SPLIT64S
+#define SPLIT64S 44
+#endif
+struct F64s : F64 {
+    static constexpr uint32_t L = SPLIT64S;
+    static constexpr uint32_t E = L & (0u - L);
+    static constexpr uint32_t LO = L / E;
+};
+template <> struct SmallSplit<F64> { using type = F64s; };
 
 // Square roots of several n at once (ok[j]: n_j is a residue): the
 // exponentiations' square-and-multiply steps interleaved across the n_j, so
@@ -1376,6 +1403,7 @@ template <class F> Poly<F> mul_poly(const Poly<F> &a, const Poly<F> &b) {
 // 45.0 us alone, 43.4-43.7 at 16, 43.3-43.4 at 24; u32 21.6 alone, 21.9 at
 // 16 and 24 — grouped for u64 only
 static size_t group_deg = 24;
+static size_t small_split_deg = 6;   // SmallSplit factors up to this degree (0: none; tools/prof_roots.cpp A/B)
 
 // a primitive L-th root of unity of GF(p) (L | p - 1)
 template <class F> typename F::T root_of_unity() {
@@ -1587,7 +1615,10 @@ template <class F> class Splitter {
 // inversion and 3 products per root instead of one inversion per factor).
 template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out, bool exact) {
     using T = typename F::T;
+    using Fs = typename SmallSplit<F>::type;
+    constexpr bool HAS_SMALL = Fs::L != F::L;
     const Splitter<F> S{};
+    const Splitter<Fs> Ss{};
     std::vector<T> num, den;
     std::vector<Poly<F>> todo{g0};
     std::vector<int> tries{0};
@@ -1642,16 +1673,29 @@ template <class F> bool split(const Poly<F> &g0, std::vector<typename F::T> &out
         for (size_t i0 = 0; i0 < big.size();) {
             size_t i1 = i0 + 1, deg = big[i0].size() - 1;
             const size_t cap = F::W == 64 ? group_deg : 0;
-            while (i1 < big.size() && deg + big[i1].size() - 1 <= cap) deg += big[i1++].size() - 1;
+            size_t dmax = deg;
+            while (i1 < big.size() && deg + big[i1].size() - 1 <= cap) {
+                dmax = std::max(dmax, big[i1].size() - 1);
+                deg += big[i1++].size() - 1;
+            }
             Poly<F> H = big[i0];
             for (size_t i = i0 + 1; i < i1; ++i) H = mul_poly<F>(H, big[i]);
-            ModRing<F> R(H);
             s += GAMMA;
             const T a = F::canon_any((T)splitmix_mix(s));
-            const typename Splitter<F>::Pw pw = Splitter<F>::powers(R, a);
+            const bool small = HAS_SMALL && dmax <= small_split_deg;   // every factor of the group small
+            typename Splitter<F>::Pw pw;
+            typename Splitter<Fs>::Pw pws;
+            if (small) {
+                ModRing<Fs> R(H);
+                pws = Splitter<Fs>::powers(R, a);
+            } else {
+                ModRing<F> R(H);
+                pw = Splitter<F>::powers(R, a);
+            }
             for (size_t i = i0; i < i1; ++i) {
                 std::vector<Poly<F>> parts;
-                S.split_with(big[i], pw, a, parts);
+                if (small) Ss.split_with(big[i], pws, a, parts);
+                else S.split_with(big[i], pw, a, parts);
                 if (parts.size() < 2) {   // no split with this a: again with the next one
                     todo.push_back(std::move(big[i]));
                     tries.push_back(bt[i] + 1);

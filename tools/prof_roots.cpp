@@ -59,20 +59,18 @@ template <class F> static void prof(const char *name, uint32_t d, int reps) {
             }
             for (uint32_t i = 1; i <= d; ++i) cv[i - 1] = h[d - i];
         }
-        const size_t gs[] = {24, 24, 24, 24, 24, 24}, vs[] = {0, 1};   // vs: pair_cuts
+        const size_t vs[] = {0, 4, 6, 8};   // small_split_deg (u32: factors split 10 ways up to it)
+        const size_t keep = small_split_deg;
         printf("{\"field\": \"%s\", \"ab\": [", name);
-        for (int r = 0; r < 6; ++r)
-            for (int v = 0; v < 2; ++v) {
-                group_deg = gs[r];
-                pair_cuts = vs[v];
+        for (int r = 0; r < 4; ++r)
+            for (int v = 0; v < 4; ++v) {
+                small_split_deg = vs[v];
                 double t = 0;
                 for (auto &cv : cs) t += best_us(reps, [&] { sink += roots<F>(cv.data(), d).size(); }) / cs.size();
-                printf("%s{\"group_deg\": %zu, \"pair_cuts\": %zu, \"roots_us\": %.2f}", r + v ? ", " : "",
-                       gs[r], vs[v], t);
+                printf("%s{\"small_split_deg\": %zu, \"roots_us\": %.2f}", r + v ? ", " : "", vs[v], t);
             }
         printf("]}\n");
-        group_deg = 24;
-        pair_cuts = true;
+        small_split_deg = keep;
     }
     const double t_ring = best_us(reps, [&] { ModRing<F> R(f); sink += R.m; });
     ModRing<F> R(f);
