@@ -289,7 +289,7 @@ def cfg_u64(ctx, dev_index, steps=10):
             "oracle_prefix": {"ids": m, "equal": q.power_sums() == want}}
 
 
-def cfg_decode(ctx, dev_index, bits=32, reps=60, warm=8):
+def cfg_decode(ctx, dev_index, bits=32, reps=200, warm=8):
     """configs[4] (u32; its u64 twin with bits = 64): a 1e8-id candidate log,
     32 seeded drops; quack_A = encode(log), quack_B = encode(log without the
     drops), diff = A - B; the timed call is qk_u*_decode_device(diff, log,
