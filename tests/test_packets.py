@@ -74,6 +74,7 @@ def test_vector_sniff_matches_oracle():
     (0, 67, 0, ()), (1, 67, 0, ()), (255, 67, 3, ()), (256, 67, 0, (255,)), (257, 67, 1, (256,)),
     (5000, 67, 7, (0, 1023, 1024)), (5000, 128, 0, (4999,)), (100_003, 67, 13, (33_333,)),
     (1_000_000, 67, 0, (123_456, 999_000)), (1_000_000, 67, 5, ()),
+    (5000, 128, 3, ()), (100_003, 67, 13, ()), (70_001, 200, 7, ()),   # t = 32 one-pass: strides, unaligned bases
 ])
 def test_gpu_packets_vs_oracle(n, stride, off, resets):
     import torch
